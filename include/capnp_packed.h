@@ -1,0 +1,188 @@
+/*
+ * capnp_packed.h — C ABI of the MI355X-native Cap'n Proto packed-stream codec.
+ *
+ * This is the drop-in boundary that replaces the bodies of the packed codec in
+ * capnproto-rust (capnp 0.27.0).  Every entry point below names the reference
+ * item it stands in for (paths relative to the capnproto-rust checkout):
+ *
+ *   PackedWrite::write_all      capnp/src/serialize_packed.rs:300-440
+ *   PackedRead::read            capnp/src/serialize_packed.rs:76-229
+ *   serialize_packed::write_message          serialize_packed.rs:446-453
+ *   serialize_packed::read_message           serialize_packed.rs:233-242
+ *   serialize_packed::try_read_message       serialize_packed.rs:246-255
+ *   serialize_packed::read_message_no_alloc  serialize_packed.rs:263-273
+ *   serialize_packed::try_read_message_no_alloc serialize_packed.rs:281-291
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no HIP or torch types.  `stream` is a
+ *     hipStream_t passed as void* (NULL = the context's own stream).
+ *   - All buffers are caller-owned.  The library never frees caller memory.
+ *   - Functions prefixed capnp_gpu_* take DEVICE pointers and are stream
+ *     ordered (asynchronous).  All other functions take HOST pointers and are
+ *     blocking; they stage through pinned memory and run the same HIP kernels.
+ *   - There is no CPU implementation of the transform in this library: if no
+ *     gfx950 device is present, capnp_ctx_create fails with CAPNP_E_NO_DEVICE.
+ *   - Status codes map 1:1 onto capnp::ErrorKind (capnp/src/lib.rs:211-426).
+ */
+#ifndef CAPNP_PACKED_H
+#define CAPNP_PACKED_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum capnp_status {
+    CAPNP_OK = 0,
+    /* try_read_message* hit a clean EOF on a message boundary: Ok(None)
+       (serialize.rs:458-461). */
+    CAPNP_NONE = 1,
+    /* ErrorKind::PrematureEndOfPackedInput (lib.rs:394). */
+    CAPNP_E_PREMATURE_END_OF_PACKED_INPUT = 2,
+    /* ErrorKind::PackedInputDidNotEndCleanlyOnASegmentBoundary (lib.rs:388). */
+    CAPNP_E_DID_NOT_END_CLEANLY = 3,
+    /* ErrorKind::FailedToFillTheWholeBuffer (lib.rs:271, io.rs:26-28). */
+    CAPNP_E_FAILED_TO_FILL_WHOLE_BUFFER = 4,
+    /* ErrorKind::PrematureEndOfFile (lib.rs:391). */
+    CAPNP_E_PREMATURE_END_OF_FILE = 5,
+    /* ErrorKind::InvalidNumberOfSegments (lib.rs:310). */
+    CAPNP_E_INVALID_NUMBER_OF_SEGMENTS = 6,
+    /* ErrorKind::MessageSizeOverflow (lib.rs:373). */
+    CAPNP_E_MESSAGE_SIZE_OVERFLOW = 7,
+    /* ErrorKind::MessageTooLarge (lib.rs:376). */
+    CAPNP_E_MESSAGE_TOO_LARGE = 8,
+    /* ErrorKind::BufferNotLargeEnough (lib.rs:232). */
+    CAPNP_E_BUFFER_NOT_LARGE_ENOUGH = 9,
+    /* ErrorKind::UnalignedSegment (lib.rs:419). */
+    CAPNP_E_UNALIGNED_SEGMENT = 10,
+    /* Replaces the panic "PackedRead reads must be word-aligned."
+       (serialize_packed.rs:86) and non-word-multiple write_all input. */
+    CAPNP_E_MISALIGNED_LEN = 11,
+    /* Library-level errors (no counterpart in the reference). */
+    CAPNP_E_INVALID_ARGUMENT = 64,
+    CAPNP_E_NO_DEVICE = 65,
+    CAPNP_E_HIP = 66,
+    CAPNP_E_OUT_OF_MEMORY = 67
+} capnp_status;
+
+/* Mirror of capnp::message::ReaderOptions (message.rs:85-120).  Only the
+   traversal limit is consulted by the framing reader (serialize.rs:501-507). */
+typedef struct capnp_reader_options {
+    uint64_t traversal_limit_in_words; /* default 8 Mi words (message.rs:117) */
+    int32_t has_traversal_limit;       /* 0 => None (no limit)               */
+    int32_t nesting_limit;             /* carried, not used by the codec      */
+} capnp_reader_options;
+
+/* Limit on segments per message (serialize.rs:39). */
+#define CAPNP_SEGMENTS_COUNT_LIMIT 512u
+
+typedef struct capnp_ctx capnp_ctx;
+
+/* ---- context ----------------------------------------------------------- */
+/* Creates a context bound to HIP device `device` (its own stream, workspace
+   and pinned staging).  Returns NULL and sets *status on failure. */
+capnp_ctx* capnp_ctx_create(int device, capnp_status* status);
+void capnp_ctx_destroy(capnp_ctx* ctx);
+/* hipStream_t owned by the context (as void*). */
+void* capnp_ctx_stream(capnp_ctx* ctx);
+/* Text of the last HIP error seen by this context ("" if none). */
+const char* capnp_ctx_last_error(capnp_ctx* ctx);
+/* Library / ABI version and the gfx target the kernels were built for. */
+const char* capnp_version(void);
+/* Default ReaderOptions (message.rs:117-120). */
+capnp_reader_options capnp_default_reader_options(void);
+
+/* ---- sizes ------------------------------------------------------------- */
+/* Upper bound on PACK output for a chunk of `words` words:
+   8n + ceil(n/2) + 2 bytes (0 for n == 0). */
+size_t capnp_packed_bound_bytes(size_t words);
+/* Bound for a batch: sum of per-chunk bounds given the total words and the
+   chunk count. */
+size_t capnp_packed_batch_bound_bytes(size_t total_words, size_t nchunks);
+
+/* ---- device batch API (the hot path) ----------------------------------- */
+/* PACK every chunk c = words [d_chunk_word_off[c], d_chunk_word_off[c+1]) of
+   d_words exactly as one PackedWrite::write_all call would
+   (serialize_packed.rs:304-439), and concatenate the results in chunk order
+   into d_out.  On completion d_out_byte_off[c] is chunk c's start in d_out
+   and d_out_byte_off[nchunks] the total packed size.  If the total exceeds
+   out_cap nothing past out_cap is written and the total still reports the
+   size that was needed (caller checks after the stream syncs).
+   d_chunk_word_off: nchunks+1 non-decreasing word offsets. */
+capnp_status capnp_gpu_pack_batch(capnp_ctx* ctx, const uint64_t* d_words,
+                                  const uint64_t* d_chunk_word_off, size_t nchunks,
+                                  uint8_t* d_out, size_t out_cap,
+                                  uint64_t* d_out_byte_off, void* stream);
+
+/* UNPACK every chunk c: decode packed bytes d_packed[d_in_byte_off[c] ..
+   d_in_byte_off[c+1]) into words d_words[d_out_word_off[c] ..
+   d_out_word_off[c+1]) exactly as one PackedRead::read_exact call of that
+   many bytes would (serialize_packed.rs:80-228, io.rs:16-31).
+   d_status[c] receives the capnp_status of the chunk; d_consumed[c] (may be
+   NULL) the packed bytes the decode used.  Bytes of d_words that belong to a
+   chunk with a non-OK status are unspecified. */
+capnp_status capnp_gpu_unpack_batch(capnp_ctx* ctx, const uint8_t* d_packed,
+                                    const uint64_t* d_in_byte_off, size_t nchunks,
+                                    uint64_t* d_words, const uint64_t* d_out_word_off,
+                                    int32_t* d_status, uint64_t* d_consumed,
+                                    void* stream);
+
+/* ---- host single-unit API (blocking; runs the same kernels) ------------ */
+/* PackedWrite::write_all of one chunk (serialize_packed.rs:304-439) into a
+   caller buffer; *written = packed length.  len must be a multiple of 8. */
+capnp_status capnp_pack(capnp_ctx* ctx, const uint8_t* in, size_t len,
+                        uint8_t* out, size_t cap, size_t* written);
+/* PackedRead::read_exact of out_len bytes from a slice of in_len bytes
+   (serialize_packed.rs:80-228 with io.rs:16-31); *consumed = bytes used. */
+capnp_status capnp_unpack(capnp_ctx* ctx, const uint8_t* in, size_t in_len,
+                          size_t* consumed, uint8_t* out, size_t out_len);
+
+/* ---- host batch API (end-to-end: pinned H2D -> kernel -> D2H) ---------- */
+capnp_status capnp_pack_batch_host(capnp_ctx* ctx, const uint64_t* words,
+                                   const uint64_t* chunk_word_off, size_t nchunks,
+                                   uint8_t* out, size_t out_cap, uint64_t* out_byte_off);
+capnp_status capnp_unpack_batch_host(capnp_ctx* ctx, const uint8_t* packed,
+                                     const uint64_t* in_byte_off, size_t nchunks,
+                                     uint64_t* words, const uint64_t* out_word_off,
+                                     int32_t* status, uint64_t* consumed);
+
+/* ---- host message API (mirrors serialize_packed) ----------------------- */
+/* serialize_packed::write_message (serialize_packed.rs:446-453 ->
+   serialize.rs:574-582): packs the segment table word 0, the rest of the
+   table, then each segment as separate write_all chunks
+   (serialize.rs:605-679).  segs[i] points at seg_words[i] words. */
+capnp_status capnp_packed_write_message(capnp_ctx* ctx, const uint64_t* const* segs,
+                                        const uint32_t* seg_words, uint32_t nseg,
+                                        uint8_t* out, size_t cap, size_t* written);
+
+/* serialize_packed::read_message / try_read_message (serialize_packed.rs:
+   233-255 -> serialize.rs:287-325, 448-524).  Read units: 8 bytes, the rest
+   of the segment table, then the whole body.  try_mode != 0 returns
+   CAPNP_NONE on an empty input instead of CAPNP_E_PREMATURE_END_OF_FILE.
+   body receives the segments back to back (body_cap_words capacity);
+   seg_words_out (capacity CAPNP_SEGMENTS_COUNT_LIMIT) the segment lengths;
+   *consumed the packed bytes used. */
+capnp_status capnp_packed_read_message(capnp_ctx* ctx, const uint8_t* in, size_t in_len,
+                                       const capnp_reader_options* opts, int try_mode,
+                                       uint64_t* body, size_t body_cap_words,
+                                       uint32_t* seg_words_out, uint32_t* nseg_out,
+                                       size_t* consumed);
+
+/* serialize_packed::read_message_no_alloc / try_read_message_no_alloc
+   (serialize_packed.rs:263-291 -> serialize.rs:333-440): the table rest is
+   read 8 bytes at a time into `buffer` and the body follows it there.
+   `buffer` must be 8-byte aligned (CAPNP_E_UNALIGNED_SEGMENT otherwise). */
+capnp_status capnp_packed_read_message_no_alloc(capnp_ctx* ctx, const uint8_t* in,
+                                                size_t in_len,
+                                                const capnp_reader_options* opts,
+                                                int try_mode, uint8_t* buffer,
+                                                size_t buffer_len, uint32_t* nseg_out,
+                                                size_t* table_bytes_out,
+                                                size_t* body_bytes_out, size_t* consumed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CAPNP_PACKED_H */

@@ -1,0 +1,186 @@
+"""ctypes wrapper of the CPU oracle (oracle/build/liboracle.so).
+
+Test infrastructure: imported only by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "build", "liboracle.so")
+
+STATUS = {
+    "OK": 0, "NONE": 1, "PREMATURE_END_OF_PACKED_INPUT": 2, "DID_NOT_END_CLEANLY": 3,
+    "FAILED_TO_FILL_WHOLE_BUFFER": 4, "PREMATURE_END_OF_FILE": 5,
+    "INVALID_NUMBER_OF_SEGMENTS": 6, "MESSAGE_SIZE_OVERFLOW": 7, "MESSAGE_TOO_LARGE": 8,
+    "BUFFER_NOT_LARGE_ENOUGH": 9, "UNALIGNED_SEGMENT": 10, "MISALIGNED_LEN": 11,
+}
+DEFAULT_TRAVERSAL_LIMIT = 8 * 1024 * 1024  # message.rs:117-120
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        u8p, u64p, szp = C.POINTER(C.c_uint8), C.POINTER(C.c_uint64), C.POINTER(C.c_size_t)
+        L.oracle_pack.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, szp]
+        L.oracle_read.argtypes = [C.c_void_p, C.c_size_t, szp, C.c_void_p, C.c_size_t, szp]
+        L.oracle_read_exact.argtypes = [C.c_void_p, C.c_size_t, szp, C.c_void_p, C.c_size_t]
+        L.oracle_bound.argtypes = [C.c_size_t]
+        L.oracle_bound.restype = C.c_size_t
+        L.oracle_write_message.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                           C.c_size_t, szp]
+        L.oracle_read_message.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_int, C.c_int,
+                                          C.c_void_p, C.c_size_t, C.c_void_p,
+                                          C.POINTER(C.c_uint32), szp]
+        L.oracle_read_message_no_alloc.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_int,
+                                                   C.c_int, C.c_void_p, C.c_size_t,
+                                                   C.POINTER(C.c_uint32), szp, szp, szp]
+        L.oracle_pack_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                        C.c_size_t, C.c_void_p, C.c_int]
+        L.oracle_unpack_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                          C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.gen_word.argtypes = [C.c_int, C.c_uint32, C.c_uint64, C.c_uint64]
+        L.gen_word.restype = C.c_uint64
+        L.gen_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_uint64,
+                               C.c_void_p, C.c_int, C.c_uint32]
+        _lib = L
+    return _lib
+
+
+def _buf(b):
+    a = np.frombuffer(bytes(b), dtype=np.uint8) if not isinstance(b, np.ndarray) else b
+    return np.ascontiguousarray(a)
+
+
+def pack(data):
+    """PackedWrite::write_all of one chunk -> (status, bytes)."""
+    a = _buf(data)
+    cap = lib().oracle_bound(len(a) // 8) + 16
+    out = np.zeros(cap, np.uint8)
+    n = C.c_size_t(0)
+    st = lib().oracle_pack(a.ctypes.data, len(a), out.ctypes.data, cap, C.byref(n))
+    return st, out[:n.value].tobytes()
+
+
+def read_exact(packed, out_len):
+    """read_exact over PackedRead -> (status, bytes, consumed)."""
+    a = _buf(packed)
+    out = np.zeros(max(out_len, 1), np.uint8)
+    used = C.c_size_t(0)
+    st = lib().oracle_read_exact(a.ctypes.data if len(a) else None, len(a), C.byref(used),
+                                 out.ctypes.data, out_len)
+    return st, out[:out_len].tobytes(), used.value
+
+
+def read(packed, out_len):
+    a = _buf(packed)
+    out = np.zeros(max(out_len, 1), np.uint8)
+    used, nread = C.c_size_t(0), C.c_size_t(0)
+    st = lib().oracle_read(a.ctypes.data if len(a) else None, len(a), C.byref(used),
+                           out.ctypes.data, out_len, C.byref(nread))
+    return st, out[:out_len].tobytes(), used.value, nread.value
+
+
+def write_message(segments):
+    """segments: list of np.uint64 arrays -> (status, packed bytes)."""
+    words = np.concatenate([np.asarray(s, np.uint64) for s in segments]) if segments else \
+        np.zeros(0, np.uint64)
+    words = np.ascontiguousarray(words)
+    lens = np.array([len(s) for s in segments], np.uint32)
+    cap = 16 + sum(lib().oracle_bound(int(n)) for n in lens) + lib().oracle_bound(
+        len(segments) // 2 + 1)
+    out = np.zeros(cap, np.uint8)
+    n = C.c_size_t(0)
+    st = lib().oracle_write_message(words.ctypes.data if len(words) else None,
+                                    lens.ctypes.data, len(segments), out.ctypes.data, cap,
+                                    C.byref(n))
+    return st, out[:n.value].tobytes()
+
+
+def read_message(packed, try_mode=False, limit=DEFAULT_TRAVERSAL_LIMIT, body_cap=None):
+    """-> (status, [segments as np.uint64 arrays], consumed)."""
+    a = _buf(packed)
+    if body_cap is None:
+        body_cap = max(8 * len(a) + 8, 1)
+    body = np.zeros(body_cap, np.uint64)
+    seg = np.zeros(512, np.uint32)
+    nseg, used = C.c_uint32(0), C.c_size_t(0)
+    st = lib().oracle_read_message(a.ctypes.data if len(a) else None, len(a),
+                                   limit if limit is not None else 0, limit is not None,
+                                   int(try_mode), body.ctypes.data, body_cap, seg.ctypes.data,
+                                   C.byref(nseg), C.byref(used))
+    segs = []
+    if st == 0:
+        o = 0
+        for i in range(nseg.value):
+            segs.append(body[o:o + seg[i]].copy())
+            o += int(seg[i])
+    return st, segs, used.value
+
+
+def read_message_no_alloc(packed, buffer_words, try_mode=False, limit=DEFAULT_TRAVERSAL_LIMIT):
+    a = _buf(packed)
+    buf = np.zeros(max(buffer_words, 1), np.uint64)
+    nseg, tb, bb, used = C.c_uint32(0), C.c_size_t(0), C.c_size_t(0), C.c_size_t(0)
+    st = lib().oracle_read_message_no_alloc(a.ctypes.data if len(a) else None, len(a),
+                                            limit if limit is not None else 0,
+                                            limit is not None, int(try_mode), buf.ctypes.data,
+                                            buffer_words * 8, C.byref(nseg), C.byref(tb),
+                                            C.byref(bb), C.byref(used))
+    return st, buf.view(np.uint8), nseg.value, tb.value, bb.value, used.value
+
+
+def pack_batch(words, offs, threads=1):
+    words = np.ascontiguousarray(words, np.uint64)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    n = len(offs) - 1
+    cap = int(sum(lib().oracle_bound(int(x)) for x in np.diff(offs))) if n < 4096 else \
+        int(8 * int(offs[-1]) + (int(offs[-1]) + 1) // 2 + 2 * n + 64)
+    out = np.zeros(max(cap, 1), np.uint8)
+    out_offs = np.zeros(n + 1, np.uint64)
+    st = lib().oracle_pack_batch(words.ctypes.data, offs.ctypes.data, n, out.ctypes.data, cap,
+                                 out_offs.ctypes.data, threads)
+    return st, out[:int(out_offs[-1])], out_offs
+
+
+def unpack_batch(packed, in_offs, out_offs, threads=1):
+    packed = np.ascontiguousarray(packed, np.uint8)
+    in_offs = np.ascontiguousarray(in_offs, np.uint64)
+    out_offs = np.ascontiguousarray(out_offs, np.uint64)
+    n = len(in_offs) - 1
+    words = np.zeros(max(int(out_offs[-1]), 1), np.uint64)
+    status = np.zeros(n, np.int32)
+    consumed = np.zeros(n, np.uint64)
+    lib().oracle_unpack_batch(packed.ctypes.data, in_offs.ctypes.data, n, words.ctypes.data,
+                              out_offs.ctypes.data, status.ctypes.data, consumed.ctypes.data,
+                              threads)
+    return words[:int(out_offs[-1])], status, consumed
+
+
+PZ30 = 1288490189  # round(0.30 * 2**32)
+PZ80 = 3435973837  # round(0.80 * 2**32)
+
+
+def gen_fill(offs, kinds=None, kind0=0, pz=PZ30, id0=0):
+    offs = np.ascontiguousarray(offs, np.uint64)
+    n = len(offs) - 1
+    words = np.zeros(max(int(offs[-1]), 1), np.uint64)
+    k = None
+    if kinds is not None:
+        k = np.ascontiguousarray(kinds, np.uint8)
+    lib().gen_fill(words.ctypes.data, offs.ctypes.data, 0, n, id0,
+                   k.ctypes.data if k is not None else None, kind0, pz)
+    return words[:int(offs[-1])]
