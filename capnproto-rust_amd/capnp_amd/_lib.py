@@ -1,0 +1,100 @@
+"""ctypes binding of the gfx950 codec library (libcapnp_packed.so, C ABI in
+include/capnp_packed.h).  No CPU fallback exists: a missing library or a
+missing gfx950 device raises."""
+import ctypes as C
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(HERE, "libcapnp_packed.so")
+
+OK = 0
+NONE = 1
+STATUS_NAMES = {
+    0: "OK", 1: "NONE", 2: "PrematureEndOfPackedInput",
+    3: "PackedInputDidNotEndCleanlyOnASegmentBoundary", 4: "FailedToFillTheWholeBuffer",
+    5: "PrematureEndOfFile", 6: "InvalidNumberOfSegments", 7: "MessageSizeOverflow",
+    8: "MessageTooLarge", 9: "BufferNotLargeEnough", 10: "UnalignedSegment",
+    11: "MisalignedLength", 64: "InvalidArgument", 65: "NoDevice", 66: "HipError",
+    67: "OutOfMemory",
+}
+
+EXPORTS = [
+    "capnp_ctx_create", "capnp_ctx_destroy", "capnp_ctx_stream", "capnp_ctx_last_error",
+    "capnp_version", "capnp_default_reader_options", "capnp_packed_bound_bytes",
+    "capnp_packed_batch_bound_bytes", "capnp_gpu_pack_batch", "capnp_gpu_unpack_batch",
+    "capnp_pack", "capnp_unpack", "capnp_pack_batch_host", "capnp_unpack_batch_host",
+    "capnp_packed_write_message", "capnp_packed_read_message",
+    "capnp_packed_read_message_no_alloc", "capnp_gpu_gen_batch", "capnp_gpu_pack_batch_tuned",
+    "capnp_ctx_reserve",
+]
+
+
+class ReaderOptionsC(C.Structure):
+    _fields_ = [("traversal_limit_in_words", C.c_uint64), ("has_traversal_limit", C.c_int32),
+                ("nesting_limit", C.c_int32)]
+
+
+class CapnpError(Exception):
+    """An error carrying a capnp::ErrorKind-style status."""
+
+    def __init__(self, status, msg=""):
+        self.status = status
+        self.kind = STATUS_NAMES.get(status, str(status))
+        super().__init__(f"{self.kind}{': ' + msg if msg else ''}")
+
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", PKG_ROOT])
+
+
+def lib():
+    """Loads the library (building it in-tree if absent and hipcc exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build()
+    L = C.CDLL(LIB_PATH)
+    vp, sz, u64, u32, i32 = C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint32, C.c_int
+    L.capnp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int)]
+    L.capnp_ctx_create.restype = vp
+    L.capnp_ctx_destroy.argtypes = [vp]
+    L.capnp_ctx_stream.argtypes = [vp]
+    L.capnp_ctx_stream.restype = vp
+    L.capnp_ctx_last_error.argtypes = [vp]
+    L.capnp_ctx_last_error.restype = C.c_char_p
+    L.capnp_version.restype = C.c_char_p
+    L.capnp_default_reader_options.restype = ReaderOptionsC
+    L.capnp_packed_bound_bytes.argtypes = [sz]
+    L.capnp_packed_bound_bytes.restype = sz
+    L.capnp_packed_batch_bound_bytes.argtypes = [sz, sz]
+    L.capnp_packed_batch_bound_bytes.restype = sz
+    L.capnp_gpu_pack_batch.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp]
+    L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, u32, vp]
+    L.capnp_gpu_unpack_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    L.capnp_gpu_gen_batch.argtypes = [vp, vp, vp, sz, u64, vp, u32, u32, vp]
+    L.capnp_ctx_reserve.argtypes = [vp, sz]
+    L.capnp_pack.argtypes = [vp, vp, sz, vp, sz, C.POINTER(C.c_size_t)]
+    L.capnp_unpack.argtypes = [vp, vp, sz, C.POINTER(C.c_size_t), vp, sz]
+    L.capnp_pack_batch_host.argtypes = [vp, vp, vp, sz, vp, sz, vp]
+    L.capnp_unpack_batch_host.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
+    L.capnp_packed_write_message.argtypes = [vp, vp, vp, u32, vp, sz, C.POINTER(C.c_size_t)]
+    L.capnp_packed_read_message.argtypes = [vp, vp, sz, C.POINTER(ReaderOptionsC), i32, vp, sz,
+                                            vp, C.POINTER(C.c_uint32), C.POINTER(C.c_size_t)]
+    L.capnp_packed_read_message_no_alloc.argtypes = [
+        vp, vp, sz, C.POINTER(ReaderOptionsC), i32, vp, sz, C.POINTER(C.c_uint32),
+        C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+    _lib = L
+    return L
+
+
+def exported_symbols():
+    """Names of the C ABI entry points the library exports (checked against
+    include/*.h by the CPU test-suite)."""
+    L = lib()
+    return [n for n in EXPORTS if hasattr(L, n)]

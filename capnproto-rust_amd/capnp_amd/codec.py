@@ -1,0 +1,152 @@
+"""Device context and the batched GPU codec (the hot path).
+
+`Context` owns a capnp_ctx (HIP stream + workspace).  The batch methods take
+torch tensors that already live in HBM (int64 views of the words / offsets)
+and enqueue the gfx950 kernels on the current torch stream:
+
+    pack_batch(words, chunk_word_off)            -> (packed u8, out_byte_off)
+    unpack_batch(packed, in_byte_off, out_word_off) -> (words, status, consumed)
+
+which are the batched bodies of PackedWrite::write_all and
+PackedRead::read_exact (capnp/src/serialize_packed.rs:304-439, :80-228).
+"""
+import ctypes as C
+
+from . import _lib
+from ._lib import CapnpError
+
+
+def _check(st, ctx=None):
+    if st != _lib.OK:
+        msg = ""
+        if ctx is not None:
+            msg = (_lib.lib().capnp_ctx_last_error(ctx) or b"").decode()
+        raise CapnpError(st, msg)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Context:
+    """A device context bound to one gfx950 GPU."""
+
+    def __init__(self, device=0):
+        L = _lib.lib()
+        st = C.c_int(0)
+        h = L.capnp_ctx_create(int(device), C.byref(st))
+        if not h:
+            raise CapnpError(st.value, f"no gfx950 device {device} available")
+        self._h = C.c_void_p(h)
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().capnp_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ------------------------------------------------------------------
+    @staticmethod
+    def bound_bytes(words):
+        return _lib.lib().capnp_packed_bound_bytes(int(words))
+
+    @staticmethod
+    def batch_bound_bytes(total_words, nchunks):
+        return _lib.lib().capnp_packed_batch_bound_bytes(int(total_words), int(nchunks))
+
+    def reserve(self, max_chunks):
+        _check(_lib.lib().capnp_ctx_reserve(self._h, int(max_chunks)), self._h)
+
+    @staticmethod
+    def _stream(stream):
+        if stream is not None:
+            return C.c_void_p(stream)
+        import torch
+        return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    # ---- device batch API (torch tensors in HBM) -----------------------
+    def pack_batch_into(self, words, chunk_word_off, out, out_off, chunks_per_tile=0,
+                        stream=None):
+        """Enqueue PACK; `out` (uint8) and `out_off` (int64, n+1) are preallocated."""
+        n = chunk_word_off.numel() - 1
+        L = _lib.lib()
+        st = L.capnp_gpu_pack_batch_tuned(self._h, _ptr(words), _ptr(chunk_word_off), n,
+                                          _ptr(out), out.numel(), _ptr(out_off),
+                                          int(chunks_per_tile), self._stream(stream))
+        _check(st, self._h)
+
+    def unpack_batch_into(self, packed, in_byte_off, out_word_off, words, status,
+                          consumed=None, stream=None):
+        n = in_byte_off.numel() - 1
+        st = _lib.lib().capnp_gpu_unpack_batch(self._h, _ptr(packed), _ptr(in_byte_off), n,
+                                               _ptr(words), _ptr(out_word_off), _ptr(status),
+                                               _ptr(consumed), self._stream(stream))
+        _check(st, self._h)
+
+    def pack_batch(self, words, chunk_word_off, chunks_per_tile=0):
+        """Returns (packed uint8 tensor trimmed to size, out_byte_off int64).
+        Synchronises the stream once to read the total size."""
+        import torch
+        n = chunk_word_off.numel() - 1
+        total_words = int(chunk_word_off[-1].item() - chunk_word_off[0].item()) if n else 0
+        cap = self.batch_bound_bytes(total_words, n)
+        out = torch.empty(cap, dtype=torch.uint8, device=words.device)
+        out_off = torch.empty(n + 1, dtype=torch.int64, device=words.device)
+        if chunks_per_tile == 0 and n:
+            chunks_per_tile = tile_chunks_for(total_words, n)
+        self.pack_batch_into(words, chunk_word_off, out, out_off, chunks_per_tile)
+        total = int(out_off[-1].item())
+        return out[:total], out_off
+
+    def unpack_batch(self, packed, in_byte_off, out_word_off):
+        import torch
+        n = in_byte_off.numel() - 1
+        total = int(out_word_off[-1].item()) if n else 0
+        dev = in_byte_off.device
+        words = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
+        status = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        consumed = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+        self.unpack_batch_into(packed, in_byte_off, out_word_off, words, status, consumed)
+        return words[:total], status[:n], consumed[:n]
+
+    def gen_batch(self, words, offs, kind=0, pz_thresh=0, kinds=None, id0=0, stream=None):
+        n = offs.numel() - 1
+        st = _lib.lib().capnp_gpu_gen_batch(self._h, _ptr(words), _ptr(offs), n, int(id0),
+                                            _ptr(kinds), int(kind), int(pz_thresh),
+                                            self._stream(stream))
+        _check(st, self._h)
+
+
+def tile_chunks_for(total_words, nchunks):
+    """Chunks per 256-thread pack workgroup: ~4096 words of work per tile."""
+    if nchunks <= 0:
+        return 16
+    mean = max(total_words / nchunks, 1.0)
+    return int(max(1, min(128, 4096 // mean)))
+
+
+_default = {}
+
+
+def default_context(device=0):
+    ctx = _default.get(device)
+    if ctx is None:
+        ctx = Context(device)
+        _default[device] = ctx
+    return ctx

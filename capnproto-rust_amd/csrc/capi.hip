@@ -1,0 +1,484 @@
+// capi.hip — the C ABI (include/capnp_packed.h, include/capnp_packed_bench.h).
+//
+// Host entry points stage through device memory and run the gfx950 kernels;
+// there is no CPU implementation of the codec in this library.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/capnp_packed.h"
+#include "../../include/capnp_packed_bench.h"
+#include "frame.h"
+
+extern "C" hipError_t capnp_launch_pack(const uint64_t*, const uint64_t*, uint64_t, uint32_t,
+                                        uint8_t*, uint64_t, uint64_t*, uint64_t*, uint32_t*,
+                                        size_t, hipStream_t);
+extern "C" hipError_t capnp_launch_unpack(const uint8_t*, const uint64_t*, uint64_t, uint64_t*,
+                                          const uint64_t*, int32_t*, uint64_t*, hipStream_t);
+extern "C" hipError_t capnp_launch_gen(uint64_t*, const uint64_t*, uint64_t, uint64_t,
+                                       const uint8_t*, uint32_t, uint32_t, hipStream_t);
+extern "C" hipError_t capnp_launch_frame(const uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t,
+                                         uint32_t, uint64_t, FrameResult*, hipStream_t);
+
+namespace {
+
+constexpr uint32_t kDefaultTileChunks = 16;
+constexpr uint32_t kMaxTileChunks = 128;
+
+size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
+
+}  // namespace
+
+struct capnp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint8_t* d_state = nullptr;   // [ticket, 16 B][tile look-back records]
+    size_t state_cap = 0;
+    uint8_t* d_stage = nullptr;   // staging for the host APIs (inputs)
+    size_t stage_cap = 0;
+    uint8_t* d_body = nullptr;    // staging for decoded message bodies
+    size_t body_cap = 0;
+    FrameResult* d_frame = nullptr;
+    FrameResult* h_frame = nullptr;  // pinned
+    std::string err;
+};
+
+namespace {
+
+capnp_status fail(capnp_ctx* ctx, hipError_t e, const char* what) {
+    if (ctx) ctx->err = std::string(what) + ": " + hipGetErrorString(e);
+    return e == hipErrorOutOfMemory ? CAPNP_E_OUT_OF_MEMORY : CAPNP_E_HIP;
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t e_ = (expr);                         \
+        if (e_ != hipSuccess) return fail(ctx, e_, #expr); \
+    } while (0)
+
+hipStream_t pick(capnp_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
+
+capnp_status ensure_state(capnp_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->state_cap) return CAPNP_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (ctx->d_state) {
+        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(hipFree(ctx->d_state));
+        ctx->d_state = nullptr;
+        ctx->state_cap = 0;
+    }
+    size_t cap = std::max<size_t>(bytes, 1 << 16);
+    HIP_TRY(hipMalloc(&ctx->d_state, cap));
+    ctx->state_cap = cap;
+    return CAPNP_OK;
+}
+
+capnp_status ensure_buf(capnp_ctx* ctx, uint8_t** buf, size_t* cap_io, size_t bytes) {
+    if (bytes <= *cap_io) return CAPNP_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (*buf) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        HIP_TRY(hipFree(*buf));
+        *buf = nullptr;
+        *cap_io = 0;
+    }
+    size_t cap = std::max<size_t>(round16(bytes) + 64, 1 << 20);
+    HIP_TRY(hipMalloc(buf, cap));
+    *cap_io = cap;
+    return CAPNP_OK;
+}
+
+capnp_status ensure_stage(capnp_ctx* ctx, size_t bytes) {
+    return ensure_buf(ctx, &ctx->d_stage, &ctx->stage_cap, bytes);
+}
+
+size_t state_bytes_for(size_t nchunks, uint32_t tc) {
+    const size_t ntiles = (nchunks + tc - 1) / tc;
+    return round16(16 + 8 * ntiles);
+}
+
+capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint64_t* d_off,
+                            size_t n, uint8_t* d_out, size_t cap, uint64_t* d_out_off,
+                            uint32_t tc, hipStream_t s) {
+    if (tc == 0) tc = kDefaultTileChunks;
+    if (tc > kMaxTileChunks) return CAPNP_E_INVALID_ARGUMENT;
+    if (n > 0 && !d_off) return CAPNP_E_INVALID_ARGUMENT;
+    if (!d_out_off) return CAPNP_E_INVALID_ARGUMENT;
+    const size_t sb = state_bytes_for(n, tc);
+    capnp_status st = ensure_state(ctx, sb);
+    if (st != CAPNP_OK) return st;
+    HIP_TRY(capnp_launch_pack(d_words, d_off, n, tc, d_out, cap, d_out_off,
+                              reinterpret_cast<uint64_t*>(ctx->d_state + 16),
+                              reinterpret_cast<uint32_t*>(ctx->d_state), sb, s));
+    return CAPNP_OK;
+}
+
+uint32_t tile_chunks_for(uint64_t total_words, size_t n) {
+    if (n == 0) return kDefaultTileChunks;
+    const double mean = (double)total_words / (double)n;
+    double t = 4096.0 / std::max(mean, 1.0);
+    uint32_t tc = (uint32_t)std::max(1.0, std::min(t, (double)kMaxTileChunks));
+    return tc;
+}
+
+// Host batch pack through the staging buffer.  Returns the needed size in
+// *total; writes min(total, out_cap) bytes to `out`.
+capnp_status pack_host(capnp_ctx* ctx, const uint64_t* words, const uint64_t* off, size_t n,
+                       uint8_t* out, size_t out_cap, uint64_t* out_off_host, uint64_t* total) {
+    const uint64_t base = n ? off[0] : 0;
+    const uint64_t nw = n ? off[n] - base : 0;
+    std::vector<uint64_t> rel(n + 1);
+    for (size_t i = 0; i <= n; i++) rel[i] = n ? off[i] - base : 0;
+    const size_t bound = capnp_packed_batch_bound_bytes(nw, n);
+    const size_t o_words = 0;
+    const size_t o_off = round16(nw * 8);
+    const size_t o_oo = o_off + round16((n + 1) * 8);
+    const size_t o_out = o_oo + round16((n + 1) * 8);
+    capnp_status st = ensure_stage(ctx, o_out + bound + 16);
+    if (st != CAPNP_OK) return st;
+    uint8_t* d = ctx->d_stage;
+    hipStream_t s = ctx->stream;
+    if (nw) HIP_TRY(hipMemcpyAsync(d + o_words, words + base, nw * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d + o_off, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    st = pack_batch_dev(ctx, reinterpret_cast<uint64_t*>(d + o_words),
+                        reinterpret_cast<uint64_t*>(d + o_off), n, d + o_out, bound,
+                        reinterpret_cast<uint64_t*>(d + o_oo), tile_chunks_for(nw, n), s);
+    if (st != CAPNP_OK) return st;
+    std::vector<uint64_t> oo(n + 1);
+    HIP_TRY(hipMemcpyAsync(oo.data(), d + o_oo, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *total = oo[n];
+    const size_t ncopy = std::min<uint64_t>(oo[n], out_cap);
+    if (ncopy) {
+        HIP_TRY(hipMemcpyAsync(out, d + o_out, ncopy, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    if (out_off_host) memcpy(out_off_host, oo.data(), (n + 1) * 8);
+    return oo[n] > out_cap ? CAPNP_E_BUFFER_NOT_LARGE_ENOUGH : CAPNP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* capnp_version(void) { return "capnp-packed-mi355x 0.1.0 (gfx950)"; }
+
+capnp_reader_options capnp_default_reader_options(void) {
+    capnp_reader_options o;
+    o.traversal_limit_in_words = 8ull * 1024 * 1024;
+    o.has_traversal_limit = 1;
+    o.nesting_limit = 64;
+    return o;
+}
+
+size_t capnp_packed_bound_bytes(size_t words) {
+    return words ? 8 * words + (words + 1) / 2 + 2 : 0;
+}
+
+size_t capnp_packed_batch_bound_bytes(size_t total_words, size_t nchunks) {
+    return 8 * total_words + (total_words + nchunks) / 2 + 2 * nchunks + 16;
+}
+
+capnp_ctx* capnp_ctx_create(int device, capnp_status* status) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) {
+        if (status) *status = CAPNP_E_NO_DEVICE;
+        return nullptr;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess ||
+        strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        if (status) *status = CAPNP_E_NO_DEVICE;
+        return nullptr;
+    }
+    capnp_ctx* ctx = new capnp_ctx();
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_frame, sizeof(FrameResult));
+    if (e == hipSuccess) e = hipHostMalloc(&ctx->h_frame, sizeof(FrameResult), 0);
+    if (e != hipSuccess) {
+        if (status) *status = CAPNP_E_HIP;
+        capnp_ctx_destroy(ctx);
+        return nullptr;
+    }
+    if (status) *status = CAPNP_OK;
+    return ctx;
+}
+
+void capnp_ctx_destroy(capnp_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    if (ctx->d_state) hipFree(ctx->d_state);
+    if (ctx->d_stage) hipFree(ctx->d_stage);
+    if (ctx->d_body) hipFree(ctx->d_body);
+    if (ctx->d_frame) hipFree(ctx->d_frame);
+    if (ctx->h_frame) hipHostFree(ctx->h_frame);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+void* capnp_ctx_stream(capnp_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+const char* capnp_ctx_last_error(capnp_ctx* ctx) { return ctx ? ctx->err.c_str() : ""; }
+
+capnp_status capnp_ctx_reserve(capnp_ctx* ctx, size_t max_chunks) {
+    if (!ctx) return CAPNP_E_INVALID_ARGUMENT;
+    return ensure_state(ctx, state_bytes_for(max_chunks, 1));
+}
+
+capnp_status capnp_gpu_pack_batch(capnp_ctx* ctx, const uint64_t* d_words,
+                                  const uint64_t* d_chunk_word_off, size_t nchunks,
+                                  uint8_t* d_out, size_t out_cap, uint64_t* d_out_byte_off,
+                                  void* stream) {
+    if (!ctx) return CAPNP_E_INVALID_ARGUMENT;
+    return pack_batch_dev(ctx, d_words, d_chunk_word_off, nchunks, d_out, out_cap,
+                          d_out_byte_off, kDefaultTileChunks, pick(ctx, stream));
+}
+
+capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
+                                        const uint64_t* d_chunk_word_off, size_t nchunks,
+                                        uint8_t* d_out, size_t out_cap,
+                                        uint64_t* d_out_byte_off, uint32_t chunks_per_tile,
+                                        void* stream) {
+    if (!ctx) return CAPNP_E_INVALID_ARGUMENT;
+    return pack_batch_dev(ctx, d_words, d_chunk_word_off, nchunks, d_out, out_cap,
+                          d_out_byte_off, chunks_per_tile, pick(ctx, stream));
+}
+
+capnp_status capnp_gpu_unpack_batch(capnp_ctx* ctx, const uint8_t* d_packed,
+                                    const uint64_t* d_in_byte_off, size_t nchunks,
+                                    uint64_t* d_words, const uint64_t* d_out_word_off,
+                                    int32_t* d_status, uint64_t* d_consumed, void* stream) {
+    if (!ctx || (nchunks && (!d_in_byte_off || !d_out_word_off || !d_status)))
+        return CAPNP_E_INVALID_ARGUMENT;
+    HIP_TRY(capnp_launch_unpack(d_packed, d_in_byte_off, nchunks, d_words, d_out_word_off,
+                                d_status, d_consumed, pick(ctx, stream)));
+    return CAPNP_OK;
+}
+
+capnp_status capnp_gpu_gen_batch(capnp_ctx* ctx, uint64_t* d_words, const uint64_t* d_offs,
+                                 size_t nchunks, uint64_t id0, const uint8_t* d_kinds,
+                                 uint32_t kind0, uint32_t pz_thresh, void* stream) {
+    if (!ctx) return CAPNP_E_INVALID_ARGUMENT;
+    HIP_TRY(capnp_launch_gen(d_words, d_offs, nchunks, id0, d_kinds, kind0, pz_thresh,
+                             pick(ctx, stream)));
+    return CAPNP_OK;
+}
+
+capnp_status capnp_pack(capnp_ctx* ctx, const uint8_t* in, size_t len, uint8_t* out,
+                        size_t cap, size_t* written) {
+    if (!ctx || !written || (len && !in)) return CAPNP_E_INVALID_ARGUMENT;
+    if (len % 8 != 0) return CAPNP_E_MISALIGNED_LEN;
+    *written = 0;
+    std::vector<uint64_t> words(len / 8);
+    if (len) memcpy(words.data(), in, len);
+    uint64_t off[2] = {0, len / 8};
+    uint64_t total = 0;
+    capnp_status st = pack_host(ctx, words.data(), off, 1, out, cap, nullptr, &total);
+    *written = std::min<uint64_t>(total, cap);
+    return st;
+}
+
+capnp_status capnp_pack_batch_host(capnp_ctx* ctx, const uint64_t* words,
+                                   const uint64_t* chunk_word_off, size_t nchunks, uint8_t* out,
+                                   size_t out_cap, uint64_t* out_byte_off) {
+    if (!ctx || !chunk_word_off || !out_byte_off) return CAPNP_E_INVALID_ARGUMENT;
+    uint64_t total = 0;
+    return pack_host(ctx, words, chunk_word_off, nchunks, out, out_cap, out_byte_off, &total);
+}
+
+capnp_status capnp_unpack_batch_host(capnp_ctx* ctx, const uint8_t* packed,
+                                     const uint64_t* in_byte_off, size_t nchunks,
+                                     uint64_t* words, const uint64_t* out_word_off,
+                                     int32_t* status, uint64_t* consumed) {
+    if (!ctx || !in_byte_off || !out_word_off || !status) return CAPNP_E_INVALID_ARGUMENT;
+    const size_t n = nchunks;
+    const uint64_t ib = n ? in_byte_off[0] : 0, ie = n ? in_byte_off[n] : 0;
+    const uint64_t ob = n ? out_word_off[0] : 0, oe = n ? out_word_off[n] : 0;
+    std::vector<uint64_t> ri(n + 1), ro(n + 1);
+    for (size_t i = 0; i <= n; i++) {
+        ri[i] = n ? in_byte_off[i] - ib : 0;
+        ro[i] = n ? out_word_off[i] - ob : 0;
+    }
+    const size_t o_in = 0;
+    const size_t o_ri = round16(ie - ib + 16);
+    const size_t o_ro = o_ri + round16((n + 1) * 8);
+    const size_t o_st = o_ro + round16((n + 1) * 8);
+    const size_t o_cs = o_st + round16(n * 4);
+    const size_t o_out = o_cs + round16(n * 8);
+    capnp_status st = ensure_stage(ctx, o_out + (oe - ob) * 8 + 16);
+    if (st != CAPNP_OK) return st;
+    uint8_t* d = ctx->d_stage;
+    hipStream_t s = ctx->stream;
+    if (ie > ib) HIP_TRY(hipMemcpyAsync(d + o_in, packed + ib, ie - ib, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d + o_ri, ri.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d + o_ro, ro.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(capnp_launch_unpack(d + o_in, reinterpret_cast<uint64_t*>(d + o_ri), n,
+                                reinterpret_cast<uint64_t*>(d + o_out),
+                                reinterpret_cast<uint64_t*>(d + o_ro),
+                                reinterpret_cast<int32_t*>(d + o_st),
+                                reinterpret_cast<uint64_t*>(d + o_cs), s));
+    if (oe > ob) HIP_TRY(hipMemcpyAsync(words + ob, d + o_out, (oe - ob) * 8, hipMemcpyDeviceToHost, s));
+    if (n) HIP_TRY(hipMemcpyAsync(status, d + o_st, n * 4, hipMemcpyDeviceToHost, s));
+    if (n && consumed) HIP_TRY(hipMemcpyAsync(consumed, d + o_cs, n * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return CAPNP_OK;
+}
+
+capnp_status capnp_unpack(capnp_ctx* ctx, const uint8_t* in, size_t in_len, size_t* consumed,
+                          uint8_t* out, size_t out_len) {
+    if (!ctx || !consumed || (in_len && !in) || (out_len && !out)) return CAPNP_E_INVALID_ARGUMENT;
+    *consumed = 0;
+    if (out_len == 0) return CAPNP_OK;                  // serialize_packed.rs:82-84
+    if (out_len % 8 != 0) return CAPNP_E_MISALIGNED_LEN;  // :86 (panic)
+    uint64_t io[2] = {0, in_len}, oo[2] = {0, out_len / 8};
+    int32_t status = 0;
+    uint64_t used = 0;
+    std::vector<uint64_t> words(out_len / 8);
+    capnp_status st = capnp_unpack_batch_host(ctx, in, io, 1, words.data(), oo, &status, &used);
+    if (st != CAPNP_OK) return st;
+    *consumed = used;
+    if (status == CAPNP_OK) memcpy(out, words.data(), out_len);
+    return (capnp_status)status;
+}
+
+capnp_status capnp_packed_write_message(capnp_ctx* ctx, const uint64_t* const* segs,
+                                        const uint32_t* seg_words, uint32_t nseg, uint8_t* out,
+                                        size_t cap, size_t* written) {
+    if (!ctx || !written || nseg == 0 || !seg_words || !segs) return CAPNP_E_INVALID_ARGUMENT;
+    *written = 0;
+    // chunks: word 0, the rest of the table, then one per segment
+    // (serialize.rs:605-679)
+    std::vector<uint64_t> off;
+    std::vector<uint64_t> words;
+    off.push_back(0);
+    words.push_back((uint64_t)(nseg - 1) | ((uint64_t)seg_words[0] << 32));
+    off.push_back(words.size());
+    if (nseg > 1) {
+        const size_t rest = nseg < 4 ? 8 : (size_t)(nseg & ~1u) * 4;
+        std::vector<uint32_t> t(rest / 4, 0u);
+        for (uint32_t i = 1; i < nseg; i++) t[i - 1] = seg_words[i];
+        const size_t w0 = words.size();
+        words.resize(w0 + rest / 8);
+        memcpy(words.data() + w0, t.data(), rest);
+        off.push_back(words.size());
+    }
+    for (uint32_t i = 0; i < nseg; i++) {
+        if (seg_words[i] && !segs[i]) return CAPNP_E_INVALID_ARGUMENT;
+        const size_t w0 = words.size();
+        words.resize(w0 + seg_words[i]);
+        if (seg_words[i]) memcpy(words.data() + w0, segs[i], (size_t)seg_words[i] * 8);
+        off.push_back(words.size());
+    }
+    uint64_t total = 0;
+    capnp_status st = pack_host(ctx, words.data(), off.data(), off.size() - 1, out, cap, nullptr,
+                                &total);
+    *written = std::min<uint64_t>(total, cap);
+    return st;
+}
+
+static capnp_status read_message_impl(capnp_ctx* ctx, const uint8_t* in, size_t in_len,
+                                      const capnp_reader_options* opts, int try_mode,
+                                      int no_alloc, uint64_t buffer_len, FrameResult* fr,
+                                      uint8_t** d_body_out) {
+    capnp_reader_options o = opts ? *opts : capnp_default_reader_options();
+    const size_t o_in = 0;
+    capnp_status st = ensure_stage(ctx, round16(in_len + 16) + 64);
+    if (st != CAPNP_OK) return st;
+    uint8_t* d = ctx->d_stage;
+    hipStream_t s = ctx->stream;
+    if (in_len) HIP_TRY(hipMemcpyAsync(d + o_in, in, in_len, hipMemcpyHostToDevice, s));
+    HIP_TRY(capnp_launch_frame(d + o_in, in_len, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
+                               o.traversal_limit_in_words, (uint32_t)(o.has_traversal_limit != 0),
+                               buffer_len, ctx->d_frame, s));
+    HIP_TRY(hipMemcpyAsync(ctx->h_frame, ctx->d_frame, sizeof(FrameResult), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *fr = *ctx->h_frame;
+    (void)d_body_out;
+    return CAPNP_OK;
+}
+
+// Decodes the body unit described by the device frame record into host memory.
+static capnp_status read_body(capnp_ctx* ctx, const FrameResult& fr, uint8_t* host_out,
+                              uint64_t* body_consumed) {
+    *body_consumed = 0;
+    if (fr.total_words == 0) return CAPNP_OK;
+    const size_t o_st = round16(fr.total_words * 8);
+    capnp_status st = ensure_buf(ctx, &ctx->d_body, &ctx->body_cap, o_st + 64);
+    if (st != CAPNP_OK) return st;
+    uint8_t* d = ctx->d_body;
+    hipStream_t s = ctx->stream;
+    HIP_TRY(capnp_launch_unpack(ctx->d_stage, ctx->d_frame->body_in_off, 1,
+                                reinterpret_cast<uint64_t*>(d), ctx->d_frame->body_out_off,
+                                reinterpret_cast<int32_t*>(d + o_st),
+                                reinterpret_cast<uint64_t*>(d + o_st + 16), s));
+    int32_t status = 0;
+    uint64_t used = 0;
+    HIP_TRY(hipMemcpyAsync(&status, d + o_st, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&used, d + o_st + 16, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (status != CAPNP_OK) return (capnp_status)status;
+    HIP_TRY(hipMemcpyAsync(host_out, d, fr.total_words * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *body_consumed = used;
+    return CAPNP_OK;
+}
+
+capnp_status capnp_packed_read_message(capnp_ctx* ctx, const uint8_t* in, size_t in_len,
+                                       const capnp_reader_options* opts, int try_mode,
+                                       uint64_t* body, size_t body_cap_words,
+                                       uint32_t* seg_words_out, uint32_t* nseg_out,
+                                       size_t* consumed) {
+    if (!ctx || !consumed || !nseg_out || !seg_words_out || (in_len && !in))
+        return CAPNP_E_INVALID_ARGUMENT;
+    *consumed = 0;
+    *nseg_out = 0;
+    FrameResult fr;
+    capnp_status st = read_message_impl(ctx, in, in_len, opts, try_mode, 0, 0, &fr, nullptr);
+    if (st != CAPNP_OK) return st;
+    if (fr.status != CAPNP_OK) return (capnp_status)fr.status;
+    if (fr.total_words > body_cap_words) return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;
+    uint64_t used = 0;
+    st = read_body(ctx, fr, reinterpret_cast<uint8_t*>(body), &used);
+    if (st != CAPNP_OK) return st;
+    memcpy(seg_words_out, fr.seg_words, fr.nseg * sizeof(uint32_t));
+    *nseg_out = fr.nseg;
+    *consumed = fr.table_consumed + used;
+    return CAPNP_OK;
+}
+
+capnp_status capnp_packed_read_message_no_alloc(capnp_ctx* ctx, const uint8_t* in,
+                                                size_t in_len, const capnp_reader_options* opts,
+                                                int try_mode, uint8_t* buffer, size_t buffer_len,
+                                                uint32_t* nseg_out, size_t* table_bytes_out,
+                                                size_t* body_bytes_out, size_t* consumed) {
+    if (!ctx || !consumed || !nseg_out || !table_bytes_out || !body_bytes_out || (in_len && !in))
+        return CAPNP_E_INVALID_ARGUMENT;
+    *consumed = 0;
+    *nseg_out = 0;
+    if (((uintptr_t)buffer) % 8 != 0) return CAPNP_E_UNALIGNED_SEGMENT;  // serialize.rs:341-343
+    if (buffer_len < 8) return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;          // :345-347
+    FrameResult fr;
+    capnp_status st = read_message_impl(ctx, in, in_len, opts, try_mode, 1, buffer_len, &fr, nullptr);
+    if (st != CAPNP_OK) return st;
+    // the table bytes land in the caller's buffer as the reference reads them
+    if (fr.status == CAPNP_OK) memcpy(buffer, fr.table, fr.table_bytes);
+    if (fr.status != CAPNP_OK) return (capnp_status)fr.status;
+    uint64_t used = 0;
+    st = read_body(ctx, fr, buffer + fr.table_bytes, &used);
+    if (st != CAPNP_OK) return st;
+    *nseg_out = fr.nseg;
+    *table_bytes_out = fr.table_bytes;
+    *body_bytes_out = fr.total_words * 8;
+    *consumed = fr.table_consumed + used;
+    return CAPNP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,92 @@
+// common.h — device helpers shared by the gfx950 packed-codec kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CAPNP_WAVE 64
+
+// Per-byte "is non-zero" flags of a 32-bit half, gathered into 4 tag bits.
+// Byte k non-zero <=> bit 7 of ((b & 0x7f) + 0x7f) | b; the multiply by
+// 0x01020408 moves bit 8k of (t >> 7) to bit 24 + k with no carries.
+__host__ __device__ __forceinline__ uint32_t nz_nibble(uint32_t x) {
+    uint32_t t = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+    return ((t >> 7) * 0x01020408u) >> 24;
+}
+
+// The packed-encoding tag of a word: bit k set iff byte k is non-zero
+// (PackedWrite::write_all, capnp/src/serialize_packed.rs:324-371).
+__host__ __device__ __forceinline__ uint32_t word_tag(uint32_t lo, uint32_t hi) {
+    return nz_nibble(lo) | (nz_nibble(hi) << 4);
+}
+
+// Byte k of the result is bit k of `tag` (0/1).  Done per nibble: the
+// multiply by 0x00204081 puts bit j at 8j with no colliding terms.
+__host__ __device__ __forceinline__ uint64_t spread_bits(uint32_t tag) {
+    uint32_t lo = ((tag & 15u) * 0x00204081u) & 0x01010101u;
+    uint32_t hi = (((tag >> 4) & 15u) * 0x00204081u) & 0x01010101u;
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// v_perm_b32 selector (two dwords, 8 bytes) that scatters the `pop` packed
+// bytes of a tag back to their word positions: output byte k = bit k ?
+// rank_k : 0x0C (zero), rank_k = number of set bits below k.
+__host__ __device__ __forceinline__ uint64_t expand_selector(uint32_t tag) {
+    uint64_t t8 = spread_bits(tag);
+    uint64_t incl = t8 * 0x0101010101010101ull;     // inclusive prefix per byte
+    uint64_t rank = incl - t8;                       // exclusive prefix
+    uint64_t m = t8 * 0xFFull;                       // 0xFF where bit set
+    return (rank & m) | (0x0C0C0C0C0C0C0C0Cull & ~m);
+}
+
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// Number of set bits of a wave-uniform mask strictly below this lane.
+__device__ __forceinline__ uint32_t mask_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }
+
+__host__ __device__ __forceinline__ uint64_t low_mask(uint32_t k) {
+    return k >= 64 ? ~0ull : ((1ull << k) - 1ull);
+}
+
+__host__ __device__ __forceinline__ uint32_t ctz64(uint64_t x) {
+    return x ? (uint32_t)__builtin_ctzll(x) : 64u;
+}
+
+__host__ __device__ __forceinline__ uint32_t popc64(uint64_t x) {
+    return (uint32_t)__builtin_popcountll(x);
+}
+
+// Orders this wave's LDS writes before its later LDS reads (other lanes of
+// the same wave): LDS ops of one wave execute in order, so a wait on the LGKM
+// counter plus a compiler barrier suffices.
+__device__ __forceinline__ void wave_lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <typename T>
+__device__ __forceinline__ T uniform(T v) {
+    return (T)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Relaxed agent-scope 64-bit accesses (single global sc1 load/store): the
+// look-back records are {flag, value} granules written by one store
+// (MI355X_MICROARCH.md, "Valid forms", R2 granule).
+__device__ __forceinline__ void store_relaxed_agent(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t load_relaxed_agent(const uint64_t* p) {
+    return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}

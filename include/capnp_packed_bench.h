@@ -1,0 +1,40 @@
+/*
+ * capnp_packed_bench.h — workload helpers exported by the same library for
+ * the benchmark and the parity tests (not part of the codec boundary).
+ */
+#ifndef CAPNP_PACKED_BENCH_H
+#define CAPNP_PACKED_BENCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "capnp_packed.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Fills d_words[d_offs[c] .. d_offs[c+1]) for c < nchunks with the synthetic
+ * workload of oracle/gen_oracle.c (bit-identical): chunk id = id0 + c,
+ * generator kind = d_kinds[c] (or kind0 when d_kinds is NULL; 0 iid, 1 long
+ * zero runs, 2 long literal runs), pz_thresh = P(zero word) * 2^32. */
+capnp_status capnp_gpu_gen_batch(capnp_ctx* ctx, uint64_t* d_words, const uint64_t* d_offs,
+                                 size_t nchunks, uint64_t id0, const uint8_t* d_kinds,
+                                 uint32_t kind0, uint32_t pz_thresh, void* stream);
+
+/* capnp_gpu_pack_batch with an explicit tile size (chunks per 256-thread
+ * workgroup, 1..128; 0 = default).  Pick ~4096 / mean_chunk_words. */
+capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
+                                        const uint64_t* d_chunk_word_off, size_t nchunks,
+                                        uint8_t* d_out, size_t out_cap,
+                                        uint64_t* d_out_byte_off, uint32_t chunks_per_tile,
+                                        void* stream);
+
+/* Pre-sizes the context workspace for batches of up to max_chunks chunks so
+ * that later calls allocate nothing (required before HIP graph capture). */
+capnp_status capnp_ctx_reserve(capnp_ctx* ctx, size_t max_chunks);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CAPNP_PACKED_BENCH_H */

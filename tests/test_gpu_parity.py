@@ -1,0 +1,297 @@
+"""GPU parity: the gfx950 kernels against the CPU oracle, bit for bit.
+
+Every test goes through the C ABI (libcapnp_packed.so).  Small cases are
+compared byte-for-byte with the oracle (and its golden vectors); the full
+BASELINE sizes are checked through size-independent properties (round trip,
+offsets = sizes, sampled chunk bytes against the oracle)."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "golden_packing.json")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from capnp_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def dev(a, dtype=torch.int64):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int64 if dtype == torch.int64 else
+                                                         np.uint8)).cuda()
+
+
+# ---------------------------------------------------------------- host API
+def test_golden_pack_unpack(ctx, golden):
+    from capnp_amd import serialize_packed as sp
+    from capnp_amd import _lib
+    import ctypes as C
+    L = _lib.lib()
+    for v in golden["packing"]:
+        u, k = bytes(v["unpacked"]), bytes(v["packed"])
+        out = bytearray()
+        sp.PackedWrite(out, ctx).write_all(u)
+        assert bytes(out) == k, v
+        r = sp.PackedRead(sp.SliceRead(k), ctx)
+        assert r.read_exact(len(u)) == u
+        assert r.inner.is_empty()
+
+
+def test_golden_unpack_errors(ctx, golden):
+    from capnp_amd import serialize_packed as sp, CapnpError
+    names = {2: "PrematureEndOfPackedInput", 3: "PackedInputDidNotEndCleanlyOnASegmentBoundary",
+             4: "FailedToFillTheWholeBuffer"}
+    for v in golden["unpack_errors"]:
+        with pytest.raises(CapnpError) as e:
+            sp.PackedRead(sp.SliceRead(bytes(v["packed"])), ctx).read_exact(v["out_len"])
+        assert e.value.status == O.STATUS[v["status"]], (v, e.value)
+    for v in golden["unpacks_to"]:
+        r = sp.PackedRead(sp.SliceRead(bytes(v["packed"])), ctx)
+        assert r.read_exact(len(v["unpacked"])) == bytes(v["unpacked"])
+
+
+def test_golden_read_message(ctx, golden):
+    from capnp_amd import serialize_packed as sp, CapnpError
+    m = sp.read_message(bytes([0x11, 4, 1, 0, 1, 0, 0]), ctx=ctx)
+    assert [len(s) for s in m.segments()] == [1, 0, 0, 0, 0]
+    assert sp.try_read_message(b"", ctx=ctx) is None
+    with pytest.raises(CapnpError) as e:
+        sp.read_message(b"", ctx=ctx)
+    assert e.value.kind == "PrematureEndOfFile"
+    # no-alloc path reads the table rest 8 bytes at a time
+    with pytest.raises(CapnpError) as e:
+        sp.read_message_no_alloc(bytes([0x11, 4, 1, 0, 1, 0, 0]), np.zeros(64, np.uint64), ctx=ctx)
+    assert e.value.kind == "PackedInputDidNotEndCleanlyOnASegmentBoundary"
+
+
+def _rand_segment(rng, n):
+    kind = rng.random()
+    w = np.zeros(n, np.uint64)
+    b = w.view(np.uint8)
+    for i in range(n):
+        r = rng.random()
+        if kind < 0.25:  # zero heavy
+            if r < 0.1:
+                b[8 * i:8 * i + 8] = [rng.randrange(256) for _ in range(8)]
+        elif kind < 0.5:  # literal heavy
+            vals = [rng.randrange(1, 256) for _ in range(8)]
+            if r < 0.05:
+                vals[rng.randrange(8)] = 0
+                vals[rng.randrange(8)] = 0
+            elif r < 0.3:
+                vals[rng.randrange(8)] = 0
+            b[8 * i:8 * i + 8] = vals
+        else:
+            if r < 0.3:
+                continue
+            b[8 * i:8 * i + 8] = [rng.randrange(256) if rng.random() < 0.56 else 0
+                                  for _ in range(8)]
+    return w
+
+
+def test_message_round_trip_vs_oracle(ctx):
+    from capnp_amd import serialize_packed as sp
+    rng = random.Random(11)
+    for _ in range(60):
+        segs = [_rand_segment(rng, rng.choice([0, 1, 3, 64, 65, 200, 300]))
+                for _ in range(rng.randrange(1, 7))]
+        out = bytearray()
+        sp.write_message(out, segs, ctx=ctx)
+        st, ref = O.write_message(segs)
+        assert st == 0 and bytes(out) == ref
+        r = sp.SliceRead(bytes(out) + b"\x00\x00")  # trailing bytes stay unconsumed
+        m = sp.read_message(r, ctx=ctx)
+        assert r.pos == len(out)
+        for a, b in zip(segs, m.segments()):
+            assert np.array_equal(a, b)
+        buf = np.zeros(8192, np.uint64)
+        if len(segs) >= 3 and all(len(s) == 0 for s in segs[1:]):
+            continue
+        m2 = sp.read_message_no_alloc(bytes(out), buf, ctx=ctx)
+        for a, b in zip(segs, m2.segments()):
+            assert np.array_equal(a, b)
+
+
+# ---------------------------------------------------------------- batch API
+def _check_batch(ctx, words, offs, tc=0):
+    st, ref, ref_offs = O.pack_batch(words, offs)
+    assert st == 0
+    dw, do = dev(words), dev(offs)
+    packed, poffs = ctx.pack_batch(dw, do, chunks_per_tile=tc)
+    torch.cuda.synchronize()
+    got = packed.cpu().numpy()
+    goffs = poffs.cpu().numpy().view(np.uint64)
+    assert np.array_equal(goffs, ref_offs), "offsets differ"
+    if not np.array_equal(got, ref):
+        bad = np.nonzero(got != ref)[0][0]
+        c = int(np.searchsorted(ref_offs, bad, side="right") - 1)
+        raise AssertionError(f"packed bytes differ at {bad} (chunk {c}, words "
+                             f"{offs[c + 1] - offs[c]})")
+    back, status, consumed = ctx.unpack_batch(packed, poffs, do)
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    assert np.array_equal(consumed.cpu().numpy().view(np.uint64), np.diff(ref_offs))
+    assert np.array_equal(back.cpu().numpy().view(np.uint64), words)
+
+
+@pytest.mark.parametrize("tc", [0, 1, 3, 16, 128])
+def test_batch_edge_sizes(ctx, tc):
+    sizes = [0, 1, 2, 7, 8, 63, 64, 65, 127, 128, 129, 191, 192, 255, 256, 257, 320, 511, 512,
+             513, 1000, 0, 0, 5]
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    for kind in (0, 1, 2):
+        words = O.gen_fill(offs, kind0=kind, pz=O.PZ30)
+        _check_batch(ctx, words, offs, tc)
+
+
+def test_batch_random_structures(ctx):
+    rng = random.Random(5)
+    segs = [_rand_segment(rng, rng.choice([0, 1, 5, 64, 100, 128, 256, 300, 700]))
+            for _ in range(120)]
+    offs = np.concatenate([[0], np.cumsum([len(s) for s in segs])]).astype(np.uint64)
+    words = np.concatenate(segs)
+    _check_batch(ctx, words, offs)
+    _check_batch(ctx, words, offs, tc=1)
+
+
+def test_batch_long_runs(ctx):
+    # zero and literal runs longer than 255 words, every alignment vs 64
+    chunks = []
+    for n in (255, 256, 257, 300, 511, 512, 513, 1023, 1500):
+        for lead in (0, 1, 63):
+            z = np.zeros(n + lead, np.uint64)
+            z[:lead] = 0x0102030400000000
+            chunks.append(z)
+            lit = np.full(n + lead, 0x1112131415161718, np.uint64)
+            lit[:lead] = 0x0000000400000001
+            chunks.append(lit)
+            mix = np.full(n + lead, 0x11121314151617, np.uint64)  # one zero byte
+            mix[lead] = 0x1112131415161718
+            chunks.append(mix)
+    offs = np.concatenate([[0], np.cumsum([len(c) for c in chunks])]).astype(np.uint64)
+    _check_batch(ctx, np.concatenate(chunks), offs)
+
+
+def test_batch_misaligned_output(ctx):
+    sizes = np.random.default_rng(3).integers(0, 200, 300)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    words = O.gen_fill(offs, kind0=0, pz=O.PZ30)
+    st, ref, ref_offs = O.pack_batch(words, offs)
+    dw, do = dev(words), dev(offs)
+    n = len(sizes)
+    cap = len(ref) + 64
+    for mis in (1, 3, 8, 15):
+        buf = torch.full((cap + 32,), 0xEE, dtype=torch.uint8, device="cuda")
+        out = buf[mis:mis + cap]
+        oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+        ctx.pack_batch_into(dw, do, out, oo)
+        torch.cuda.synchronize()
+        b = buf.cpu().numpy()
+        assert (b[:mis] == 0xEE).all()
+        assert np.array_equal(b[mis:mis + len(ref)], ref)
+        assert (b[mis + len(ref):mis + len(ref) + 8] == 0xEE).all()
+
+
+def test_batch_small_capacity_writes_nothing_past_cap(ctx):
+    offs = np.arange(0, 129 * 64, 128, dtype=np.uint64)[:65]
+    words = O.gen_fill(offs, kind0=0, pz=O.PZ30)
+    st, ref, ref_offs = O.pack_batch(words, offs)
+    cap = len(ref) // 2
+    buf = torch.full((len(ref) + 64,), 0xEE, dtype=torch.uint8, device="cuda")
+    oo = torch.empty(65, dtype=torch.int64, device="cuda")
+    ctx.pack_batch_into(dev(words), dev(offs), buf[:cap], oo)
+    torch.cuda.synchronize()
+    assert int(oo[-1]) == len(ref)
+    assert (buf[cap:].cpu().numpy() == 0xEE).all()
+
+
+def test_unpack_error_statuses_vs_oracle(ctx):
+    rng = random.Random(17)
+    packed_chunks, lens = [], []
+    for _ in range(600):
+        n = rng.choice([1, 2, 5, 40, 64, 65, 130])
+        w = _rand_segment(rng, n)
+        st, k = O.pack(w.tobytes())
+        k = bytearray(k)
+        r = rng.random()
+        if r < 0.3 and len(k) > 1:
+            k = k[:rng.randrange(len(k))]          # truncate
+        elif r < 0.5 and len(k):
+            k[rng.randrange(len(k))] = rng.choice([0, 0xFF, rng.randrange(256)])  # corrupt
+        elif r < 0.6:
+            n = max(0, n + rng.choice([-3, -1, 1, 4]))  # wrong output size
+        packed_chunks.append(bytes(k))
+        lens.append(n)
+    in_offs = np.concatenate([[0], np.cumsum([len(k) for k in packed_chunks])]).astype(np.uint64)
+    out_offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    packed = np.frombuffer(b"".join(packed_chunks), np.uint8)
+    ref_words, ref_st, ref_used = O.unpack_batch(packed, in_offs, out_offs)
+    pk = torch.from_numpy(packed.copy()).cuda() if len(packed) else torch.zeros(1, dtype=torch.uint8, device="cuda")
+    words, status, consumed = ctx.unpack_batch(pk, dev(in_offs), dev(out_offs))
+    torch.cuda.synchronize()
+    g_st = status.cpu().numpy()
+    assert np.array_equal(g_st, ref_st), np.nonzero(g_st != ref_st)
+    ok = ref_st == 0
+    assert np.array_equal(consumed.cpu().numpy().view(np.uint64)[ok], ref_used[ok])
+    gw = words.cpu().numpy().view(np.uint64)
+    for c in np.nonzero(ok)[0]:
+        a, b = int(out_offs[c]), int(out_offs[c + 1])
+        assert np.array_equal(gw[a:b], ref_words[a:b])
+    assert ok.sum() > 100 and (~ok).sum() > 100
+
+
+def test_generator_matches_oracle(ctx):
+    from capnp_amd import _lib
+    sizes = np.random.default_rng(0).integers(0, 400, 500)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    kinds = np.random.default_rng(1).integers(0, 3, 500).astype(np.uint8)
+    for pz in (O.PZ30, O.PZ80):
+        ref = O.gen_fill(offs, kinds=kinds, pz=pz, id0=77)
+        w = torch.empty(int(offs[-1]), dtype=torch.int64, device="cuda")
+        ctx.gen_batch(w, dev(offs), pz_thresh=pz,
+                      kinds=torch.from_numpy(kinds).cuda(), id0=77)
+        torch.cuda.synchronize()
+        assert np.array_equal(w.cpu().numpy().view(np.uint64), ref)
+
+
+@pytest.mark.parametrize("pz", [O.PZ30, O.PZ80])
+def test_full_size_config_round_trip(ctx, pz):
+    """BASELINE configs 2/3 shape (1 Mi x 1 KiB): round trip on the device,
+    offsets = chunk sizes, and 2048 sampled chunks byte-equal to the oracle."""
+    n, cw = 1 << 20, 128
+    offs = torch.arange(0, (n + 1) * cw, cw, dtype=torch.int64, device="cuda")
+    words = torch.empty(n * cw, dtype=torch.int64, device="cuda")
+    ctx.gen_batch(words, offs, pz_thresh=pz)
+    packed, poffs = ctx.pack_batch(words, offs)
+    back, status, consumed = ctx.unpack_batch(packed, poffs, offs)
+    torch.cuda.synchronize()
+    assert int((status != 0).sum()) == 0
+    assert torch.equal(back, words)
+    assert torch.equal(consumed, poffs[1:] - poffs[:-1])
+    idx = np.random.default_rng(9).choice(n, 2048, replace=False)
+    po = poffs.cpu().numpy()
+    pk = packed.cpu().numpy()
+    for c in idx[:2048]:
+        w = O.gen_fill(np.array([0, cw], np.uint64), pz=pz, id0=int(c))
+        st, k = O.pack(w.tobytes())
+        assert pk[po[c]:po[c + 1]].tobytes() == k
