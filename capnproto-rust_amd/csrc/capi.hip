@@ -61,7 +61,9 @@ capnp_status fail(capnp_ctx* ctx, hipError_t e, const char* what) {
         if (e_ != hipSuccess) return fail(ctx, e_, #expr); \
     } while (0)
 
-hipStream_t pick(capnp_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
+// Device batch APIs are ordered on the caller's stream; NULL is the HIP null
+// (default) stream, as everywhere in HIP.
+hipStream_t pick(capnp_ctx*, void* s) { return (hipStream_t)s; }
 
 capnp_status ensure_state(capnp_ctx* ctx, size_t bytes) {
     if (bytes <= ctx->state_cap) return CAPNP_OK;

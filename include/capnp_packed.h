@@ -15,7 +15,8 @@
  *
  * Conventions
  *   - Plain pointers and sizes only; no HIP or torch types.  `stream` is a
- *     hipStream_t passed as void* (NULL = the context's own stream).
+ *     hipStream_t passed as void* (NULL = the HIP null stream; the context's
+ *     own stream is returned by capnp_ctx_stream).
  *   - All buffers are caller-owned.  The library never frees caller memory.
  *   - Functions prefixed capnp_gpu_* take DEVICE pointers and are stream
  *     ordered (asynchronous).  All other functions take HOST pointers and are
