@@ -123,7 +123,7 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
 uint32_t tile_chunks_for(uint64_t total_words, size_t n) {
     if (n == 0) return kDefaultTileChunks;
     const double mean = (double)total_words / (double)n;
-    double t = 4096.0 / std::max(mean, 1.0);
+    double t = 2048.0 / std::max(mean, 1.0);  // ~512 words per wave (staged path)
     uint32_t tc = (uint32_t)std::max(1.0, std::min(t, (double)kMaxTileChunks));
     return tc;
 }

@@ -5,11 +5,16 @@
 //   * A tile = `tc` consecutive chunks; one 256-thread workgroup (4 waves)
 //     per tile; tiles are claimed through an atomic ticket so a tile only
 //     ever waits on tiles that were claimed before it (forward progress).
-//   * A wave packs whole chunks, 64 words per step (lane = word).
-//   * Pass A computes each chunk's packed size; the tile aggregate is
-//     published and the tile's global byte offset found by a decoupled
-//     look-back over {flag, value} 64-bit granules; pass B re-runs the chunk
-//     (input re-read from L2 / Infinity Cache) and writes the bytes.
+//   * Staged path (every wave's share fits kStageSteps 64-word steps): wave
+//     w owns a contiguous run of the tile's chunks, loads all its words into
+//     registers at once, packs them into its own zeroed LDS region (offsets
+//     local to the wave need no look-back), and after the tile's global
+//     offset is known copies the region out with aligned 16-byte stores.
+//   * Streaming path (tiles with larger chunks): wave w owns chunks w, w+4,
+//     ...; pass A computes sizes, pass B re-reads the words (L2 / MALL) and
+//     flushes whole 16-byte blocks through a 4 KiB LDS ring.
+//   * The tile offset comes from a decoupled look-back over {flag, value}
+//     64-bit granules (one relaxed agent-scope store / load each).
 //
 // Run segmentation without a serial loop
 //   The reference walks words one at a time: a zero word absorbs up to 255
@@ -27,23 +32,36 @@
 //   not absorbed; their bytes are [tag][non-zero bytes] (+ count), absorbed
 //   literal words emit 8 raw bytes, absorbed zero words emit nothing.
 //
-// Output path
-//   Each wave stages its chunk's bytes in a 4 KiB LDS ring (byte writes at
-//   the wave-scanned offsets) and streams whole 16-byte blocks to HBM with
-//   dwordx4 stores; only the first and last block of a chunk (shared with
-//   the neighbouring chunks) are written byte by byte.  A run's count byte
-//   is only known once the run ends, possibly several steps later, so the
-//   ring holds back the block containing a pending count until it is
-//   patched.
+// Byte compaction
+//   Every lane ORs its (<= 10-byte) record, shifted to its byte offset, into
+//   <= 4 dwords of a zeroed LDS buffer (ds_or_b32).  A run's count byte is
+//   only known once the run ends, possibly several steps later; it is
+//   patched in LDS (the ring holds back the block that contains it).
 #include "common.h"
+
+#ifndef PACK_ABLATE
+#define PACK_ABLATE 0  // diagnostic builds only (scripts/ablate.py); 0 = product
+#endif
 
 namespace {
 
 constexpr int kWaves = 4;
 constexpr int kThreads = kWaves * CAPNP_WAVE;
-constexpr uint32_t kRing = 4096;           // per-wave staging ring (bytes)
+constexpr uint32_t kRing = 4096;           // streaming path: per-wave ring (bytes)
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr int kMaxTileChunks = 128;
+constexpr uint32_t kZeroAhead = 1024;      // ring bytes zeroed per refill
+constexpr uint32_t kStepMax = 64 * 10 + 16;
+constexpr uint32_t kRegionBytes = 4864;    // per-wave LDS region
+
+// Staged path capacity: 8 steps of 64 words per wave.
+constexpr uint32_t kStageSteps = 8;
+constexpr uint32_t kStageWords = 64 * kStageSteps;
+// >= sum of per-chunk bounds for <= 32 chunks totalling kStageWords words,
+// plus the 32 bytes copy_out may read past the end
+constexpr uint32_t kStageBytes = 8 * kStageWords + kStageWords / 2 + 3 * 32 + 64;
+constexpr uint32_t kRegion = (kStageBytes + 32 + 15) & ~15u;
+static_assert(kRegion <= kRegionBytes && kRing <= kRegionBytes, "staging region too small");
 
 constexpr uint64_t kFlagAgg = 1ull << 62;  // tile aggregate available
 constexpr uint64_t kFlagInc = 2ull << 62;  // tile inclusive prefix available
@@ -51,12 +69,16 @@ constexpr uint64_t kValMask = (1ull << 62) - 1;
 
 struct Smem {
     uint64_t sel[256];                  // compaction selectors per tag
+    uint64_t off[kMaxTileChunks + 1];   // chunk word offsets of the tile
     uint64_t chunk_size[kMaxTileChunks];
     uint64_t chunk_pos[kMaxTileChunks];
-    uint64_t prefix;
+    uint64_t wave_bytes[kWaves];
+    uint64_t wave_steps[kWaves];
     uint32_t tile;
-    uint32_t pad;
-    alignas(16) uint8_t ring[kWaves][kRing];
+    uint32_t pad[3];
+    // per-wave staging region; the streaming path uses its first 4 KiB as
+    // the flush ring
+    alignas(16) uint8_t stage[kWaves][kRegionBytes];
 };
 
 // Carried run state between 64-word steps of one chunk.
@@ -66,7 +88,7 @@ struct Carry {
 };
 
 struct StepMasks {
-    uint64_t H;      // heads
+    uint64_t H;               // heads
     uint32_t absorbed_carry;  // words absorbed by the carried run
     Carry next;
 };
@@ -76,61 +98,90 @@ __device__ __forceinline__ StepMasks resolve_step(uint64_t Zm, uint64_t Lm, uint
     StepMasks r;
     uint64_t AC = 0;
     uint32_t k = 0;
-    if (c.type == 1) {
-        uint32_t lead = ctz64(~Zm);
-        k = lead < c.rem ? lead : c.rem;
-        AC = low_mask(k);
-    } else if (c.type == 2) {
-        uint32_t lead = ctz64(~Lm);
+    if (c.type != 0) {
+        const uint32_t lead = ctz64(~(c.type == 1 ? Zm : Lm));
         k = lead < c.rem ? lead : c.rem;
         AC = low_mask(k);
     }
-    uint64_t Z2 = Zm & ~AC;
-    uint64_t AZ = Z2 & (Z2 << 1);
-    uint64_t L2 = Lm & ~AC;
-    uint64_t F2 = Fm & ~AC;
-    uint64_t filled = ((L2 ^ (L2 + F2)) & L2) | F2;
-    uint64_t AF = filled & (filled << 1);
-    uint64_t H = low_mask(nvalid) & ~(AC | AZ | AF);
+    const uint64_t Z2 = Zm & ~AC;
+    const uint64_t AZ = Z2 & (Z2 << 1);
+    const uint64_t L2 = Lm & ~AC;
+    const uint64_t F2 = Fm & ~AC;
+    const uint64_t filled = ((L2 ^ (L2 + F2)) & L2) | F2;
+    const uint64_t AF = filled & (filled << 1);
+    const uint64_t H = low_mask(nvalid) & ~(AC | AZ | AF);
     r.H = H;
     r.absorbed_carry = k;
     if (H == 0) {
         r.next.type = c.type;
         r.next.rem = c.rem - 64;  // only reachable when the carry covered the step
     } else {
-        uint32_t h = 63u - (uint32_t)__builtin_clzll(H);
-        uint64_t hb = 1ull << h;
-        if (Zm & hb) { r.next.type = 1; r.next.rem = 255u - (63u - h); }
-        else if (Fm & hb) { r.next.type = 2; r.next.rem = 255u - (63u - h); }
-        else { r.next.type = 0; r.next.rem = 0; }
+        const uint32_t h = 63u - (uint32_t)__builtin_clzll(H);
+        const uint64_t hb = 1ull << h;
+        r.next.type = (Zm & hb) ? 1u : ((Fm & hb) ? 2u : 0u);
+        r.next.rem = r.next.type ? 255u - (63u - h) : 0u;
     }
     return r;
 }
 
-// Packs one chunk of `nwords` words starting at in[w0].  WRITE=false returns
-// the packed size only; WRITE=true stages and stores the bytes at out[o_c..].
-template <bool WRITE>
-__device__ uint64_t pack_chunk(const uint64_t* __restrict__ in, uint64_t w0, uint64_t nwords,
-                               uint8_t* __restrict__ out, uint64_t o_c, uint8_t* ring,
-                               const uint64_t* sel, uint32_t lane) {
-    Carry carry = {0, 0};
-    uint64_t total = 0;
-    bool pend = false;        // a run's count byte is not yet known
-    uint64_t pend_pos = 0;    // absolute output position of that count byte
-    uint32_t pend_cnt = 0;
-    uint64_t flushed = o_c & ~15ull;
+// Stores output bytes [lo, hi) (16-aligned coordinates) from the ring: byte
+// stores for the unaligned head and tail, dwordx4 for the rest.
+__device__ __forceinline__ void flush_range(const uint8_t* ring, uint8_t* __restrict__ out,
+                                            uint64_t lo, uint64_t hi, uint32_t lane) {
+    if (hi <= lo) return;
+    const uint64_t a = (lo + 15) & ~15ull, b = hi & ~15ull;
+    if (a > b) {  // inside one block
+        if (lane < hi - lo) out[lo + lane] = ring[(lo + lane) & kRingMask];
+        return;
+    }
+    if (lane < a - lo) out[lo + lane] = ring[(lo + lane) & kRingMask];
+    for (uint64_t blk = a + 16ull * lane; blk < b; blk += 16ull * CAPNP_WAVE)
+        *reinterpret_cast<uint4*>(out + blk) =
+            *reinterpret_cast<const uint4*>(ring + (blk & kRingMask));
+    if (lane < hi - b) out[b + lane] = ring[(b + lane) & kRingMask];
+}
 
-    uint64_t wnext = 0;
-    if (nwords) wnext = lane < nwords ? in[w0 + lane] : 0;
-    for (uint64_t base = 0; base < nwords; base += 64) {
-        const uint32_t nvalid = (uint32_t)((nwords - base) < 64 ? (nwords - base) : 64);
-        const bool last = base + 64 >= nwords;
+// Where a step's bytes go.
+enum StepMode {
+    MODE_SIZE = 0,   // pass A of the streaming path: sizes only
+    MODE_RING = 1,   // pass B of the streaming path: 4 KiB ring + flush
+    MODE_STAGE = 2,  // staged path: wave-local LDS region, copied out later
+};
+
+// Per-wave packing state of the chunk in progress (wave-uniform).
+struct Packer {
+    Carry carry;
+    uint64_t total;     // packed bytes of the chunk so far
+    uint64_t o_c;       // chunk start (absolute for RING, region-local for STAGE)
+    uint64_t flushed;   // RING: everything below is stored
+    uint64_t zeroed;    // RING: ring zeroed up to here
+    uint64_t pend_pos;  // position of a pending run count byte
+    uint32_t pend_cnt;
+    bool pend;
+
+    __device__ __forceinline__ void begin(uint64_t oc) {
+        carry.type = 0;
+        carry.rem = 0;
+        total = 0;
+        o_c = oc;
+        flushed = oc;
+        zeroed = oc & ~15ull;
+        pend = false;
+        pend_pos = 0;
+        pend_cnt = 0;
+    }
+
+    template <int MODE>
+    __device__ __forceinline__ static uint32_t at(uint64_t p) {
+        return MODE == MODE_RING ? (uint32_t)(p & kRingMask) : (uint32_t)p;
+    }
+
+    // One 64-word step.
+    template <int MODE>
+    __device__ __forceinline__ void step(uint64_t w, uint32_t nvalid, bool last, uint32_t lane,
+                                         uint8_t* buf, uint8_t* __restrict__ out,
+                                         const uint64_t* sel) {
         const bool valid = lane < nvalid;
-        const uint64_t w = wnext;
-        if (!last) {
-            uint64_t nb = base + 64;
-            wnext = (nb + lane < nwords) ? in[w0 + nb + lane] : 0;
-        }
         const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
         const uint32_t tag = word_tag(lo, hi);
         const uint32_t pop = __builtin_popcount(tag);
@@ -144,92 +195,195 @@ __device__ uint64_t pack_chunk(const uint64_t* __restrict__ in, uint64_t w0, uin
         else size = (valid && tag != 0) ? 8u : 0u;
         const uint64_t B0 = ballot64(size & 1), B1 = ballot64(size & 2);
         const uint64_t B2 = ballot64(size & 4), B3 = ballot64(size & 8);
-        const uint32_t step_bytes = popc64(B0) + 2 * popc64(B1) + 4 * popc64(B2) + 8 * popc64(B3);
-
-        if (WRITE) {
-            const uint32_t off = mask_rank(B0) + 2 * mask_rank(B1) + 4 * mask_rank(B2) +
-                                 8 * mask_rank(B3);
-            // count byte of a Z/F head whose run ends inside this step
-            uint32_t cnt = 0;
-            const uint64_t later = sm.H & ~low_mask(lane + 1);
-            if (later) cnt = ctz64(later) - lane - 1;
-            else cnt = nvalid - lane - 1;   // run reaches the step end
-            const uint64_t pos = o_c + total + off;
-            if (head || size) {
-                uint32_t d0, d1 = 0, d2 = 0, len = size;
-                if (head && tag == 0) {
-                    d0 = cnt << 8;
-                } else if (head) {
-                    uint32_t clo = lo, chi = hi;
-                    if (tag != 0xFF) {
-                        const uint64_t s = sel[tag];
-                        clo = __builtin_amdgcn_perm(hi, lo, (uint32_t)s);
-                        chi = __builtin_amdgcn_perm(hi, lo, (uint32_t)(s >> 32));
-                    }
-                    d0 = tag | (clo << 8);
-                    d1 = (clo >> 24) | (chi << 8);
-                    d2 = (chi >> 24) | (cnt << 8);
-                } else {
-                    d0 = lo;
-                    d1 = hi;
-                }
-#pragma unroll
-                for (uint32_t k = 0; k < 10; k++) {
-                    if (k < len) {
-                        const uint32_t d = k < 4 ? d0 : (k < 8 ? d1 : d2);
-                        ring[(pos + k) & kRingMask] = (uint8_t)(d >> (8 * (k & 3)));
-                    }
-                }
-            }
-            // Resolve the count carried in from earlier steps.
-            if (pend) {
-                pend_cnt += sm.absorbed_carry;
-                if (sm.absorbed_carry < 64 || last) {
-                    if (lane == 0) ring[pend_pos & kRingMask] = (uint8_t)pend_cnt;
-                    pend = false;
-                }
-            }
-            // A Z/F head whose run reaches the end of a non-final step: its
-            // count continues into the next step.
-            if (!last && nvalid == 64 && sm.H) {
-                const uint32_t h = 63u - (uint32_t)__builtin_clzll(sm.H);
-                const uint64_t hb = 1ull << h;
-                if ((Zm | Fm) & hb) {
-                    // the last head absorbs every later word of the step
-                    pend = true;
-                    pend_cnt = 63u - h;
-                    // its output offset: bytes of lanes below h
-                    const uint64_t below = low_mask(h);
-                    const uint32_t hoff = popc64(B0 & below) + 2 * popc64(B1 & below) +
-                                          4 * popc64(B2 & below) + 8 * popc64(B3 & below);
-                    pend_pos = o_c + total + hoff + ((Zm & hb) ? 1u : 9u);
-                }
-            }
-            total += step_bytes;
-            wave_lds_sync();
-            // Flush whole blocks that can no longer change.
-            const uint64_t produced = o_c + total;
-            uint64_t limit;
-            if (last) limit = produced;
-            else limit = (pend ? pend_pos : produced) & ~15ull;
-            for (uint64_t b = flushed + 16ull * lane; b < limit; b += 16ull * CAPNP_WAVE) {
-                const uint8_t* src = ring + (b & kRingMask);
-                const uint64_t own_lo = b < o_c ? o_c : b;
-                const uint64_t own_hi = (b + 16 < produced) ? b + 16 : produced;
-                if (own_lo == b && own_hi == b + 16) {
-                    *reinterpret_cast<uint4*>(out + b) = *reinterpret_cast<const uint4*>(src);
-                } else {
-                    for (uint64_t a = own_lo; a < own_hi; a++) out[a] = src[a - b];
-                }
-            }
-            if (limit > flushed) flushed = (limit + 15) & ~15ull;
-            wave_lds_sync();
-        } else {
-            total += step_bytes;
-        }
+        const uint32_t step_bytes =
+            popc64(B0) + 2 * popc64(B1) + 4 * popc64(B2) + 8 * popc64(B3);
         carry = sm.next;
+        if (MODE == MODE_SIZE) {
+            total += step_bytes;
+            return;
+        }
+        const uint64_t start = o_c + total;
+        if (MODE == MODE_RING && zeroed < start + kStepMax) {  // zero the next KiB
+            *reinterpret_cast<uint4*>(buf + ((zeroed + 16ull * lane) & kRingMask)) =
+                make_uint4(0, 0, 0, 0);
+            zeroed += kZeroAhead;
+            wave_lds_sync();
+        }
+        const uint32_t off =
+            mask_rank(B0) + 2 * mask_rank(B1) + 4 * mask_rank(B2) + 8 * mask_rank(B3);
+        if (size) {
+            // count byte of a Z/F head: words up to the next head (or step end)
+            const uint64_t later = sm.H & ~low_mask(lane + 1);
+            const uint32_t cnt = later ? ctz64(later) - lane - 1 : nvalid - lane - 1;
+            uint32_t r0, r1 = 0, r2 = 0;
+            if (head && tag == 0) {
+                r0 = cnt << 8;
+            } else if (head) {
+                uint32_t clo = lo, chi = hi;
+                if (tag != 0xFF) {
+                    const uint64_t s = sel[tag];
+                    clo = __builtin_amdgcn_perm(hi, lo, (uint32_t)s);
+                    chi = __builtin_amdgcn_perm(hi, lo, (uint32_t)(s >> 32));
+                }
+                r0 = tag | (clo << 8);
+                r1 = (clo >> 24) | (chi << 8);
+                r2 = (chi >> 24) | (tag == 0xFF ? cnt << 8 : 0u);
+            } else {
+                r0 = lo;
+                r1 = hi;
+            }
+            const uint64_t pos = start + off;
+            const uint32_t sh = (uint32_t)(pos & 3) * 8;
+            const uint32_t e0 = r0 << sh;
+            const uint32_t e1 = (uint32_t)((((uint64_t)r1 << 32) | r0) >> (32 - sh));
+            const uint32_t e2 = (uint32_t)((((uint64_t)r2 << 32) | r1) >> (32 - sh));
+            const uint32_t e3 = (uint32_t)((uint64_t)r2 >> (32 - sh));
+            const uint32_t nd = ((uint32_t)(pos & 3) + size + 3) >> 2;
+            const uint64_t d = pos & ~3ull;
+            uint32_t* b32 = reinterpret_cast<uint32_t*>(buf);
+            __hip_atomic_fetch_or(b32 + (at<MODE>(d) >> 2), e0, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WAVEFRONT);
+            if (nd > 1)
+                __hip_atomic_fetch_or(b32 + (at<MODE>(d + 4) >> 2), e1, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WAVEFRONT);
+            if (nd > 2)
+                __hip_atomic_fetch_or(b32 + (at<MODE>(d + 8) >> 2), e2, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WAVEFRONT);
+            if (nd > 3)
+                __hip_atomic_fetch_or(b32 + (at<MODE>(d + 12) >> 2), e3, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WAVEFRONT);
+        }
+        // resolve a count carried in from earlier steps
+        if (pend) {
+            pend_cnt += sm.absorbed_carry;
+            if (sm.absorbed_carry < 64 || last) {
+                wave_lds_sync();
+                if (lane == 0) buf[at<MODE>(pend_pos)] = (uint8_t)pend_cnt;
+                pend = false;
+            }
+        }
+        // a Z/F head whose run reaches the end of a non-final step
+        if (!last && nvalid == 64 && sm.H) {
+            const uint32_t h = 63u - (uint32_t)__builtin_clzll(sm.H);
+            const uint64_t hb = 1ull << h;
+            if ((Zm | Fm) & hb) {
+                pend = true;
+                pend_cnt = 63u - h;
+                const uint64_t below = low_mask(h);
+                const uint32_t hoff = popc64(B0 & below) + 2 * popc64(B1 & below) +
+                                      4 * popc64(B2 & below) + 8 * popc64(B3 & below);
+                pend_pos = start + hoff + ((Zm & hb) ? 1u : 9u);
+            }
+        }
+        total += step_bytes;
+        if (MODE == MODE_RING) {
+            wave_lds_sync();
+            const uint64_t produced = o_c + total;
+            const uint64_t limit = last ? produced : ((pend ? pend_pos : produced) & ~15ull);
+            if (limit > flushed) {
+                flush_range(buf, out, flushed, limit, lane);
+                flushed = limit;
+            }
+        }
     }
-    return total;
+};
+
+__device__ __forceinline__ uint64_t lds_u64(const uint64_t* p) { return uniform64(*p); }
+
+// Copies region bytes [0, len) to out[D0 .. D0+len) (16-aligned coordinates),
+// never writing at or past `cap`.
+__device__ __forceinline__ void copy_out(const uint8_t* region, uint8_t* __restrict__ out,
+                                         uint64_t D0, uint64_t len, uint64_t cap,
+                                         uint32_t lane) {
+    const uint64_t lo = D0;
+    const uint64_t hi = (D0 + len < cap) ? D0 + len : cap;
+    if (hi <= lo) return;
+    const uint64_t a = (lo + 15) & ~15ull, b = hi & ~15ull;
+    if (a > b) {
+        if (lane < hi - lo) out[lo + lane] = region[lane];
+        return;
+    }
+    if (lane < a - lo) out[lo + lane] = region[lane];
+    const uint32_t m = (uint32_t)((a - D0) & 15);  // source misalignment (uniform)
+    const uint32_t q = m >> 2, sb = m & 3;
+    for (uint64_t blk = a + 16ull * lane; blk < b; blk += 16ull * CAPNP_WAVE) {
+        const uint32_t s = (uint32_t)(blk - D0) & ~15u;
+        const uint4 A = *reinterpret_cast<const uint4*>(region + s);
+        const uint4 B = *reinterpret_cast<const uint4*>(region + s + 16);
+        const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+        uint4 o;
+        if (q == 0) {
+            o = make_uint4(__builtin_amdgcn_alignbyte(w[1], w[0], sb),
+                           __builtin_amdgcn_alignbyte(w[2], w[1], sb),
+                           __builtin_amdgcn_alignbyte(w[3], w[2], sb),
+                           __builtin_amdgcn_alignbyte(w[4], w[3], sb));
+        } else if (q == 1) {
+            o = make_uint4(__builtin_amdgcn_alignbyte(w[2], w[1], sb),
+                           __builtin_amdgcn_alignbyte(w[3], w[2], sb),
+                           __builtin_amdgcn_alignbyte(w[4], w[3], sb),
+                           __builtin_amdgcn_alignbyte(w[5], w[4], sb));
+        } else if (q == 2) {
+            o = make_uint4(__builtin_amdgcn_alignbyte(w[3], w[2], sb),
+                           __builtin_amdgcn_alignbyte(w[4], w[3], sb),
+                           __builtin_amdgcn_alignbyte(w[5], w[4], sb),
+                           __builtin_amdgcn_alignbyte(w[6], w[5], sb));
+        } else {
+            o = make_uint4(__builtin_amdgcn_alignbyte(w[4], w[3], sb),
+                           __builtin_amdgcn_alignbyte(w[5], w[4], sb),
+                           __builtin_amdgcn_alignbyte(w[6], w[5], sb),
+                           __builtin_amdgcn_alignbyte(w[7], w[6], sb));
+        }
+        *reinterpret_cast<uint4*>(out + blk) = o;
+    }
+    if (lane < hi - b) out[b + lane] = region[(b - D0) + lane];
+}
+
+// Iterates the steps of chunks [ci, ce) of the tile in 64-word windows.
+struct RangeIter {
+    uint32_t ci, ce;
+    uint64_t base, len, woff;
+    __device__ __forceinline__ void skip(const uint64_t* off) {
+        while (ci < ce) {
+            woff = lds_u64(&off[ci]);
+            len = lds_u64(&off[ci + 1]) - woff;
+            if (base < len) break;
+            ci++;
+            base = 0;
+        }
+    }
+};
+
+// Streaming path: wave w owns chunks w, w+4, ...  MODE_SIZE fills
+// chunk_size; MODE_RING re-reads and writes at chunk_pos.
+template <int MODE>
+__device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* off,
+                              uint64_t* chunk_size, const uint64_t* chunk_pos, uint32_t nc,
+                              uint32_t wave, uint32_t lane, uint8_t* ring, const uint64_t* sel,
+                              uint8_t* out, uint32_t mis, uint64_t out_cap) {
+    Packer pk;
+    for (uint32_t ci = wave; ci < nc; ci += kWaves) {
+        const uint64_t woff = lds_u64(&off[ci]);
+        const uint64_t len = lds_u64(&off[ci + 1]) - woff;
+        if (len == 0) continue;
+        if (MODE == MODE_RING) {
+            const uint64_t pos = lds_u64(&chunk_pos[ci]);
+            if (pos + lds_u64(&chunk_size[ci]) > out_cap) continue;  // does not fit
+            pk.begin(pos + mis);
+        } else {
+            pk.begin(0);
+        }
+        const uint64_t* src = in + woff;
+        uint64_t wnext = lane < len ? src[lane] : 0;
+        for (uint64_t base = 0;; base += 64) {
+            const uint32_t nvalid = (uint32_t)((len - base) < 64 ? len - base : 64);
+            const bool last = base + 64 >= len;
+            const uint64_t w = wnext;
+            if (!last) wnext = (base + 64 + lane < len) ? src[base + 64 + lane] : 0;
+            pk.step<MODE>(w, nvalid, last, lane, ring, out, sel);
+            if (last) break;
+        }
+        if (MODE == MODE_SIZE && lane == 0) chunk_size[ci] = pk.total;
+    }
 }
 
 __global__ void __launch_bounds__(kThreads)
@@ -240,7 +394,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     __shared__ Smem sm;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
-    const uint32_t wave = tid >> 6;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
 
     if (tid == 0) sm.tile = atomicAdd(ticket, 1u);
     // compaction selectors: byte r = index of the r-th set bit of the tag
@@ -260,30 +414,94 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     const uint64_t c0 = (uint64_t)tile * tc;
     const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
     const uint32_t nc = (uint32_t)(c1 - c0);
+    for (uint32_t i = tid; i <= nc; i += kThreads) sm.off[i] = chunk_off[c0 + i];
+    for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
+    __syncthreads();
 
-    // ---- pass A: packed size of every chunk of the tile
-    for (uint32_t i = wave; i < nc; i += kWaves) {
-        const uint64_t a = chunk_off[c0 + i], b = chunk_off[c0 + i + 1];
-        const uint64_t sz = pack_chunk<false>(in, a, b - a, out, 0, nullptr, sm.sel, lane);
-        if (lane == 0) sm.chunk_size[i] = sz;
+    // contiguous chunk ranges per wave for the staged path; a range fits when
+    // its 64-word steps fit the register cache
+    const uint32_t q = (nc + kWaves - 1) / kWaves;
+    const uint32_t wc0 = wave * q < nc ? wave * q : nc;
+    const uint32_t wc1 = wc0 + q < nc ? wc0 + q : nc;
+    {
+        uint64_t my_steps = 0;
+        for (uint32_t i = wc0 + lane; i < wc1; i += CAPNP_WAVE)
+            my_steps += (sm.off[i + 1] - sm.off[i] + 63) / 64;
+        for (uint32_t d = 32; d >= 1; d >>= 1) my_steps += __shfl_xor(my_steps, d, 64);
+        if (lane == 0) sm.wave_steps[wave] = my_steps;
+    }
+    __syncthreads();
+    bool staged = true;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) staged &= sm.wave_steps[w] <= kStageSteps;
+    staged = __builtin_amdgcn_readfirstlane((int)staged) != 0;
+
+    uint8_t* region = sm.stage[wave];
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
+    uint8_t* const outa = out - mis;
+
+    if (staged) {
+        // zero the region, load every step of the range into registers
+        for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
+            *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
+        uint64_t cache[kStageSteps];
+        {
+            RangeIter it{wc0, wc1, 0, 0, 0};
+#pragma unroll
+            for (uint32_t s = 0; s < kStageSteps; s++) {
+                it.skip(sm.off);
+                cache[s] = 0;
+                if (it.ci < it.ce) {
+                    if (it.base + lane < it.len) cache[s] = in[it.woff + it.base + lane];
+                    it.base += 64;
+                }
+            }
+        }
+        wave_lds_sync();
+        Packer pk;
+        uint64_t local = 0;
+        {
+            RangeIter it{wc0, wc1, 0, 0, 0};
+#pragma unroll
+            for (uint32_t s = 0; s < kStageSteps; s++) {
+                it.skip(sm.off);
+                if (it.ci >= it.ce) break;
+                if (it.base == 0) pk.begin(local);
+                const uint32_t nvalid =
+                    (uint32_t)((it.len - it.base) < 64 ? it.len - it.base : 64);
+                const bool last = it.base + 64 >= it.len;
+                pk.step<MODE_STAGE>(cache[s], nvalid, last, lane, region, outa, sm.sel);
+                if (last) {
+                    if (lane == 0) sm.chunk_size[it.ci] = pk.total;
+                    local += pk.total;
+                }
+                it.base += 64;
+            }
+        }
+        if (lane == 0) sm.wave_bytes[wave] = local;
+    } else {
+        run_streaming<MODE_SIZE>(in, sm.off, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
+                                 region, sm.sel, outa, mis, out_cap);
     }
     __syncthreads();
 
     // ---- tile scan + decoupled look-back (wave 0)
     if (wave == 0) {
-        uint64_t v = lane < nc ? sm.chunk_size[lane] : 0;
-        uint64_t v2 = (lane + 64 < nc) ? sm.chunk_size[lane + 64] : 0;
-        // inclusive scan over 64 lanes (two halves of up to 128 chunks)
+        const uint64_t v = lane < nc ? sm.chunk_size[lane] : 0;
+        const uint64_t v2 = (lane + 64 < nc) ? sm.chunk_size[lane + 64] : 0;
         uint64_t s = v, s2 = v2;
         for (uint32_t d = 1; d < 64; d <<= 1) {
-            uint64_t t = __shfl_up(s, d, 64);
-            uint64_t t2 = __shfl_up(s2, d, 64);
+            const uint64_t t = __shfl_up(s, d, 64);
+            const uint64_t t2 = __shfl_up(s2, d, 64);
             if (lane >= d) { s += t; s2 += t2; }
         }
-        const uint64_t half = __shfl(s, 63, 64);
-        s2 += half;
+        s2 += __shfl(s, 63, 64);
         const uint64_t agg = __shfl(s2, 63, 64);
         uint64_t excl = 0;
+#if PACK_ABLATE == 1
+        // timing-only: no look-back (fake, in-bounds prefix); output is wrong
+        excl = (uint64_t)tile * agg;
+#else
         if (tile == 0) {
             if (lane == 0) store_relaxed_agent(&tile_state[0], kFlagInc | agg);
         } else {
@@ -291,7 +509,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             int64_t idx = (int64_t)tile - 1;
             for (;;) {
                 const int64_t j = idx - (int64_t)lane;
-                uint64_t st = j >= 0 ? load_relaxed_agent(&tile_state[j]) : kFlagInc;
+                const uint64_t st = j >= 0 ? load_relaxed_agent(&tile_state[j]) : kFlagInc;
                 const uint64_t inc = ballot64((st & kFlagInc) != 0);
                 const uint64_t none = ballot64((st >> 62) == 0);
                 const uint32_t first_inc = ctz64(inc);
@@ -308,23 +526,26 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             }
             if (lane == 0) store_relaxed_agent(&tile_state[tile], kFlagInc | (excl + agg));
         }
+#endif
         if (lane < nc) sm.chunk_pos[lane] = excl + s - v;
         if (lane + 64 < nc) sm.chunk_pos[lane + 64] = excl + s2 - v2;
-        if (lane == 0) sm.prefix = excl;
         if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
     }
     __syncthreads();
     for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
 
-    // ---- pass B: write the bytes.  Block arithmetic runs on addresses
-    // aligned to 16 in memory: positions are shifted by out's misalignment.
-    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
-    uint8_t* const outa = out - mis;
-    for (uint32_t i = wave; i < nc; i += kWaves) {
-        const uint64_t a = chunk_off[c0 + i], b = chunk_off[c0 + i + 1];
-        const uint64_t pos = sm.chunk_pos[i];
-        if (pos + sm.chunk_size[i] > out_cap) continue;  // does not fit: skip
-        pack_chunk<true>(in, a, b - a, outa, pos + mis, sm.ring[wave], sm.sel, lane);
+    // ---- write the bytes
+#if PACK_ABLATE == 2
+    return;  // timing-only: no output stores
+#endif
+    if (staged) {
+        if (wc1 > wc0) {
+            const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
+            copy_out(region, outa, D0, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
+        }
+    } else {
+        run_streaming<MODE_RING>(in, sm.off, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
+                                 region, sm.sel, outa, mis, out_cap);
     }
 }
 

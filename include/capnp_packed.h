@@ -109,8 +109,9 @@ size_t capnp_packed_batch_bound_bytes(size_t total_words, size_t nchunks);
    (serialize_packed.rs:304-439), and concatenate the results in chunk order
    into d_out.  On completion d_out_byte_off[c] is chunk c's start in d_out
    and d_out_byte_off[nchunks] the total packed size.  If the total exceeds
-   out_cap nothing past out_cap is written and the total still reports the
-   size that was needed (caller checks after the stream syncs).
+   out_cap nothing at or past out_cap is written (the chunk that straddles
+   out_cap may be partially written) and the total still reports the size
+   that was needed (caller checks after the stream syncs).
    d_chunk_word_off: nchunks+1 non-decreasing word offsets. */
 capnp_status capnp_gpu_pack_batch(capnp_ctx* ctx, const uint64_t* d_words,
                                   const uint64_t* d_chunk_word_off, size_t nchunks,
