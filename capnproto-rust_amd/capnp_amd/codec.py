@@ -134,12 +134,12 @@ class Context:
 
 
 def tile_chunks_for(total_words, nchunks):
-    """Chunks per 256-thread pack workgroup: ~2048 words per tile, i.e. one
-    512-word staged range per wave (pack.hip kStageWords)."""
+    """Chunks per 256-thread pack workgroup: ~1024 words per tile, i.e. one
+    256-word staged range per wave (pack.hip kStageWords)."""
     if nchunks <= 0:
         return 16
     mean = max(total_words / nchunks, 1.0)
-    return int(max(1, min(128, 2048 // mean)))
+    return int(max(1, min(64, 1024 // mean)))
 
 
 _default = {}

@@ -16,8 +16,8 @@
 #include "frame.h"
 
 extern "C" hipError_t capnp_launch_pack(const uint64_t*, const uint64_t*, uint64_t, uint32_t,
-                                        uint8_t*, uint64_t, uint64_t*, uint64_t*, uint32_t*,
-                                        size_t, hipStream_t);
+                                        uint8_t*, uint64_t, uint64_t*, uint64_t*, hipStream_t);
+extern "C" size_t capnp_pack_state_bytes(uint64_t, uint32_t);
 extern "C" hipError_t capnp_launch_unpack(const uint8_t*, const uint64_t*, uint64_t, uint64_t*,
                                           const uint64_t*, int32_t*, uint64_t*, hipStream_t);
 extern "C" hipError_t capnp_launch_gen(uint64_t*, const uint64_t*, uint64_t, uint64_t,
@@ -28,7 +28,7 @@ extern "C" hipError_t capnp_launch_frame(const uint8_t*, uint64_t, uint32_t, uin
 namespace {
 
 constexpr uint32_t kDefaultTileChunks = 16;
-constexpr uint32_t kMaxTileChunks = 128;
+constexpr uint32_t kMaxTileChunks = 64;
 
 size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
 
@@ -37,7 +37,7 @@ size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
 struct capnp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    uint8_t* d_state = nullptr;   // [ticket, 16 B][tile look-back records]
+    uint8_t* d_state = nullptr;   // pack look-back records (tiles, groups)
     size_t state_cap = 0;
     uint8_t* d_stage = nullptr;   // staging for the host APIs (inputs)
     size_t stage_cap = 0;
@@ -100,8 +100,7 @@ capnp_status ensure_stage(capnp_ctx* ctx, size_t bytes) {
 }
 
 size_t state_bytes_for(size_t nchunks, uint32_t tc) {
-    const size_t ntiles = (nchunks + tc - 1) / tc;
-    return round16(16 + 8 * ntiles);
+    return capnp_pack_state_bytes(nchunks, tc) + 16;
 }
 
 capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint64_t* d_off,
@@ -115,15 +114,14 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
     capnp_status st = ensure_state(ctx, sb);
     if (st != CAPNP_OK) return st;
     HIP_TRY(capnp_launch_pack(d_words, d_off, n, tc, d_out, cap, d_out_off,
-                              reinterpret_cast<uint64_t*>(ctx->d_state + 16),
-                              reinterpret_cast<uint32_t*>(ctx->d_state), sb, s));
+                              reinterpret_cast<uint64_t*>(ctx->d_state), s));
     return CAPNP_OK;
 }
 
 uint32_t tile_chunks_for(uint64_t total_words, size_t n) {
     if (n == 0) return kDefaultTileChunks;
     const double mean = (double)total_words / (double)n;
-    double t = 2048.0 / std::max(mean, 1.0);  // ~512 words per wave (staged path)
+    double t = 1024.0 / std::max(mean, 1.0);  // ~256 words per wave (staged path)
     uint32_t tc = (uint32_t)std::max(1.0, std::min(t, (double)kMaxTileChunks));
     return tc;
 }

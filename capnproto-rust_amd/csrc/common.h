@@ -80,6 +80,12 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // Relaxed agent-scope 64-bit accesses (single global sc1 load/store): the
 // look-back records are {flag, value} granules written by one store
 // (MI355X_MICROARCH.md, "Valid forms", R2 granule).

@@ -49,13 +49,13 @@ constexpr int kWaves = 4;
 constexpr int kThreads = kWaves * CAPNP_WAVE;
 constexpr uint32_t kRing = 4096;           // streaming path: per-wave ring (bytes)
 constexpr uint32_t kRingMask = kRing - 1;
-constexpr int kMaxTileChunks = 128;
+constexpr int kMaxTileChunks = 64;
 constexpr uint32_t kZeroAhead = 1024;      // ring bytes zeroed per refill
 constexpr uint32_t kStepMax = 64 * 10 + 16;
-constexpr uint32_t kRegionBytes = 4864;    // per-wave LDS region
+constexpr uint32_t kRegionBytes = 4096;    // per-wave LDS region (= ring size)
 
-// Staged path capacity: 8 steps of 64 words per wave.
-constexpr uint32_t kStageSteps = 8;
+// Staged path capacity: kStageSteps steps of 64 words per wave.
+constexpr uint32_t kStageSteps = 4;
 constexpr uint32_t kStageWords = 64 * kStageSteps;
 // >= sum of per-chunk bounds for <= 32 chunks totalling kStageWords words,
 // plus the 32 bytes copy_out may read past the end
@@ -74,8 +74,6 @@ struct Smem {
     uint64_t chunk_pos[kMaxTileChunks];
     uint64_t wave_bytes[kWaves];
     uint64_t wave_steps[kWaves];
-    uint32_t tile;
-    uint32_t pad[3];
     // per-wave staging region; the streaming path uses its first 4 KiB as
     // the flush ring
     alignas(16) uint8_t stage[kWaves][kRegionBytes];
@@ -290,6 +288,88 @@ struct Packer {
 
 __device__ __forceinline__ uint64_t lds_u64(const uint64_t* p) { return uniform64(*p); }
 
+// Wave-wide inclusive prefix sum with DPP (VALU only): Kogge-Stone inside
+// each 16-lane row, then row_bcast:15 / row_bcast:31 carry the row totals.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
+// Branch-free step of the staged path (the hot loop).  Mask arithmetic is
+// kept on the scalar unit only where it is inherently wave-wide (run
+// segmentation); offsets come from a DPP scan, so the shared SALU is not
+// the bottleneck.
+__device__ __forceinline__ void stage_step(Packer& pk, uint64_t w, uint32_t nvalid, bool last,
+                                           uint32_t lane, uint8_t* region, const uint64_t* sel) {
+    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+    const uint32_t tag = word_tag(lo, hi);
+    const uint32_t pop = __builtin_popcount(tag);
+    const bool isz = tag == 0, isf = tag == 0xFF;
+    const uint64_t V = low_mask(nvalid);
+    const uint64_t Zm = ballot64(isz) & V;
+    const uint64_t Lm = ballot64(pop >= 7) & V;
+    const uint64_t Fm = ballot64(isf) & V;
+    const StepMasks sm = resolve_step(Zm, Lm, Fm, nvalid, pk.carry);
+    const uint64_t hsh = sm.H >> lane;
+    const bool head = hsh & 1;
+    const bool valid = lane < nvalid;
+    const uint32_t hsize = isz ? 2u : (isf ? 10u : 1u + pop);
+    const uint32_t size = head ? hsize : ((valid && !isz) ? 8u : 0u);
+    const uint32_t incl = wave_incl_scan(size);
+    const uint32_t step_bytes = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t start = (uint32_t)(pk.o_c + pk.total);
+    const uint32_t pos = start + incl - size;
+    // run count of a Z/F head: words up to the next head, or to the step end
+    const uint64_t nxt = hsh >> 1;
+    const uint32_t cnt = nxt ? ctz64(nxt) : nvalid - lane - 1;
+    // record: [tag][non-zero bytes][count] for heads (sel[0xFF] is the
+    // identity, sel[0] yields zeros), the raw word for absorbed words
+    const uint64_t sv = sel[tag];
+    const uint32_t clo = __builtin_amdgcn_perm(hi, lo, (uint32_t)sv);
+    const uint32_t chi = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32));
+    uint32_t r0 = isz ? (cnt << 8) : (tag | (clo << 8));
+    uint32_t r1 = (clo >> 24) | (chi << 8);
+    uint32_t r2 = (chi >> 24) | (isf ? (cnt << 8) : 0u);
+    r0 = head ? r0 : lo;
+    r1 = head ? (isz ? 0u : r1) : hi;
+    r2 = head ? (isz ? 0u : r2) : 0u;
+    const uint32_t sh = (pos & 3) * 8;
+    const uint32_t e0 = r0 << sh;
+    const uint32_t e1 = (uint32_t)((((uint64_t)r1 << 32) | r0) >> (32 - sh));
+    const uint32_t e2 = (uint32_t)((((uint64_t)r2 << 32) | r1) >> (32 - sh));
+    const uint32_t e3 = (uint32_t)((uint64_t)r2 >> (32 - sh));
+    uint32_t* b32 = reinterpret_cast<uint32_t*>(region) + (pos >> 2);
+    __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    // a count carried in from earlier steps
+    if (pk.pend) {
+        pk.pend_cnt += sm.absorbed_carry;
+        if (sm.absorbed_carry < 64 || last) {
+            wave_lds_sync();
+            if (lane == 0) region[pk.pend_pos] = (uint8_t)pk.pend_cnt;
+            pk.pend = false;
+        }
+    }
+    // a Z/F head whose run reaches the end of a non-final step: its count
+    // byte sits 1 (Z) or 9 (F) bytes into its record
+    if (!last && sm.next.type != 0 && sm.H) {
+        const uint32_t h = 63u - (uint32_t)__builtin_clzll(sm.H);
+        pk.pend = true;
+        pk.pend_cnt = 63u - h;
+        pk.pend_pos = (uint32_t)__builtin_amdgcn_readlane((int)pos, h) +
+                      (sm.next.type == 1 ? 1u : 9u);
+    }
+    pk.carry = sm.next;
+    pk.total += step_bytes;
+}
+
 // Copies region bytes [0, len) to out[D0 .. D0+len) (16-aligned coordinates),
 // never writing at or past `cap`.
 __device__ __forceinline__ void copy_out(const uint8_t* region, uint8_t* __restrict__ out,
@@ -386,17 +466,146 @@ __device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* o
     }
 }
 
-__global__ void __launch_bounds__(kThreads)
+// Packed size of tile j computed by one wave from the input (the look-back
+// fallback below; normally never executed).
+__device__ uint64_t tile_aggregate(const uint64_t* __restrict__ in,
+                                   const uint64_t* __restrict__ chunk_off, uint64_t nchunks,
+                                   uint32_t tc, uint64_t j, uint32_t lane) {
+    const uint64_t c0 = j * tc;
+    const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
+    uint64_t total = 0;
+    for (uint64_t ci = c0; ci < c1; ci++) {
+        const uint64_t woff = uniform64(chunk_off[ci]);
+        const uint64_t len = uniform64(chunk_off[ci + 1]) - woff;
+        Packer pk;
+        pk.begin(0);
+        for (uint64_t base = 0; base < len; base += 64) {
+            const uint32_t nvalid = (uint32_t)((len - base) < 64 ? len - base : 64);
+            const uint64_t w = lane < nvalid ? in[woff + base + lane] : 0;
+            pk.step<MODE_SIZE>(w, nvalid, base + 64 >= len, lane, nullptr, nullptr, nullptr);
+        }
+        total += pk.total;
+    }
+    return total;
+}
+
+// Two-level decoupled look-back.  Tile records ts[t] and group records gs[g]
+// (64 tiles per group) are {flag, value} granules.  Tile t publishes its
+// aggregate, sums the aggregates of the tiles before it in its group, and
+// finds the group's exclusive prefix by scanning group records (64 groups =
+// 4096 tiles per round trip).  The last tile of a group publishes the group
+// aggregate and, once known, the group's inclusive prefix.
+//
+// Tiles are blockIdx.x, so a tile may in principle wait on a tile whose
+// workgroup has not been dispatched; every wait is bounded and on timeout the
+// waiter computes the missing aggregate itself (records are idempotent), so
+// the kernel terminates with the right answer under any dispatch order.
+constexpr uint32_t kGroup = 64;
+constexpr uint32_t kSpinLimit = 4096;
+
+__device__ uint64_t group_aggregate(uint64_t* __restrict__ ts, const uint64_t* __restrict__ in,
+                                    const uint64_t* __restrict__ chunk_off, uint64_t nchunks,
+                                    uint32_t tc, uint64_t ntiles, uint64_t g, uint32_t lane) {
+    const uint64_t t0 = g * kGroup;
+    const uint64_t tn = (t0 + kGroup < ntiles) ? kGroup : ntiles - t0;
+    uint64_t st = lane < tn ? load_relaxed_agent(&ts[t0 + lane]) : kFlagAgg;
+    uint64_t miss = ballot64((st >> 62) == 0);
+    while (miss) {
+        const uint32_t k = ctz64(miss);
+        const uint64_t a = tile_aggregate(in, chunk_off, nchunks, tc, t0 + k, lane);
+        if (lane == 0) store_relaxed_agent(&ts[t0 + k], kFlagAgg | a);
+        if (lane == k) st = kFlagAgg | a;
+        miss &= miss - 1;
+    }
+    uint64_t v = st & kValMask;
+    for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+__device__ uint64_t lookback(uint64_t* __restrict__ ts, uint64_t* __restrict__ gs,
+                             uint64_t tile, uint64_t ntiles, uint64_t agg, uint32_t lane,
+                             const uint64_t* __restrict__ in,
+                             const uint64_t* __restrict__ chunk_off, uint64_t nchunks,
+                             uint32_t tc) {
+#if PACK_ABLATE == 1 || PACK_ABLATE == 4
+    return tile * agg;  // timing-only: fake, in-bounds prefix; output is wrong
+#endif
+    const uint64_t g = tile / kGroup;
+    const uint32_t r = (uint32_t)(tile % kGroup);
+    if (lane == 0) store_relaxed_agent(&ts[tile], kFlagAgg | agg);
+    // aggregates of the group's earlier tiles
+    uint64_t within;
+    for (uint32_t spins = 0;;) {
+        const uint64_t st = lane < r ? load_relaxed_agent(&ts[g * kGroup + lane]) : kFlagAgg;
+        const uint64_t miss = ballot64((st >> 62) == 0);
+        if (miss) {
+            if (++spins < kSpinLimit) {
+                __builtin_amdgcn_s_sleep(2);
+                continue;
+            }
+            const uint64_t j = g * kGroup + ctz64(miss);
+            const uint64_t a = tile_aggregate(in, chunk_off, nchunks, tc, j, lane);
+            if (lane == 0) store_relaxed_agent(&ts[j], kFlagAgg | a);
+            continue;
+        }
+        uint64_t v = st & kValMask;
+        for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        within = v;
+        break;
+    }
+    const bool group_last = (r == kGroup - 1) || (tile + 1 == ntiles);
+    const uint64_t gtotal = within + agg;
+    if (group_last && lane == 0) store_relaxed_agent(&gs[g], kFlagAgg | gtotal);
+    // exclusive prefix of the group
+    uint64_t gexcl = 0;
+    int64_t idx = (int64_t)g - 1;
+    for (uint32_t spins = 0; idx >= 0;) {
+        const int64_t j = idx - (int64_t)lane;
+        const uint64_t st = j >= 0 ? load_relaxed_agent(&gs[j]) : kFlagInc;
+        const uint64_t inc = ballot64((st & kFlagInc) != 0);
+        const uint64_t none = ballot64((st >> 62) == 0);
+        const uint32_t first_inc = ctz64(inc);
+        const uint64_t need = first_inc < 64 ? low_mask(first_inc + 1) : ~0ull;
+        if (none & need) {
+            if (++spins < kSpinLimit) {
+                __builtin_amdgcn_s_sleep(2);
+                continue;  // a predecessor group has not published yet
+            }
+            const uint64_t jg = (uint64_t)(idx - (int64_t)ctz64(none & need));
+            const uint64_t a = group_aggregate(ts, in, chunk_off, nchunks, tc, ntiles, jg, lane);
+            if (lane == 0) store_relaxed_agent(&gs[jg], kFlagAgg | a);
+            continue;
+        }
+        uint64_t val = (lane <= first_inc) ? (st & kValMask) : 0;
+        for (uint32_t d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
+        gexcl += val;
+        if (first_inc < 64) break;
+        idx -= 64;
+        spins = 0;
+    }
+    if (group_last && lane == 0) store_relaxed_agent(&gs[g], kFlagInc | (gexcl + gtotal));
+    return gexcl + within;
+}
+
+// One workgroup per tile (tile = blockIdx.x).  8 waves per SIMD (<= 64
+// VGPRs): the step loop is latency-bound, occupancy hides it.
+__global__ void __launch_bounds__(kThreads, 8) __attribute__((amdgpu_num_sgpr(80)))
 pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
             uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
-            uint64_t* __restrict__ out_off, uint64_t* __restrict__ tile_state,
-            uint32_t* __restrict__ ticket) {
+            uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts,
+            uint64_t* __restrict__ gs) {
     __shared__ Smem sm;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint64_t ntiles = (nchunks + tc - 1) / tc;
+    const uint64_t tile = blockIdx.x;
 
-    if (tid == 0) sm.tile = atomicAdd(ticket, 1u);
+    const uint64_t c0 = tile * tc;
+    const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
+    const uint32_t nc = (uint32_t)(c1 - c0);
+    for (uint32_t i = tid; i <= nc; i += kThreads) sm.off[i] = chunk_off[c0 + i];
+    for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
     // compaction selectors: byte r = index of the r-th set bit of the tag
     {
         uint64_t s = 0x0C0C0C0C0C0C0C0Cull;
@@ -409,73 +618,74 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         }
         sm.sel[tid] = s;
     }
-    __syncthreads();
-    const uint32_t tile = sm.tile;
-    const uint64_t c0 = (uint64_t)tile * tc;
-    const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
-    const uint32_t nc = (uint32_t)(c1 - c0);
-    for (uint32_t i = tid; i <= nc; i += kThreads) sm.off[i] = chunk_off[c0 + i];
-    for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
+    uint8_t* region = sm.stage[wave];
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
+    uint8_t* const outa = out - mis;
     __syncthreads();
 
-    // contiguous chunk ranges per wave for the staged path; a range fits when
-    // its 64-word steps fit the register cache
+    // contiguous chunk ranges per wave for the staged path.  Lane s of the
+    // wave describes step s of the range: source word offset and
+    // (nvalid | first << 7 | last << 8 | chunk << 9).
     const uint32_t q = (nc + kWaves - 1) / kWaves;
     const uint32_t wc0 = wave * q < nc ? wave * q : nc;
     const uint32_t wc1 = wc0 + q < nc ? wc0 + q : nc;
-    {
-        uint64_t my_steps = 0;
-        for (uint32_t i = wc0 + lane; i < wc1; i += CAPNP_WAVE)
-            my_steps += (sm.off[i + 1] - sm.off[i] + 63) / 64;
-        for (uint32_t d = 32; d >= 1; d >>= 1) my_steps += __shfl_xor(my_steps, d, 64);
-        if (lane == 0) sm.wave_steps[wave] = my_steps;
+    uint64_t d_src = 0;
+    uint32_t d_meta = 0;
+    uint32_t nsteps = 0;
+    for (uint32_t ci = wc0; ci < wc1; ci++) {
+        const uint64_t woff = lds_u64(&sm.off[ci]);
+        const uint64_t len = lds_u64(&sm.off[ci + 1]) - woff;
+        const uint32_t nst = (uint32_t)((len + 63) / 64);
+        const uint32_t k = lane - nsteps;
+        if (lane >= nsteps && k < nst) {
+            const uint64_t rest = len - 64ull * k;
+            d_src = woff + 64ull * k;
+            d_meta = (uint32_t)(rest < 64 ? rest : 64) | ((k == 0) << 7) |
+                     ((k + 1 == nst) << 8) | ((ci - wc0) << 9);
+        }
+        nsteps += nst;
     }
+    if (lane == 0) sm.wave_steps[wave] = nsteps;
     __syncthreads();
     bool staged = true;
 #pragma unroll
     for (int w = 0; w < kWaves; w++) staged &= sm.wave_steps[w] <= kStageSteps;
     staged = __builtin_amdgcn_readfirstlane((int)staged) != 0;
 
-    uint8_t* region = sm.stage[wave];
-    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
-    uint8_t* const outa = out - mis;
-
     if (staged) {
-        // zero the region, load every step of the range into registers
-        for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
-            *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
+        // load every step of the range into registers, zero the region
         uint64_t cache[kStageSteps];
-        {
-            RangeIter it{wc0, wc1, 0, 0, 0};
 #pragma unroll
-            for (uint32_t s = 0; s < kStageSteps; s++) {
-                it.skip(sm.off);
-                cache[s] = 0;
-                if (it.ci < it.ce) {
-                    if (it.base + lane < it.len) cache[s] = in[it.woff + it.base + lane];
-                    it.base += 64;
-                }
+        for (uint32_t s = 0; s < kStageSteps; s++) {
+            cache[s] = 0;
+            if (s < nsteps) {
+                const uint64_t src = readlane64(d_src, s);
+                const uint32_t nv = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s) & 127u;
+                if (lane < nv) cache[s] = in[src + lane];
             }
         }
+        for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
+            *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
         wave_lds_sync();
         Packer pk;
         uint64_t local = 0;
-        {
-            RangeIter it{wc0, wc1, 0, 0, 0};
 #pragma unroll
-            for (uint32_t s = 0; s < kStageSteps; s++) {
-                it.skip(sm.off);
-                if (it.ci >= it.ce) break;
-                if (it.base == 0) pk.begin(local);
-                const uint32_t nvalid =
-                    (uint32_t)((it.len - it.base) < 64 ? it.len - it.base : 64);
-                const bool last = it.base + 64 >= it.len;
-                pk.step<MODE_STAGE>(cache[s], nvalid, last, lane, region, outa, sm.sel);
-                if (last) {
-                    if (lane == 0) sm.chunk_size[it.ci] = pk.total;
-                    local += pk.total;
-                }
-                it.base += 64;
+        for (uint32_t s = 0; s < kStageSteps; s++) {
+            if (s >= nsteps) break;
+            const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
+            const uint32_t nvalid = meta & 127u;
+            const bool first = (meta >> 7) & 1, last = (meta >> 8) & 1;
+            if (first) pk.begin(local);
+#if PACK_ABLATE == 3 || PACK_ABLATE == 4
+            // timing-only: keep the loads, skip the packing arithmetic
+            asm volatile("" ::"v"(cache[s]));
+            pk.total += 34 * nvalid / 8;
+#else
+            stage_step(pk, cache[s], nvalid, last, lane, region, sm.sel);
+#endif
+            if (last) {
+                if (lane == 0) sm.chunk_size[wc0 + (meta >> 9)] = pk.total;
+                local += pk.total;
             }
         }
         if (lane == 0) sm.wave_bytes[wave] = local;
@@ -485,7 +695,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     }
     __syncthreads();
 
-    // ---- tile scan + decoupled look-back (wave 0)
+    // ---- tile scan + look-back (wave 0)
     if (wave == 0) {
         const uint64_t v = lane < nc ? sm.chunk_size[lane] : 0;
         const uint64_t v2 = (lane + 64 < nc) ? sm.chunk_size[lane + 64] : 0;
@@ -497,36 +707,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         }
         s2 += __shfl(s, 63, 64);
         const uint64_t agg = __shfl(s2, 63, 64);
-        uint64_t excl = 0;
-#if PACK_ABLATE == 1
-        // timing-only: no look-back (fake, in-bounds prefix); output is wrong
-        excl = (uint64_t)tile * agg;
-#else
-        if (tile == 0) {
-            if (lane == 0) store_relaxed_agent(&tile_state[0], kFlagInc | agg);
-        } else {
-            if (lane == 0) store_relaxed_agent(&tile_state[tile], kFlagAgg | agg);
-            int64_t idx = (int64_t)tile - 1;
-            for (;;) {
-                const int64_t j = idx - (int64_t)lane;
-                const uint64_t st = j >= 0 ? load_relaxed_agent(&tile_state[j]) : kFlagInc;
-                const uint64_t inc = ballot64((st & kFlagInc) != 0);
-                const uint64_t none = ballot64((st >> 62) == 0);
-                const uint32_t first_inc = ctz64(inc);
-                const uint64_t need = first_inc < 64 ? low_mask(first_inc + 1) : ~0ull;
-                if (none & need) {
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;  // a predecessor has not published yet
-                }
-                uint64_t val = (lane <= first_inc) ? (st & kValMask) : 0;
-                for (uint32_t d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
-                excl += val;
-                if (first_inc < 64) break;
-                idx -= 64;
-            }
-            if (lane == 0) store_relaxed_agent(&tile_state[tile], kFlagInc | (excl + agg));
-        }
-#endif
+        const uint64_t excl = lookback(ts, gs, tile, ntiles, agg, lane, in, chunk_off, nchunks, tc);
         if (lane < nc) sm.chunk_pos[lane] = excl + s - v;
         if (lane + 64 < nc) sm.chunk_pos[lane + 64] = excl + s2 - v2;
         if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
@@ -551,20 +732,26 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 
 }  // namespace
 
+// Workspace layout (zeroed every call): ts[ntiles] tile records, then
+// gs[ngroups] group records.
+extern "C" size_t capnp_pack_state_bytes(uint64_t nchunks, uint32_t tc) {
+    const uint64_t ntiles = (nchunks + tc - 1) / tc;
+    const uint64_t ngroups = (ntiles + kGroup - 1) / kGroup;
+    return ((ntiles + ngroups) * 8 + 15) & ~size_t(15);
+}
+
 extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_chunk_off,
                                         uint64_t nchunks, uint32_t tc, uint8_t* d_out,
                                         uint64_t out_cap, uint64_t* d_out_off,
-                                        uint64_t* d_tile_state, uint32_t* d_ticket,
-                                        size_t state_bytes, hipStream_t stream) {
+                                        uint64_t* d_state, hipStream_t stream) {
     if (tc == 0 || tc > kMaxTileChunks) return hipErrorInvalidValue;
     const uint64_t ntiles = (nchunks + tc - 1) / tc;
     if (nchunks == 0) {
         return hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), stream);
     }
-    hipError_t e = hipMemsetAsync(d_ticket, 0, state_bytes, stream);
+    hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(nchunks, tc), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(pack_kernel, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream, d_in,
-                       d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_tile_state,
-                       d_ticket);
+    hipLaunchKernelGGL(pack_kernel, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream, d_in, d_chunk_off,
+                       nchunks, tc, d_out, out_cap, d_out_off, d_state, d_state + ntiles);
     return hipGetLastError();
 }

@@ -66,12 +66,6 @@ __device__ __forceinline__ uint64_t expand_word(uint32_t tag, uint64_t packed) {
     return ((uint64_t)rhi << 32) | rlo;
 }
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
-    uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-    uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
-    return ((uint64_t)hi << 32) | lo;
-}
-
 __global__ void __launch_bounds__(kThreads)
 unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
               uint64_t nchunks, uint64_t* __restrict__ out,

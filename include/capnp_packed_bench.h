@@ -23,7 +23,7 @@ capnp_status capnp_gpu_gen_batch(capnp_ctx* ctx, uint64_t* d_words, const uint64
                                  uint32_t kind0, uint32_t pz_thresh, void* stream);
 
 /* capnp_gpu_pack_batch with an explicit tile size (chunks per 256-thread
- * workgroup, 1..128; 0 = default).  Pick ~4096 / mean_chunk_words. */
+ * workgroup, 1..64; 0 = default).  Pick ~1024 / mean_chunk_words. */
 capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
                                         const uint64_t* d_chunk_word_off, size_t nchunks,
                                         uint8_t* d_out, size_t out_cap,

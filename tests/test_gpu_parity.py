@@ -154,7 +154,7 @@ def _check_batch(ctx, words, offs, tc=0):
     assert np.array_equal(back.cpu().numpy().view(np.uint64), words)
 
 
-@pytest.mark.parametrize("tc", [0, 1, 3, 16, 128])
+@pytest.mark.parametrize("tc", [0, 1, 3, 16, 64])
 def test_batch_edge_sizes(ctx, tc):
     sizes = [0, 1, 2, 7, 8, 63, 64, 65, 127, 128, 129, 191, 192, 255, 256, 257, 320, 511, 512,
              513, 1000, 0, 0, 5]
