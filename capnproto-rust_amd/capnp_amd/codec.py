@@ -133,13 +133,14 @@ class Context:
         _check(st, self._h)
 
 
-def tile_chunks_for(total_words, nchunks):
-    """Chunks per 256-thread pack workgroup: ~1024 words per tile, i.e. one
-    256-word staged range per wave (pack.hip kStageWords)."""
+def tile_chunks_for(total_words, nchunks, lib=None):
+    """Chunks per 256-thread pack workgroup: about capnp_pack_tile_words()
+    words per tile, i.e. one staged range per wave (pack.hip kStageSteps)."""
     if nchunks <= 0:
         return 16
+    tw = (lib or _lib.lib()).capnp_pack_tile_words()
     mean = max(total_words / nchunks, 1.0)
-    return int(max(1, min(64, 1024 // mean)))
+    return int(max(1, min(64, tw // mean)))
 
 
 _default = {}

@@ -17,6 +17,7 @@
 
 extern "C" hipError_t capnp_launch_pack(const uint64_t*, const uint64_t*, uint64_t, uint32_t,
                                         uint8_t*, uint64_t, uint64_t*, uint64_t*, hipStream_t);
+extern "C" uint32_t capnp_pack_tile_words(void);
 extern "C" size_t capnp_pack_state_bytes(uint64_t, uint32_t);
 extern "C" hipError_t capnp_launch_unpack(const uint8_t*, const uint64_t*, uint64_t, uint64_t*,
                                           const uint64_t*, int32_t*, uint64_t*, hipStream_t);
@@ -121,7 +122,7 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
 uint32_t tile_chunks_for(uint64_t total_words, size_t n) {
     if (n == 0) return kDefaultTileChunks;
     const double mean = (double)total_words / (double)n;
-    double t = 1024.0 / std::max(mean, 1.0);  // ~256 words per wave (staged path)
+    double t = (double)capnp_pack_tile_words() / std::max(mean, 1.0);  // staged path size
     uint32_t tc = (uint32_t)std::max(1.0, std::min(t, (double)kMaxTileChunks));
     return tc;
 }

@@ -52,16 +52,19 @@ constexpr uint32_t kRingMask = kRing - 1;
 constexpr int kMaxTileChunks = 64;
 constexpr uint32_t kZeroAhead = 1024;      // ring bytes zeroed per refill
 constexpr uint32_t kStepMax = 64 * 10 + 16;
-constexpr uint32_t kRegionBytes = 4096;    // per-wave LDS region (= ring size)
 
 // Staged path capacity: kStageSteps steps of 64 words per wave.
-constexpr uint32_t kStageSteps = 4;
+#ifndef PACK_STAGE_STEPS
+#define PACK_STAGE_STEPS 4
+#endif
+constexpr uint32_t kStageSteps = PACK_STAGE_STEPS;
 constexpr uint32_t kStageWords = 64 * kStageSteps;
 // >= sum of per-chunk bounds for <= 32 chunks totalling kStageWords words,
 // plus the 32 bytes copy_out may read past the end
 constexpr uint32_t kStageBytes = 8 * kStageWords + kStageWords / 2 + 3 * 32 + 64;
 constexpr uint32_t kRegion = (kStageBytes + 32 + 15) & ~15u;
-static_assert(kRegion <= kRegionBytes && kRing <= kRegionBytes, "staging region too small");
+// per-wave LDS region: the staged bytes, or the streaming path's flush ring
+constexpr uint32_t kRegionBytes = kRegion > kRing ? kRegion : kRing;
 
 constexpr uint64_t kFlagAgg = 1ull << 62;  // tile aggregate available
 constexpr uint64_t kFlagInc = 2ull << 62;  // tile inclusive prefix available
@@ -731,6 +734,10 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 }
 
 }  // namespace
+
+// Words per tile the staged path is sized for (kWaves waves x kStageSteps
+// 64-word steps); the host picks chunks_per_tile ~ this / mean chunk words.
+extern "C" uint32_t capnp_pack_tile_words(void) { return kWaves * 64 * kStageSteps; }
 
 // Workspace layout (zeroed every call): ts[ntiles] tile records, then
 // gs[ngroups] group records.

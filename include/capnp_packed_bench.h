@@ -30,6 +30,10 @@ capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
                                         uint64_t* d_out_byte_off, uint32_t chunks_per_tile,
                                         void* stream);
 
+/* Words per pack tile the staged path is sized for (4 waves x steps of 64
+ * words); chunks_per_tile ~ this / mean chunk words. */
+uint32_t capnp_pack_tile_words(void);
+
 /* Pre-sizes the context workspace for batches of up to max_chunks chunks so
  * that later calls allocate nothing (required before HIP graph capture). */
 capnp_status capnp_ctx_reserve(capnp_ctx* ctx, size_t max_chunks);

@@ -25,6 +25,7 @@ def load(path):
     L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, u32, vp]
     L.capnp_gpu_unpack_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.capnp_ctx_reserve.argtypes = [vp, sz]
+    L.capnp_pack_tile_words.restype = C.c_uint32
     st = C.c_int(0)
     ctx = L.capnp_ctx_create(0, C.byref(st))
     assert ctx, st.value
@@ -57,7 +58,6 @@ def main():
     packed = ref_out.clone()
     back = torch.empty_like(words)
     status = torch.empty(n, dtype=torch.int32, device="cuda")
-    tc = a.tc or tile_chunks_for(n * cw, n)
     stream = torch.cuda.current_stream()
     variants = [(os.path.basename(p), *load(p)) for p in libs]
     for _, L, h in variants:
@@ -72,6 +72,7 @@ def main():
                 e0.record(stream)
                 for _ in range(a.iters):
                     if kind == "pack":
+                        tc = a.tc or tile_chunks_for(n * cw, n, L)
                         L.capnp_gpu_pack_batch_tuned(h, P(words.data_ptr()), P(offs.data_ptr()), n,
                                                      P(out.data_ptr()), cap, P(oo.data_ptr()), tc,
                                                      P(stream.cuda_stream))
