@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--chunks", type=int, default=1 << 20, help="segments per GPU")
     ap.add_argument("--chunk-words", type=int, default=128)
     ap.add_argument("--workload", default="config2", choices=["config2", "config3"])
-    ap.add_argument("--cpu-sample-chunks", type=int, default=1 << 16)
+    ap.add_argument("--cpu-sample-chunks", type=int, default=1 << 18)
+    ap.add_argument("--cpu-reps", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time host->device->host")
@@ -61,27 +62,37 @@ def cpu_baseline(args):
         min(16, os.cpu_count() or 1)
     offs = np.arange(0, (n + 1) * cw, cw, dtype=np.uint64)
     words = O.gen_fill(offs, kind0=0, pz=PZ[args.workload])
-    best = None
-    for _ in range(3):
-        t0 = time.perf_counter()
-        st, packed, poffs = O.pack_batch(words, offs, threads=threads)
-        t1 = time.perf_counter()
-        back, status, _ = O.unpack_batch(packed, poffs, offs, threads=threads)
-        t2 = time.perf_counter()
-        assert st == 0 and (status == 0).all() and np.array_equal(back, words)
-        dt = t2 - t0
-        if best is None or dt < best[0]:
-            best = (dt, t1 - t0, t2 - t1)
+
+    def timed(nn, thr, reps):
+        w, o = words[:nn * cw], offs[:nn + 1]
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            st, packed, poffs = O.pack_batch(w, o, threads=thr)
+            t1 = time.perf_counter()
+            back, status, _ = O.unpack_batch(packed, poffs, o, threads=thr)
+            t2 = time.perf_counter()
+            assert st == 0 and (status == 0).all() and np.array_equal(back, w)
+            if best is None or t2 - t0 < best[0]:
+                best = (t2 - t0, t1 - t0, t2 - t1)
+        return best
+
+    best = timed(n, threads, args.cpu_reps)
+    n1 = max(1, n // 16)
+    one = timed(n1, 1, 2)
     u = n * cw * 8
+    u1 = n1 * cw * 8
     return {
         "value": round(u / best[0] / GiB, 3),
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
         "sample": f"{n} segments x {cw * 8} B ({u / GiB:.3f} GiB) of the same generator, "
-                  f"pack+unpack, best of 3, {threads} threads",
+                  f"pack+unpack, best of {args.cpu_reps}, {threads} threads "
+                  f"(oracle/packed_oracle.c, gcc -O3)",
         "pack_gibps": round(u / best[1] / GiB, 3),
         "unpack_gibps": round(u / best[2] / GiB, 3),
+        "single_thread_gibps": round(u1 / one[0] / GiB, 3),
     }
 
 
