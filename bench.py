@@ -110,7 +110,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from capnp_amd import Context, tile_chunks_for
+    from capnp_amd import Context, tile_chunks_for, unpack_tile_chunks_for
     ctx = Context(local)
     n, cw = args.chunks, args.chunk_words
     total_words = n * cw
@@ -124,6 +124,7 @@ def main():
     status = torch.empty(n, dtype=torch.int32, device=dev)
     consumed = torch.empty(n, dtype=torch.int64, device=dev)
     tc = tile_chunks_for(total_words, n)
+    utc = unpack_tile_chunks_for(total_words, n)
     ctx.reserve(n)
     stream = torch.cuda.current_stream()
 
@@ -136,7 +137,7 @@ def main():
         ctx.pack_batch_into(words, offs, packed, poffs, chunks_per_tile=tc)
         if record:
             e[1].record(stream)
-        ctx.unpack_batch_into(packed, poffs, offs, back, status, consumed)
+        ctx.unpack_batch_into(packed, poffs, offs, back, status, consumed, chunks_per_tile=utc)
         if record:
             e[2].record(stream)
             ev.append(e)
@@ -261,7 +262,8 @@ def end_to_end(ctx, torch, words, offs, n, cw, tc, dev):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         d_packed[:P].copy_(h_packed[:P], non_blocking=True)
-        ctx.unpack_batch_into(d_packed, d_poffs, offs, d_back, status)
+        ctx.unpack_batch_into(d_packed, d_poffs, offs, d_back, status,
+                              chunks_per_tile=unpack_tile_chunks_for(n * cw, n))
         h_back.copy_(d_back, non_blocking=True)
         torch.cuda.synchronize()
         t2 = time.perf_counter()

@@ -27,7 +27,7 @@ EXPORTS = [
     "capnp_pack", "capnp_unpack", "capnp_pack_batch_host", "capnp_unpack_batch_host",
     "capnp_packed_write_message", "capnp_packed_read_message",
     "capnp_packed_read_message_no_alloc", "capnp_gpu_gen_batch", "capnp_gpu_pack_batch_tuned",
-    "capnp_ctx_reserve", "capnp_pack_tile_words",
+    "capnp_ctx_reserve", "capnp_pack_tile_words", "capnp_gpu_unpack_batch_tuned",
 ]
 
 
@@ -77,6 +77,7 @@ def lib():
     L.capnp_gpu_pack_batch.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp]
     L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, u32, vp]
     L.capnp_gpu_unpack_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    L.capnp_gpu_unpack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, C.c_uint32, vp]
     L.capnp_gpu_gen_batch.argtypes = [vp, vp, vp, sz, u64, vp, u32, u32, vp]
     L.capnp_ctx_reserve.argtypes = [vp, sz]
     L.capnp_pack_tile_words.argtypes = []

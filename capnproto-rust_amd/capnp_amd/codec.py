@@ -92,11 +92,12 @@ class Context:
         _check(st, self._h)
 
     def unpack_batch_into(self, packed, in_byte_off, out_word_off, words, status,
-                          consumed=None, stream=None):
+                          consumed=None, chunks_per_tile=0, stream=None):
+        """Enqueue UNPACK; chunks_per_tile 0 = library default (32)."""
         n = in_byte_off.numel() - 1
-        st = _lib.lib().capnp_gpu_unpack_batch(self._h, _ptr(packed), _ptr(in_byte_off), n,
-                                               _ptr(words), _ptr(out_word_off), _ptr(status),
-                                               _ptr(consumed), self._stream(stream))
+        st = _lib.lib().capnp_gpu_unpack_batch_tuned(
+            self._h, _ptr(packed), _ptr(in_byte_off), n, _ptr(words), _ptr(out_word_off),
+            _ptr(status), _ptr(consumed), int(chunks_per_tile), self._stream(stream))
         _check(st, self._h)
 
     def pack_batch(self, words, chunk_word_off, chunks_per_tile=0):
@@ -114,7 +115,7 @@ class Context:
         total = int(out_off[-1].item())
         return out[:total], out_off
 
-    def unpack_batch(self, packed, in_byte_off, out_word_off):
+    def unpack_batch(self, packed, in_byte_off, out_word_off, chunks_per_tile=0):
         import torch
         n = in_byte_off.numel() - 1
         total = int(out_word_off[-1].item()) if n else 0
@@ -122,7 +123,8 @@ class Context:
         words = torch.empty(max(total, 1), dtype=torch.int64, device=dev)
         status = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
         consumed = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
-        self.unpack_batch_into(packed, in_byte_off, out_word_off, words, status, consumed)
+        self.unpack_batch_into(packed, in_byte_off, out_word_off, words, status, consumed,
+                               chunks_per_tile)
         return words[:total], status[:n], consumed[:n]
 
     def gen_batch(self, words, offs, kind=0, pz_thresh=0, kinds=None, id0=0, stream=None):
@@ -141,6 +143,15 @@ def tile_chunks_for(total_words, nchunks, lib=None):
     tw = (lib or _lib.lib()).capnp_pack_tile_words()
     mean = max(total_words / nchunks, 1.0)
     return int(max(1, min(64, tw // mean)))
+
+
+def unpack_tile_chunks_for(total_words, nchunks):
+    """Chunks per unpack workgroup: about 4096 output words per tile (the
+    staged path's descriptor capacity, unpack.hip kTileWords)."""
+    if nchunks <= 0:
+        return 32
+    mean = max(total_words / nchunks, 1.0)
+    return int(max(1, min(256, 4096 // mean)))
 
 
 _default = {}

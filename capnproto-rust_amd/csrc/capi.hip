@@ -19,8 +19,9 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t*, const uint64_t*, uint64
                                         uint8_t*, uint64_t, uint64_t*, uint64_t*, hipStream_t);
 extern "C" uint32_t capnp_pack_tile_words(void);
 extern "C" size_t capnp_pack_state_bytes(uint64_t, uint32_t);
-extern "C" hipError_t capnp_launch_unpack(const uint8_t*, const uint64_t*, uint64_t, uint64_t*,
-                                          const uint64_t*, int32_t*, uint64_t*, hipStream_t);
+extern "C" hipError_t capnp_launch_unpack(const uint8_t*, const uint64_t*, uint64_t, uint32_t,
+                                          uint64_t*, const uint64_t*, int32_t*, uint64_t*,
+                                          hipStream_t);
 extern "C" hipError_t capnp_launch_gen(uint64_t*, const uint64_t*, uint64_t, uint64_t,
                                        const uint8_t*, uint32_t, uint32_t, hipStream_t);
 extern "C" hipError_t capnp_launch_frame(const uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t,
@@ -253,15 +254,34 @@ capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
                           d_out_byte_off, chunks_per_tile, pick(ctx, stream));
 }
 
+static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
+                                     const uint64_t* d_in_byte_off, size_t nchunks,
+                                     uint64_t* d_words, const uint64_t* d_out_word_off,
+                                     int32_t* d_status, uint64_t* d_consumed, uint32_t tc,
+                                     void* stream) {
+    if (!ctx || (nchunks && (!d_in_byte_off || !d_out_word_off || !d_status)))
+        return CAPNP_E_INVALID_ARGUMENT;
+    if (tc > 256) return CAPNP_E_INVALID_ARGUMENT;
+    HIP_TRY(capnp_launch_unpack(d_packed, d_in_byte_off, nchunks, tc, d_words, d_out_word_off,
+                                d_status, d_consumed, pick(ctx, stream)));
+    return CAPNP_OK;
+}
+
 capnp_status capnp_gpu_unpack_batch(capnp_ctx* ctx, const uint8_t* d_packed,
                                     const uint64_t* d_in_byte_off, size_t nchunks,
                                     uint64_t* d_words, const uint64_t* d_out_word_off,
                                     int32_t* d_status, uint64_t* d_consumed, void* stream) {
-    if (!ctx || (nchunks && (!d_in_byte_off || !d_out_word_off || !d_status)))
-        return CAPNP_E_INVALID_ARGUMENT;
-    HIP_TRY(capnp_launch_unpack(d_packed, d_in_byte_off, nchunks, d_words, d_out_word_off,
-                                d_status, d_consumed, pick(ctx, stream)));
-    return CAPNP_OK;
+    return unpack_batch_dev(ctx, d_packed, d_in_byte_off, nchunks, d_words, d_out_word_off,
+                            d_status, d_consumed, 0, stream);
+}
+
+capnp_status capnp_gpu_unpack_batch_tuned(capnp_ctx* ctx, const uint8_t* d_packed,
+                                          const uint64_t* d_in_byte_off, size_t nchunks,
+                                          uint64_t* d_words, const uint64_t* d_out_word_off,
+                                          int32_t* d_status, uint64_t* d_consumed,
+                                          uint32_t chunks_per_tile, void* stream) {
+    return unpack_batch_dev(ctx, d_packed, d_in_byte_off, nchunks, d_words, d_out_word_off,
+                            d_status, d_consumed, chunks_per_tile, stream);
 }
 
 capnp_status capnp_gpu_gen_batch(capnp_ctx* ctx, uint64_t* d_words, const uint64_t* d_offs,
@@ -321,7 +341,7 @@ capnp_status capnp_unpack_batch_host(capnp_ctx* ctx, const uint8_t* packed,
     if (ie > ib) HIP_TRY(hipMemcpyAsync(d + o_in, packed + ib, ie - ib, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d + o_ri, ri.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d + o_ro, ro.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(capnp_launch_unpack(d + o_in, reinterpret_cast<uint64_t*>(d + o_ri), n,
+    HIP_TRY(capnp_launch_unpack(d + o_in, reinterpret_cast<uint64_t*>(d + o_ri), n, 0,
                                 reinterpret_cast<uint64_t*>(d + o_out),
                                 reinterpret_cast<uint64_t*>(d + o_ro),
                                 reinterpret_cast<int32_t*>(d + o_st),
@@ -416,7 +436,7 @@ static capnp_status read_body(capnp_ctx* ctx, const FrameResult& fr, uint8_t* ho
     if (st != CAPNP_OK) return st;
     uint8_t* d = ctx->d_body;
     hipStream_t s = ctx->stream;
-    HIP_TRY(capnp_launch_unpack(ctx->d_stage, ctx->d_frame->body_in_off, 1,
+    HIP_TRY(capnp_launch_unpack(ctx->d_stage, ctx->d_frame->body_in_off, 1, 0,
                                 reinterpret_cast<uint64_t*>(d), ctx->d_frame->body_out_off,
                                 reinterpret_cast<int32_t*>(d + o_st),
                                 reinterpret_cast<uint64_t*>(d + o_st + 16), s));

@@ -2,20 +2,26 @@
 // under read_exact (capnp/src/serialize_packed.rs:80-228, io.rs:16-31).
 //
 // The decode of one chunk is a serial chain: the position of tag k+1 depends
-// on the value of tag k.  Parallelism therefore comes from independent
-// chunks (the batch carries a side-band index: each chunk's packed range and
-// unpacked length, produced by the encoder's offsets):
+// on the value of tag k.  Parallelism comes from independent chunks (the
+// batch carries a side-band index: each chunk's packed range and unpacked
+// length, produced by the encoder's offsets).
 //
-//   walk       lane l of a wave owns chunk 64g + l and follows its tag chain
-//              for the next 64 output words, writing one 16-bit descriptor
-//              per head word (kind + packed position relative to the round's
-//              base) into an LDS table desc[chunk][word];
-//   expand     the whole wave then takes the chunks one at a time, lane =
-//              output word: the head covering each word is the highest
-//              descriptor at or below it (ballot + clz), the word is rebuilt
-//              from the tag and its non-zero bytes (v_perm with a SWAR rank
-//              selector), zero-run words are 0, literal-run words are copied;
-//              every chunk's 64 words leave as one 512-byte coalesced store.
+// Staged path (one 256-thread workgroup per tile of `tc` consecutive chunks
+// whose packed bytes and output words fit the LDS tables):
+//   stage      the tile's packed bytes (one contiguous range) are copied into
+//              LDS with aligned 16-byte loads;
+//   walk       one thread per chunk follows the tag chain in LDS (~50-cycle
+//              hops instead of L2/MALL round trips) and records, per output
+//              word, a descriptor for every record head plus a continuation
+//              entry wherever a run covers a 64-word group boundary;
+//   expand     lane = output word of the tile (the tile's words are one
+//              contiguous range): the covering descriptor is the highest entry
+//              at or below the lane in its 64-word group (ballot + clz), the
+//              word is rebuilt from LDS (v_perm with a SWAR rank selector) and
+//              leaves in coalesced 512-byte stores.
+// Global path (tiles that do not fit): lane = chunk walks the chain in
+// global memory 64 output words at a time, then the wave expands chunk by
+// chunk (the round-1 kernel).
 //
 // Status per chunk follows the reference exactly (first error in stream
 // order): PrematureEndOfPackedInput when a tag, a tag's bytes or a run count
@@ -66,18 +72,15 @@ __device__ __forceinline__ uint64_t expand_word(uint32_t tag, uint64_t packed) {
     return ((uint64_t)rhi << 32) | rlo;
 }
 
-__global__ void __launch_bounds__(kThreads)
-unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-              uint64_t nchunks, uint64_t* __restrict__ out,
-              const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
-              uint64_t* __restrict__ consumed) {
-    __shared__ alignas(16) uint16_t desc_all[kWaves][CAPNP_WAVE][CAPNP_WAVE];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = threadIdx.x >> 6;
-    uint16_t(*desc)[CAPNP_WAVE] = desc_all[wave];
-
-    const uint64_t c = ((uint64_t)blockIdx.x * kWaves + wave) * CAPNP_WAVE + lane;
-    const bool have = c < nchunks;
+// Global path: lane l of the wave decodes chunk c0 + l (c < c_end); `desc` is
+// this wave's 64 x 64 descriptor table (8 KiB of LDS).
+__device__ void unpack_global(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                              uint64_t c0, uint64_t c_end, uint64_t* __restrict__ out,
+                              const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
+                              uint64_t* __restrict__ consumed, uint16_t (*desc)[CAPNP_WAVE],
+                              uint32_t lane) {
+    const uint64_t c = c0 + lane;
+    const bool have = c < c_end;
     uint64_t p = 0, in_end = 0, n = 0, obase = 0;
     if (have) {
         p = in_off[c];
@@ -197,16 +200,193 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
     }
 }
 
+constexpr uint32_t kMaxTileChunks = kWaves * CAPNP_WAVE;
+
+// ---------------------------------------------------------------------------
+// Staged path.
+
+constexpr uint32_t kTileBytes = 20000;   // LDS capacity for a tile's packed bytes
+constexpr uint32_t kTileWords = 4096;    // descriptor capacity (output words)
+constexpr uint32_t kStageChunks = 64;    // walkers: one lane of wave 0 per chunk
+
+// Descriptor of an output word (u16): the LDS position of its record's tag
+// for a record head (the tag byte gives the kind), kContLit | position of
+// the raw word for a literal run crossing a 64-word group boundary, kContZero
+// for a zero run crossing one, kNone otherwise.
+constexpr uint16_t kNone = 0xFFFF;
+constexpr uint16_t kContZero = 0xFFFE;
+constexpr uint16_t kContLit = 0x8000;
+
+struct StageSmem {
+    alignas(16) uint8_t bytes[kTileBytes + 16];
+    alignas(16) uint16_t dpos[kTileWords];
+};
+
+union USmem {
+    StageSmem st;
+    uint16_t desc[kWaves][CAPNP_WAVE][CAPNP_WAVE];  // global path
+};
+
+// 8 bytes at LDS byte position `pos` (two aligned 8-byte reads, funnel).
+__device__ __forceinline__ uint64_t lds_load8(const uint8_t* b, uint32_t pos) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(b + (pos & ~7u));
+    const uint32_t s = pos & 7u;
+    const uint64_t lo = q[0], hi = q[1];
+    return s ? (lo >> (8 * s)) | (hi << (64 - 8 * s)) : lo;
+}
+
+// Exact status of a record that failed the fast check in walk_chunk, in the
+// reference's order (serialize_packed.rs:109-145, :157-205).
+__device__ __forceinline__ int32_t record_error(uint32_t p, uint32_t q, uint32_t pe, bool run,
+                                                bool isf, uint32_t cnt, uint32_t left) {
+    if (p >= pe || q > pe || (run && q >= pe)) return ST_PREMATURE;
+    if (cnt > left) return ST_NOT_CLEAN;
+    if (isf && pe - q - 1 < 8 * cnt) return ST_FAILED_FILL;
+    return ST_OK;
+}
+
+// Walks one chunk: bytes [p, pe) of the staged tile, output words [wb, wb+n)
+// of the tile.  One hop per record: the tag and both possible count bytes
+// (p+1 for 0x00, p+9 for 0xFF) are read together, one check covers every
+// error, and only continuation entries branch.
+__device__ __forceinline__ void walk_chunk(StageSmem& S, uint32_t p, uint32_t pe, uint32_t wb,
+                                           uint32_t n, int32_t& st, uint32_t& used) {
+    const uint32_t p0 = p;
+    uint32_t w = 0;
+    st = ST_OK;
+    if (n > 0 && p == pe) st = ST_FAILED_FILL;  // read() returns Ok(0)
+    bool go = n > 0 && st == ST_OK;
+    while (go) {
+        // three independent reads in flight together (the empty asm keeps
+        // the compiler from reading the count byte after the tag, in a branch)
+        uint32_t tag = S.bytes[p];
+        uint32_t b1 = S.bytes[p + 1];
+        uint32_t b9 = S.bytes[p + 9];
+        asm volatile("" : "+v"(tag), "+v"(b1), "+v"(b9));
+        const uint32_t q = p + 1 + __builtin_popcount(tag);
+        const bool isz = tag == 0, isf = tag == 0xFF, run = isz || isf;
+        const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+        const uint32_t end = run ? q + 1 + (isf ? 8 * cnt : 0u) : q;
+        const uint32_t left = n - w - 1;
+        if (p < pe && end <= pe && cnt <= left) {
+            S.dpos[wb + w] = (uint16_t)p;
+            const uint32_t r0 = wb + w + 1, r1 = r0 + cnt;
+            uint32_t bnd = (r0 + 63) & ~63u;
+            if (bnd < r1) {  // the run covers a group boundary
+                for (; bnd < r1; bnd += 64)
+                    S.dpos[bnd] = isz ? kContZero
+                                      : (uint16_t)(kContLit | (q + 1 + 8 * (bnd - r0)));
+            }
+            w += 1 + cnt;
+            p = end;
+            go = w < n;
+        } else {
+            st = record_error(p, q, pe, run, isf, cnt, left);
+            go = false;
+        }
+    }
+    used = st == ST_OK ? p - p0 : (st == ST_FAILED_FILL ? pe - p0 : 0);
+}
+
+__global__ void __launch_bounds__(kThreads)
+unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+              uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
+              const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
+              uint64_t* __restrict__ consumed) {
+    __shared__ USmem sm;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint64_t ca = (uint64_t)blockIdx.x * tc;
+    const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
+    const uint32_t nc = (uint32_t)(cb - ca);
+    const uint64_t B0 = uniform64(in_off[ca]), B1 = uniform64(in_off[cb]);
+    const uint64_t W0 = uniform64(out_off[ca]), W1 = uniform64(out_off[cb]);
+    const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
+    const bool fits = nc <= kStageChunks && B1 - B0 <= kTileBytes - off0 &&
+                      W1 - W0 <= kTileWords;
+    if (!fits) {
+        for (uint64_t c0 = ca + (uint64_t)wave * CAPNP_WAVE; c0 < cb;
+             c0 += (uint64_t)kWaves * CAPNP_WAVE)
+            unpack_global(in, in_off, c0, cb, out, out_off, status, consumed, sm.desc[wave],
+                          lane);
+        return;
+    }
+    StageSmem& S = sm.st;
+    const uint32_t nbytes = (uint32_t)(B1 - B0) + off0;
+    const uint32_t Wt = (uint32_t)(W1 - W0);
+    // stage the tile's packed bytes: every load issued before any LDS write
+    // (aligned 16-byte blocks holding at least one byte of the range never
+    // cross a page), and clear the descriptors
+    {
+        constexpr uint32_t kLoads = (kTileBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
+        const uint4* src = reinterpret_cast<const uint4*>(in + B0 - off0);
+        uint4* dst = reinterpret_cast<uint4*>(S.bytes);
+        const uint32_t nblk = (nbytes + 15) / 16;
+        uint4 r[kLoads];
+#pragma unroll
+        for (uint32_t k = 0; k < kLoads; k++) {
+            const uint32_t idx = tid + k * kThreads;
+            r[k] = nblk ? src[idx < nblk ? idx : nblk - 1] : make_uint4(0, 0, 0, 0);
+        }
+        uint4* dd = reinterpret_cast<uint4*>(S.dpos);
+        const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
+        for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
+#pragma unroll
+        for (uint32_t k = 0; k < kLoads; k++)
+            if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
+    }
+    __syncthreads();
+    // walk: lane j of wave 0 follows chunk j
+    if (tid < nc) {
+        const uint64_t c = ca + tid;
+        const uint64_t gp = in_off[c], ge = in_off[c + 1];
+        const uint64_t ow = out_off[c], oe = out_off[c + 1];
+        int32_t st;
+        uint32_t used;
+        walk_chunk(S, (uint32_t)(gp - B0) + off0, (uint32_t)(ge - B0) + off0,
+                   (uint32_t)(ow - W0), (uint32_t)(oe - ow), st, used);
+        status[c] = st;
+        if (consumed) consumed[c] = used;
+    }
+    __syncthreads();
+    // expand: lane = output word; 64-word groups interleaved over waves
+    for (uint32_t g = wave; g * CAPNP_WAVE < Wt; g += kWaves) {
+        const uint32_t i = g * CAPNP_WAVE + lane;
+        const bool valid = i < Wt;
+        const uint32_t d = valid ? S.dpos[i] : kNone;
+        const uint64_t hm = ballot64(d != kNone) & low_mask(lane + 1);
+        uint64_t word = 0;
+        if (hm) {  // (no entry only after a decode error: output unspecified)
+            const uint32_t h = 63u - (uint32_t)__builtin_clzll(hm);
+            const uint32_t dh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(h << 2), (int)d);
+            if (dh == kContZero) {
+                word = 0;
+            } else if (dh & kContLit) {
+                word = lds_load8(S.bytes, (dh & 0x7FFFu) + 8 * (lane - h));
+            } else {
+                const uint32_t tag = S.bytes[dh];
+                if (tag == 0xFF)
+                    word = lds_load8(S.bytes, h == lane ? dh + 1 : dh + 10 + 8 * (lane - h - 1));
+                else if (tag != 0 && h == lane)
+                    word = expand_word(tag, lds_load8(S.bytes, dh + 1));
+            }
+        }
+        if (valid) out[W0 + i] = word;
+    }
+}
+
 }  // namespace
 
 extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d_in_off,
-                                          uint64_t nchunks, uint64_t* d_out,
+                                          uint64_t nchunks, uint32_t tc, uint64_t* d_out,
                                           const uint64_t* d_out_off, int32_t* d_status,
                                           uint64_t* d_consumed, hipStream_t stream) {
     if (nchunks == 0) return hipSuccess;
-    const uint64_t per_block = (uint64_t)kWaves * CAPNP_WAVE;
-    const uint64_t blocks = (nchunks + per_block - 1) / per_block;
+    if (tc == 0) tc = 32;
+    if (tc > kMaxTileChunks) return hipErrorInvalidValue;  // global path: 4 waves x 64
+    const uint64_t blocks = (nchunks + tc - 1) / tc;
     hipLaunchKernelGGL(unpack_kernel, dim3((uint32_t)blocks), dim3(kThreads), 0, stream, d_in,
-                       d_in_off, nchunks, d_out, d_out_off, d_status, d_consumed);
+                       d_in_off, nchunks, tc, d_out, d_out_off, d_status, d_consumed);
     return hipGetLastError();
 }

@@ -24,6 +24,8 @@ def load(path):
     L.capnp_ctx_create.restype = vp
     L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, u32, vp]
     L.capnp_gpu_unpack_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    if hasattr(L, "capnp_gpu_unpack_batch_tuned"):
+        L.capnp_gpu_unpack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, u32, vp]
     L.capnp_ctx_reserve.argtypes = [vp, sz]
     L.capnp_pack_tile_words.restype = C.c_uint32
     st = C.c_int(0)
@@ -40,10 +42,11 @@ def main():
     ap.add_argument("--chunks", type=int, default=1 << 20)
     ap.add_argument("--chunk-words", type=int, default=128)
     ap.add_argument("--tc", type=int, default=0)
+    ap.add_argument("--utc", type=int, default=0, help="unpack chunks per tile")
     ap.add_argument("libs", nargs="*")
     a = ap.parse_args()
     import torch
-    from capnp_amd import Context, tile_chunks_for
+    from capnp_amd import Context, tile_chunks_for, unpack_tile_chunks_for
     libs = a.libs or ([os.path.join(ROOT, "capnproto-rust_amd/capnp_amd/libcapnp_packed.so")] +
                       sorted(glob.glob(os.path.join(ROOT, "capnproto-rust_amd/build/abl/*.so"))))
     n, cw = a.chunks, a.chunk_words
@@ -77,9 +80,17 @@ def main():
                                                      P(out.data_ptr()), cap, P(oo.data_ptr()), tc,
                                                      P(stream.cuda_stream))
                     else:
-                        L.capnp_gpu_unpack_batch(h, P(packed.data_ptr()), P(ref_oo.data_ptr()), n,
-                                                 P(back.data_ptr()), P(offs.data_ptr()),
-                                                 P(status.data_ptr()), None, P(stream.cuda_stream))
+                        if hasattr(L, "capnp_gpu_unpack_batch_tuned"):
+                            L.capnp_gpu_unpack_batch_tuned(
+                                h, P(packed.data_ptr()), P(ref_oo.data_ptr()), n,
+                                P(back.data_ptr()), P(offs.data_ptr()), P(status.data_ptr()),
+                                None, a.utc or unpack_tile_chunks_for(n * cw, n),
+                                P(stream.cuda_stream))
+                        else:
+                            L.capnp_gpu_unpack_batch(h, P(packed.data_ptr()), P(ref_oo.data_ptr()),
+                                                     n, P(back.data_ptr()), P(offs.data_ptr()),
+                                                     P(status.data_ptr()), None,
+                                                     P(stream.cuda_stream))
                 e1.record(stream)
                 e1.synchronize()
                 res[name][kind].append(e0.elapsed_time(e1) / a.iters)

@@ -133,7 +133,7 @@ def test_message_round_trip_vs_oracle(ctx):
 
 
 # ---------------------------------------------------------------- batch API
-def _check_batch(ctx, words, offs, tc=0):
+def _check_batch(ctx, words, offs, tc=0, utcs=(0, 1, 7, 256)):
     st, ref, ref_offs = O.pack_batch(words, offs)
     assert st == 0
     dw, do = dev(words), dev(offs)
@@ -147,11 +147,14 @@ def _check_batch(ctx, words, offs, tc=0):
         c = int(np.searchsorted(ref_offs, bad, side="right") - 1)
         raise AssertionError(f"packed bytes differ at {bad} (chunk {c}, words "
                              f"{offs[c + 1] - offs[c]})")
-    back, status, consumed = ctx.unpack_batch(packed, poffs, do)
-    torch.cuda.synchronize()
-    assert (status.cpu().numpy() == 0).all()
-    assert np.array_equal(consumed.cpu().numpy().view(np.uint64), np.diff(ref_offs))
-    assert np.array_equal(back.cpu().numpy().view(np.uint64), words)
+    # unpack tile sizes: staged (LDS) path, tiny tiles, and tiles that overflow
+    # the LDS tables (global path)
+    for utc in utcs:
+        back, status, consumed = ctx.unpack_batch(packed, poffs, do, chunks_per_tile=utc)
+        torch.cuda.synchronize()
+        assert (status.cpu().numpy() == 0).all(), utc
+        assert np.array_equal(consumed.cpu().numpy().view(np.uint64), np.diff(ref_offs)), utc
+        assert np.array_equal(back.cpu().numpy().view(np.uint64), words), utc
 
 
 @pytest.mark.parametrize("tc", [0, 1, 3, 16, 64])
@@ -247,17 +250,19 @@ def test_unpack_error_statuses_vs_oracle(ctx):
     packed = np.frombuffer(b"".join(packed_chunks), np.uint8)
     ref_words, ref_st, ref_used = O.unpack_batch(packed, in_offs, out_offs)
     pk = torch.from_numpy(packed.copy()).cuda() if len(packed) else torch.zeros(1, dtype=torch.uint8, device="cuda")
-    words, status, consumed = ctx.unpack_batch(pk, dev(in_offs), dev(out_offs))
-    torch.cuda.synchronize()
-    g_st = status.cpu().numpy()
-    assert np.array_equal(g_st, ref_st), np.nonzero(g_st != ref_st)
     ok = ref_st == 0
-    assert np.array_equal(consumed.cpu().numpy().view(np.uint64)[ok], ref_used[ok])
-    gw = words.cpu().numpy().view(np.uint64)
-    for c in np.nonzero(ok)[0]:
-        a, b = int(out_offs[c]), int(out_offs[c + 1])
-        assert np.array_equal(gw[a:b], ref_words[a:b])
     assert ok.sum() > 100 and (~ok).sum() > 100
+    for utc in (0, 1, 13, 64, 256):
+        words, status, consumed = ctx.unpack_batch(pk, dev(in_offs), dev(out_offs),
+                                                   chunks_per_tile=utc)
+        torch.cuda.synchronize()
+        g_st = status.cpu().numpy()
+        assert np.array_equal(g_st, ref_st), (utc, np.nonzero(g_st != ref_st))
+        assert np.array_equal(consumed.cpu().numpy().view(np.uint64)[ok], ref_used[ok]), utc
+        gw = words.cpu().numpy().view(np.uint64)
+        for c in np.nonzero(ok)[0]:
+            a, b = int(out_offs[c]), int(out_offs[c + 1])
+            assert np.array_equal(gw[a:b], ref_words[a:b]), (utc, c)
 
 
 def test_generator_matches_oracle(ctx):
