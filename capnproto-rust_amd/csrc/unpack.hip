@@ -31,6 +31,18 @@
 // empty (read() returns 0, io.rs:26-28).
 #include "common.h"
 
+#ifndef UNPACK_PROF
+#define UNPACK_PROF 0  // phase timers (scripts/unpack_prof.py); 0 = product
+#endif
+#if UNPACK_PROF
+// [0] stage, [1] walk, [2] expand (s_memtime cycles, wave 0, summed over
+// workgroups), [3] staged tiles, [4] global-path tiles
+__device__ unsigned long long g_uprof[8];
+#define UPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#else
+#define UPROF_T(v)
+#endif
+
 namespace {
 
 constexpr int kWaves = 4;
@@ -218,6 +230,7 @@ constexpr uint16_t kContZero = 0xFFFE;
 constexpr uint16_t kContLit = 0x8000;
 
 struct StageSmem {
+    uint64_t sel[256];  // expand_selector(tag): 0x00 -> zeros, 0xFF -> identity
     alignas(16) uint8_t bytes[kTileBytes + 16];
     alignas(16) uint16_t dpos[kTileWords];
 };
@@ -306,6 +319,9 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
     const bool fits = nc <= kStageChunks && B1 - B0 <= kTileBytes - off0 &&
                       W1 - W0 <= kTileWords;
     if (!fits) {
+#if UNPACK_PROF
+        if (tid == 0) atomicAdd(&g_uprof[4], 1ull);
+#endif
         for (uint64_t c0 = ca + (uint64_t)wave * CAPNP_WAVE; c0 < cb;
              c0 += (uint64_t)kWaves * CAPNP_WAVE)
             unpack_global(in, in_off, c0, cb, out, out_off, status, consumed, sm.desc[wave],
@@ -313,6 +329,7 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
         return;
     }
     StageSmem& S = sm.st;
+    UPROF_T(t0);
     const uint32_t nbytes = (uint32_t)(B1 - B0) + off0;
     const uint32_t Wt = (uint32_t)(W1 - W0);
     // stage the tile's packed bytes: every load issued before any LDS write
@@ -332,11 +349,13 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
         uint4* dd = reinterpret_cast<uint4*>(S.dpos);
         const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
         for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
+        S.sel[tid] = expand_selector(tid);
 #pragma unroll
         for (uint32_t k = 0; k < kLoads; k++)
             if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
     }
     __syncthreads();
+    UPROF_T(t1);
     // walk: lane j of wave 0 follows chunk j
     if (tid < nc) {
         const uint64_t c = ca + tid;
@@ -350,30 +369,46 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
         if (consumed) consumed[c] = used;
     }
     __syncthreads();
-    // expand: lane = output word; 64-word groups interleaved over waves
+    UPROF_T(t2);
+    // expand: lane = output word; 64-word groups interleaved over waves.
+    // Branch-free: every word is perm(8 bytes at src, sel[t]) with t = the
+    // head's tag for a normal head, 0xFF for literal words (identity), 0 for
+    // zero-run words (zeros).
     for (uint32_t g = wave; g * CAPNP_WAVE < Wt; g += kWaves) {
         const uint32_t i = g * CAPNP_WAVE + lane;
         const bool valid = i < Wt;
         const uint32_t d = valid ? S.dpos[i] : kNone;
         const uint64_t hm = ballot64(d != kNone) & low_mask(lane + 1);
-        uint64_t word = 0;
-        if (hm) {  // (no entry only after a decode error: output unspecified)
-            const uint32_t h = 63u - (uint32_t)__builtin_clzll(hm);
-            const uint32_t dh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(h << 2), (int)d);
-            if (dh == kContZero) {
-                word = 0;
-            } else if (dh & kContLit) {
-                word = lds_load8(S.bytes, (dh & 0x7FFFu) + 8 * (lane - h));
-            } else {
-                const uint32_t tag = S.bytes[dh];
-                if (tag == 0xFF)
-                    word = lds_load8(S.bytes, h == lane ? dh + 1 : dh + 10 + 8 * (lane - h - 1));
-                else if (tag != 0 && h == lane)
-                    word = expand_word(tag, lds_load8(S.bytes, dh + 1));
-            }
-        }
+        // (no entry at or below the lane only after a decode error: output
+        // unspecified, the lane's own kNone yields a zero word)
+        const uint32_t h = hm ? 63u - (uint32_t)__builtin_clzll(hm) : lane;
+        const uint32_t dh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(h << 2), (int)d);
+        const uint32_t k = lane - h;
+        const bool cz = dh >= kContZero;                 // zero-run continuation / none
+        const bool cl = !cz && (dh & kContLit) != 0;     // literal-run continuation
+        const uint32_t pos = cz ? 0u : (dh & 0x7FFFu);
+        const uint32_t tag = S.bytes[pos];
+        const bool lit = cl || (!cz && tag == 0xFF);
+        const uint32_t t = cz ? 0u : (lit ? 0xFFu : (k == 0 ? tag : 0u));
+        const uint32_t src = cl ? pos + 8 * k : (lit && k ? pos + 2 + 8 * k : pos + 1);
+        const uint64_t v = lds_load8(S.bytes, src);
+        const uint64_t sv = S.sel[t];
+        const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+        const uint64_t word =
+            ((uint64_t)__builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32)) << 32) |
+            __builtin_amdgcn_perm(hi, lo, (uint32_t)sv);
         if (valid) out[W0 + i] = word;
     }
+#if UNPACK_PROF
+    __syncthreads();
+    UPROF_T(t3);
+    if (tid == 0) {
+        atomicAdd(&g_uprof[0], (unsigned long long)(t1 - t0));
+        atomicAdd(&g_uprof[1], (unsigned long long)(t2 - t1));
+        atomicAdd(&g_uprof[2], (unsigned long long)(t3 - t2));
+        atomicAdd(&g_uprof[3], 1ull);
+    }
+#endif
 }
 
 }  // namespace
@@ -390,3 +425,14 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
                        d_in_off, nchunks, tc, d_out, d_out_off, d_status, d_consumed);
     return hipGetLastError();
 }
+
+#if UNPACK_PROF
+extern "C" hipError_t capnp_unpack_prof(unsigned long long* host8, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_uprof), sizeof(g_uprof));
+    if (e == hipSuccess && reset) {
+        static const unsigned long long z[8] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_uprof), z, sizeof(z));
+    }
+    return e;
+}
+#endif

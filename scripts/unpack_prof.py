@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""Phase breakdown of the unpack kernel from the UNPACK_PROF=1 build
+(`make -C capnproto-rust_amd uprof`): s_memtime cycles of wave 0 per phase
+(stage bytes, walk, expand) summed over staged tiles.  Diagnostic only.
+
+    python3 scripts/unpack_prof.py [--chunks N] [--chunk-words W] [--utc T]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "capnproto-rust_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--chunks", type=int, default=1 << 20)
+    ap.add_argument("--chunk-words", type=int, default=128)
+    ap.add_argument("--pz", type=int, default=1288490189)
+    ap.add_argument("--utc", type=int, default=0)
+    ap.add_argument("--iters", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    from capnp_amd import Context, unpack_tile_chunks_for
+    L = C.CDLL(os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_uprof.so"))
+    vp, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
+    L.capnp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int)]
+    L.capnp_ctx_create.restype = vp
+    L.capnp_gpu_unpack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, u32, vp]
+    L.capnp_unpack_prof.argtypes = [vp, C.c_int]
+    st = C.c_int(0)
+    h = vp(L.capnp_ctx_create(0, C.byref(st)))
+    n, cw = a.chunks, a.chunk_words
+    ctx = Context(0)
+    offs = torch.arange(0, (n + 1) * cw, cw, dtype=torch.int64, device="cuda")
+    words = torch.empty(n * cw, dtype=torch.int64, device="cuda")
+    ctx.gen_batch(words, offs, pz_thresh=a.pz)
+    packed, poffs = ctx.pack_batch(words, offs)
+    back = torch.empty_like(words)
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    utc = a.utc or unpack_tile_chunks_for(n * cw, n)
+    buf = (C.c_ulonglong * 8)()
+    stream = torch.cuda.current_stream()
+    P = C.c_void_p
+    for it in range(a.iters + 1):
+        torch.cuda.synchronize()
+        L.capnp_unpack_prof(buf, 1)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        L.capnp_gpu_unpack_batch_tuned(h, P(packed.data_ptr()), P(poffs.data_ptr()), n,
+                                       P(back.data_ptr()), P(offs.data_ptr()),
+                                       P(status.data_ptr()), None, utc, P(stream.cuda_stream))
+        e1.record(stream)
+        e1.synchronize()
+        L.capnp_unpack_prof(buf, 1)
+        if it == 0:
+            continue
+        ok = torch.equal(back, words)
+        tiles = max(buf[3], 1)
+        tot = buf[0] + buf[1] + buf[2]
+        print(f"iter {it}: {e0.elapsed_time(e1) * 1e3:.1f} us ok={ok} staged={buf[3]} "
+              f"global={buf[4]} cycles/tile: stage={buf[0] / tiles:.0f} walk={buf[1] / tiles:.0f} "
+              f"expand={buf[2] / tiles:.0f} ({100 * buf[1] / max(tot, 1):.0f}% walk)")
+
+
+if __name__ == "__main__":
+    main()
