@@ -2,6 +2,11 @@
 //
 // Host entry points stage through device memory and run the gfx950 kernels;
 // there is no CPU implementation of the codec in this library.
+#ifndef CAPNP_STATE_ALLOC
+// pack look-back records: 1 uncached device memory (default; see pack.hip),
+// 0 hipMalloc, 2 fine-grained (diagnostic builds)
+#define CAPNP_STATE_ALLOC 1
+#endif
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -77,7 +82,15 @@ capnp_status ensure_state(capnp_ctx* ctx, size_t bytes) {
         ctx->state_cap = 0;
     }
     size_t cap = std::max<size_t>(bytes, 1 << 16);
+#if CAPNP_STATE_ALLOC == 1
+    HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->d_state), cap,
+                                  hipDeviceMallocUncached));
+#elif CAPNP_STATE_ALLOC == 2
+    HIP_TRY(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->d_state), cap,
+                                  hipDeviceMallocFinegrained));
+#else
     HIP_TRY(hipMalloc(&ctx->d_state, cap));
+#endif
     ctx->state_cap = cap;
     return CAPNP_OK;
 }

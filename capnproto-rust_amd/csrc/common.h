@@ -96,3 +96,16 @@ __device__ __forceinline__ uint64_t load_relaxed_agent(const uint64_t* p) {
     return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// Cross-workgroup records (look-back): relaxed agent-scope 8-byte accesses
+// to UNCACHED device memory (hipDeviceMallocUncached, capi.hip), so the
+// reader and writer meet at memory.  In cached memory a relaxed agent load is
+// served by the reader XCD's L2 (MI355X_MICROARCH.md: sc1 loads bypass L1
+// only), where a line an earlier poll brought in stays stale after another
+// XCD's store.
+__device__ __forceinline__ uint64_t poll_agent(uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void publish_agent(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}

@@ -43,6 +43,27 @@
 #define PACK_ABLATE 0  // diagnostic builds only (scripts/ablate.py); 0 = product
 #endif
 
+#ifndef PACK_PROF
+#define PACK_PROF 0  // look-back counters (scripts/pack_prof.py); 0 = product
+#endif
+#if PACK_PROF
+// [0] within-group spin rounds, [1] group-scan spin rounds, [2] tile
+// fallbacks, [3] group fallbacks, [4] group windows scanned, [5] tiles,
+// [6] s_memtime cycles in lookback (wave 0), [7] cycles in pass 2
+__device__ unsigned long long g_prof[8];
+// per-tile trace (set by capnp_pack_trace), 8 words per tile: [0] start,
+// [1] published, [2] offset known, [3] end (s_memrealtime, 100 MHz),
+// [4] XCC id << 32 | HW_ID, [5] within spins, [6] group spins, [7] windows
+__device__ uint64_t* g_trace;
+#define PROF_ADD(i, v) atomicAdd(&g_prof[i], (unsigned long long)(v))
+#define TRACE(tile, k, v) do { if (g_trace) g_trace[(tile) * 8 + (k)] = (v); } while (0)
+#define RT() __builtin_amdgcn_s_memrealtime()
+#else
+#define PROF_ADD(i, v) ((void)0)
+#define TRACE(tile, k, v) ((void)0)
+#define RT() 0ull
+#endif
+
 namespace {
 
 constexpr int kWaves = 4;
@@ -303,14 +324,28 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     return x;
 }
 
-// Branch-free step of the staged path (the hot loop).  Mask arithmetic is
-// kept on the scalar unit only where it is inherently wave-wide (run
-// segmentation); offsets come from a DPP scan, so the shared SALU is not
-// the bottleneck.
-__device__ __forceinline__ void stage_step(Packer& pk, uint64_t w, uint32_t nvalid, bool last,
-                                           uint32_t lane, uint8_t* region, const uint64_t* sel) {
-    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
-    const uint32_t tag = word_tag(lo, hi);
+// Staged path, two passes over the register-cached words of a wave's range.
+//
+// Pass 1 (size): per 64-word step, the tag, the three ballots, the run
+// segmentation (resolve_step) and a DPP scan of the record sizes give every
+// lane its byte position inside the wave's region.  Only sizes are needed to
+// publish the tile's aggregate, so the aggregate goes out before the bytes are
+// assembled and the look-back latency overlaps pass 2.
+//
+// Pass 2 (emit): every lane ORs its record (<= 10 bytes) into the zeroed
+// region.  The count byte of a Z/F head whose run crosses into later steps is
+// completed from those steps' absorbed counts (ext), so nothing is patched.
+struct StepInfo {
+    uint64_t H;        // heads of the step
+    uint32_t pos;      // this lane's byte position in the region (per lane)
+    uint32_t tag;      // this lane's tag (per lane)
+    uint32_t kin;      // words absorbed by the run carried into the step
+    uint32_t meta;     // nvalid | first << 7 | last << 8 | chunk << 9
+};
+
+__device__ __forceinline__ void size_step(Packer& pk, uint64_t w, uint32_t nvalid, uint32_t lane,
+                                          StepInfo& si) {
+    const uint32_t tag = word_tag((uint32_t)w, (uint32_t)(w >> 32));
     const uint32_t pop = __builtin_popcount(tag);
     const bool isz = tag == 0, isf = tag == 0xFF;
     const uint64_t V = low_mask(nvalid);
@@ -318,20 +353,31 @@ __device__ __forceinline__ void stage_step(Packer& pk, uint64_t w, uint32_t nval
     const uint64_t Lm = ballot64(pop >= 7) & V;
     const uint64_t Fm = ballot64(isf) & V;
     const StepMasks sm = resolve_step(Zm, Lm, Fm, nvalid, pk.carry);
-    const uint64_t hsh = sm.H >> lane;
-    const bool head = hsh & 1;
+    const bool head = (sm.H >> lane) & 1;
     const bool valid = lane < nvalid;
     const uint32_t hsize = isz ? 2u : (isf ? 10u : 1u + pop);
     const uint32_t size = head ? hsize : ((valid && !isz) ? 8u : 0u);
     const uint32_t incl = wave_incl_scan(size);
-    const uint32_t step_bytes = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    const uint32_t start = (uint32_t)(pk.o_c + pk.total);
-    const uint32_t pos = start + incl - size;
-    // run count of a Z/F head: words up to the next head, or to the step end
+    si.H = sm.H;
+    si.pos = (uint32_t)(pk.o_c + pk.total) + incl - size;
+    si.tag = tag;
+    si.kin = sm.absorbed_carry;
+    pk.carry = sm.next;
+    pk.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+}
+
+__device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32_t ext,
+                                          uint32_t lane, uint8_t* region, const uint64_t* sel) {
+    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+    const uint32_t tag = si.tag;
+    const uint32_t nvalid = si.meta & 127u;
+    const bool isz = tag == 0, isf = tag == 0xFF;
+    const uint64_t hsh = si.H >> lane;
+    const bool head = hsh & 1;
+    // run count of a Z/F head: words up to the next head, else to the step
+    // end plus what the run absorbs in later steps
     const uint64_t nxt = hsh >> 1;
-    const uint32_t cnt = nxt ? ctz64(nxt) : nvalid - lane - 1;
-    // record: [tag][non-zero bytes][count] for heads (sel[0xFF] is the
-    // identity, sel[0] yields zeros), the raw word for absorbed words
+    const uint32_t cnt = nxt ? ctz64(nxt) : nvalid - lane - 1 + ext;
     const uint64_t sv = sel[tag];
     const uint32_t clo = __builtin_amdgcn_perm(hi, lo, (uint32_t)sv);
     const uint32_t chi = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32));
@@ -341,6 +387,8 @@ __device__ __forceinline__ void stage_step(Packer& pk, uint64_t w, uint32_t nval
     r0 = head ? r0 : lo;
     r1 = head ? (isz ? 0u : r1) : hi;
     r2 = head ? (isz ? 0u : r2) : 0u;
+    // (absorbed zero words and lanes past nvalid hold w == 0: all zeros)
+    const uint32_t pos = si.pos;
     const uint32_t sh = (pos & 3) * 8;
     const uint32_t e0 = r0 << sh;
     const uint32_t e1 = (uint32_t)((((uint64_t)r1 << 32) | r0) >> (32 - sh));
@@ -351,26 +399,6 @@ __device__ __forceinline__ void stage_step(Packer& pk, uint64_t w, uint32_t nval
     __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    // a count carried in from earlier steps
-    if (pk.pend) {
-        pk.pend_cnt += sm.absorbed_carry;
-        if (sm.absorbed_carry < 64 || last) {
-            wave_lds_sync();
-            if (lane == 0) region[pk.pend_pos] = (uint8_t)pk.pend_cnt;
-            pk.pend = false;
-        }
-    }
-    // a Z/F head whose run reaches the end of a non-final step: its count
-    // byte sits 1 (Z) or 9 (F) bytes into its record
-    if (!last && sm.next.type != 0 && sm.H) {
-        const uint32_t h = 63u - (uint32_t)__builtin_clzll(sm.H);
-        pk.pend = true;
-        pk.pend_cnt = 63u - h;
-        pk.pend_pos = (uint32_t)__builtin_amdgcn_readlane((int)pos, h) +
-                      (sm.next.type == 1 ? 1u : 9u);
-    }
-    pk.carry = sm.next;
-    pk.total += step_bytes;
 }
 
 // Copies region bytes [0, len) to out[D0 .. D0+len) (16-aligned coordinates),
@@ -492,17 +520,25 @@ __device__ uint64_t tile_aggregate(const uint64_t* __restrict__ in,
     return total;
 }
 
-// Two-level decoupled look-back.  Tile records ts[t] and group records gs[g]
-// (64 tiles per group) are {flag, value} granules.  Tile t publishes its
-// aggregate, sums the aggregates of the tiles before it in its group, and
-// finds the group's exclusive prefix by scanning group records (64 groups =
-// 4096 tiles per round trip).  The last tile of a group publishes the group
-// aggregate and, once known, the group's inclusive prefix.
+// Two-level decoupled look-back.  Tile records ts[t] ({flag, value}
+// granules) carry each tile's aggregate, published as soon as the tile's
+// sizes are known (before its bytes are assembled, so the wait overlaps pass
+// 2).  The last tile of each group of 64 publishes the group aggregate, and
+// once known the group's inclusive prefix, in gs[g].  A tile's offset = its
+// group's earlier tiles (one 64-record load) + the group's exclusive prefix
+// (64 groups = 4096 tiles per load).
 //
-// Tiles are blockIdx.x, so a tile may in principle wait on a tile whose
-// workgroup has not been dispatched; every wait is bounded and on timeout the
-// waiter computes the missing aggregate itself (records are idempotent), so
-// the kernel terminates with the right answer under any dispatch order.
+// The records live in uncached device memory (capi.hip), so relaxed
+// agent-scope loads and stores meet at memory: in cached (hipMalloc) memory
+// a poll is served by the reader XCD's L2 and can stay stale for tens of
+// microseconds after another XCD's store.  Measured alternatives (round 1,
+// config 2): hipMalloc'd records 1154 us/launch, uncached 748 us; adding
+// per-group atomic totals (memory-side atomics) 2295 us; issuing the first
+// polls before pass 2 822 us.
+//
+// Every wait is bounded: on timeout the waiter computes the missing aggregate
+// itself from the input (records are idempotent), so the kernel finishes with
+// the right answer under any workgroup dispatch order.
 constexpr uint32_t kGroup = 64;
 constexpr uint32_t kSpinLimit = 4096;
 
@@ -511,12 +547,12 @@ __device__ uint64_t group_aggregate(uint64_t* __restrict__ ts, const uint64_t* _
                                     uint32_t tc, uint64_t ntiles, uint64_t g, uint32_t lane) {
     const uint64_t t0 = g * kGroup;
     const uint64_t tn = (t0 + kGroup < ntiles) ? kGroup : ntiles - t0;
-    uint64_t st = lane < tn ? load_relaxed_agent(&ts[t0 + lane]) : kFlagAgg;
+    uint64_t st = lane < tn ? poll_agent(&ts[t0 + lane]) : kFlagAgg;
     uint64_t miss = ballot64((st >> 62) == 0);
     while (miss) {
         const uint32_t k = ctz64(miss);
         const uint64_t a = tile_aggregate(in, chunk_off, nchunks, tc, t0 + k, lane);
-        if (lane == 0) store_relaxed_agent(&ts[t0 + k], kFlagAgg | a);
+        if (lane == 0) publish_agent(&ts[t0 + k], kFlagAgg | a);
         if (lane == k) st = kFlagAgg | a;
         miss &= miss - 1;
     }
@@ -525,74 +561,123 @@ __device__ uint64_t group_aggregate(uint64_t* __restrict__ ts, const uint64_t* _
     return v;
 }
 
-__device__ uint64_t lookback(uint64_t* __restrict__ ts, uint64_t* __restrict__ gs,
-                             uint64_t tile, uint64_t ntiles, uint64_t agg, uint32_t lane,
-                             const uint64_t* __restrict__ in,
-                             const uint64_t* __restrict__ chunk_off, uint64_t nchunks,
-                             uint32_t tc) {
-#if PACK_ABLATE == 1 || PACK_ABLATE == 4
-    return tile * agg;  // timing-only: fake, in-bounds prefix; output is wrong
+struct LookbackArgs {
+    uint64_t* ts;
+    uint64_t* gs;
+    uint64_t ntiles;
+    const uint64_t* in;
+    const uint64_t* chunk_off;
+    uint64_t nchunks;
+    uint32_t tc;
+};
+
+// Wave 0: publishes tile t's aggregate.
+__device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint64_t agg,
+                                        uint32_t lane) {
+#if PACK_ABLATE != 1 && PACK_ABLATE != 4
+    if (lane == 0) publish_agent(&A.ts[t], kFlagAgg | agg);
 #endif
-    const uint64_t g = tile / kGroup;
-    const uint32_t r = (uint32_t)(tile % kGroup);
-    if (lane == 0) store_relaxed_agent(&ts[tile], kFlagAgg | agg);
+}
+
+// Wave 0: global byte offset of tile t (aggregate already published).
+__device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, uint32_t lane) {
+#if PACK_ABLATE == 1 || PACK_ABLATE == 4
+    return t * agg;  // timing-only: fake, in-bounds prefix; output is wrong
+#endif
+    const uint64_t g = t / kGroup;
+    const uint32_t r = (uint32_t)(t % kGroup);
+#if PACK_PROF
+    const uint64_t tp0 = __builtin_amdgcn_s_memtime();
+    uint32_t n_ws = 0, n_gs = 0, n_win = 0;
+#endif
     // aggregates of the group's earlier tiles
     uint64_t within;
+    uint64_t st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
     for (uint32_t spins = 0;;) {
-        const uint64_t st = lane < r ? load_relaxed_agent(&ts[g * kGroup + lane]) : kFlagAgg;
         const uint64_t miss = ballot64((st >> 62) == 0);
-        if (miss) {
-            if (++spins < kSpinLimit) {
-                __builtin_amdgcn_s_sleep(2);
-                continue;
-            }
+        if (!miss) break;
+#if PACK_PROF
+        n_ws++;
+#endif
+        if (++spins >= kSpinLimit) {
+            if (lane == 0) PROF_ADD(2, 1);
             const uint64_t j = g * kGroup + ctz64(miss);
-            const uint64_t a = tile_aggregate(in, chunk_off, nchunks, tc, j, lane);
-            if (lane == 0) store_relaxed_agent(&ts[j], kFlagAgg | a);
-            continue;
+            const uint64_t a = tile_aggregate(A.in, A.chunk_off, A.nchunks, A.tc, j, lane);
+            if (lane == 0) publish_agent(&A.ts[j], kFlagAgg | a);
+        } else {
+            __builtin_amdgcn_s_sleep(2);
         }
+        st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
+    }
+    {
         uint64_t v = st & kValMask;
         for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
         within = v;
-        break;
     }
-    const bool group_last = (r == kGroup - 1) || (tile + 1 == ntiles);
-    const uint64_t gtotal = within + agg;
-    if (group_last && lane == 0) store_relaxed_agent(&gs[g], kFlagAgg | gtotal);
-    // exclusive prefix of the group
+    const bool group_last = (r == kGroup - 1) || (t + 1 == A.ntiles);
+    if (group_last && lane == 0) publish_agent(&A.gs[g], kFlagAgg | (within + agg));
+    // exclusive prefix of the group: 64 groups per round; a group contributes
+    // its inclusive record (and ends the scan), else its aggregate
     uint64_t gexcl = 0;
     int64_t idx = (int64_t)g - 1;
     for (uint32_t spins = 0; idx >= 0;) {
         const int64_t j = idx - (int64_t)lane;
-        const uint64_t st = j >= 0 ? load_relaxed_agent(&gs[j]) : kFlagInc;
-        const uint64_t inc = ballot64((st & kFlagInc) != 0);
-        const uint64_t none = ballot64((st >> 62) == 0);
+        const uint64_t rec = j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc;
+        const uint64_t inc = ballot64((rec & kFlagInc) != 0);
         const uint32_t first_inc = ctz64(inc);
-        const uint64_t need = first_inc < 64 ? low_mask(first_inc + 1) : ~0ull;
-        if (none & need) {
-            if (++spins < kSpinLimit) {
+        const uint64_t need = first_inc < 64 ? low_mask(first_inc) : ~0ull;
+        const uint64_t missing = ballot64((rec >> 62) == 0) & need;
+#if PACK_PROF
+        n_win++;
+#endif
+        if (missing) {
+#if PACK_PROF
+            n_gs++;
+#endif
+            if (++spins >= kSpinLimit) {
+                const uint64_t jg = (uint64_t)(idx - (int64_t)ctz64(missing));
+                const uint64_t a = group_aggregate(A.ts, A.in, A.chunk_off, A.nchunks, A.tc,
+                                                   A.ntiles, jg, lane);
+                if (lane == 0) publish_agent(&A.gs[jg], kFlagAgg | a);
+            } else {
                 __builtin_amdgcn_s_sleep(2);
-                continue;  // a predecessor group has not published yet
             }
-            const uint64_t jg = (uint64_t)(idx - (int64_t)ctz64(none & need));
-            const uint64_t a = group_aggregate(ts, in, chunk_off, nchunks, tc, ntiles, jg, lane);
-            if (lane == 0) store_relaxed_agent(&gs[jg], kFlagAgg | a);
             continue;
         }
-        uint64_t val = (lane <= first_inc) ? (st & kValMask) : 0;
+        uint64_t val = (lane <= first_inc) ? (rec & kValMask) : 0;
         for (uint32_t d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
         gexcl += val;
         if (first_inc < 64) break;
         idx -= 64;
         spins = 0;
     }
-    if (group_last && lane == 0) store_relaxed_agent(&gs[g], kFlagInc | (gexcl + gtotal));
+    if (group_last && lane == 0) publish_agent(&A.gs[g], kFlagInc | (gexcl + within + agg));
+#if PACK_PROF
+    if (lane == 0) {
+        TRACE(t, 5, n_ws);
+        TRACE(t, 6, n_gs);
+        TRACE(t, 7, n_win);
+    }
+    (void)tp0;
+#endif
     return gexcl + within;
 }
 
-// One workgroup per tile (tile = blockIdx.x).  8 waves per SIMD (<= 64
-// VGPRs): the step loop is latency-bound, occupancy hides it.
-__global__ void __launch_bounds__(kThreads, 8) __attribute__((amdgpu_num_sgpr(80)))
+// Wave 0: exclusive scan of the tile's chunk sizes (<= 64) into chunk_pos
+// (tile-relative); returns the tile aggregate.
+__device__ __forceinline__ uint64_t scan_chunks(Smem& sm, uint32_t nc, uint32_t lane) {
+    const uint64_t v = lane < nc ? sm.chunk_size[lane] : 0;
+    uint64_t s = v;
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t t = __shfl_up(s, d, 64);
+        if (lane >= d) s += t;
+    }
+    if (lane < nc) sm.chunk_pos[lane] = s - v;
+    return __shfl(s, 63, 64);
+}
+
+// One workgroup per tile (tile = blockIdx.x), 4 waves.
+__global__ void __launch_bounds__(kThreads, 8)
 pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
             uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
             uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts,
@@ -603,10 +688,27 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     const uint64_t ntiles = (nchunks + tc - 1) / tc;
     const uint64_t tile = blockIdx.x;
+    LookbackArgs LA;
+    LA.ts = ts;
+    LA.gs = gs;
+    LA.ntiles = ntiles;
+    LA.in = in;
+    LA.chunk_off = chunk_off;
+    LA.nchunks = nchunks;
+    LA.tc = tc;
 
     const uint64_t c0 = tile * tc;
     const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
     const uint32_t nc = (uint32_t)(c1 - c0);
+#if PACK_PROF
+    if (tid == 0) {
+        uint32_t xcc, hwid;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        TRACE(tile, 0, RT());
+        TRACE(tile, 4, ((uint64_t)xcc << 32) | hwid);
+    }
+#endif
     for (uint32_t i = tid; i <= nc; i += kThreads) sm.off[i] = chunk_off[c0 + i];
     for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
     // compaction selectors: byte r = index of the r-th set bit of the tag
@@ -669,65 +771,96 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         }
         for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
             *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
-        wave_lds_sync();
-        Packer pk;
-        uint64_t local = 0;
+        // pass 1: sizes and positions
+        StepInfo si[kStageSteps];
+        {
+            Packer pk;
+            uint64_t local = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < kStageSteps; s++) {
-            if (s >= nsteps) break;
-            const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
-            const uint32_t nvalid = meta & 127u;
-            const bool first = (meta >> 7) & 1, last = (meta >> 8) & 1;
-            if (first) pk.begin(local);
+            for (uint32_t s = 0; s < kStageSteps; s++) {
+                si[s].H = 0;
+                si[s].kin = 0;
+                si[s].meta = 0;
+                si[s].pos = 0;
+                si[s].tag = 0;
+                if (s < nsteps) {
+                    const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
+                    si[s].meta = meta;
+                    if ((meta >> 7) & 1) pk.begin(local);
 #if PACK_ABLATE == 3 || PACK_ABLATE == 4
-            // timing-only: keep the loads, skip the packing arithmetic
-            asm volatile("" ::"v"(cache[s]));
-            pk.total += 34 * nvalid / 8;
+                    asm volatile("" ::"v"(cache[s]));  // timing-only: skip the arithmetic
+                    pk.total += 34 * (meta & 127u) / 8;
 #else
-            stage_step(pk, cache[s], nvalid, last, lane, region, sm.sel);
+                    size_step(pk, cache[s], meta & 127u, lane, si[s]);
 #endif
-            if (last) {
-                if (lane == 0) sm.chunk_size[wc0 + (meta >> 9)] = pk.total;
-                local += pk.total;
+                    if ((meta >> 8) & 1) {
+                        if (lane == 0) sm.chunk_size[wc0 + (meta >> 9)] = pk.total;
+                        local += pk.total;
+                    }
+                }
+            }
+            if (lane == 0) sm.wave_bytes[wave] = local;
+        }
+        __syncthreads();
+        uint64_t agg = 0;
+        if (wave == 0) {
+            agg = scan_chunks(sm, nc, lane);
+            publish(LA, tile, agg, lane);
+            if (lane == 0) TRACE(tile, 1, RT());
+        }
+        // pass 2: assemble the bytes (the look-back loads are in flight)
+#if PACK_ABLATE != 3 && PACK_ABLATE != 4
+        wave_lds_sync();
+        {
+            uint32_t ext = 0;  // words the run open at the step end absorbs later
+#pragma unroll
+            for (int s = (int)kStageSteps - 1; s >= 0; s--) {
+                if ((uint32_t)s < nsteps) {
+                    const uint32_t meta = si[s].meta;
+                    const uint32_t e = ((meta >> 8) & 1) ? 0u : ext;
+                    emit_step(cache[s], si[s], e, lane, region, sm.sel);
+                    // ext for step s-1: absorbed here, plus later if the run
+                    // covered this whole step
+                    ext = ((meta >> 7) & 1) ? 0u : si[s].kin + (si[s].H == 0 ? e : 0u);
+                }
             }
         }
-        if (lane == 0) sm.wave_bytes[wave] = local;
-    } else {
-        run_streaming<MODE_SIZE>(in, sm.off, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
-                                 region, sm.sel, outa, mis, out_cap);
-    }
-    __syncthreads();
-
-    // ---- tile scan + look-back (wave 0)
-    if (wave == 0) {
-        const uint64_t v = lane < nc ? sm.chunk_size[lane] : 0;
-        const uint64_t v2 = (lane + 64 < nc) ? sm.chunk_size[lane + 64] : 0;
-        uint64_t s = v, s2 = v2;
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint64_t t = __shfl_up(s, d, 64);
-            const uint64_t t2 = __shfl_up(s2, d, 64);
-            if (lane >= d) { s += t; s2 += t2; }
-        }
-        s2 += __shfl(s, 63, 64);
-        const uint64_t agg = __shfl(s2, 63, 64);
-        const uint64_t excl = lookback(ts, gs, tile, ntiles, agg, lane, in, chunk_off, nchunks, tc);
-        if (lane < nc) sm.chunk_pos[lane] = excl + s - v;
-        if (lane + 64 < nc) sm.chunk_pos[lane + 64] = excl + s2 - v2;
-        if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
-
-    // ---- write the bytes
-#if PACK_ABLATE == 2
-    return;  // timing-only: no output stores
 #endif
-    if (staged) {
+        if (wave == 0) {
+            const uint64_t excl = lookback(LA, tile, agg, lane);
+            if (lane == 0) TRACE(tile, 2, RT());
+            if (lane < nc) sm.chunk_pos[lane] += excl;
+            if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
+#if PACK_ABLATE == 2
+        return;  // timing-only: no output stores
+#endif
         if (wc1 > wc0) {
             const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
             copy_out(region, outa, D0, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
         }
+#if PACK_PROF
+        __syncthreads();
+        if (tid == 0) TRACE(tile, 3, RT());
+#endif
     } else {
+        run_streaming<MODE_SIZE>(in, sm.off, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
+                                 region, sm.sel, outa, mis, out_cap);
+        __syncthreads();
+        if (wave == 0) {
+            const uint64_t agg = scan_chunks(sm, nc, lane);
+            publish(LA, tile, agg, lane);
+            const uint64_t excl = lookback(LA, tile, agg, lane);
+            if (lane < nc) sm.chunk_pos[lane] += excl;
+            if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
+#if PACK_ABLATE == 2
+        return;
+#endif
         run_streaming<MODE_RING>(in, sm.off, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
                                  region, sm.sel, outa, mis, out_cap);
     }
@@ -739,8 +872,8 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 // 64-word steps); the host picks chunks_per_tile ~ this / mean chunk words.
 extern "C" uint32_t capnp_pack_tile_words(void) { return kWaves * 64 * kStageSteps; }
 
-// Workspace layout (zeroed every call): ts[ntiles] tile records, then
-// gs[ngroups] group records.
+// Workspace layout (zeroed every call; uncached memory, capi.hip):
+// ts[ntiles] tile records, then gs[ngroups] group records.
 extern "C" size_t capnp_pack_state_bytes(uint64_t nchunks, uint32_t tc) {
     const uint64_t ntiles = (nchunks + tc - 1) / tc;
     const uint64_t ngroups = (ntiles + kGroup - 1) / kGroup;
@@ -758,7 +891,23 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_
     }
     hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(nchunks, tc), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(pack_kernel, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream, d_in, d_chunk_off,
-                       nchunks, tc, d_out, out_cap, d_out_off, d_state, d_state + ntiles);
+    hipLaunchKernelGGL(pack_kernel, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream, d_in,
+                       d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_state,
+                       d_state + ntiles);
     return hipGetLastError();
 }
+
+#if PACK_PROF
+extern "C" hipError_t capnp_pack_trace(uint64_t* d_buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &d_buf, sizeof(d_buf));
+}
+
+extern "C" hipError_t capnp_pack_prof(unsigned long long* host8, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_prof), sizeof(g_prof));
+    if (e == hipSuccess && reset) {
+        static const unsigned long long z[8] = {};
+        e = hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z));
+    }
+    return e;
+}
+#endif

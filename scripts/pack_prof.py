@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Phase breakdown of the pack kernel from the PACK_PROF=1 build
-(`make -C capnproto-rust_amd prof`): s_memtime cycles per phase summed over
-workgroups (wave 0), look-back spin rounds and fallbacks.  Diagnostic only.
+"""Look-back statistics of the pack kernel from the PACK_PROF=1 build
+(`make -C capnproto-rust_amd prof`): spin rounds, fallbacks, group windows
+scanned and s_memtime cycles spent in the look-back.  Diagnostic only.
 
     python3 scripts/pack_prof.py [--chunks N] [--chunk-words W] [--tc T]
 """
@@ -13,8 +13,6 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "capnproto-rust_amd"))
 
-PHASES = ["advance+meta", "compute", "bar1", "publish+plan", "bar2", "lookback",
-          "bar_fin", "copy_out", "bar_end", "pre_finish"]
 
 
 def main():
@@ -24,10 +22,12 @@ def main():
     ap.add_argument("--pz", type=int, default=1288490189)
     ap.add_argument("--tc", type=int, default=0)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--lib", default="")
+    ap.add_argument("--trace", default="", help="save the per-tile timeline (.npy)")
     a = ap.parse_args()
     import torch
     from capnp_amd import Context, tile_chunks_for
-    path = os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_prof.so")
+    path = a.lib or os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_prof.so")
     L = C.CDLL(path)
     vp, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
     L.capnp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int)]
@@ -48,7 +48,11 @@ def main():
     oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
     tc = a.tc or tile_chunks_for(n * cw, n)
     L.capnp_ctx_reserve(h, n)
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 8)()
+    ntiles = (n + tc - 1) // tc
+    trace = torch.zeros(ntiles * 8, dtype=torch.int64, device="cuda")
+    L.capnp_pack_trace.argtypes = [vp]
+    L.capnp_pack_trace(C.c_void_p(trace.data_ptr()))
     stream = torch.cuda.current_stream()
     P = C.c_void_p
     for it in range(a.iters + 1):
@@ -66,14 +70,15 @@ def main():
         if it == 0:
             continue
         ok = torch.equal(oo, ref_oo) and torch.equal(out[:ref_out.numel()], ref_out)
-        wgs = max(buf[15], 1)
-        tot = sum(buf[i] for i in range(10))
-        print(f"iter {it}: {e0.elapsed_time(e1) * 1e3:.1f} us, ok={ok}, WGs={buf[15]}, "
-              f"tiles={buf[14]}, spins={buf[12]}, fallbacks={buf[13]}, "
-              f"cycles/WG={tot / wgs:.0f}")
-        print("   " + "  ".join(f"{PHASES[i]}={100 * buf[i] / max(tot, 1):.1f}%"
-                                 for i in range(10)))
-
+        T = trace.view(ntiles, 8).cpu().numpy().astype("int64")
+        us = lambda a, b: (T[:, b] - T[:, a]).mean() / 100.0
+        print(f"iter {it}: {e0.elapsed_time(e1) * 1e3:.1f} us ok={ok} tiles={ntiles} "
+              f"within-spins/tile={T[:, 5].mean():.2f} group-spins/tile={T[:, 6].mean():.2f} "
+              f"windows/tile={T[:, 7].mean():.2f} pass1={us(0, 1):.1f}us "
+              f"pub->offset={us(1, 2):.1f}us offset->end={us(2, 3):.1f}us")
+    if a.trace:
+        import numpy as np
+        np.save(a.trace, trace.view(ntiles, 8).cpu().numpy())
 
 if __name__ == "__main__":
     main()
