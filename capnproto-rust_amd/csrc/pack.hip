@@ -76,7 +76,7 @@ constexpr uint32_t kStepMax = 64 * 10 + 16;
 
 // Staged path capacity: kStageSteps steps of 64 words per wave.
 #ifndef PACK_STAGE_STEPS
-#define PACK_STAGE_STEPS 4
+#define PACK_STAGE_STEPS 8
 #endif
 constexpr uint32_t kStageSteps = PACK_STAGE_STEPS;
 constexpr uint32_t kStageWords = 64 * kStageSteps;
