@@ -35,10 +35,11 @@
 #define UNPACK_PROF 0  // phase timers (scripts/unpack_prof.py); 0 = product
 #endif
 #if UNPACK_PROF
-// [0] stage, [1] walk, [2] expand (s_memtime cycles, wave 0, summed over
-// workgroups), [3] staged tiles, [4] global-path tiles
+// per-tile trace (capnp_unpack_trace): s_memrealtime (100 MHz) at
+// [0] start, [1] staged, [2] walked, [3] expanded; [4] 1 = global path
+__device__ uint64_t* g_utrace;
 __device__ unsigned long long g_uprof[8];
-#define UPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define UPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
 #else
 #define UPROF_T(v)
 #endif
@@ -260,12 +261,15 @@ __device__ __forceinline__ int32_t record_error(uint32_t p, uint32_t q, uint32_t
 
 // Walks one chunk: bytes [p, pe) of the staged tile, output words [wb, wb+n)
 // of the tile.  One hop per record: the tag and both possible count bytes
-// (p+1 for 0x00, p+9 for 0xFF) are read together, one check covers every
-// error, and only continuation entries branch.
+// (p+1 for 0x00, p+9 for 0xFF) are read together, and one check
+// (record end <= pe, run end <= chunk end) covers every error; only the rare
+// continuation entries branch.  Status precedence and consumed bytes as in
+// unpack_global.
 __device__ __forceinline__ void walk_chunk(StageSmem& S, uint32_t p, uint32_t pe, uint32_t wb,
                                            uint32_t n, int32_t& st, uint32_t& used) {
     const uint32_t p0 = p;
-    uint32_t w = 0;
+    const uint32_t wend = wb + n;
+    uint32_t w = wb;
     st = ST_OK;
     if (n > 0 && p == pe) st = ST_FAILED_FILL;  // read() returns Ok(0)
     bool go = n > 0 && st == ST_OK;
@@ -277,24 +281,22 @@ __device__ __forceinline__ void walk_chunk(StageSmem& S, uint32_t p, uint32_t pe
         uint32_t b9 = S.bytes[p + 9];
         asm volatile("" : "+v"(tag), "+v"(b1), "+v"(b9));
         const uint32_t q = p + 1 + __builtin_popcount(tag);
-        const bool isz = tag == 0, isf = tag == 0xFF, run = isz || isf;
+        const bool isz = tag == 0, isf = tag == 0xFF;
         const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
-        const uint32_t end = run ? q + 1 + (isf ? 8 * cnt : 0u) : q;
-        const uint32_t left = n - w - 1;
-        if (p < pe && end <= pe && cnt <= left) {
-            S.dpos[wb + w] = (uint16_t)p;
-            const uint32_t r0 = wb + w + 1, r1 = r0 + cnt;
-            uint32_t bnd = (r0 + 63) & ~63u;
-            if (bnd < r1) {  // the run covers a group boundary
-                for (; bnd < r1; bnd += 64)
+        const uint32_t end = q + (uint32_t)(isz | isf) + (isf ? 8 * cnt : 0u);
+        const uint32_t wn = w + 1 + cnt;
+        if (end <= pe && wn <= wend) {
+            S.dpos[w] = (uint16_t)p;
+            if ((w >> 6) != ((wn - 1) >> 6)) {  // the run covers a group boundary
+                for (uint32_t bnd = (w + 64) & ~63u; bnd < wn; bnd += 64)
                     S.dpos[bnd] = isz ? kContZero
-                                      : (uint16_t)(kContLit | (q + 1 + 8 * (bnd - r0)));
+                                      : (uint16_t)(kContLit | (q + 1 + 8 * (bnd - w - 1)));
             }
-            w += 1 + cnt;
+            w = wn;
             p = end;
-            go = w < n;
+            go = w < wend;
         } else {
-            st = record_error(p, q, pe, run, isf, cnt, left);
+            st = record_error(p, q, pe, isz || isf, isf, cnt, wend - w - 1);
             go = false;
         }
     }
@@ -320,7 +322,7 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
                       W1 - W0 <= kTileWords;
     if (!fits) {
 #if UNPACK_PROF
-        if (tid == 0) atomicAdd(&g_uprof[4], 1ull);
+        if (tid == 0 && g_utrace) g_utrace[blockIdx.x * 8 + 4] = 1;
 #endif
         for (uint64_t c0 = ca + (uint64_t)wave * CAPNP_WAVE; c0 < cb;
              c0 += (uint64_t)kWaves * CAPNP_WAVE)
@@ -356,9 +358,19 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
     }
     __syncthreads();
     UPROF_T(t1);
-    // walk: lane j of wave 0 follows chunk j
-    if (tid < nc) {
-        const uint64_t c = ca + tid;
+    // walk: lane j of one wave follows chunk j.  The walking wave rotates
+    // with the tile so that the walks of the workgroups sharing a CU spread
+    // over its four SIMDs instead of all landing on wave 0's.
+#ifndef UNPACK_ROTATE_WALKER
+#define UNPACK_ROTATE_WALKER 1
+#endif
+#if UNPACK_ROTATE_WALKER
+    const uint32_t walker = blockIdx.x & (kWaves - 1);
+#else
+    const uint32_t walker = 0;
+#endif
+    if (wave == walker && lane < nc) {
+        const uint64_t c = ca + lane;
         const uint64_t gp = in_off[c], ge = in_off[c + 1];
         const uint64_t ow = out_off[c], oe = out_off[c + 1];
         int32_t st;
@@ -402,11 +414,12 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
 #if UNPACK_PROF
     __syncthreads();
     UPROF_T(t3);
-    if (tid == 0) {
-        atomicAdd(&g_uprof[0], (unsigned long long)(t1 - t0));
-        atomicAdd(&g_uprof[1], (unsigned long long)(t2 - t1));
-        atomicAdd(&g_uprof[2], (unsigned long long)(t3 - t2));
-        atomicAdd(&g_uprof[3], 1ull);
+    if (tid == 0 && g_utrace) {
+        uint64_t* tr = g_utrace + blockIdx.x * 8;
+        tr[0] = t0;
+        tr[1] = t1;
+        tr[2] = t2;
+        tr[3] = t3;
     }
 #endif
 }
@@ -427,6 +440,10 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
 }
 
 #if UNPACK_PROF
+extern "C" hipError_t capnp_unpack_trace(uint64_t* d_buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_utrace), &d_buf, sizeof(d_buf));
+}
+
 extern "C" hipError_t capnp_unpack_prof(unsigned long long* host8, int reset) {
     hipError_t e = hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_uprof), sizeof(g_uprof));
     if (e == hipSuccess && reset) {

@@ -24,7 +24,7 @@ def main():
     a = ap.parse_args()
     import torch
     from capnp_amd import Context, unpack_tile_chunks_for
-    L = C.CDLL(os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_uprof.so"))
+    L = C.CDLL(os.path.join(ROOT, "capnproto-rust_amd/build/libcapnp_packed_uprof.so"))
     vp, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
     L.capnp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int)]
     L.capnp_ctx_create.restype = vp
@@ -42,6 +42,10 @@ def main():
     status = torch.empty(n, dtype=torch.int32, device="cuda")
     utc = a.utc or unpack_tile_chunks_for(n * cw, n)
     buf = (C.c_ulonglong * 8)()
+    ntiles = (n + utc - 1) // utc
+    trace = torch.zeros(ntiles * 8, dtype=torch.int64, device="cuda")
+    L.capnp_unpack_trace.argtypes = [vp]
+    L.capnp_unpack_trace(C.c_void_p(trace.data_ptr()))
     stream = torch.cuda.current_stream()
     P = C.c_void_p
     for it in range(a.iters + 1):
@@ -59,12 +63,15 @@ def main():
         if it == 0:
             continue
         ok = torch.equal(back, words)
-        tiles = max(buf[3], 1)
-        tot = buf[0] + buf[1] + buf[2]
-        print(f"iter {it}: {e0.elapsed_time(e1) * 1e3:.1f} us ok={ok} staged={buf[3]} "
-              f"global={buf[4]} cycles/tile: stage={buf[0] / tiles:.0f} walk={buf[1] / tiles:.0f} "
-              f"expand={buf[2] / tiles:.0f} ({100 * buf[1] / max(tot, 1):.0f}% walk)")
-
+        T = trace.view(ntiles, 8).cpu().numpy().astype("int64")
+        st = T[:, 4] == 0
+        d = lambda a, b: (T[st, b] - T[st, a]).mean() / 100.0
+        life = (T[st, 3] - T[st, 0]) / 100.0
+        span = (T[st, 3].max() - T[st, 0].min()) / 100.0
+        print(f"iter {it}: {e0.elapsed_time(e1) * 1e3:.1f} us ok={ok} staged={st.sum()} "
+              f"global={(~st).sum()} per tile: stage={d(0, 1):.2f}us walk={d(1, 2):.2f}us "
+              f"expand={d(2, 3):.2f}us life={life.mean():.2f}us "
+              f"concurrency={life.sum() / max(span, 1e-9):.0f}")
 
 if __name__ == "__main__":
     main()
