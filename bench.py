@@ -238,6 +238,7 @@ def main():
 def end_to_end(ctx, torch, words, offs, n, cw, tc, dev):
     """Host pinned buffer -> H2D -> pack -> D2H and back (PCIe-bound).
     Reported in DESIGN.md only; never the headline value."""
+    from capnp_amd import unpack_tile_chunks_for
     U = n * cw * 8
     h_words = torch.empty(n * cw, dtype=torch.int64, pin_memory=True)
     h_words.copy_(words)
