@@ -28,6 +28,7 @@ EXPORTS = [
     "capnp_packed_write_message", "capnp_packed_read_message",
     "capnp_packed_read_message_no_alloc", "capnp_gpu_gen_batch", "capnp_gpu_pack_batch_tuned",
     "capnp_ctx_reserve", "capnp_pack_tile_words", "capnp_gpu_unpack_batch_tuned",
+    "capnp_unpack_tile_words",
 ]
 
 
@@ -82,6 +83,8 @@ def lib():
     L.capnp_ctx_reserve.argtypes = [vp, sz]
     L.capnp_pack_tile_words.argtypes = []
     L.capnp_pack_tile_words.restype = C.c_uint32
+    L.capnp_unpack_tile_words.argtypes = []
+    L.capnp_unpack_tile_words.restype = C.c_uint32
     L.capnp_pack.argtypes = [vp, vp, sz, vp, sz, C.POINTER(C.c_size_t)]
     L.capnp_unpack.argtypes = [vp, vp, sz, C.POINTER(C.c_size_t), vp, sz]
     L.capnp_pack_batch_host.argtypes = [vp, vp, vp, sz, vp, sz, vp]

@@ -93,7 +93,7 @@ class Context:
 
     def unpack_batch_into(self, packed, in_byte_off, out_word_off, words, status,
                           consumed=None, chunks_per_tile=0, stream=None):
-        """Enqueue UNPACK; chunks_per_tile 0 = library default (32)."""
+        """Enqueue UNPACK; chunks_per_tile 0 = library default."""
         n = in_byte_off.numel() - 1
         st = _lib.lib().capnp_gpu_unpack_batch_tuned(
             self._h, _ptr(packed), _ptr(in_byte_off), n, _ptr(words), _ptr(out_word_off),
@@ -145,13 +145,14 @@ def tile_chunks_for(total_words, nchunks, lib=None):
     return int(max(1, min(64, tw // mean)))
 
 
-def unpack_tile_chunks_for(total_words, nchunks):
-    """Chunks per unpack workgroup: about 4096 output words per tile (the
-    staged path's descriptor capacity, unpack.hip kTileWords)."""
+def unpack_tile_chunks_for(total_words, nchunks, lib=None):
+    """Chunks per unpack workgroup: about capnp_unpack_tile_words() output
+    words per tile (the staged path's descriptor capacity, unpack.hip)."""
+    tw = (lib or _lib.lib()).capnp_unpack_tile_words()
     if nchunks <= 0:
-        return 32
+        return max(1, tw // 128)
     mean = max(total_words / nchunks, 1.0)
-    return int(max(1, min(256, 4096 // mean)))
+    return int(max(1, min(64, tw // mean)))
 
 
 _default = {}

@@ -218,8 +218,18 @@ constexpr uint32_t kMaxTileChunks = kWaves * CAPNP_WAVE;
 // ---------------------------------------------------------------------------
 // Staged path.
 
-constexpr uint32_t kTileBytes = 20000;   // LDS capacity for a tile's packed bytes
-constexpr uint32_t kTileWords = 4096;    // descriptor capacity (output words)
+// Tile tables sized for UNPACK_TILE_WORDS output words (~4.5 packed bytes per
+// word of capacity: P/U up to 0.56).  The walk and the expansion are latency
+// chains, so throughput scales with resident workgroups: smaller tiles, more
+// of them per CU (2048 words: ~16 KB of LDS, 9 workgroups per CU).
+#ifndef UNPACK_TILE_WORDS
+#define UNPACK_TILE_WORDS 2048
+#endif
+constexpr uint32_t kTileWords = UNPACK_TILE_WORDS;   // descriptor capacity (output words)
+constexpr uint32_t kTileBytes = kTileWords * 9 / 2;  // LDS capacity for packed bytes
+// The global path (tiles that do not fit) runs on as many waves as the
+// staged tables' LDS can hold descriptor tables for (8 KiB each).
+constexpr uint32_t kGlobalWaves = kTileWords >= 4096 ? 4 : 2;
 constexpr uint32_t kStageChunks = 64;    // walkers: one lane of wave 0 per chunk
 
 // Descriptor of an output word (u16): the LDS position of its record's tag
@@ -238,7 +248,7 @@ struct StageSmem {
 
 union USmem {
     StageSmem st;
-    uint16_t desc[kWaves][CAPNP_WAVE][CAPNP_WAVE];  // global path
+    uint16_t desc[kGlobalWaves][CAPNP_WAVE][CAPNP_WAVE];  // global path
 };
 
 // 8 bytes at LDS byte position `pos` (two aligned 8-byte reads, funnel).
@@ -324,8 +334,9 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
 #if UNPACK_PROF
         if (tid == 0 && g_utrace) g_utrace[blockIdx.x * 8 + 4] = 1;
 #endif
+        if (wave >= kGlobalWaves) return;
         for (uint64_t c0 = ca + (uint64_t)wave * CAPNP_WAVE; c0 < cb;
-             c0 += (uint64_t)kWaves * CAPNP_WAVE)
+             c0 += (uint64_t)kGlobalWaves * CAPNP_WAVE)
             unpack_global(in, in_off, c0, cb, out, out_off, status, consumed, sm.desc[wave],
                           lane);
         return;
@@ -426,15 +437,23 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
 
 }  // namespace
 
+// Output words per unpack tile the staged path is sized for; the host picks
+// chunks_per_tile ~ this / mean chunk words.
+extern "C" uint32_t capnp_unpack_tile_words(void) { return kTileWords; }
+
 extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d_in_off,
                                           uint64_t nchunks, uint32_t tc, uint64_t* d_out,
                                           const uint64_t* d_out_off, int32_t* d_status,
                                           uint64_t* d_consumed, hipStream_t stream) {
     if (nchunks == 0) return hipSuccess;
-    if (tc == 0) tc = 32;
+    if (tc == 0) tc = kTileWords / 128;
     if (tc > kMaxTileChunks) return hipErrorInvalidValue;  // global path: 4 waves x 64
     const uint64_t blocks = (nchunks + tc - 1) / tc;
-    hipLaunchKernelGGL(unpack_kernel, dim3((uint32_t)blocks), dim3(kThreads), 0, stream, d_in,
+#ifndef UNPACK_EXTRA_LDS
+#define UNPACK_EXTRA_LDS 0  // diagnostic: dynamic LDS padding to cap workgroups per CU
+#endif
+    hipLaunchKernelGGL(unpack_kernel, dim3((uint32_t)blocks), dim3(kThreads), UNPACK_EXTRA_LDS,
+                       stream, d_in,
                        d_in_off, nchunks, tc, d_out, d_out_off, d_status, d_consumed);
     return hipGetLastError();
 }

@@ -31,14 +31,18 @@ capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
                                         void* stream);
 
 /* capnp_gpu_unpack_batch with an explicit tile size (chunks per 256-thread
- * workgroup, 1..256; 0 = default 32).  A tile takes the LDS-staged path when
- * its packed bytes fit 20000 B and its output 4096 words; pick about
- * 4096 / mean_chunk_words. */
+ * workgroup, 1..256; 0 = default).  A tile takes the LDS-staged path when it
+ * has <= 64 chunks, <= capnp_unpack_tile_words() output words and <= 4.5x
+ * that many packed bytes; pick about capnp_unpack_tile_words() / mean chunk
+ * words. */
 capnp_status capnp_gpu_unpack_batch_tuned(capnp_ctx* ctx, const uint8_t* d_packed,
                                           const uint64_t* d_in_byte_off, size_t nchunks,
                                           uint64_t* d_words, const uint64_t* d_out_word_off,
                                           int32_t* d_status, uint64_t* d_consumed,
                                           uint32_t chunks_per_tile, void* stream);
+
+/* Output words per unpack tile the staged path is sized for. */
+uint32_t capnp_unpack_tile_words(void);
 
 /* Words per pack tile the staged path is sized for (4 waves x steps of 64
  * words); chunks_per_tile ~ this / mean chunk words. */

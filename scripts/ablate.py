@@ -28,6 +28,8 @@ def load(path):
         L.capnp_gpu_unpack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, u32, vp]
     L.capnp_ctx_reserve.argtypes = [vp, sz]
     L.capnp_pack_tile_words.restype = C.c_uint32
+    if hasattr(L, "capnp_unpack_tile_words"):
+        L.capnp_unpack_tile_words.restype = C.c_uint32
     st = C.c_int(0)
     ctx = L.capnp_ctx_create(0, C.byref(st))
     assert ctx, st.value
@@ -84,7 +86,7 @@ def main():
                             L.capnp_gpu_unpack_batch_tuned(
                                 h, P(packed.data_ptr()), P(ref_oo.data_ptr()), n,
                                 P(back.data_ptr()), P(offs.data_ptr()), P(status.data_ptr()),
-                                None, a.utc or unpack_tile_chunks_for(n * cw, n),
+                                None, a.utc or unpack_tile_chunks_for(n * cw, n, L),
                                 P(stream.cuda_stream))
                         else:
                             L.capnp_gpu_unpack_batch(h, P(packed.data_ptr()), P(ref_oo.data_ptr()),

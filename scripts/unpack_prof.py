@@ -21,10 +21,11 @@ def main():
     ap.add_argument("--pz", type=int, default=1288490189)
     ap.add_argument("--utc", type=int, default=0)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--lib", default="")
     a = ap.parse_args()
     import torch
     from capnp_amd import Context, unpack_tile_chunks_for
-    L = C.CDLL(os.path.join(ROOT, "capnproto-rust_amd/build/libcapnp_packed_uprof.so"))
+    L = C.CDLL(a.lib or os.path.join(ROOT, "capnproto-rust_amd/build/libcapnp_packed_uprof.so"))
     vp, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
     L.capnp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int)]
     L.capnp_ctx_create.restype = vp
