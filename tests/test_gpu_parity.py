@@ -300,3 +300,72 @@ def test_full_size_config_round_trip(ctx, pz):
         w = O.gen_fill(np.array([0, cw], np.uint64), pz=pz, id0=int(c))
         st, k = O.pack(w.tobytes())
         assert pk[po[c]:po[c + 1]].tobytes() == k
+
+
+def _check_sampled(packed, poffs, ids_kinds, pz, cw_of):
+    po = poffs.cpu().numpy()
+    for c, kind in ids_kinds:
+        w = O.gen_fill(np.array([0, cw_of(c)], np.uint64), kinds=np.array([kind], np.uint8),
+                       pz=pz, id0=int(c))
+        st, k = O.pack(w.tobytes())
+        got = packed[int(po[c]):int(po[c + 1])].cpu().numpy().tobytes()
+        assert got == k, f"chunk {c} (kind {kind}, {cw_of(c)} words) differs"
+
+
+def test_config3_high_sparsity_4gib_packed(ctx):
+    """BASELINE config 3: >= 80 % zero words, 4 GiB of packed input
+    (~23.4 Mi chunks x 1 KiB, ~22 GiB unpacked): device round trip, status,
+    consumed bytes, and 512 sampled chunks byte-equal to the oracle."""
+    from capnp_amd import unpack_tile_chunks_for
+    cw = 128
+    n = 23_400_000
+    offs = torch.arange(0, (n + 1) * cw, cw, dtype=torch.int64, device="cuda")
+    words = torch.empty(n * cw, dtype=torch.int64, device="cuda")
+    ctx.gen_batch(words, offs, pz_thresh=O.PZ80)
+    packed, poffs = ctx.pack_batch(words, offs)
+    assert packed.numel() >= 4 * 10**9 * 0.93
+    back = torch.empty_like(words)
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    consumed = torch.empty(n, dtype=torch.int64, device="cuda")
+    ctx.unpack_batch_into(packed, poffs, offs, back, status, consumed,
+                          chunks_per_tile=unpack_tile_chunks_for(n * cw, n))
+    torch.cuda.synchronize()
+    assert int((status != 0).sum()) == 0
+    assert torch.equal(back, words)
+    assert torch.equal(consumed, poffs[1:] - poffs[:-1])
+    del back, words
+    idx = np.random.default_rng(3).choice(n, 512, replace=False)
+    _check_sampled(packed, poffs, [(int(c), 0) for c in idx], O.PZ80, lambda c: cw)
+
+
+def test_config4_mixed_sizes_round_trip(ctx):
+    """BASELINE config 4: chunk sizes log-uniform in [8, 8192] words (64 B -
+    64 KiB), ~1 GiB, 80 % config-2 words / 10 % long zero runs / 10 % long
+    literal runs: round trip and sampled chunks (the largest included)
+    byte-equal to the oracle."""
+    from capnp_amd import tile_chunks_for, unpack_tile_chunks_for
+    rng = np.random.default_rng(4)
+    target = (1 << 30) // 8
+    sizes = []
+    total = 0
+    while total < target:
+        s = int(np.exp(rng.uniform(np.log(8), np.log(8193))))
+        sizes.append(s)
+        total += s
+    n = len(sizes)
+    kinds = rng.choice(3, size=n, p=[0.8, 0.1, 0.1]).astype(np.uint8)
+    offs_h = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    offs = dev(offs_h)
+    words = torch.empty(total, dtype=torch.int64, device="cuda")
+    ctx.gen_batch(words, offs, pz_thresh=O.PZ30, kinds=torch.from_numpy(kinds).cuda())
+    packed, poffs = ctx.pack_batch(words, offs, chunks_per_tile=tile_chunks_for(total, n))
+    back, status, consumed = ctx.unpack_batch(packed, poffs, offs,
+                                              chunks_per_tile=unpack_tile_chunks_for(total, n))
+    torch.cuda.synchronize()
+    assert int((status != 0).sum()) == 0
+    assert torch.equal(back, words)
+    assert torch.equal(consumed, poffs[1:] - poffs[:-1])
+    big = np.argsort(sizes)[-32:]
+    idx = np.concatenate([big, rng.choice(n, 224, replace=False)])
+    _check_sampled(packed, poffs, [(int(c), int(kinds[c])) for c in idx], O.PZ30,
+                   lambda c: sizes[c])
