@@ -283,17 +283,26 @@ __device__ __forceinline__ void walk_chunk(StageSmem& S, uint32_t p, uint32_t pe
     st = ST_OK;
     if (n > 0 && p == pe) st = ST_FAILED_FILL;  // read() returns Ok(0)
     bool go = n > 0 && st == ST_OK;
-    while (go) {
-        // three independent reads in flight together (the empty asm keeps
-        // the compiler from reading the count byte after the tag, in a branch)
-        uint32_t tag = S.bytes[p];
-        uint32_t b1 = S.bytes[p + 1];
-        uint32_t b9 = S.bytes[p + 9];
+    // Software-pipelined: the next record's three bytes are requested as soon
+    // as its position is known, before this record's checks, descriptor
+    // write and loop control, which then overlap the LDS latency.  (The
+    // empty asm statements pin the reads where they are written.)
+    uint32_t tag = 0, b1 = 0, b9 = 0;
+    if (go) {
+        tag = S.bytes[p];
+        b1 = S.bytes[p + 1];
+        b9 = S.bytes[p + 9];
         asm volatile("" : "+v"(tag), "+v"(b1), "+v"(b9));
+    }
+    while (go) {
         const uint32_t q = p + 1 + __builtin_popcount(tag);
         const bool isz = tag == 0, isf = tag == 0xFF;
         const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
         const uint32_t end = q + (uint32_t)(isz | isf) + (isf ? 8 * cnt : 0u);
+        const uint32_t pn = end < pe ? end : p;  // stays inside the staged bytes
+        const uint32_t ntag = S.bytes[pn];
+        const uint32_t nb1 = S.bytes[pn + 1];
+        const uint32_t nb9 = S.bytes[pn + 9];
         const uint32_t wn = w + 1 + cnt;
         if (end <= pe && wn <= wend) {
             S.dpos[w] = (uint16_t)p;
@@ -309,6 +318,9 @@ __device__ __forceinline__ void walk_chunk(StageSmem& S, uint32_t p, uint32_t pe
             st = record_error(p, q, pe, isz || isf, isf, cnt, wend - w - 1);
             go = false;
         }
+        tag = ntag;
+        b1 = nb1;
+        b9 = nb9;
     }
     used = st == ST_OK ? p - p0 : (st == ST_FAILED_FILL ? pe - p0 : 0);
 }
