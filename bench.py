@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time host->device->host")
+    ap.add_argument("--no-sync", action="store_true",
+                    help="pack without the record sync index; unpack walks whole chunks")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     return ap.parse_args()
 
@@ -123,6 +125,9 @@ def main():
     back = torch.empty(total_words, dtype=torch.int64, device=dev)
     status = torch.empty(n, dtype=torch.int32, device=dev)
     consumed = torch.empty(n, dtype=torch.int64, device=dev)
+    sync = None
+    if not args.no_sync:
+        sync = torch.empty(ctx.sync_entries(total_words), dtype=torch.int32, device=dev)
     tc = tile_chunks_for(total_words, n)
     utc = unpack_tile_chunks_for(total_words, n)
     ctx.reserve(n)
@@ -134,10 +139,11 @@ def main():
         if record:
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record(stream)
-        ctx.pack_batch_into(words, offs, packed, poffs, chunks_per_tile=tc)
+        ctx.pack_batch_into(words, offs, packed, poffs, chunks_per_tile=tc, sync=sync)
         if record:
             e[1].record(stream)
-        ctx.unpack_batch_into(packed, poffs, offs, back, status, consumed, chunks_per_tile=utc)
+        ctx.unpack_batch_into(packed, poffs, offs, back, status, consumed, chunks_per_tile=utc,
+                              sync=sync)
         if record:
             e[2].record(stream)
             ev.append(e)

@@ -28,7 +28,9 @@ EXPORTS = [
     "capnp_packed_write_message", "capnp_packed_read_message",
     "capnp_packed_read_message_no_alloc", "capnp_gpu_gen_batch", "capnp_gpu_pack_batch_tuned",
     "capnp_ctx_reserve", "capnp_pack_tile_words", "capnp_gpu_unpack_batch_tuned",
-    "capnp_unpack_tile_words",
+    "capnp_unpack_tile_words", "capnp_sync_index_entries", "capnp_gpu_pack_batch_sync",
+    "capnp_gpu_unpack_batch_sync", "capnp_gpu_pack_batch_sync_tuned",
+    "capnp_gpu_unpack_batch_sync_tuned",
 ]
 
 
@@ -80,6 +82,12 @@ def lib():
     L.capnp_gpu_unpack_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.capnp_gpu_unpack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, C.c_uint32, vp]
     L.capnp_gpu_gen_batch.argtypes = [vp, vp, vp, sz, u64, vp, u32, u32, vp]
+    L.capnp_sync_index_entries.argtypes = [sz]
+    L.capnp_sync_index_entries.restype = sz
+    L.capnp_gpu_pack_batch_sync.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, vp]
+    L.capnp_gpu_unpack_batch_sync.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, vp]
+    L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, u32, vp]
+    L.capnp_gpu_unpack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, u32, vp]
     L.capnp_ctx_reserve.argtypes = [vp, sz]
     L.capnp_pack_tile_words.argtypes = []
     L.capnp_pack_tile_words.restype = C.c_uint32

@@ -81,23 +81,45 @@ class Context:
         return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
     # ---- device batch API (torch tensors in HBM) -----------------------
+    @staticmethod
+    def sync_entries(total_words):
+        """Entries of the record sync index for a batch of total_words words
+        (int32 tensor of this length; include/capnp_packed.h)."""
+        return _lib.lib().capnp_sync_index_entries(int(total_words))
+
     def pack_batch_into(self, words, chunk_word_off, out, out_off, chunks_per_tile=0,
-                        stream=None):
-        """Enqueue PACK; `out` (uint8) and `out_off` (int64, n+1) are preallocated."""
+                        stream=None, sync=None):
+        """Enqueue PACK; `out` (uint8) and `out_off` (int64, n+1) are
+        preallocated; `sync` (int32, sync_entries(total words)) receives the
+        record sync index when given."""
         n = chunk_word_off.numel() - 1
         L = _lib.lib()
-        st = L.capnp_gpu_pack_batch_tuned(self._h, _ptr(words), _ptr(chunk_word_off), n,
-                                          _ptr(out), out.numel(), _ptr(out_off),
-                                          int(chunks_per_tile), self._stream(stream))
+        if sync is None:
+            st = L.capnp_gpu_pack_batch_tuned(self._h, _ptr(words), _ptr(chunk_word_off), n,
+                                              _ptr(out), out.numel(), _ptr(out_off),
+                                              int(chunks_per_tile), self._stream(stream))
+        else:
+            st = L.capnp_gpu_pack_batch_sync_tuned(self._h, _ptr(words), _ptr(chunk_word_off),
+                                                   n, _ptr(out), out.numel(), _ptr(out_off),
+                                                   _ptr(sync), int(chunks_per_tile),
+                                                   self._stream(stream))
         _check(st, self._h)
 
     def unpack_batch_into(self, packed, in_byte_off, out_word_off, words, status,
-                          consumed=None, chunks_per_tile=0, stream=None):
-        """Enqueue UNPACK; chunks_per_tile 0 = library default."""
+                          consumed=None, chunks_per_tile=0, stream=None, sync=None):
+        """Enqueue UNPACK; chunks_per_tile 0 = library default; `sync` = the
+        record sync index from pack_batch_into (same word offsets), optional."""
         n = in_byte_off.numel() - 1
-        st = _lib.lib().capnp_gpu_unpack_batch_tuned(
-            self._h, _ptr(packed), _ptr(in_byte_off), n, _ptr(words), _ptr(out_word_off),
-            _ptr(status), _ptr(consumed), int(chunks_per_tile), self._stream(stream))
+        L = _lib.lib()
+        if sync is None:
+            st = L.capnp_gpu_unpack_batch_tuned(
+                self._h, _ptr(packed), _ptr(in_byte_off), n, _ptr(words), _ptr(out_word_off),
+                _ptr(status), _ptr(consumed), int(chunks_per_tile), self._stream(stream))
+        else:
+            st = L.capnp_gpu_unpack_batch_sync_tuned(
+                self._h, _ptr(packed), _ptr(in_byte_off), n, _ptr(words), _ptr(out_word_off),
+                _ptr(sync), _ptr(status), _ptr(consumed), int(chunks_per_tile),
+                self._stream(stream))
         _check(st, self._h)
 
     def pack_batch(self, words, chunk_word_off, chunks_per_tile=0):

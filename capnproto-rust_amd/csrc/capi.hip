@@ -21,12 +21,13 @@
 #include "frame.h"
 
 extern "C" hipError_t capnp_launch_pack(const uint64_t*, const uint64_t*, uint64_t, uint32_t,
-                                        uint8_t*, uint64_t, uint64_t*, uint64_t*, hipStream_t);
+                                        uint8_t*, uint64_t, uint64_t*, uint64_t*, uint32_t*,
+                                        hipStream_t);
 extern "C" uint32_t capnp_pack_tile_words(void);
 extern "C" size_t capnp_pack_state_bytes(uint64_t, uint32_t);
 extern "C" hipError_t capnp_launch_unpack(const uint8_t*, const uint64_t*, uint64_t, uint32_t,
                                           uint64_t*, const uint64_t*, int32_t*, uint64_t*,
-                                          hipStream_t);
+                                          const uint32_t*, hipStream_t);
 extern "C" hipError_t capnp_launch_gen(uint64_t*, const uint64_t*, uint64_t, uint64_t,
                                        const uint8_t*, uint32_t, uint32_t, hipStream_t);
 extern "C" hipError_t capnp_launch_frame(const uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t,
@@ -120,7 +121,7 @@ size_t state_bytes_for(size_t nchunks, uint32_t tc) {
 
 capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint64_t* d_off,
                             size_t n, uint8_t* d_out, size_t cap, uint64_t* d_out_off,
-                            uint32_t tc, hipStream_t s) {
+                            uint32_t tc, hipStream_t s, uint32_t* d_sync = nullptr) {
     if (tc == 0) tc = kDefaultTileChunks;
     if (tc > kMaxTileChunks) return CAPNP_E_INVALID_ARGUMENT;
     if (n > 0 && !d_off) return CAPNP_E_INVALID_ARGUMENT;
@@ -129,7 +130,7 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
     capnp_status st = ensure_state(ctx, sb);
     if (st != CAPNP_OK) return st;
     HIP_TRY(capnp_launch_pack(d_words, d_off, n, tc, d_out, cap, d_out_off,
-                              reinterpret_cast<uint64_t*>(ctx->d_state), s));
+                              reinterpret_cast<uint64_t*>(ctx->d_state), d_sync, s));
     return CAPNP_OK;
 }
 
@@ -271,12 +272,12 @@ static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
                                      const uint64_t* d_in_byte_off, size_t nchunks,
                                      uint64_t* d_words, const uint64_t* d_out_word_off,
                                      int32_t* d_status, uint64_t* d_consumed, uint32_t tc,
-                                     void* stream) {
+                                     void* stream, const uint32_t* d_sync = nullptr) {
     if (!ctx || (nchunks && (!d_in_byte_off || !d_out_word_off || !d_status)))
         return CAPNP_E_INVALID_ARGUMENT;
     if (tc > 256) return CAPNP_E_INVALID_ARGUMENT;
     HIP_TRY(capnp_launch_unpack(d_packed, d_in_byte_off, nchunks, tc, d_words, d_out_word_off,
-                                d_status, d_consumed, pick(ctx, stream)));
+                                d_status, d_consumed, d_sync, pick(ctx, stream)));
     return CAPNP_OK;
 }
 
@@ -295,6 +296,50 @@ capnp_status capnp_gpu_unpack_batch_tuned(capnp_ctx* ctx, const uint8_t* d_packe
                                           uint32_t chunks_per_tile, void* stream) {
     return unpack_batch_dev(ctx, d_packed, d_in_byte_off, nchunks, d_words, d_out_word_off,
                             d_status, d_consumed, chunks_per_tile, stream);
+}
+
+size_t capnp_sync_index_entries(size_t total_words) {
+    return (total_words + CAPNP_SYNC_WORDS - 1) / CAPNP_SYNC_WORDS;
+}
+
+capnp_status capnp_gpu_pack_batch_sync(capnp_ctx* ctx, const uint64_t* d_words,
+                                       const uint64_t* d_chunk_word_off, size_t nchunks,
+                                       uint8_t* d_out, size_t out_cap, uint64_t* d_out_byte_off,
+                                       uint32_t* d_sync, void* stream) {
+    if (!ctx || !d_sync) return CAPNP_E_INVALID_ARGUMENT;
+    return pack_batch_dev(ctx, d_words, d_chunk_word_off, nchunks, d_out, out_cap,
+                          d_out_byte_off, kDefaultTileChunks, pick(ctx, stream), d_sync);
+}
+
+capnp_status capnp_gpu_unpack_batch_sync(capnp_ctx* ctx, const uint8_t* d_packed,
+                                         const uint64_t* d_in_byte_off, size_t nchunks,
+                                         uint64_t* d_words, const uint64_t* d_out_word_off,
+                                         const uint32_t* d_sync, int32_t* d_status,
+                                         uint64_t* d_consumed, void* stream) {
+    if (!d_sync) return CAPNP_E_INVALID_ARGUMENT;
+    return unpack_batch_dev(ctx, d_packed, d_in_byte_off, nchunks, d_words, d_out_word_off,
+                            d_status, d_consumed, 0, stream, d_sync);
+}
+
+capnp_status capnp_gpu_pack_batch_sync_tuned(capnp_ctx* ctx, const uint64_t* d_words,
+                                             const uint64_t* d_chunk_word_off, size_t nchunks,
+                                             uint8_t* d_out, size_t out_cap,
+                                             uint64_t* d_out_byte_off, uint32_t* d_sync,
+                                             uint32_t chunks_per_tile, void* stream) {
+    if (!ctx || !d_sync) return CAPNP_E_INVALID_ARGUMENT;
+    return pack_batch_dev(ctx, d_words, d_chunk_word_off, nchunks, d_out, out_cap,
+                          d_out_byte_off, chunks_per_tile, pick(ctx, stream), d_sync);
+}
+
+capnp_status capnp_gpu_unpack_batch_sync_tuned(capnp_ctx* ctx, const uint8_t* d_packed,
+                                               const uint64_t* d_in_byte_off, size_t nchunks,
+                                               uint64_t* d_words, const uint64_t* d_out_word_off,
+                                               const uint32_t* d_sync, int32_t* d_status,
+                                               uint64_t* d_consumed, uint32_t chunks_per_tile,
+                                               void* stream) {
+    if (!d_sync) return CAPNP_E_INVALID_ARGUMENT;
+    return unpack_batch_dev(ctx, d_packed, d_in_byte_off, nchunks, d_words, d_out_word_off,
+                            d_status, d_consumed, chunks_per_tile, stream, d_sync);
 }
 
 capnp_status capnp_gpu_gen_batch(capnp_ctx* ctx, uint64_t* d_words, const uint64_t* d_offs,
@@ -358,7 +403,7 @@ capnp_status capnp_unpack_batch_host(capnp_ctx* ctx, const uint8_t* packed,
                                 reinterpret_cast<uint64_t*>(d + o_out),
                                 reinterpret_cast<uint64_t*>(d + o_ro),
                                 reinterpret_cast<int32_t*>(d + o_st),
-                                reinterpret_cast<uint64_t*>(d + o_cs), s));
+                                reinterpret_cast<uint64_t*>(d + o_cs), nullptr, s));
     if (oe > ob) HIP_TRY(hipMemcpyAsync(words + ob, d + o_out, (oe - ob) * 8, hipMemcpyDeviceToHost, s));
     if (n) HIP_TRY(hipMemcpyAsync(status, d + o_st, n * 4, hipMemcpyDeviceToHost, s));
     if (n && consumed) HIP_TRY(hipMemcpyAsync(consumed, d + o_cs, n * 8, hipMemcpyDeviceToHost, s));
@@ -452,7 +497,7 @@ static capnp_status read_body(capnp_ctx* ctx, const FrameResult& fr, uint8_t* ho
     HIP_TRY(capnp_launch_unpack(ctx->d_stage, ctx->d_frame->body_in_off, 1, 0,
                                 reinterpret_cast<uint64_t*>(d), ctx->d_frame->body_out_off,
                                 reinterpret_cast<int32_t*>(d + o_st),
-                                reinterpret_cast<uint64_t*>(d + o_st + 16), s));
+                                reinterpret_cast<uint64_t*>(d + o_st + 16), nullptr, s));
     int32_t status = 0;
     uint64_t used = 0;
     HIP_TRY(hipMemcpyAsync(&status, d + o_st, 4, hipMemcpyDeviceToHost, s));

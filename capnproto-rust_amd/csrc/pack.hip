@@ -38,6 +38,7 @@
 //   only known once the run ends, possibly several steps later; it is
 //   patched in LDS (the ring holds back the block that contains it).
 #include "common.h"
+#include "../../include/capnp_packed.h"
 
 #ifndef PACK_ABLATE
 #define PACK_ABLATE 0  // diagnostic builds only (scripts/ablate.py); 0 = product
@@ -87,6 +88,17 @@ constexpr uint32_t kRegion = (kStageBytes + 32 + 15) & ~15u;
 // per-wave LDS region: the staged bytes, or the streaming path's flush ring
 constexpr uint32_t kRegionBytes = kRegion > kRing ? kRegion : kRing;
 
+// Record sync index (optional side-band): one entry per global word index
+// m = 32k, for the chunk that holds word m: the chunk-relative packed offset of
+// the first record that starts at a word >= m (24 bits) and that word minus m
+// (8 bits; a run covers at most 255 words after its head, so it fits).  An
+// unpack that has the index walks 32-word segments in parallel and checks that
+// consecutive segments meet (unpack.hip).  kSyncNone marks an entry the
+// kernel does not provide (streaming path); the decoder then walks serially.
+constexpr uint32_t kSyncWords = CAPNP_SYNC_WORDS;
+constexpr uint32_t kSyncNone = 0xFFFFFFFFu;
+constexpr uint32_t kMaxSync = kWaves * 64 * kStageSteps / kSyncWords + 2;
+
 constexpr uint64_t kFlagAgg = 1ull << 62;  // tile aggregate available
 constexpr uint64_t kFlagInc = 2ull << 62;  // tile inclusive prefix available
 constexpr uint64_t kValMask = (1ull << 62) - 1;
@@ -98,6 +110,7 @@ struct Smem {
     uint64_t chunk_pos[kMaxTileChunks];
     uint64_t wave_bytes[kWaves];
     uint64_t wave_steps[kWaves];
+    uint32_t sync[kMaxSync];            // the tile's record sync entries
     // per-wave staging region; the streaming path uses its first 4 KiB as
     // the flush ring
     alignas(16) uint8_t stage[kWaves][kRegionBytes];
@@ -401,6 +414,55 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
     __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
+// Sync points whose first record lies in a later step (a run covers them).
+struct SyncPend {
+    uint32_t m = 0;  // first pending point (tile-relative word)
+    uint32_t k = 0;  // pending points: m, m + 32, ...
+};
+
+// Record sync entries of one staged step, in tile-relative words (run after
+// pass 2, so it overlaps the look-back instead of delaying the publish):
+// g = the step's lane-0 word, t0 = the first sync word of the tile (entry
+// index i <-> word t0 + kSyncWords i), si = the step's heads and byte
+// positions, oc = the chunk's start in the region, total = the chunk's bytes.
+// Lane-parallel: a lane on a sync point finds the first head at or after it
+// in the step; points with none (a run covers the rest of the step) wait for
+// a later step's first head or the chunk end.
+__device__ __forceinline__ void sync_step(uint32_t* tab, uint32_t t0, uint32_t g, uint32_t meta,
+                                          const StepInfo& si, uint32_t oc, uint32_t total,
+                                          SyncPend& ps, uint32_t lane) {
+    const uint32_t nv = meta & 127u;
+    const uint64_t H = si.H;
+    if (ps.k && H) {  // pending points end at this step's first head
+        const uint32_t h = ctz64(H);
+        const uint32_t ph = (uint32_t)__builtin_amdgcn_readlane((int)si.pos, h) - oc;
+        if (lane < ps.k) {
+            const uint32_t m = ps.m + kSyncWords * lane;
+            tab[(m - t0) / kSyncWords] = ph | ((g + h - m) << 24);
+        }
+        ps.k = 0;
+    }
+    const uint32_t sl0 = (t0 - g) & (kSyncWords - 1);
+    const bool pt = lane < nv && lane >= sl0 && ((lane - sl0) & (kSyncWords - 1)) == 0;
+    const uint64_t Hl = H >> lane;
+    const uint32_t h = lane + ctz64(Hl);
+    const uint32_t ph =
+        (uint32_t)__builtin_amdgcn_ds_bpermute((int)((h & 63u) << 2), (int)si.pos) - oc;
+    if (pt && Hl) tab[(g + lane - t0) / kSyncWords] = ph | ((h - lane) << 24);
+    const uint64_t nohead = ballot64(pt && !Hl);
+    if (nohead) {
+        if (!ps.k) ps.m = g + ctz64(nohead);
+        ps.k += popc64(nohead);
+    }
+    if (((meta >> 8) & 1) && ps.k) {  // chunk end inside a run
+        if (lane < ps.k) {
+            const uint32_t m = ps.m + kSyncWords * lane;
+            tab[(m - t0) / kSyncWords] = total | ((g + nv - m) << 24);
+        }
+        ps.k = 0;
+    }
+}
+
 // Copies region bytes [0, len) to out[D0 .. D0+len) (16-aligned coordinates),
 // never writing at or past `cap`.
 __device__ __forceinline__ void copy_out(const uint8_t* region, uint8_t* __restrict__ out,
@@ -681,7 +743,7 @@ __global__ void __launch_bounds__(kThreads, 8)
 pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
             uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
             uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts,
-            uint64_t* __restrict__ gs) {
+            uint64_t* __restrict__ gs, uint32_t* __restrict__ sync) {
     __shared__ Smem sm;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -710,6 +772,11 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     }
 #endif
     for (uint32_t i = tid; i <= nc; i += kThreads) sm.off[i] = chunk_off[c0 + i];
+    // sync entries of the tile: k in [k0, k1), words 32k in [W0, W1)
+    const uint64_t TW0 = uniform64(chunk_off[c0]);
+    const uint64_t k0 = (TW0 + kSyncWords - 1) / kSyncWords;
+    const uint64_t k1 = (uniform64(chunk_off[c1]) + kSyncWords - 1) / kSyncWords;
+    const uint32_t t0 = (uint32_t)(k0 * kSyncWords - TW0);  // first sync word, tile-relative
     for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
     // compaction selectors: byte r = index of the r-th set bit of the tag
     {
@@ -735,6 +802,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     const uint32_t wc0 = wave * q < nc ? wave * q : nc;
     const uint32_t wc1 = wc0 + q < nc ? wc0 + q : nc;
     uint64_t d_src = 0;
+    uint32_t d_g = 0;  // tile-relative word of the step's lane 0
     uint32_t d_meta = 0;
     uint32_t nsteps = 0;
     for (uint32_t ci = wc0; ci < wc1; ci++) {
@@ -745,6 +813,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         if (lane >= nsteps && k < nst) {
             const uint64_t rest = len - 64ull * k;
             d_src = woff + 64ull * k;
+            d_g = (uint32_t)(d_src - TW0);
             d_meta = (uint32_t)(rest < 64 ? rest : 64) | ((k == 0) << 7) |
                      ((k + 1 == nst) << 8) | ((ci - wc0) << 9);
         }
@@ -826,6 +895,21 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             }
         }
 #endif
+        if (sync) {  // record sync entries (overlaps the look-back)
+            SyncPend ps;
+            uint32_t oc = 0;
+#pragma unroll
+            for (uint32_t s = 0; s < kStageSteps; s++) {
+                if (s < nsteps) {
+                    const uint32_t meta = si[s].meta;
+                    if ((meta >> 7) & 1) oc = (uint32_t)__builtin_amdgcn_readlane((int)si[s].pos, 0);
+                    const uint32_t total =
+                        (meta >> 8) & 1 ? (uint32_t)lds_u64(&sm.chunk_size[wc0 + (meta >> 9)]) : 0u;
+                    sync_step(sm.sync, t0, (uint32_t)__builtin_amdgcn_readlane((int)d_g, s), meta,
+                              si[s], oc, total, ps, lane);
+                }
+            }
+        }
         if (wave == 0) {
             const uint64_t excl = lookback(LA, tile, agg, lane);
             if (lane == 0) TRACE(tile, 2, RT());
@@ -834,6 +918,8 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         }
         __syncthreads();
         for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
+        if (sync)
+            for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = sm.sync[i];
 #if PACK_ABLATE == 2
         return;  // timing-only: no output stores
 #endif
@@ -846,6 +932,8 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         if (tid == 0) TRACE(tile, 3, RT());
 #endif
     } else {
+        if (sync)
+            for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
         run_streaming<MODE_SIZE>(in, sm.off, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
                                  region, sm.sel, outa, mis, out_cap);
         __syncthreads();
@@ -883,7 +971,8 @@ extern "C" size_t capnp_pack_state_bytes(uint64_t nchunks, uint32_t tc) {
 extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_chunk_off,
                                         uint64_t nchunks, uint32_t tc, uint8_t* d_out,
                                         uint64_t out_cap, uint64_t* d_out_off,
-                                        uint64_t* d_state, hipStream_t stream) {
+                                        uint64_t* d_state, uint32_t* d_sync,
+                                        hipStream_t stream) {
     if (tc == 0 || tc > kMaxTileChunks) return hipErrorInvalidValue;
     const uint64_t ntiles = (nchunks + tc - 1) / tc;
     if (nchunks == 0) {
@@ -893,7 +982,7 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(pack_kernel, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream, d_in,
                        d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_state,
-                       d_state + ntiles);
+                       d_state + ntiles, d_sync);
     return hipGetLastError();
 }
 

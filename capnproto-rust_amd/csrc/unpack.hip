@@ -30,7 +30,11 @@
 // literal run's bytes are missing (:195-205 + io.rs:26-28) or the input is
 // empty (read() returns 0, io.rs:26-28).
 #include "common.h"
+#include "../../include/capnp_packed.h"
 
+#ifndef UNPACK_EXP
+#define UNPACK_EXP 0  // diagnostic variants of the segment walk (scripts/uvar.py)
+#endif
 #ifndef UNPACK_PROF
 #define UNPACK_PROF 0  // phase timers (scripts/unpack_prof.py); 0 = product
 #endif
@@ -233,17 +237,27 @@ constexpr uint32_t kGlobalWaves = kTileWords >= 4096 ? 4 : 2;
 constexpr uint32_t kStageChunks = 64;    // walkers: one lane of wave 0 per chunk
 
 // Descriptor of an output word (u16): the LDS position of its record's tag
-// for a record head (the tag byte gives the kind), kContLit | position of
-// the raw word for a literal run crossing a 64-word group boundary, kContZero
-// for a zero run crossing one, kNone otherwise.
+// when a record starts at the word (the tag byte gives the kind), kNone for
+// a word inside a run.  The expansion finds a run word's head as the highest
+// head at or below it in its 64-word group, or, for words before the group's
+// first head, the last head of the nearest earlier group that has one.
 constexpr uint16_t kNone = 0xFFFF;
-constexpr uint16_t kContZero = 0xFFFE;
-constexpr uint16_t kContLit = 0x8000;
+
+
+// Record sync index (pack.hip): entry k describes global word kSyncWords * k.
+constexpr uint32_t kSyncWords = CAPNP_SYNC_WORDS;
+constexpr uint32_t kSyncNone = 0xFFFFFFFFu;
+constexpr uint32_t kMaxSeg = kTileWords / kSyncWords + 2;
 
 struct StageSmem {
     uint64_t sel[256];  // expand_selector(tag): 0x00 -> zeros, 0xFF -> identity
+    uint8_t badc[kStageChunks];     // sync walk: 1 = the chunk needs the exact walk
+    uint32_t cw[kStageChunks + 1];  // sync walk: chunk word offsets (tile-relative)
+    uint32_t cp[kStageChunks + 1];  // sync walk: chunk packed offsets (LDS positions)
+    uint32_t ent[kMaxSeg];          // sync walk: entry of segment b (b >= 1)
+    uint8_t segc[kMaxSeg];          // sync walk: chunk that holds segment b's first word
     alignas(16) uint8_t bytes[kTileBytes + 16];
-    alignas(16) uint16_t dpos[kTileWords];
+    alignas(16) uint16_t dpos[kTileWords + 2 * CAPNP_WAVE];  // [kTileWords + 2 lane]: dummy slots
 };
 
 union USmem {
@@ -251,13 +265,6 @@ union USmem {
     uint16_t desc[kGlobalWaves][CAPNP_WAVE][CAPNP_WAVE];  // global path
 };
 
-// 8 bytes at LDS byte position `pos` (two aligned 8-byte reads, funnel).
-__device__ __forceinline__ uint64_t lds_load8(const uint8_t* b, uint32_t pos) {
-    const uint64_t* q = reinterpret_cast<const uint64_t*>(b + (pos & ~7u));
-    const uint32_t s = pos & 7u;
-    const uint64_t lo = q[0], hi = q[1];
-    return s ? (lo >> (8 * s)) | (hi << (64 - 8 * s)) : lo;
-}
 
 // Exact status of a record that failed the fast check in walk_chunk, in the
 // reference's order (serialize_packed.rs:109-145, :157-205).
@@ -272,9 +279,9 @@ __device__ __forceinline__ int32_t record_error(uint32_t p, uint32_t q, uint32_t
 // Walks one chunk: bytes [p, pe) of the staged tile, output words [wb, wb+n)
 // of the tile.  One hop per record: the tag and both possible count bytes
 // (p+1 for 0x00, p+9 for 0xFF) are read together, and one check
-// (record end <= pe, run end <= chunk end) covers every error; only the rare
-// continuation entries branch.  Status precedence and consumed bytes as in
-// unpack_global.
+// (record end <= pe, run end <= chunk end) covers every error.  Status
+// precedence and consumed bytes as in unpack_global.  (The exact path behind
+// walk_wave: it only runs for chunks whose fast walk failed a check.)
 __device__ __forceinline__ void walk_chunk(StageSmem& S, uint32_t p, uint32_t pe, uint32_t wb,
                                            uint32_t n, int32_t& st, uint32_t& used) {
     const uint32_t p0 = p;
@@ -306,11 +313,6 @@ __device__ __forceinline__ void walk_chunk(StageSmem& S, uint32_t p, uint32_t pe
         const uint32_t wn = w + 1 + cnt;
         if (end <= pe && wn <= wend) {
             S.dpos[w] = (uint16_t)p;
-            if ((w >> 6) != ((wn - 1) >> 6)) {  // the run covers a group boundary
-                for (uint32_t bnd = (w + 64) & ~63u; bnd < wn; bnd += 64)
-                    S.dpos[bnd] = isz ? kContZero
-                                      : (uint16_t)(kContLit | (q + 1 + 8 * (bnd - w - 1)));
-            }
             w = wn;
             p = end;
             go = w < wend;
@@ -325,11 +327,226 @@ __device__ __forceinline__ void walk_chunk(StageSmem& S, uint32_t p, uint32_t pe
     used = st == ST_OK ? p - p0 : (st == ST_FAILED_FILL ? pe - p0 : 0);
 }
 
+// Branch-free walk of the walker wave: lane = chunk, same contract as
+// walk_chunk.  Every lane runs every hop (the loop exits on a wave-uniform
+// ballot), so there is no exec-mask bookkeeping per record: a lane that has
+// finished keeps its state and sends its descriptor store to its own dummy
+// slot (one dword per lane: same-address stores from many lanes serialise).
+// The hop's dependent chain is the LDS read of the record's three bytes
+// (tag, p+1, p+9) and four VALU ops to the next position (popcount with the
+// position as accumulator, +isz, select of the 0xFF length, clamp); the
+// next reads are issued before the descriptor store, the word count and the
+// checks, which overlap their latency.  A record that would fail any check
+// stops the lane and marks it bad; bad lanes re-walk with walk_chunk, which
+// yields the exact status and consumed count.
+__device__ __forceinline__ void walk_wave(StageSmem& S, uint32_t p, uint32_t pe, uint32_t wb,
+                                          uint32_t n, int32_t& st, uint32_t& used) {
+    const uint32_t p0 = p;
+    const uint32_t wend = wb + n;
+    // q = p + 1 (the position after the tag) is the loop state: the popcount
+    // accumulates into it directly.  All selects are arithmetic (no branch).
+    uint32_t q = p + 1u;
+    uint32_t w = wb;
+    bool act = n > 0 && p < pe;
+    bool bad = n > 0 && p >= pe;
+    const uint32_t dummy = kTileWords + 2u * lane_id();
+    const uint8_t* B = S.bytes;
+    uint32_t tag = B[q - 1], b1 = B[q], b9 = B[q + 8];
+    while (ballot64(act)) {
+        const bool isz = tag == 0, isf = tag == 0xFF;
+        // end of the record + 1: q + popc + isz (+ 1 + 8 b9 for 0xFF)
+        const uint32_t fx = isf ? 8u * b9 + 1u : 0u;
+        const uint32_t qe = __builtin_popcount(tag) + q + (isz ? 1u : 0u) + fx + 1u;
+        const uint32_t qn = qe < pe + 1u ? qe : pe + 1u;
+        const uint32_t ntag = B[qn - 1], nb1 = B[qn], nb9 = B[qn + 8];
+        const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+        const uint32_t wn = w + 1u + cnt;
+        const bool ok = act && qe <= pe + 1u && wn <= wend;
+        bad = bad || (act && !ok);
+        S.dpos[ok ? w : dummy] = (uint16_t)(q - 1u);
+        q = ok ? qe : q;
+        w = ok ? wn : w;
+        act = ok && wn < wend;
+        tag = ntag;
+        b1 = nb1;
+        b9 = nb9;
+    }
+    if (bad) {
+        walk_chunk(S, p0, pe, wb, n, st, used);
+    } else {
+        st = ST_OK;
+        used = q - 1u - p0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Sync walk: with the record sync index the tile's words split into segments
+// at every multiple of 32 (global word index); lane b of the walker wave(s)
+// walks segment b from the record the index names, across chunk ends, until
+// its word reaches the segment end.  The walks are exact if they meet: lane
+// b's end state (position, word) must equal the start lane b+1 derives from
+// the index, the first segment starts at the tile's first chunk, and every
+// chunk must end exactly at its packed end.  Any mismatch, a failed record
+// check or a missing entry marks the chunk bad, and bad chunks re-walk
+// serially (walk_chunk) with exact status, so the index can only change the
+// speed, never the result.
+
+__device__ __forceinline__ void mark_bad(StageSmem& S, uint32_t c, bool& marked) {
+    S.badc[c] = 1;
+    marked = true;
+}
+
+// Start state of segment b (starting at tile word sb): chunk, position + 1,
+// word.  An unusable entry yields the end of its chunk and marks it bad.
+__device__ __forceinline__ void seg_start(StageSmem& S, uint32_t nc, uint32_t b, uint32_t sb,
+                                          uint32_t& c, uint32_t& q, uint32_t& w, bool mark,
+                                          bool& marked) {
+    c = S.segc[b];
+    if (b == 0) {
+        q = S.cp[c] + 1u;
+        w = 0;
+        return;
+    }
+    const uint32_t e = S.ent[b];
+    const uint32_t off = e & 0xFFFFFFu, d = e >> 24;
+    if (e == kSyncNone || off > S.cp[c + 1] - S.cp[c] || sb + d > S.cw[c + 1]) {
+        if (mark) mark_bad(S, c, marked);
+        q = S.cp[c + 1] + 1u;
+        w = S.cw[c + 1];
+        return;
+    }
+    q = S.cp[c] + off + 1u;
+    w = sb + d;
+}
+
+// Returns true if it marked a chunk bad.
+//
+// The hop loop is kept short: a lane hops while w < stopw = min(segment
+// end, chunk end), one compare per hop; lanes that reach stopw wait for the
+// (rare, wave-uniform) stop branch, which moves a lane at a chunk end to the
+// next chunk or retires it.  Record checks accumulate into a sticky error
+// flag (a failed record ends its chunk; the chunk is re-walked exactly).
+__device__ __forceinline__ bool walk_segment(StageSmem& S, uint32_t nc, uint32_t b, uint32_t sb,
+                                             uint32_t eb, bool last) {
+    bool marked = false;
+    uint32_t c, q, w;
+    seg_start(S, nc, b, sb, c, q, w, true, marked);
+    const uint8_t* B = S.bytes;
+    const uint32_t dummy = kTileWords + 2u * lane_id();
+    uint32_t cwe = S.cw[c + 1], cpe1 = S.cp[c + 1] + 1u;
+    uint32_t stopw = cwe < eb ? cwe : eb;
+    uint32_t tag = B[q - 1], b1 = B[q], b9 = B[q + 8];
+    bool err = false;
+    const uint64_t all = ballot64(true);
+    uint64_t done = 0;
+#if UNPACK_PROF
+    const uint64_t lt0 = __builtin_amdgcn_s_memtime();
+    uint32_t iters = 0;
+#endif
+    // Phase A: kSyncWords hops with no branch at all (a record covers >= 1
+    // word, so a lane reaches stopw within kSyncWords hops; a lane already
+    // there only sends its store to the dummy slot).  Phase B below handles
+    // chunk ends and whatever is left.
+#pragma unroll
+    for (uint32_t it = 0; it < kSyncWords; it++) {
+        const bool hop = w < stopw;
+        const bool isz = tag == 0, isf = tag == 0xFF;
+        const uint32_t fx = isf ? 8u * b9 + 1u : 0u;
+        const uint32_t qe = __builtin_popcount(tag) + q + (isz ? 1u : 0u) + fx + 1u;
+        const uint32_t qn = qe < cpe1 ? qe : cpe1;
+        const uint32_t ntag = B[qn - 1], nb1 = B[qn], nb9 = B[qn + 8];
+        const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+        const uint32_t wn0 = w + 1u + cnt;
+        err = err || (hop && (qe > cpe1 || wn0 > cwe));
+        const uint32_t wn = wn0 < cwe ? wn0 : cwe;
+        S.dpos[hop ? w : dummy] = (uint16_t)(q - 1u);
+        q = hop ? qn : q;
+        w = hop ? wn : w;
+        tag = hop ? ntag : tag;
+        b1 = hop ? nb1 : b1;
+        b9 = hop ? nb9 : b9;
+    }
+    for (;;) {
+#if UNPACK_PROF
+        iters++;
+#endif
+        const bool hop = w < stopw;
+        const uint64_t pend = ballot64(!hop) & ~done;
+        if (pend) {  // lanes at a chunk end or at their segment end
+            if (!hop && !((done >> lane_id()) & 1)) {
+                if (w == cwe) {
+                    // a non-empty chunk must end exactly at its packed end
+                    if (err || (S.cw[c] < cwe && q != cpe1)) mark_bad(S, c, marked);
+                    err = false;
+                    c++;
+                    while (c < nc && S.cw[c + 1] == w) c++;  // empty chunks: status OK
+                    if (c < nc) {
+                        cwe = S.cw[c + 1];
+                        cpe1 = S.cp[c + 1] + 1u;
+                        q = S.cp[c] + 1u;
+                        tag = B[q - 1];
+                        b1 = B[q];
+                        b9 = B[q + 8];
+                    }
+                }
+                stopw = (c < nc && cwe < eb) ? cwe : eb;
+                if (c >= nc) stopw = 0;
+            }
+            done = ballot64(w >= eb || c >= nc);
+            if (done == all) break;
+            continue;
+        }
+        const bool isz = tag == 0, isf = tag == 0xFF;
+        const uint32_t fx = isf ? 8u * b9 + 1u : 0u;
+        const uint32_t qe = __builtin_popcount(tag) + q + (isz ? 1u : 0u) + fx + 1u;
+        const uint32_t qn = qe < cpe1 ? qe : cpe1;
+#if UNPACK_EXP == 2  // one unaligned 16-byte read per record
+        typedef uint4 u4u __attribute__((aligned(1)));
+        const uint4 nv = *reinterpret_cast<const u4u*>(B + qn - 1);
+        const uint32_t ntag = nv.x & 0xFFu, nb1 = (nv.x >> 8) & 0xFFu, nb9 = (nv.z >> 8) & 0xFFu;
+#else
+        const uint32_t ntag = B[qn - 1], nb1 = B[qn], nb9 = B[qn + 8];
+#endif
+        const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+        const uint32_t wn0 = w + 1u + cnt;
+        err = err || (hop && (qe > cpe1 || wn0 > cwe));
+        const uint32_t wn = wn0 < cwe ? wn0 : cwe;  // (an overrun ends the chunk)
+#if UNPACK_EXP != 1  // 1: timing only, no descriptors
+        S.dpos[hop ? w : dummy] = (uint16_t)(q - 1u);
+#endif
+        q = hop ? qn : q;
+        w = hop ? wn : w;
+        tag = ntag;
+        b1 = nb1;
+        b9 = nb9;
+    }
+#if UNPACK_PROF
+    if (lane_id() == 0 && g_utrace) {
+        g_utrace[blockIdx.x * 8 + 5] = iters;
+        g_utrace[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memtime() - lt0;
+    }
+#endif
+    // the walks must meet
+    if (last) {
+        if (c < nc) mark_bad(S, c, marked);
+    } else {
+        uint32_t c2, q2, w2;
+        seg_start(S, nc, b + 1, eb, c2, q2, w2, false, marked);
+        // (positions and words decide: "end of chunk c" and "start of chunk
+        // c+1" are the same state)
+        if (q2 != q || w2 != w || err) {
+            if (c < nc) mark_bad(S, c, marked);
+            mark_bad(S, c2, marked);
+        }
+    }
+    return marked;
+}
+
 __global__ void __launch_bounds__(kThreads)
 unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
               uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
               const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
-              uint64_t* __restrict__ consumed) {
+              uint64_t* __restrict__ consumed, const uint32_t* __restrict__ sync) {
     __shared__ USmem sm;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -357,6 +574,10 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
     UPROF_T(t0);
     const uint32_t nbytes = (uint32_t)(B1 - B0) + off0;
     const uint32_t Wt = (uint32_t)(W1 - W0);
+    // sync segments: [0, 32 kf - W0), then 32-word blocks up to Wt
+    const uint64_t kf = W0 / kSyncWords + 1;
+    const uint32_t nseg =
+        W1 > W0 ? 1u + (uint32_t)((W1 - 1) / kSyncWords + 1 - kf) : 0u;
     // stage the tile's packed bytes: every load issued before any LDS write
     // (aligned 16-byte blocks holding at least one byte of the range never
     // cross a page), and clear the descriptors
@@ -375,6 +596,25 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
         const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
         for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
         S.sel[tid] = expand_selector(tid);
+        if (sync) {
+            // chunk tables and the tile's sync entries (segment b >= 1 starts
+            // at global word 32 (kf + b - 1))
+            if (tid <= nc) {
+                const uint32_t wa = (uint32_t)(out_off[ca + tid] - W0);
+                S.cw[tid] = wa;
+                S.cp[tid] = (uint32_t)(in_off[ca + tid] - B0) + off0;
+                // segments whose first word (max(0, b G - r0)) lies in this chunk
+                const uint32_t wz = tid < nc ? (uint32_t)(out_off[ca + tid + 1] - W0) : wa;
+                const uint32_t r0 = (uint32_t)(W0 % kSyncWords);
+                if (wz > wa) {
+                    const uint32_t blo = wa == 0 ? 0u : (wa + r0 + kSyncWords - 1) / kSyncWords;
+                    const uint32_t bhi = (wz + r0 + kSyncWords - 1) / kSyncWords;
+                    for (uint32_t bb = blo; bb < bhi; bb++) S.segc[bb] = (uint8_t)tid;
+                }
+            }
+            if (tid >= 1 && tid < nseg) S.ent[tid] = sync[kf + tid - 1];
+            if (tid < kStageChunks) S.badc[tid] = 0;
+        }
 #pragma unroll
         for (uint32_t k = 0; k < kLoads; k++)
             if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
@@ -392,47 +632,105 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
 #else
     const uint32_t walker = 0;
 #endif
-    if (wave == walker && lane < nc) {
+    if (sync) {
+        const uint32_t wrel = (wave - walker) & (kWaves - 1);
+        const uint32_t b = wrel * CAPNP_WAVE + lane;
+        bool marked = false;
+        if (b < nseg) {
+            const uint32_t sb = b == 0 ? 0u : (uint32_t)((kf + b - 1) * kSyncWords - W0);
+            const bool last = b + 1 == nseg;
+            const uint32_t eb = last ? Wt : (uint32_t)((kf + b) * kSyncWords - W0);
+            marked = walk_segment(S, nc, b, sb, eb, last);
+        }
+        const bool anybad = __syncthreads_or(marked);
+        if (tid < nc) {
+            const uint64_t c = ca + tid;
+            if (anybad && S.badc[tid]) {  // exact serial walk of the chunk
+                const uint32_t wa = S.cw[tid], wz = S.cw[tid + 1];
+                for (uint32_t i = wa; i < wz; i++) S.dpos[i] = kNone;
+                int32_t st;
+                uint32_t used;
+                walk_chunk(S, S.cp[tid], S.cp[tid + 1], wa, wz - wa, st, used);
+                status[c] = st;
+                if (consumed) consumed[c] = used;
+            } else {
+                status[c] = ST_OK;
+                if (consumed)
+                    consumed[c] = S.cw[tid + 1] > S.cw[tid] ? S.cp[tid + 1] - S.cp[tid] : 0u;
+            }
+        }
+        if (anybad) __syncthreads();
+    } else if (wave == walker && lane < nc) {  // (idle lanes stay off: their LDS traffic counts)
         const uint64_t c = ca + lane;
         const uint64_t gp = in_off[c], ge = in_off[c + 1];
         const uint64_t ow = out_off[c], oe = out_off[c + 1];
         int32_t st;
         uint32_t used;
-        walk_chunk(S, (uint32_t)(gp - B0) + off0, (uint32_t)(ge - B0) + off0,
-                   (uint32_t)(ow - W0), (uint32_t)(oe - ow), st, used);
+        walk_wave(S, (uint32_t)(gp - B0) + off0, (uint32_t)(ge - B0) + off0,
+                  (uint32_t)(ow - W0), (uint32_t)(oe - ow), st, used);
         status[c] = st;
         if (consumed) consumed[c] = used;
     }
-    __syncthreads();
+    if (!sync) __syncthreads();
     UPROF_T(t2);
-    // expand: lane = output word; 64-word groups interleaved over waves.
-    // Branch-free: every word is perm(8 bytes at src, sel[t]) with t = the
-    // head's tag for a normal head, 0xFF for literal words (identity), 0 for
-    // zero-run words (zeros).
-    for (uint32_t g = wave; g * CAPNP_WAVE < Wt; g += kWaves) {
-        const uint32_t i = g * CAPNP_WAVE + lane;
-        const bool valid = i < Wt;
-        const uint32_t d = valid ? S.dpos[i] : kNone;
-        const uint64_t hm = ballot64(d != kNone) & low_mask(lane + 1);
-        // (no entry at or below the lane only after a decode error: output
-        // unspecified, the lane's own kNone yields a zero word)
-        const uint32_t h = hm ? 63u - (uint32_t)__builtin_clzll(hm) : lane;
-        const uint32_t dh = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(h << 2), (int)d);
-        const uint32_t k = lane - h;
-        const bool cz = dh >= kContZero;                 // zero-run continuation / none
-        const bool cl = !cz && (dh & kContLit) != 0;     // literal-run continuation
-        const uint32_t pos = cz ? 0u : (dh & 0x7FFFu);
-        const uint32_t tag = S.bytes[pos];
-        const bool lit = cl || (!cz && tag == 0xFF);
-        const uint32_t t = cz ? 0u : (lit ? 0xFFu : (k == 0 ? tag : 0u));
-        const uint32_t src = cl ? pos + 8 * k : (lit && k ? pos + 2 + 8 * k : pos + 1);
-        const uint64_t v = lds_load8(S.bytes, src);
-        const uint64_t sv = S.sel[t];
-        const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-        const uint64_t word =
-            ((uint64_t)__builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32)) << 32) |
-            __builtin_amdgcn_perm(hi, lo, (uint32_t)sv);
-        if (valid) out[W0 + i] = word;
+    // expand: lane = output word; 64-word groups interleaved over waves, two
+    // groups per iteration so that their LDS round trips overlap.
+    // Branch-free per word: perm(8 bytes at src, sel[t]) with t = the head's
+    // tag at the head word, 0xFF (identity) for a literal run's raw words, 0
+    // (zeros) for a zero run's words.  src does not depend on the tag (a zero
+    // run's words read bytes they then discard), so the tag and the bytes
+    // are read together.
+    {
+        const uint32_t ng = (Wt + CAPNP_WAVE - 1) / CAPNP_WAVE;
+        for (uint32_t g0 = wave; g0 < ng; g0 += 2 * kWaves) {
+            uint32_t dh[2], k[2], ii[2];
+            bool valid[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint32_t g = g0 + u * kWaves;
+                const uint32_t i = g * CAPNP_WAVE + lane;
+                ii[u] = i;
+                valid[u] = g < ng && i < Wt;
+                const uint32_t d = valid[u] ? S.dpos[i] : kNone;
+                const uint64_t heads = ballot64(d != kNone);
+                // carry-in: the run covering the group's first words started in
+                // an earlier group (its last head); rare, a wave-uniform branch
+                uint32_t dc = kNone, hc = 0;
+                if (g < ng && !(heads & 1ull)) {
+                    for (uint32_t gg = g; gg-- > 0;) {
+                        const uint32_t d2 = S.dpos[gg * CAPNP_WAVE + lane];
+                        const uint64_t m2 = ballot64(d2 != kNone);
+                        if (m2) {
+                            const uint32_t h2 = 63u - (uint32_t)__builtin_clzll(m2);
+                            dc = (uint32_t)__builtin_amdgcn_readlane((int)d2, h2);
+                            hc = gg * CAPNP_WAVE + h2;
+                            break;
+                        }
+                    }
+                }
+                const uint64_t hm = heads & low_mask(lane + 1);
+                const uint32_t h = hm ? 63u - (uint32_t)__builtin_clzll(hm) : lane;
+                const uint32_t dh0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(h << 2), (int)d);
+                // (no head at all only after a decode error: output unspecified)
+                dh[u] = hm ? dh0 : dc;
+                k[u] = hm ? lane - h : i - hc;
+            }
+            typedef uint64_t u64u __attribute__((aligned(1)));
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                const uint32_t pos = dh[u] == kNone ? 0u : dh[u];
+                const uint32_t src = k[u] ? pos + 2 + 8 * k[u] : pos + 1;
+                const uint32_t tag = S.bytes[pos];
+                const uint64_t v = *reinterpret_cast<const u64u*>(S.bytes + src);
+                const uint32_t t = k[u] == 0 ? tag : (tag == 0xFF ? 0xFFu : 0u);
+                const uint64_t sv = S.sel[t];
+                const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+                const uint64_t word =
+                    ((uint64_t)__builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32)) << 32) |
+                    __builtin_amdgcn_perm(hi, lo, (uint32_t)sv);
+                if (valid[u]) out[W0 + ii[u]] = word;
+            }
+        }
     }
 #if UNPACK_PROF
     __syncthreads();
@@ -456,7 +754,8 @@ extern "C" uint32_t capnp_unpack_tile_words(void) { return kTileWords; }
 extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d_in_off,
                                           uint64_t nchunks, uint32_t tc, uint64_t* d_out,
                                           const uint64_t* d_out_off, int32_t* d_status,
-                                          uint64_t* d_consumed, hipStream_t stream) {
+                                          uint64_t* d_consumed, const uint32_t* d_sync,
+                                          hipStream_t stream) {
     if (nchunks == 0) return hipSuccess;
     if (tc == 0) tc = kTileWords / 128;
     if (tc > kMaxTileChunks) return hipErrorInvalidValue;  // global path: 4 waves x 64
@@ -466,7 +765,7 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
 #endif
     hipLaunchKernelGGL(unpack_kernel, dim3((uint32_t)blocks), dim3(kThreads), UNPACK_EXTRA_LDS,
                        stream, d_in,
-                       d_in_off, nchunks, tc, d_out, d_out_off, d_status, d_consumed);
+                       d_in_off, nchunks, tc, d_out, d_out_off, d_status, d_consumed, d_sync);
     return hipGetLastError();
 }
 

@@ -131,6 +131,33 @@ capnp_status capnp_gpu_unpack_batch(capnp_ctx* ctx, const uint8_t* d_packed,
                                     int32_t* d_status, uint64_t* d_consumed,
                                     void* stream);
 
+/* ---- record sync index (optional side-band of the device batch API) ---- */
+/* The batch pack can also emit a record sync index: one uint32 entry per
+   word index m = CAPNP_SYNC_WORDS * k of the batch's word space
+   (k < ceil(total_words / CAPNP_SYNC_WORDS)).
+   Entry k describes the chunk c that holds word m: bits 0-23 are the
+   chunk-relative packed offset of the first record (tag) that starts at a
+   word >= m, bits 24-31 that word minus m (a run covers at most 255 words
+   after its head).  0xFFFFFFFF = not provided (chunks packed by the
+   streaming path, i.e. larger than the staged tile).  The packed bytes are
+   unchanged: the index is metadata, like d_out_byte_off.
+   An unpack given the index (with the same word offsets as the pack, as
+   d_out_word_off) decodes CAPNP_SYNC_WORDS-word segments in parallel and checks
+   that consecutive segments meet exactly; any mismatch (a corrupt or
+   foreign index) falls back to the serial walk for that chunk, so results
+   and statuses are always those of capnp_gpu_unpack_batch. */
+#define CAPNP_SYNC_WORDS 16
+size_t capnp_sync_index_entries(size_t total_words);
+capnp_status capnp_gpu_pack_batch_sync(capnp_ctx* ctx, const uint64_t* d_words,
+                                       const uint64_t* d_chunk_word_off, size_t nchunks,
+                                       uint8_t* d_out, size_t out_cap, uint64_t* d_out_byte_off,
+                                       uint32_t* d_sync, void* stream);
+capnp_status capnp_gpu_unpack_batch_sync(capnp_ctx* ctx, const uint8_t* d_packed,
+                                         const uint64_t* d_in_byte_off, size_t nchunks,
+                                         uint64_t* d_words, const uint64_t* d_out_word_off,
+                                         const uint32_t* d_sync, int32_t* d_status,
+                                         uint64_t* d_consumed, void* stream);
+
 /* ---- host single-unit API (blocking; runs the same kernels) ------------ */
 /* PackedWrite::write_all of one chunk (serialize_packed.rs:304-439) into a
    caller buffer; *written = packed length.  len must be a multiple of 8. */

@@ -41,6 +41,19 @@ capnp_status capnp_gpu_unpack_batch_tuned(capnp_ctx* ctx, const uint8_t* d_packe
                                           int32_t* d_status, uint64_t* d_consumed,
                                           uint32_t chunks_per_tile, void* stream);
 
+/* The record-sync-index batch calls with an explicit tile size. */
+capnp_status capnp_gpu_pack_batch_sync_tuned(capnp_ctx* ctx, const uint64_t* d_words,
+                                             const uint64_t* d_chunk_word_off, size_t nchunks,
+                                             uint8_t* d_out, size_t out_cap,
+                                             uint64_t* d_out_byte_off, uint32_t* d_sync,
+                                             uint32_t chunks_per_tile, void* stream);
+capnp_status capnp_gpu_unpack_batch_sync_tuned(capnp_ctx* ctx, const uint8_t* d_packed,
+                                               const uint64_t* d_in_byte_off, size_t nchunks,
+                                               uint64_t* d_words, const uint64_t* d_out_word_off,
+                                               const uint32_t* d_sync, int32_t* d_status,
+                                               uint64_t* d_consumed, uint32_t chunks_per_tile,
+                                               void* stream);
+
 /* Output words per unpack tile the staged path is sized for. */
 uint32_t capnp_unpack_tile_words(void);
 

@@ -52,6 +52,9 @@ def lib():
                                         C.c_size_t, C.c_void_p, C.c_int]
         L.oracle_unpack_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.oracle_sync_index.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                        C.c_void_p]
+        L.oracle_sync_words.restype = C.c_size_t
         L.gen_word.argtypes = [C.c_int, C.c_uint32, C.c_uint64, C.c_uint64]
         L.gen_word.restype = C.c_uint64
         L.gen_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_uint64,
@@ -168,6 +171,24 @@ def unpack_batch(packed, in_offs, out_offs, threads=1):
                               out_offs.ctypes.data, status.ctypes.data, consumed.ctypes.data,
                               threads)
     return words[:int(out_offs[-1])], status, consumed
+
+
+def sync_index(packed, in_offs, out_offs):
+    """Record sync index of a cleanly packed batch (oracle_sync_index)."""
+    packed = np.ascontiguousarray(packed, np.uint8)
+    in_offs = np.ascontiguousarray(in_offs, np.uint64)
+    out_offs = np.ascontiguousarray(out_offs, np.uint64)
+    n = len(in_offs) - 1
+    ne = -(-int(out_offs[-1]) // sync_words())
+    sync = np.full(max(ne, 1), 0xFFFFFFFF, np.uint32)
+    r = lib().oracle_sync_index(packed.ctypes.data, in_offs.ctypes.data, out_offs.ctypes.data,
+                                n, sync.ctypes.data)
+    assert r == 0, "batch does not decode cleanly"
+    return sync[:ne]
+
+
+def sync_words():
+    return int(lib().oracle_sync_words())
 
 
 PZ30 = 1288490189  # round(0.30 * 2**32)

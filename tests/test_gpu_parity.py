@@ -369,3 +369,160 @@ def test_config4_mixed_sizes_round_trip(ctx):
     idx = np.concatenate([big, rng.choice(n, 224, replace=False)])
     _check_sampled(packed, poffs, [(int(c), int(kinds[c])) for c in idx], O.PZ30,
                    lambda c: sizes[c])
+
+
+# ------------------------------------------------------- record sync index
+def _pack_sync(ctx, dw, do, n, total, tc=0):
+    cap = ctx.batch_bound_bytes(total, n)
+    out = torch.empty(max(cap, 1), dtype=torch.uint8, device="cuda")
+    oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    sync = torch.empty(max(ctx.sync_entries(total), 1), dtype=torch.int32, device="cuda")
+    ctx.pack_batch_into(dw, do, out, oo, chunks_per_tile=tc, sync=sync)
+    return out, oo, sync
+
+
+def _unpack_sync(ctx, packed, poffs, do, total, n, sync, utc=0):
+    back = torch.empty(max(total, 1), dtype=torch.int64, device="cuda")
+    status = torch.empty(max(n, 1), dtype=torch.int32, device="cuda")
+    consumed = torch.empty(max(n, 1), dtype=torch.int64, device="cuda")
+    ctx.unpack_batch_into(packed, poffs, do, back, status, consumed, chunks_per_tile=utc,
+                          sync=sync)
+    torch.cuda.synchronize()
+    return (back.cpu().numpy().view(np.uint64)[:total], status.cpu().numpy()[:n],
+            consumed.cpu().numpy().view(np.uint64)[:n])
+
+
+def _check_sync_batch(ctx, words, offs, tc=0, utcs=(0, 1, 7, 64)):
+    """Pack with the record sync index (bytes == oracle, index == oracle
+    where provided) and unpack through it (== the words, status OK); then
+    the same unpack with a scrambled index and with no entries: the result
+    must not change (segments that do not meet fall back to the serial walk)."""
+    st, ref, ref_offs = O.pack_batch(words, offs)
+    assert st == 0
+    n, total = len(offs) - 1, int(offs[-1])
+    ref_sync = O.sync_index(ref, ref_offs, offs)
+    dw, do = dev(words), dev(offs)
+    out, oo, sync = _pack_sync(ctx, dw, do, n, total, tc)
+    torch.cuda.synchronize()
+    assert np.array_equal(oo.cpu().numpy().view(np.uint64), ref_offs)
+    assert np.array_equal(out[:len(ref)].cpu().numpy(), ref)
+    gs = sync.cpu().numpy().view(np.uint32)[:len(ref_sync)]
+    provided = gs != 0xFFFFFFFF
+    assert np.array_equal(gs[provided], ref_sync[provided]), np.nonzero(gs != ref_sync)
+    packed = out[:max(len(ref), 1)]
+    rng = np.random.default_rng(total)
+    bad = ref_sync.copy()
+    if len(bad):
+        k = rng.choice(len(bad), max(1, len(bad) // 5))
+        bad[k] = rng.integers(0, 1 << 32, len(k), dtype=np.uint64).astype(np.uint32)
+    variants = [sync, torch.from_numpy(bad.view(np.int32).copy()).cuda() if len(bad) else sync,
+                torch.full_like(sync, -1)]
+    for utc in utcs:
+        for sv in variants:
+            w, s, c = _unpack_sync(ctx, packed, oo, do, total, n, sv, utc)
+            assert (s == 0).all(), utc
+            assert np.array_equal(c, np.diff(ref_offs)), utc
+            assert np.array_equal(w, words), utc
+
+
+@pytest.mark.parametrize("tc", [0, 1, 3, 16])
+def test_sync_edge_sizes(ctx, tc):
+    sizes = [0, 1, 2, 7, 8, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 129, 255, 256, 257, 320, 511,
+             512, 513, 1000, 0, 0, 5]
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    for kind in (0, 1, 2):
+        words = O.gen_fill(offs, kind0=kind, pz=O.PZ30)
+        _check_sync_batch(ctx, words, offs, tc)
+
+
+def test_sync_random_structures(ctx):
+    rng = random.Random(23)
+    segs = [_rand_segment(rng, rng.choice([0, 1, 5, 31, 33, 64, 100, 128, 256, 300]))
+            for _ in range(200)]
+    offs = np.concatenate([[0], np.cumsum([len(s) for s in segs])]).astype(np.uint64)
+    _check_sync_batch(ctx, np.concatenate(segs), offs)
+
+
+def test_sync_long_runs(ctx):
+    chunks = []
+    for n in (31, 32, 33, 255, 256, 257, 300, 500):
+        for lead in (0, 1, 31, 63):
+            z = np.zeros(n + lead, np.uint64)
+            z[:lead] = 0x0102030400000000
+            chunks.append(z)
+            lit = np.full(n + lead, 0x1112131415161718, np.uint64)
+            lit[:lead] = 0x0000000400000001
+            chunks.append(lit)
+    offs = np.concatenate([[0], np.cumsum([len(c) for c in chunks])]).astype(np.uint64)
+    _check_sync_batch(ctx, np.concatenate(chunks), offs, utcs=(0, 3))
+
+
+def test_sync_unpack_error_statuses_vs_oracle(ctx):
+    """Malformed chunks through the sync path (index garbage or absent):
+    statuses, consumed counts and the words of good chunks equal the oracle."""
+    rng = random.Random(29)
+    packed_chunks, lens = [], []
+    for _ in range(600):
+        n = rng.choice([1, 2, 5, 31, 32, 40, 64, 65, 130])
+        w = _rand_segment(rng, n)
+        st, k = O.pack(w.tobytes())
+        k = bytearray(k)
+        r = rng.random()
+        if r < 0.3 and len(k) > 1:
+            k = k[:rng.randrange(len(k))]
+        elif r < 0.5 and len(k):
+            k[rng.randrange(len(k))] = rng.choice([0, 0xFF, rng.randrange(256)])
+        elif r < 0.6:
+            n = max(0, n + rng.choice([-3, -1, 1, 4]))
+        elif r < 0.7:
+            k = k + bytes([rng.randrange(256) for _ in range(rng.randrange(1, 12))])
+        packed_chunks.append(bytes(k))
+        lens.append(n)
+    in_offs = np.concatenate([[0], np.cumsum([len(k) for k in packed_chunks])]).astype(np.uint64)
+    out_offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    packed = np.frombuffer(b"".join(packed_chunks), np.uint8)
+    ref_words, ref_st, ref_used = O.unpack_batch(packed, in_offs, out_offs)
+    total, n = int(out_offs[-1]), len(lens)
+    pk = torch.from_numpy(packed.copy()).cuda()
+    ok = ref_st == 0
+    ne = -(-total // O.sync_words())
+    garbage = torch.from_numpy(np.random.default_rng(2).integers(
+        0, 1 << 32, ne, dtype=np.uint64).astype(np.uint32).view(np.int32)).cuda()
+    small = torch.from_numpy(np.random.default_rng(3).integers(
+        0, 1 << 12, ne, dtype=np.uint64).astype(np.uint32).view(np.int32)).cuda()
+    for sv in (garbage, small, torch.full((ne,), -1, dtype=torch.int32, device="cuda")):
+        for utc in (0, 1, 13):
+            gw, g_st, g_used = _unpack_sync(ctx, pk, dev(in_offs), dev(out_offs), total, n, sv,
+                                            utc)
+            assert np.array_equal(g_st, ref_st), (utc, np.nonzero(g_st != ref_st))
+            assert np.array_equal(g_used[ok], ref_used[ok]), utc
+            for c in np.nonzero(ok)[0]:
+                a, b = int(out_offs[c]), int(out_offs[c + 1])
+                assert np.array_equal(gw[a:b], ref_words[a:b]), (utc, c)
+
+
+@pytest.mark.parametrize("pz", [O.PZ30, O.PZ80])
+def test_sync_full_size_config(ctx, pz):
+    """Config 2/3 shape (1 Mi x 1 KiB) through the sync path: index == the
+    oracle's on sampled tiles, device round trip exact."""
+    n, cw = 1 << 20, 128
+    total = n * cw
+    offs = torch.arange(0, (n + 1) * cw, cw, dtype=torch.int64, device="cuda")
+    words = torch.empty(total, dtype=torch.int64, device="cuda")
+    ctx.gen_batch(words, offs, pz_thresh=pz)
+    out, oo, sync = _pack_sync(ctx, words, offs, n, total)
+    torch.cuda.synchronize()
+    gs = sync.cpu().numpy().view(np.uint32)
+    assert (gs != 0xFFFFFFFF).all()
+    w, s, c = _unpack_sync(ctx, out, oo, offs, total, n, sync)
+    assert (s == 0).all()
+    assert np.array_equal(w, words.cpu().numpy().view(np.uint64))
+    po = oo.cpu().numpy().view(np.uint64)
+    assert np.array_equal(c, np.diff(po))
+    pk = out.cpu().numpy()
+    for ch in np.random.default_rng(5).choice(n, 256, replace=False):
+        a, b = int(po[ch]), int(po[ch + 1])
+        ref = O.sync_index(pk[a:b], np.array([0, b - a], np.uint64),
+                           np.array([0, cw], np.uint64))
+        k = cw // O.sync_words()
+        assert np.array_equal(gs[ch * k:ch * k + k], ref), ch
