@@ -129,7 +129,7 @@ def main():
     if not args.no_sync:
         sync = torch.empty(ctx.sync_entries(total_words), dtype=torch.int32, device=dev)
     tc = tile_chunks_for(total_words, n)
-    utc = unpack_tile_chunks_for(total_words, n)
+    utc = unpack_tile_chunks_for(total_words, n, sync=sync is not None)
     ctx.reserve(n)
     stream = torch.cuda.current_stream()
 

@@ -30,7 +30,7 @@ EXPORTS = [
     "capnp_ctx_reserve", "capnp_pack_tile_words", "capnp_gpu_unpack_batch_tuned",
     "capnp_unpack_tile_words", "capnp_sync_index_entries", "capnp_gpu_pack_batch_sync",
     "capnp_gpu_unpack_batch_sync", "capnp_gpu_pack_batch_sync_tuned",
-    "capnp_gpu_unpack_batch_sync_tuned",
+    "capnp_gpu_unpack_batch_sync_tuned", "capnp_unpack_sync_tile_words",
 ]
 
 
@@ -82,6 +82,8 @@ def lib():
     L.capnp_gpu_unpack_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.capnp_gpu_unpack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, C.c_uint32, vp]
     L.capnp_gpu_gen_batch.argtypes = [vp, vp, vp, sz, u64, vp, u32, u32, vp]
+    L.capnp_unpack_sync_tile_words.argtypes = []
+    L.capnp_unpack_sync_tile_words.restype = u32
     L.capnp_sync_index_entries.argtypes = [sz]
     L.capnp_sync_index_entries.restype = sz
     L.capnp_gpu_pack_batch_sync.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, vp]

@@ -167,10 +167,13 @@ def tile_chunks_for(total_words, nchunks, lib=None):
     return int(max(1, min(64, tw // mean)))
 
 
-def unpack_tile_chunks_for(total_words, nchunks, lib=None):
-    """Chunks per unpack workgroup: about capnp_unpack_tile_words() output
-    words per tile (the staged path's descriptor capacity, unpack.hip)."""
-    tw = (lib or _lib.lib()).capnp_unpack_tile_words()
+def unpack_tile_chunks_for(total_words, nchunks, lib=None, sync=False):
+    """Chunks per unpack tile: about capnp_unpack_tile_words() output words
+    per 256-thread tile (the staged path's descriptor capacity, unpack.hip),
+    or capnp_unpack_sync_tile_words() per wave sub-tile when the record sync
+    index is used."""
+    L = lib or _lib.lib()
+    tw = L.capnp_unpack_sync_tile_words() if sync else L.capnp_unpack_tile_words()
     if nchunks <= 0:
         return max(1, tw // 128)
     mean = max(total_words / nchunks, 1.0)

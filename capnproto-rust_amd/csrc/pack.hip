@@ -431,6 +431,9 @@ struct SyncPend {
 __device__ __forceinline__ void sync_step(uint32_t* tab, uint32_t t0, uint32_t g, uint32_t meta,
                                           const StepInfo& si, uint32_t oc, uint32_t total,
                                           SyncPend& ps, uint32_t lane) {
+#if PACK_ABLATE == 5
+    return;  // timing-only: no sync entries
+#endif
     const uint32_t nv = meta & 127u;
     const uint64_t H = si.H;
     if (ps.k && H) {  // pending points end at this step's first head

@@ -32,6 +32,9 @@
 #include "common.h"
 #include "../../include/capnp_packed.h"
 
+#ifndef UNPACK_SYNC_WAVES
+#define UNPACK_SYNC_WAVES 0  // 1: wave-autonomous sync kernel (measured slower)
+#endif
 #ifndef UNPACK_EXP
 #define UNPACK_EXP 0  // diagnostic variants of the segment walk (scripts/uvar.py)
 #endif
@@ -89,15 +92,16 @@ __device__ __forceinline__ uint64_t expand_word(uint32_t tag, uint64_t packed) {
     return ((uint64_t)rhi << 32) | rlo;
 }
 
-// Global path: lane l of the wave decodes chunk c0 + l (c < c_end); `desc` is
-// this wave's 64 x 64 descriptor table (8 KiB of LDS).
+// Global path: lane l < NL of the wave decodes chunk c0 + l (c < c_end);
+// `desc` is this wave's NL x 64 descriptor table (NL * 128 bytes of LDS).
+template <uint32_t NL>
 __device__ void unpack_global(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                               uint64_t c0, uint64_t c_end, uint64_t* __restrict__ out,
                               const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
                               uint64_t* __restrict__ consumed, uint16_t (*desc)[CAPNP_WAVE],
                               uint32_t lane) {
     const uint64_t c = c0 + lane;
-    const bool have = c < c_end;
+    const bool have = lane < NL && c < c_end;
     uint64_t p = 0, in_end = 0, n = 0, obase = 0;
     if (have) {
         p = in_off[c];
@@ -121,7 +125,7 @@ __device__ void unpack_global(const uint8_t* __restrict__ in, const uint64_t* __
         {
             uint4* d4 = reinterpret_cast<uint4*>(&desc[0][0]);
 #pragma unroll
-            for (int k = 0; k < 8; k++) d4[k * CAPNP_WAVE + lane] = make_uint4(0, 0, 0, 0);
+            for (uint32_t k = 0; k < NL / 8; k++) d4[k * CAPNP_WAVE + lane] = make_uint4(0, 0, 0, 0);
         }
         wave_lds_sync();
 
@@ -177,7 +181,7 @@ __device__ void unpack_global(const uint8_t* __restrict__ in, const uint64_t* __
         wave_lds_sync();
 
         // ---- expand: lane = word of one chunk at a time
-        for (uint32_t s = 0; s < CAPNP_WAVE; s++) {
+        for (uint32_t s = 0; s < NL; s++) {
             const uint32_t cr = (uint32_t)__builtin_amdgcn_readlane((int)cnt_round, s);
             if (cr == 0) continue;
             const uint64_t pbs = readlane64(pb, s);
@@ -250,6 +254,7 @@ constexpr uint32_t kSyncNone = 0xFFFFFFFFu;
 constexpr uint32_t kMaxSeg = kTileWords / kSyncWords + 2;
 
 struct StageSmem {
+    static constexpr uint32_t kDummy = kTileWords;  // dpos[kDummy + 2 lane]: dummy slots
     uint64_t sel[256];  // expand_selector(tag): 0x00 -> zeros, 0xFF -> identity
     uint8_t badc[kStageChunks];     // sync walk: 1 = the chunk needs the exact walk
     uint32_t cw[kStageChunks + 1];  // sync walk: chunk word offsets (tile-relative)
@@ -265,6 +270,41 @@ union USmem {
     uint16_t desc[kGlobalWaves][CAPNP_WAVE][CAPNP_WAVE];  // global path
 };
 
+
+// LDS byte reads that stay naturally aligned.  gfx950 executes misaligned
+// LDS accesses correctly, but they stall the LDS pipeline
+// (SQ_LDS_UNALIGNED_STALL was half of the LDS busy time when the compiler
+// merged a record's tag and count bytes into one ds_read_u16): the three
+// record bytes are read as three bytes, the empty asm hiding that q and q-1
+// are adjacent.
+#ifndef UNPACK_ALIGNED_LDS
+#define UNPACK_ALIGNED_LDS 0  // measured: no gain (the merged u16 read is cheaper)
+#endif
+__device__ __forceinline__ void rec_bytes(const uint8_t* B, uint32_t q, uint32_t& tag,
+                                          uint32_t& b1, uint32_t& b9) {
+    uint32_t qq = q;
+#if UNPACK_ALIGNED_LDS
+    asm volatile("" : "+v"(qq));
+#endif
+    tag = B[q - 1];
+    b1 = B[qq];
+    b9 = B[q + 8];
+}
+
+// 8 bytes at LDS byte position `pos` from one aligned 16-byte read.
+__device__ __forceinline__ uint64_t lds_bytes8(const uint8_t* B, uint32_t pos) {
+#if !UNPACK_ALIGNED_LDS
+    typedef uint64_t u64u __attribute__((aligned(1)));
+    return *reinterpret_cast<const u64u*>(B + pos);
+#endif
+    const uint4 v = *reinterpret_cast<const uint4*>(B + (pos & ~7u));
+    const uint32_t o = pos & 7u, sh = o & 3u;
+    const bool hi = o >= 4;
+    const uint32_t d0 = hi ? v.y : v.x, d1 = hi ? v.z : v.y, d2 = hi ? v.w : v.z;
+    const uint32_t lo32 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+    const uint32_t hi32 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+    return ((uint64_t)hi32 << 32) | lo32;
+}
 
 // Exact status of a record that failed the fast check in walk_chunk, in the
 // reference's order (serialize_packed.rs:109-145, :157-205).
@@ -282,7 +322,8 @@ __device__ __forceinline__ int32_t record_error(uint32_t p, uint32_t q, uint32_t
 // (record end <= pe, run end <= chunk end) covers every error.  Status
 // precedence and consumed bytes as in unpack_global.  (The exact path behind
 // walk_wave: it only runs for chunks whose fast walk failed a check.)
-__device__ __forceinline__ void walk_chunk(StageSmem& S, uint32_t p, uint32_t pe, uint32_t wb,
+template <class SM>
+__device__ __forceinline__ void walk_chunk(SM& S, uint32_t p, uint32_t pe, uint32_t wb,
                                            uint32_t n, int32_t& st, uint32_t& used) {
     const uint32_t p0 = p;
     const uint32_t wend = wb + n;
@@ -339,7 +380,8 @@ __device__ __forceinline__ void walk_chunk(StageSmem& S, uint32_t p, uint32_t pe
 // checks, which overlap their latency.  A record that would fail any check
 // stops the lane and marks it bad; bad lanes re-walk with walk_chunk, which
 // yields the exact status and consumed count.
-__device__ __forceinline__ void walk_wave(StageSmem& S, uint32_t p, uint32_t pe, uint32_t wb,
+template <class SM>
+__device__ __forceinline__ void walk_wave(SM& S, uint32_t p, uint32_t pe, uint32_t wb,
                                           uint32_t n, int32_t& st, uint32_t& used) {
     const uint32_t p0 = p;
     const uint32_t wend = wb + n;
@@ -349,16 +391,18 @@ __device__ __forceinline__ void walk_wave(StageSmem& S, uint32_t p, uint32_t pe,
     uint32_t w = wb;
     bool act = n > 0 && p < pe;
     bool bad = n > 0 && p >= pe;
-    const uint32_t dummy = kTileWords + 2u * lane_id();
+    const uint32_t dummy = SM::kDummy + 2u * lane_id();
     const uint8_t* B = S.bytes;
-    uint32_t tag = B[q - 1], b1 = B[q], b9 = B[q + 8];
+    uint32_t tag, b1, b9;
+    rec_bytes(B, q, tag, b1, b9);
     while (ballot64(act)) {
         const bool isz = tag == 0, isf = tag == 0xFF;
         // end of the record + 1: q + popc + isz (+ 1 + 8 b9 for 0xFF)
         const uint32_t fx = isf ? 8u * b9 + 1u : 0u;
         const uint32_t qe = __builtin_popcount(tag) + q + (isz ? 1u : 0u) + fx + 1u;
         const uint32_t qn = qe < pe + 1u ? qe : pe + 1u;
-        const uint32_t ntag = B[qn - 1], nb1 = B[qn], nb9 = B[qn + 8];
+        uint32_t ntag, nb1, nb9;
+        rec_bytes(B, qn, ntag, nb1, nb9);
         const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
         const uint32_t wn = w + 1u + cnt;
         const bool ok = act && qe <= pe + 1u && wn <= wend;
@@ -391,14 +435,16 @@ __device__ __forceinline__ void walk_wave(StageSmem& S, uint32_t p, uint32_t pe,
 // serially (walk_chunk) with exact status, so the index can only change the
 // speed, never the result.
 
-__device__ __forceinline__ void mark_bad(StageSmem& S, uint32_t c, bool& marked) {
+template <class SM>
+__device__ __forceinline__ void mark_bad(SM& S, uint32_t c, bool& marked) {
     S.badc[c] = 1;
     marked = true;
 }
 
 // Start state of segment b (starting at tile word sb): chunk, position + 1,
 // word.  An unusable entry yields the end of its chunk and marks it bad.
-__device__ __forceinline__ void seg_start(StageSmem& S, uint32_t nc, uint32_t b, uint32_t sb,
+template <class SM>
+__device__ __forceinline__ void seg_start(SM& S, uint32_t nc, uint32_t b, uint32_t sb,
                                           uint32_t& c, uint32_t& q, uint32_t& w, bool mark,
                                           bool& marked) {
     c = S.segc[b];
@@ -426,16 +472,18 @@ __device__ __forceinline__ void seg_start(StageSmem& S, uint32_t nc, uint32_t b,
 // (rare, wave-uniform) stop branch, which moves a lane at a chunk end to the
 // next chunk or retires it.  Record checks accumulate into a sticky error
 // flag (a failed record ends its chunk; the chunk is re-walked exactly).
-__device__ __forceinline__ bool walk_segment(StageSmem& S, uint32_t nc, uint32_t b, uint32_t sb,
+template <class SM>
+__device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uint32_t sb,
                                              uint32_t eb, bool last) {
     bool marked = false;
     uint32_t c, q, w;
     seg_start(S, nc, b, sb, c, q, w, true, marked);
     const uint8_t* B = S.bytes;
-    const uint32_t dummy = kTileWords + 2u * lane_id();
+    const uint32_t dummy = SM::kDummy + 2u * lane_id();
     uint32_t cwe = S.cw[c + 1], cpe1 = S.cp[c + 1] + 1u;
     uint32_t stopw = cwe < eb ? cwe : eb;
-    uint32_t tag = B[q - 1], b1 = B[q], b9 = B[q + 8];
+    uint32_t tag, b1, b9;
+    rec_bytes(B, q, tag, b1, b9);
     bool err = false;
     const uint64_t all = ballot64(true);
     uint64_t done = 0;
@@ -454,7 +502,8 @@ __device__ __forceinline__ bool walk_segment(StageSmem& S, uint32_t nc, uint32_t
         const uint32_t fx = isf ? 8u * b9 + 1u : 0u;
         const uint32_t qe = __builtin_popcount(tag) + q + (isz ? 1u : 0u) + fx + 1u;
         const uint32_t qn = qe < cpe1 ? qe : cpe1;
-        const uint32_t ntag = B[qn - 1], nb1 = B[qn], nb9 = B[qn + 8];
+        uint32_t ntag, nb1, nb9;
+        rec_bytes(B, qn, ntag, nb1, nb9);
         const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
         const uint32_t wn0 = w + 1u + cnt;
         err = err || (hop && (qe > cpe1 || wn0 > cwe));
@@ -484,9 +533,7 @@ __device__ __forceinline__ bool walk_segment(StageSmem& S, uint32_t nc, uint32_t
                         cwe = S.cw[c + 1];
                         cpe1 = S.cp[c + 1] + 1u;
                         q = S.cp[c] + 1u;
-                        tag = B[q - 1];
-                        b1 = B[q];
-                        b9 = B[q + 8];
+                        rec_bytes(B, q, tag, b1, b9);
                     }
                 }
                 stopw = (c < nc && cwe < eb) ? cwe : eb;
@@ -505,7 +552,8 @@ __device__ __forceinline__ bool walk_segment(StageSmem& S, uint32_t nc, uint32_t
         const uint4 nv = *reinterpret_cast<const u4u*>(B + qn - 1);
         const uint32_t ntag = nv.x & 0xFFu, nb1 = (nv.x >> 8) & 0xFFu, nb9 = (nv.z >> 8) & 0xFFu;
 #else
-        const uint32_t ntag = B[qn - 1], nb1 = B[qn], nb9 = B[qn + 8];
+        uint32_t ntag, nb1, nb9;
+        rec_bytes(B, qn, ntag, nb1, nb9);
 #endif
         const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
         const uint32_t wn0 = w + 1u + cnt;
@@ -566,8 +614,8 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
         if (wave >= kGlobalWaves) return;
         for (uint64_t c0 = ca + (uint64_t)wave * CAPNP_WAVE; c0 < cb;
              c0 += (uint64_t)kGlobalWaves * CAPNP_WAVE)
-            unpack_global(in, in_off, c0, cb, out, out_off, status, consumed, sm.desc[wave],
-                          lane);
+            unpack_global<CAPNP_WAVE>(in, in_off, c0, cb, out, out_off, status, consumed,
+                                      sm.desc[wave], lane);
         return;
     }
     StageSmem& S = sm.st;
@@ -721,7 +769,7 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
                 const uint32_t pos = dh[u] == kNone ? 0u : dh[u];
                 const uint32_t src = k[u] ? pos + 2 + 8 * k[u] : pos + 1;
                 const uint32_t tag = S.bytes[pos];
-                const uint64_t v = *reinterpret_cast<const u64u*>(S.bytes + src);
+                const uint64_t v = lds_bytes8(S.bytes, src);
                 const uint32_t t = k[u] == 0 ? tag : (tag == 0xFF ? 0xFFu : 0u);
                 const uint64_t sv = S.sel[t];
                 const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
@@ -745,11 +793,236 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Sync kernel (the record sync index is given): every wave is autonomous.  A
+// sub-tile = `tc` consecutive chunks of about kSubWords output words; wave w
+// of workgroup g takes sub-tile 4 g + w, stages its packed bytes in its own
+// LDS region, walks its 16-word segments (walk_segment, one lane each),
+// re-walks chunks whose segments did not meet, and expands - with no
+// workgroup barrier after the selector table, so the 16-32 resident waves of
+// a CU overlap each other's load latency, walks and expansions freely.
+#ifndef UNPACK_SUB_WORDS
+#define UNPACK_SUB_WORDS 1024
+#endif
+constexpr uint32_t kSubWords = UNPACK_SUB_WORDS;
+constexpr uint32_t kSubBytes = kSubWords * 9 / 2;
+constexpr uint32_t kSubChunks = 64;
+constexpr uint32_t kSubSeg = kSubWords / kSyncWords + 2;
+constexpr uint32_t kSubGlobalLanes = 16;  // fallback walkers (desc table in the byte area)
+
+struct WaveSmem {
+    static constexpr uint32_t kDummy = kSubWords;  // dpos[kDummy + 2 lane]: dummy slots
+    uint8_t badc[kSubChunks];
+    uint32_t cw[kSubChunks + 1];
+    uint32_t cp[kSubChunks + 1];
+    uint32_t ent[kSubSeg];
+    uint8_t segc[kSubSeg];
+    alignas(16) uint8_t bytes[kSubBytes + 16];
+    alignas(16) uint16_t dpos[kSubWords + 2 * CAPNP_WAVE];
+};
+static_assert(sizeof(uint16_t) * kSubGlobalLanes * CAPNP_WAVE <= kSubBytes,
+              "fallback descriptor table must fit the byte area");
+
+struct SyncSmem {
+    uint64_t sel[256];
+    WaveSmem w[kWaves];
+};
+
+// Wave-wide inclusive max-scan (DPP, VALU only).
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return x;
+}
+
+// Expansion of the sub-tile's segments, lane b = segment b (rounds of 64).
+// A head is encoded (word + 1) << 16 | LDS position; the word's record is the
+// largest code at or below it.
+__device__ __forceinline__ void expand_segments(const WaveSmem& S, const uint64_t* sel,
+                                                uint32_t nseg, uint64_t kf, uint64_t W0,
+                                                uint32_t Wt, uint64_t* __restrict__ out,
+                                                uint32_t lane) {
+    typedef uint64_t u64u __attribute__((aligned(1)));
+    typedef uint4 u4u __attribute__((aligned(2)));
+    uint32_t carry = 0;  // last head of the previous rounds
+    for (uint32_t r0 = 0; r0 < nseg; r0 += CAPNP_WAVE) {
+        const uint32_t b = r0 + lane;
+        const bool have = b < nseg;
+        const uint32_t sb = b == 0 ? 0u : (uint32_t)((kf + b - 1) * kSyncWords - W0);
+        const uint32_t eb =
+            b + 1 >= nseg ? Wt : (uint32_t)((kf + b) * kSyncWords - W0);
+        const uint32_t n = have ? eb - sb : 0u;
+        uint32_t d[kSyncWords];
+        {
+            const uint32_t base = have ? sb : 0u;
+#pragma unroll
+            for (uint32_t j = 0; j < kSyncWords; j += 8) {
+                const uint4 v = *reinterpret_cast<const u4u*>(S.dpos + base + j);
+                d[j + 0] = v.x & 0xFFFFu; d[j + 1] = v.x >> 16;
+                d[j + 2] = v.y & 0xFFFFu; d[j + 3] = v.y >> 16;
+                d[j + 4] = v.z & 0xFFFFu; d[j + 5] = v.z >> 16;
+                d[j + 6] = v.w & 0xFFFFu; d[j + 7] = v.w >> 16;
+            }
+        }
+        uint32_t last = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kSyncWords; j++)
+            if (j < n && d[j] != kNone) last = ((sb + j + 1) << 16) | d[j];
+        const uint32_t incl = max(wave_incl_max(last), carry);
+        uint32_t cur = (uint32_t)__shfl_up((int)incl, 1, CAPNP_WAVE);
+        cur = lane == 0 ? carry : cur;
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        uint64_t word[kSyncWords];
+#pragma unroll
+        for (uint32_t j = 0; j < kSyncWords; j++) {
+            if (d[j] != kNone) cur = ((sb + j + 1) << 16) | d[j];
+            const uint32_t pos = cur & 0xFFFFu;
+            const uint32_t k = sb + j + 1 - (cur >> 16);
+            const uint32_t src = k ? pos + 2 + 8 * k : pos + 1;
+            const uint32_t tag = S.bytes[pos];
+            const uint64_t v = lds_bytes8(S.bytes, src < kSubBytes ? src : 0u);
+            const uint32_t t = k == 0 ? tag : (tag == 0xFF ? 0xFFu : 0u);
+            const uint64_t sv = sel[t];
+            const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+            word[j] = ((uint64_t)__builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32)) << 32) |
+                      __builtin_amdgcn_perm(hi, lo, (uint32_t)sv);
+        }
+        uint64_t* o = out + W0 + sb;
+        if (n == kSyncWords) {
+#pragma unroll
+            for (uint32_t j = 0; j < kSyncWords; j += 2)
+                *reinterpret_cast<ulonglong2*>(o + j) = make_ulonglong2(word[j], word[j + 1]);
+        } else {
+#pragma unroll
+            for (uint32_t j = 0; j < kSyncWords; j++)
+                if (j < n) o[j] = word[j];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kThreads)
+unpack_sync_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                   uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
+                   const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
+                   uint64_t* __restrict__ consumed, const uint32_t* __restrict__ sync) {
+    __shared__ SyncSmem sm;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    sm.sel[tid] = expand_selector(tid);
+    __syncthreads();
+    const uint64_t ca = ((uint64_t)blockIdx.x * kWaves + wave) * tc;
+    if (ca >= nchunks) return;
+    const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
+    const uint32_t nc = (uint32_t)(cb - ca);
+    WaveSmem& S = sm.w[wave];
+    const uint64_t B0 = uniform64(in_off[ca]), B1 = uniform64(in_off[cb]);
+    const uint64_t W0 = uniform64(out_off[ca]), W1 = uniform64(out_off[cb]);
+    const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
+    const bool fits = nc <= kSubChunks && B1 - B0 <= kSubBytes - off0 && W1 - W0 <= kSubWords;
+    if (!fits) {
+        for (uint64_t c0 = ca; c0 < cb; c0 += kSubGlobalLanes)
+            unpack_global<kSubGlobalLanes>(in, in_off, c0, cb, out, out_off, status, consumed,
+                                           reinterpret_cast<uint16_t(*)[CAPNP_WAVE]>(S.bytes),
+                                           lane);
+        return;
+    }
+    const uint32_t nbytes = (uint32_t)(B1 - B0) + off0;
+    const uint32_t Wt = (uint32_t)(W1 - W0);
+    const uint64_t kf = W0 / kSyncWords + 1;
+    const uint32_t nseg = W1 > W0 ? 1u + (uint32_t)((W1 - 1) / kSyncWords + 1 - kf) : 0u;
+    // stage: every global load issued before any LDS write
+    {
+        constexpr uint32_t kLoads = (kSubBytes + 15 + 16 * CAPNP_WAVE - 1) / (16 * CAPNP_WAVE);
+        const uint4* src = reinterpret_cast<const uint4*>(in + B0 - off0);
+        const uint32_t nblk = (nbytes + 15) / 16;
+        uint4 r[kLoads];
+#pragma unroll
+        for (uint32_t k = 0; k < kLoads; k++) {
+            const uint32_t idx = lane + k * CAPNP_WAVE;
+            r[k] = nblk ? src[idx < nblk ? idx : nblk - 1] : make_uint4(0, 0, 0, 0);
+        }
+        uint32_t wa = 0, wz = 0, pa = 0;
+        if (lane <= nc) {
+            wa = (uint32_t)(out_off[ca + lane] - W0);
+            pa = (uint32_t)(in_off[ca + lane] - B0) + off0;
+            wz = lane < nc ? (uint32_t)(out_off[ca + lane + 1] - W0) : wa;
+        }
+        uint32_t e0 = 0, e1 = 0;
+        if (lane + 1 < nseg) e0 = sync[kf + lane];
+        if (lane + 65 < nseg) e1 = sync[kf + lane + 64];
+        uint4* dd = reinterpret_cast<uint4*>(S.dpos);
+        const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
+        for (uint32_t k = lane; k < (Wt + 7) / 8; k += CAPNP_WAVE) dd[k] = none;
+        if (lane < kSubChunks) S.badc[lane] = 0;
+        if (lane <= nc) {
+            S.cw[lane] = wa;
+            S.cp[lane] = pa;
+            // segments whose first word (max(0, b G - r0)) lies in this chunk
+            const uint32_t r0 = (uint32_t)(W0 % kSyncWords);
+            if (wz > wa) {
+                const uint32_t blo = wa == 0 ? 0u : (wa + r0 + kSyncWords - 1) / kSyncWords;
+                const uint32_t bhi = (wz + r0 + kSyncWords - 1) / kSyncWords;
+                for (uint32_t bb = blo; bb < bhi; bb++) S.segc[bb] = (uint8_t)lane;
+            }
+        }
+        if (lane + 1 < nseg) S.ent[lane + 1] = e0;
+        if (lane + 65 < nseg) S.ent[lane + 65] = e1;
+        uint4* dst = reinterpret_cast<uint4*>(S.bytes);
+#pragma unroll
+        for (uint32_t k = 0; k < kLoads; k++)
+            if (lane + k * CAPNP_WAVE < nblk) dst[lane + k * CAPNP_WAVE] = r[k];
+    }
+    wave_lds_sync();
+    // walk: lane b = segment b (and b + 64 when the sub-tile has more)
+    bool marked = false;
+    for (uint32_t b = lane; b < nseg; b += CAPNP_WAVE) {
+        const uint32_t sb = b == 0 ? 0u : (uint32_t)((kf + b - 1) * kSyncWords - W0);
+        const bool last = b + 1 == nseg;
+        const uint32_t eb = last ? Wt : (uint32_t)((kf + b) * kSyncWords - W0);
+        marked |= walk_segment(S, nc, b, sb, eb, last);
+    }
+    wave_lds_sync();
+    const bool anybad = ballot64(marked) != 0;
+    if (lane < nc) {
+        const uint64_t c = ca + lane;
+        if (anybad && S.badc[lane]) {  // exact serial walk of the chunk
+            const uint32_t wa = S.cw[lane], wz = S.cw[lane + 1];
+            for (uint32_t i = wa; i < wz; i++) S.dpos[i] = kNone;
+            int32_t st;
+            uint32_t used;
+            walk_chunk(S, S.cp[lane], S.cp[lane + 1], wa, wz - wa, st, used);
+            status[c] = st;
+            if (consumed) consumed[c] = used;
+        } else {
+            status[c] = ST_OK;
+            if (consumed)
+                consumed[c] = S.cw[lane + 1] > S.cw[lane] ? S.cp[lane + 1] - S.cp[lane] : 0u;
+        }
+    }
+    wave_lds_sync();
+    // expand: lane b = segment b again.  The lane reads its 16 descriptors,
+    // finds each word's head (its own, or the last head of an earlier
+    // segment through a wave max-scan), and rebuilds its words from LDS with
+    // every read of the 16 words in flight at once.
+    expand_segments(S, sm.sel, nseg, kf, W0, Wt, out, lane);
+}
+
 }  // namespace
 
 // Output words per unpack tile the staged path is sized for; the host picks
 // chunks_per_tile ~ this / mean chunk words.
 extern "C" uint32_t capnp_unpack_tile_words(void) { return kTileWords; }
+
+// Output words per wave sub-tile of the sync kernel (chunks_per_tile for the
+// record-sync-index calls ~ this / mean chunk words).
+extern "C" uint32_t capnp_unpack_sync_tile_words(void) {
+    return UNPACK_SYNC_WAVES ? kSubWords : kTileWords;
+}
 
 extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d_in_off,
                                           uint64_t nchunks, uint32_t tc, uint64_t* d_out,
@@ -757,12 +1030,20 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
                                           uint64_t* d_consumed, const uint32_t* d_sync,
                                           hipStream_t stream) {
     if (nchunks == 0) return hipSuccess;
-    if (tc == 0) tc = kTileWords / 128;
+    if (tc == 0) tc = ((d_sync && UNPACK_SYNC_WAVES) ? kSubWords : kTileWords) / 128;
     if (tc > kMaxTileChunks) return hipErrorInvalidValue;  // global path: 4 waves x 64
     const uint64_t blocks = (nchunks + tc - 1) / tc;
 #ifndef UNPACK_EXTRA_LDS
 #define UNPACK_EXTRA_LDS 0  // diagnostic: dynamic LDS padding to cap workgroups per CU
 #endif
+    if (d_sync && UNPACK_SYNC_WAVES) {
+        if (tc > kSubChunks) return hipErrorInvalidValue;
+        const uint64_t subs = (nchunks + tc - 1) / tc;
+        hipLaunchKernelGGL(unpack_sync_kernel, dim3((uint32_t)((subs + kWaves - 1) / kWaves)),
+                           dim3(kThreads), UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc,
+                           d_out, d_out_off, d_status, d_consumed, d_sync);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(unpack_kernel, dim3((uint32_t)blocks), dim3(kThreads), UNPACK_EXTRA_LDS,
                        stream, d_in,
                        d_in_off, nchunks, tc, d_out, d_out_off, d_status, d_consumed, d_sync);

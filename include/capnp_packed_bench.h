@@ -54,6 +54,10 @@ capnp_status capnp_gpu_unpack_batch_sync_tuned(capnp_ctx* ctx, const uint8_t* d_
                                                uint64_t* d_consumed, uint32_t chunks_per_tile,
                                                void* stream);
 
+/* Output words per wave sub-tile of the record-sync-index unpack (the
+ * chunks_per_tile of the _sync_ calls ~ this / mean chunk words). */
+uint32_t capnp_unpack_sync_tile_words(void);
+
 /* Output words per unpack tile the staged path is sized for. */
 uint32_t capnp_unpack_tile_words(void);
 

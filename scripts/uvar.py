@@ -52,9 +52,10 @@ def main():
             L.capnp_gpu_unpack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp,
                                                             u32, vp]
         L.capnp_unpack_tile_words.restype = u32
+        L.capnp_unpack_sync_tile_words.restype = u32
         st = C.c_int(0)
         h = vp(L.capnp_ctx_create(0, C.byref(st)))
-        utc = a.utc or unpack_tile_chunks_for(n * cw, n, lib=L)
+        utc = a.utc or unpack_tile_chunks_for(n * cw, n, lib=L, sync=a.sync)
         ntiles = (n + utc - 1) // utc
         prof = hasattr(L, "capnp_unpack_trace")
         trace = None
