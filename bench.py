@@ -173,8 +173,12 @@ def main():
     pack_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / len(ev)
     unpack_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / len(ev)
     offs_bytes = 8 * (n + 1)
-    pack_bytes = U + P + 2 * offs_bytes
-    unpack_bytes = P + U + 2 * offs_bytes + 4 * n + 8 * n
+    sync_bytes = 4 * ctx.sync_entries(total_words) if sync is not None else 0
+    # algorithmic bytes per launch: words + packed bytes + offsets (+ the
+    # record sync index written by pack / read by unpack; + unpack's status
+    # and consumed arrays)
+    pack_bytes = U + P + 2 * offs_bytes + sync_bytes
+    unpack_bytes = P + U + 2 * offs_bytes + 4 * n + 8 * n + sync_bytes
     kernels = {
         "pack": {"ms": round(pack_ms, 4), "alg_bytes": pack_bytes,
                  "GBps": round(pack_bytes / (pack_ms * 1e-3) / 1e9, 1),
@@ -189,7 +193,7 @@ def main():
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        key = f"{args.workload}:{n}x{cw}"
+        key = f"{args.workload}:{n}x{cw}" + (":sync" if sync is not None else "")
         traffic = tj.get(key, {}).get(dom)
     except (OSError, ValueError):
         pass
@@ -228,6 +232,7 @@ def main():
             },
             "kernels": kernels,
             "packed_ratio": round(P / U, 4),
+            "sync_index": sync is not None,
             "roundtrip_ok": ok,
         }
         if e2e:

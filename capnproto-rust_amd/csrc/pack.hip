@@ -898,7 +898,15 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             }
         }
 #endif
-        if (sync) {  // record sync entries (overlaps the look-back)
+        if (wave == 0) {
+            const uint64_t excl = lookback(LA, tile, agg, lane);
+            if (lane == 0) TRACE(tile, 2, RT());
+            if (lane < nc) sm.chunk_pos[lane] += excl;
+            if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
+        }
+        // record sync entries: waves 1-3 while wave 0 waits on the look-back,
+        // wave 0 after it (its look-back is not delayed)
+        if (sync) {
             SyncPend ps;
             uint32_t oc = 0;
 #pragma unroll
@@ -912,12 +920,6 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                               si[s], oc, total, ps, lane);
                 }
             }
-        }
-        if (wave == 0) {
-            const uint64_t excl = lookback(LA, tile, agg, lane);
-            if (lane == 0) TRACE(tile, 2, RT());
-            if (lane < nc) sm.chunk_pos[lane] += excl;
-            if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
         }
         __syncthreads();
         for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];

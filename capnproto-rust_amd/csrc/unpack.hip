@@ -35,6 +35,15 @@
 #ifndef UNPACK_SYNC_WAVES
 #define UNPACK_SYNC_WAVES 0  // 1: wave-autonomous sync kernel (measured slower)
 #endif
+#ifndef UNPACK_GROUPS
+#define UNPACK_GROUPS 2  // expansion groups in flight per wave
+#endif
+#ifndef UNPACK_MIN_WAVES
+#define UNPACK_MIN_WAVES 8  // __launch_bounds__ waves per SIMD of the tile kernel
+#endif
+#ifndef UNPACK_PHASEA_UNROLL
+#define UNPACK_PHASEA_UNROLL 1
+#endif
 #ifndef UNPACK_EXP
 #define UNPACK_EXP 0  // diagnostic variants of the segment walk (scripts/uvar.py)
 #endif
@@ -240,12 +249,49 @@ constexpr uint32_t kTileBytes = kTileWords * 9 / 2;  // LDS capacity for packed 
 constexpr uint32_t kGlobalWaves = kTileWords >= 4096 ? 4 : 2;
 constexpr uint32_t kStageChunks = 64;    // walkers: one lane of wave 0 per chunk
 
-// Descriptor of an output word (u16): the LDS position of its record's tag
-// when a record starts at the word (the tag byte gives the kind), kNone for
-// a word inside a run.  The expansion finds a run word's head as the highest
-// head at or below it in its 64-word group, or, for words before the group's
-// first head, the last head of the nearest earlier group that has one.
+// Descriptor of an output word (u16), all the expansion needs for the word:
+//   p < 0x8000       a record starts at the word, its tag is at LDS byte p
+//                    (the tag gives the kind; the word's bytes follow it);
+//   kRaw | p         the word is a raw word of a literal run, at LDS byte p;
+//   kNone            the word is a word of a zero run (or of a chunk whose
+//                    decode failed: output unspecified).
+// The walkers write one entry per record plus one per literal-run word
+// (rare), so the expansion is a plain per-word lookup: no head search.
 constexpr uint16_t kNone = 0xFFFF;
+constexpr uint16_t kRaw = 0x8000;
+
+// Raw-word entries of a 0xFF record whose tag is at LDS byte p, head at word
+// w, whose run covers words w+1 .. w+n (n <= 255).
+template <class SM>
+__device__ __forceinline__ void lit_entries(SM& S, uint32_t w, uint32_t p, uint32_t n) {
+    for (uint32_t i = 0; i < n; i++) S.dpos[w + 1 + i] = (uint16_t)(kRaw | (p + 10 + 8 * i));
+}
+
+// Rebuilds one output word from its descriptor (sel = expand selectors).
+__device__ __forceinline__ uint64_t expand_desc(const uint8_t* B, const uint64_t* sel,
+                                                uint32_t d) {
+    const bool none = d == kNone, raw = !none && (d & kRaw);
+    const uint32_t pos = none ? 0u : (d & 0x7FFFu);
+    const uint32_t tag = B[pos];
+    // (two naturally aligned 8-byte reads and a funnel shift: a ds_read_b64
+    // off 8-byte alignment is replayed at 64 LDS cycles, MI355X_MICROARCH.md
+    // §LDS, and was half the LDS time of this kernel)
+    const uint32_t src = raw ? pos : pos + 1;
+    const uint64_t* q8 = reinterpret_cast<const uint64_t*>(B + (src & ~7u));
+    const uint64_t a = q8[0], b = q8[1];
+    const uint32_t o = src & 7u, sh = o & 3u;
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
+    const uint32_t b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const bool up = o >= 4;
+    const uint32_t x0 = up ? a1 : a0, x1 = up ? b0 : a1, x2 = up ? b1 : b0;
+    const uint64_t v = ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sh) << 32) |
+                       __builtin_amdgcn_alignbyte(x1, x0, sh);
+    const uint32_t t = none ? 0u : (raw ? 0xFFu : tag);
+    const uint64_t sv = sel[t];
+    const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    return ((uint64_t)__builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32)) << 32) |
+           __builtin_amdgcn_perm(hi, lo, (uint32_t)sv);
+}
 
 
 // Record sync index (pack.hip): entry k describes global word kSyncWords * k.
@@ -271,39 +317,19 @@ union USmem {
 };
 
 
-// LDS byte reads that stay naturally aligned.  gfx950 executes misaligned
-// LDS accesses correctly, but they stall the LDS pipeline
-// (SQ_LDS_UNALIGNED_STALL was half of the LDS busy time when the compiler
-// merged a record's tag and count bytes into one ds_read_u16): the three
-// record bytes are read as three bytes, the empty asm hiding that q and q-1
-// are adjacent.
-#ifndef UNPACK_ALIGNED_LDS
-#define UNPACK_ALIGNED_LDS 0  // measured: no gain (the merged u16 read is cheaper)
-#endif
+// The three bytes of the record whose tag is at LDS byte q-1: tag, q (zero
+// run count) and q+8 (literal run count).  Left alone, the compiler merges
+// the adjacent tag and count reads into one ds_read_u16, which at an odd
+// address is a misaligned LDS access: replayed, and SQ_LDS_UNALIGNED_STALL
+// was half of this kernel's LDS cycles.  The tag is extracted from its
+// aligned dword instead (32-bit reads are never misaligned).
 __device__ __forceinline__ void rec_bytes(const uint8_t* B, uint32_t q, uint32_t& tag,
                                           uint32_t& b1, uint32_t& b9) {
-    uint32_t qq = q;
-#if UNPACK_ALIGNED_LDS
-    asm volatile("" : "+v"(qq));
-#endif
-    tag = B[q - 1];
-    b1 = B[qq];
+    const uint32_t p = q - 1u;
+    const uint32_t dw = *reinterpret_cast<const uint32_t*>(B + (p & ~3u));
+    tag = __builtin_amdgcn_ubfe(dw, (p & 3u) * 8u, 8u);
+    b1 = B[q];
     b9 = B[q + 8];
-}
-
-// 8 bytes at LDS byte position `pos` from one aligned 16-byte read.
-__device__ __forceinline__ uint64_t lds_bytes8(const uint8_t* B, uint32_t pos) {
-#if !UNPACK_ALIGNED_LDS
-    typedef uint64_t u64u __attribute__((aligned(1)));
-    return *reinterpret_cast<const u64u*>(B + pos);
-#endif
-    const uint4 v = *reinterpret_cast<const uint4*>(B + (pos & ~7u));
-    const uint32_t o = pos & 7u, sh = o & 3u;
-    const bool hi = o >= 4;
-    const uint32_t d0 = hi ? v.y : v.x, d1 = hi ? v.z : v.y, d2 = hi ? v.w : v.z;
-    const uint32_t lo32 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-    const uint32_t hi32 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-    return ((uint64_t)hi32 << 32) | lo32;
 }
 
 // Exact status of a record that failed the fast check in walk_chunk, in the
@@ -354,6 +380,7 @@ __device__ __forceinline__ void walk_chunk(SM& S, uint32_t p, uint32_t pe, uint3
         const uint32_t wn = w + 1 + cnt;
         if (end <= pe && wn <= wend) {
             S.dpos[w] = (uint16_t)p;
+            if (isf) lit_entries(S, w, p, cnt);
             w = wn;
             p = end;
             go = w < wend;
@@ -408,6 +435,9 @@ __device__ __forceinline__ void walk_wave(SM& S, uint32_t p, uint32_t pe, uint32
         const bool ok = act && qe <= pe + 1u && wn <= wend;
         bad = bad || (act && !ok);
         S.dpos[ok ? w : dummy] = (uint16_t)(q - 1u);
+        if (ballot64(ok && isf && cnt)) {  // literal-run words (rare)
+            if (ok && isf) lit_entries(S, w, q - 1u, cnt);
+        }
         q = ok ? qe : q;
         w = ok ? wn : w;
         act = ok && wn < wend;
@@ -495,7 +525,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     // word, so a lane reaches stopw within kSyncWords hops; a lane already
     // there only sends its store to the dummy slot).  Phase B below handles
     // chunk ends and whatever is left.
-#pragma unroll
+#pragma unroll UNPACK_PHASEA_UNROLL
     for (uint32_t it = 0; it < kSyncWords; it++) {
         const bool hop = w < stopw;
         const bool isz = tag == 0, isf = tag == 0xFF;
@@ -509,6 +539,9 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
         err = err || (hop && (qe > cpe1 || wn0 > cwe));
         const uint32_t wn = wn0 < cwe ? wn0 : cwe;
         S.dpos[hop ? w : dummy] = (uint16_t)(q - 1u);
+        if (ballot64(hop && isf && wn > w + 1)) {  // literal-run words (rare)
+            if (hop && isf) lit_entries(S, w, q - 1u, wn - w - 1);
+        }
         q = hop ? qn : q;
         w = hop ? wn : w;
         tag = hop ? ntag : tag;
@@ -561,6 +594,9 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
         const uint32_t wn = wn0 < cwe ? wn0 : cwe;  // (an overrun ends the chunk)
 #if UNPACK_EXP != 1  // 1: timing only, no descriptors
         S.dpos[hop ? w : dummy] = (uint16_t)(q - 1u);
+        if (ballot64(hop && isf && wn > w + 1)) {  // literal-run words (rare)
+            if (hop && isf) lit_entries(S, w, q - 1u, wn - w - 1);
+        }
 #endif
         q = hop ? qn : q;
         w = hop ? wn : w;
@@ -590,7 +626,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     return marked;
 }
 
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, UNPACK_MIN_WAVES)
 unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
               uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
               const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
@@ -721,62 +757,23 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
     }
     if (!sync) __syncthreads();
     UPROF_T(t2);
-    // expand: lane = output word; 64-word groups interleaved over waves, two
-    // groups per iteration so that their LDS round trips overlap.
-    // Branch-free per word: perm(8 bytes at src, sel[t]) with t = the head's
-    // tag at the head word, 0xFF (identity) for a literal run's raw words, 0
-    // (zeros) for a zero run's words.  src does not depend on the tag (a zero
-    // run's words read bytes they then discard), so the tag and the bytes
-    // are read together.
+    // expand: lane = output word (a plain descriptor lookup, no head
+    // search); 64-word groups interleaved over waves, UNPACK_GROUPS per iteration so
+    // that their LDS round trips overlap; coalesced 512-byte stores.
     {
         const uint32_t ng = (Wt + CAPNP_WAVE - 1) / CAPNP_WAVE;
-        for (uint32_t g0 = wave; g0 < ng; g0 += 2 * kWaves) {
-            uint32_t dh[2], k[2], ii[2];
-            bool valid[2];
+        for (uint32_t g0 = wave; g0 < ng; g0 += UNPACK_GROUPS * kWaves) {
+            uint32_t d[UNPACK_GROUPS];
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const uint32_t g = g0 + u * kWaves;
-                const uint32_t i = g * CAPNP_WAVE + lane;
-                ii[u] = i;
-                valid[u] = g < ng && i < Wt;
-                const uint32_t d = valid[u] ? S.dpos[i] : kNone;
-                const uint64_t heads = ballot64(d != kNone);
-                // carry-in: the run covering the group's first words started in
-                // an earlier group (its last head); rare, a wave-uniform branch
-                uint32_t dc = kNone, hc = 0;
-                if (g < ng && !(heads & 1ull)) {
-                    for (uint32_t gg = g; gg-- > 0;) {
-                        const uint32_t d2 = S.dpos[gg * CAPNP_WAVE + lane];
-                        const uint64_t m2 = ballot64(d2 != kNone);
-                        if (m2) {
-                            const uint32_t h2 = 63u - (uint32_t)__builtin_clzll(m2);
-                            dc = (uint32_t)__builtin_amdgcn_readlane((int)d2, h2);
-                            hc = gg * CAPNP_WAVE + h2;
-                            break;
-                        }
-                    }
-                }
-                const uint64_t hm = heads & low_mask(lane + 1);
-                const uint32_t h = hm ? 63u - (uint32_t)__builtin_clzll(hm) : lane;
-                const uint32_t dh0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(h << 2), (int)d);
-                // (no head at all only after a decode error: output unspecified)
-                dh[u] = hm ? dh0 : dc;
-                k[u] = hm ? lane - h : i - hc;
+            for (int u = 0; u < UNPACK_GROUPS; u++) {
+                const uint32_t i = (g0 + u * kWaves) * CAPNP_WAVE + lane;
+                d[u] = i < Wt ? S.dpos[i] : kNone;
             }
-            typedef uint64_t u64u __attribute__((aligned(1)));
 #pragma unroll
-            for (int u = 0; u < 2; u++) {
-                const uint32_t pos = dh[u] == kNone ? 0u : dh[u];
-                const uint32_t src = k[u] ? pos + 2 + 8 * k[u] : pos + 1;
-                const uint32_t tag = S.bytes[pos];
-                const uint64_t v = lds_bytes8(S.bytes, src);
-                const uint32_t t = k[u] == 0 ? tag : (tag == 0xFF ? 0xFFu : 0u);
-                const uint64_t sv = S.sel[t];
-                const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-                const uint64_t word =
-                    ((uint64_t)__builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32)) << 32) |
-                    __builtin_amdgcn_perm(hi, lo, (uint32_t)sv);
-                if (valid[u]) out[W0 + ii[u]] = word;
+            for (int u = 0; u < UNPACK_GROUPS; u++) {
+                const uint32_t i = (g0 + u * kWaves) * CAPNP_WAVE + lane;
+                const uint64_t word = expand_desc(S.bytes, S.sel, d[u]);
+                if (i < Wt) out[W0 + i] = word;
             }
         }
     }
@@ -828,83 +825,7 @@ struct SyncSmem {
     WaveSmem w[kWaves];
 };
 
-// Wave-wide inclusive max-scan (DPP, VALU only).
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));  // row_shr:1
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));  // row_shr:2
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));  // row_shr:4
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));  // row_shr:8
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));  // row_bcast:15
-    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));  // row_bcast:31
-    return x;
-}
-
-// Expansion of the sub-tile's segments, lane b = segment b (rounds of 64).
-// A head is encoded (word + 1) << 16 | LDS position; the word's record is the
-// largest code at or below it.
-__device__ __forceinline__ void expand_segments(const WaveSmem& S, const uint64_t* sel,
-                                                uint32_t nseg, uint64_t kf, uint64_t W0,
-                                                uint32_t Wt, uint64_t* __restrict__ out,
-                                                uint32_t lane) {
-    typedef uint64_t u64u __attribute__((aligned(1)));
-    typedef uint4 u4u __attribute__((aligned(2)));
-    uint32_t carry = 0;  // last head of the previous rounds
-    for (uint32_t r0 = 0; r0 < nseg; r0 += CAPNP_WAVE) {
-        const uint32_t b = r0 + lane;
-        const bool have = b < nseg;
-        const uint32_t sb = b == 0 ? 0u : (uint32_t)((kf + b - 1) * kSyncWords - W0);
-        const uint32_t eb =
-            b + 1 >= nseg ? Wt : (uint32_t)((kf + b) * kSyncWords - W0);
-        const uint32_t n = have ? eb - sb : 0u;
-        uint32_t d[kSyncWords];
-        {
-            const uint32_t base = have ? sb : 0u;
-#pragma unroll
-            for (uint32_t j = 0; j < kSyncWords; j += 8) {
-                const uint4 v = *reinterpret_cast<const u4u*>(S.dpos + base + j);
-                d[j + 0] = v.x & 0xFFFFu; d[j + 1] = v.x >> 16;
-                d[j + 2] = v.y & 0xFFFFu; d[j + 3] = v.y >> 16;
-                d[j + 4] = v.z & 0xFFFFu; d[j + 5] = v.z >> 16;
-                d[j + 6] = v.w & 0xFFFFu; d[j + 7] = v.w >> 16;
-            }
-        }
-        uint32_t last = 0;
-#pragma unroll
-        for (uint32_t j = 0; j < kSyncWords; j++)
-            if (j < n && d[j] != kNone) last = ((sb + j + 1) << 16) | d[j];
-        const uint32_t incl = max(wave_incl_max(last), carry);
-        uint32_t cur = (uint32_t)__shfl_up((int)incl, 1, CAPNP_WAVE);
-        cur = lane == 0 ? carry : cur;
-        carry = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        uint64_t word[kSyncWords];
-#pragma unroll
-        for (uint32_t j = 0; j < kSyncWords; j++) {
-            if (d[j] != kNone) cur = ((sb + j + 1) << 16) | d[j];
-            const uint32_t pos = cur & 0xFFFFu;
-            const uint32_t k = sb + j + 1 - (cur >> 16);
-            const uint32_t src = k ? pos + 2 + 8 * k : pos + 1;
-            const uint32_t tag = S.bytes[pos];
-            const uint64_t v = lds_bytes8(S.bytes, src < kSubBytes ? src : 0u);
-            const uint32_t t = k == 0 ? tag : (tag == 0xFF ? 0xFFu : 0u);
-            const uint64_t sv = sel[t];
-            const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-            word[j] = ((uint64_t)__builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32)) << 32) |
-                      __builtin_amdgcn_perm(hi, lo, (uint32_t)sv);
-        }
-        uint64_t* o = out + W0 + sb;
-        if (n == kSyncWords) {
-#pragma unroll
-            for (uint32_t j = 0; j < kSyncWords; j += 2)
-                *reinterpret_cast<ulonglong2*>(o + j) = make_ulonglong2(word[j], word[j + 1]);
-        } else {
-#pragma unroll
-            for (uint32_t j = 0; j < kSyncWords; j++)
-                if (j < n) o[j] = word[j];
-        }
-    }
-}
-
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, 8)
 unpack_sync_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                    uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
                    const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
@@ -1005,11 +926,21 @@ unpack_sync_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ 
         }
     }
     wave_lds_sync();
-    // expand: lane b = segment b again.  The lane reads its 16 descriptors,
-    // finds each word's head (its own, or the last head of an earlier
-    // segment through a wave max-scan), and rebuilds its words from LDS with
-    // every read of the 16 words in flight at once.
-    expand_segments(S, sm.sel, nseg, kf, W0, Wt, out, lane);
+    // expand: lane = output word, four 64-word groups per iteration
+    for (uint32_t g0 = 0; g0 * CAPNP_WAVE < Wt; g0 += 4) {
+        uint32_t d[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = (g0 + u) * CAPNP_WAVE + lane;
+            d[u] = i < Wt ? S.dpos[i] : kNone;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i = (g0 + u) * CAPNP_WAVE + lane;
+            const uint64_t word = expand_desc(S.bytes, sm.sel, d[u]);
+            if (i < Wt) out[W0 + i] = word;
+        }
+    }
 }
 
 }  // namespace
