@@ -39,7 +39,7 @@
 #define UNPACK_GROUPS 2  // expansion groups in flight per wave
 #endif
 #ifndef UNPACK_MIN_WAVES
-#define UNPACK_MIN_WAVES 8  // __launch_bounds__ waves per SIMD of the tile kernel
+#define UNPACK_MIN_WAVES 7  // __launch_bounds__ waves per SIMD of the tile kernel (8 spills)
 #endif
 #ifndef UNPACK_PHASEA_UNROLL
 #define UNPACK_PHASEA_UNROLL 1
@@ -626,6 +626,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     return marked;
 }
 
+template <bool SYNC>
 __global__ void __launch_bounds__(kThreads, UNPACK_MIN_WAVES)
 unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
               uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
@@ -680,7 +681,7 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
         const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
         for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
         S.sel[tid] = expand_selector(tid);
-        if (sync) {
+        if constexpr (SYNC) {
             // chunk tables and the tile's sync entries (segment b >= 1 starts
             // at global word 32 (kf + b - 1))
             if (tid <= nc) {
@@ -716,7 +717,7 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
 #else
     const uint32_t walker = 0;
 #endif
-    if (sync) {
+    if constexpr (SYNC) {
         const uint32_t wrel = (wave - walker) & (kWaves - 1);
         const uint32_t b = wrel * CAPNP_WAVE + lane;
         bool marked = false;
@@ -755,7 +756,7 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
         status[c] = st;
         if (consumed) consumed[c] = used;
     }
-    if (!sync) __syncthreads();
+    if constexpr (!SYNC) __syncthreads();
     UPROF_T(t2);
     // expand: lane = output word (a plain descriptor lookup, no head
     // search); 64-word groups interleaved over waves, UNPACK_GROUPS per iteration so
@@ -825,7 +826,7 @@ struct SyncSmem {
     WaveSmem w[kWaves];
 };
 
-__global__ void __launch_bounds__(kThreads, 8)
+__global__ void __launch_bounds__(kThreads)
 unpack_sync_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                    uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
                    const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
@@ -975,9 +976,14 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
                            d_out, d_out_off, d_status, d_consumed, d_sync);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(unpack_kernel, dim3((uint32_t)blocks), dim3(kThreads), UNPACK_EXTRA_LDS,
-                       stream, d_in,
-                       d_in_off, nchunks, tc, d_out, d_out_off, d_status, d_consumed, d_sync);
+    if (d_sync)
+        hipLaunchKernelGGL(unpack_kernel<true>, dim3((uint32_t)blocks), dim3(kThreads),
+                           UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
+                           d_status, d_consumed, d_sync);
+    else
+        hipLaunchKernelGGL(unpack_kernel<false>, dim3((uint32_t)blocks), dim3(kThreads),
+                           UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
+                           d_status, d_consumed, d_sync);
     return hipGetLastError();
 }
 
