@@ -89,10 +89,10 @@ constexpr uint32_t kRegion = (kStageBytes + 32 + 15) & ~15u;
 constexpr uint32_t kRegionBytes = kRegion > kRing ? kRegion : kRing;
 
 // Record sync index (optional side-band): one entry per global word index
-// m = 32k, for the chunk that holds word m: the chunk-relative packed offset of
-// the first record that starts at a word >= m (24 bits) and that word minus m
-// (8 bits; a run covers at most 255 words after its head, so it fits).  An
-// unpack that has the index walks 32-word segments in parallel and checks that
+// m = 16k, for the chunk that holds word m: the chunk-relative packed offset of
+// the record that covers word m (24 bits) and m minus that record's first
+// word (8 bits; a run covers at most 255 words after its head, so it fits).  An
+// unpack that has the index walks 16-word segments in parallel and checks that
 // consecutive segments meet (unpack.hip).  kSyncNone marks an entry the
 // kernel does not provide (streaming path); the decoder then walks serially.
 constexpr uint32_t kSyncWords = CAPNP_SYNC_WORDS;
@@ -111,6 +111,7 @@ struct Smem {
     uint64_t wave_bytes[kWaves];
     uint64_t wave_steps[kWaves];
     uint32_t sync[kMaxSync];            // the tile's record sync entries
+    uint32_t chunk_oc[kMaxTileChunks];  // staged path: chunk start in its wave's region
     // per-wave staging region; the streaming path uses its first 4 KiB as
     // the flush ring
     alignas(16) uint8_t stage[kWaves][kRegionBytes];
@@ -379,8 +380,15 @@ __device__ __forceinline__ void size_step(Packer& pk, uint64_t w, uint32_t nvali
     pk.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
 }
 
+// Pass 2 of one staged step.  With `tab` (record sync index), every head
+// lane also writes the entries of the sync points its record covers: words
+// g + lane .. + the run (t0 = the tile's first sync word, oc = the chunk's
+// start in the region); usually none or one, more only for runs of > 16
+// words.  The head lane knows its own position and run length, so this is
+// a few VALU ops and a masked LDS store per step.
 __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32_t ext,
-                                          uint32_t lane, uint8_t* region, const uint64_t* sel) {
+                                          uint32_t lane, uint8_t* region, const uint64_t* sel,
+                                          uint32_t* tab, uint32_t t0, uint32_t g, uint32_t oc) {
     const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
     const uint32_t tag = si.tag;
     const uint32_t nvalid = si.meta & 127u;
@@ -412,58 +420,19 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
     __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-}
-
-// Sync points whose first record lies in a later step (a run covers them).
-struct SyncPend {
-    uint32_t m = 0;  // first pending point (tile-relative word)
-    uint32_t k = 0;  // pending points: m, m + 32, ...
-};
-
-// Record sync entries of one staged step, in tile-relative words (run after
-// pass 2, so it overlaps the look-back instead of delaying the publish):
-// g = the step's lane-0 word, t0 = the first sync word of the tile (entry
-// index i <-> word t0 + kSyncWords i), si = the step's heads and byte
-// positions, oc = the chunk's start in the region, total = the chunk's bytes.
-// Lane-parallel: a lane on a sync point finds the first head at or after it
-// in the step; points with none (a run covers the rest of the step) wait for
-// a later step's first head or the chunk end.
-__device__ __forceinline__ void sync_step(uint32_t* tab, uint32_t t0, uint32_t g, uint32_t meta,
-                                          const StepInfo& si, uint32_t oc, uint32_t total,
-                                          SyncPend& ps, uint32_t lane) {
-#if PACK_ABLATE == 5
-    return;  // timing-only: no sync entries
+#if PACK_ABLATE != 5
+    if (tab) {
+        const uint32_t hw = g + lane;
+        const uint32_t words = head ? 1u + ((isz || isf) ? cnt : 0u) : 0u;
+        uint32_t m = hw + ((t0 - hw) & (kSyncWords - 1));
+        const uint32_t rel = pos - oc;
+        if (m < hw + words) {
+            tab[(m - t0) / kSyncWords] = rel | ((m - hw) << 24);
+            for (m += kSyncWords; m < hw + words; m += kSyncWords)
+                tab[(m - t0) / kSyncWords] = rel | ((m - hw) << 24);
+        }
+    }
 #endif
-    const uint32_t nv = meta & 127u;
-    const uint64_t H = si.H;
-    if (ps.k && H) {  // pending points end at this step's first head
-        const uint32_t h = ctz64(H);
-        const uint32_t ph = (uint32_t)__builtin_amdgcn_readlane((int)si.pos, h) - oc;
-        if (lane < ps.k) {
-            const uint32_t m = ps.m + kSyncWords * lane;
-            tab[(m - t0) / kSyncWords] = ph | ((g + h - m) << 24);
-        }
-        ps.k = 0;
-    }
-    const uint32_t sl0 = (t0 - g) & (kSyncWords - 1);
-    const bool pt = lane < nv && lane >= sl0 && ((lane - sl0) & (kSyncWords - 1)) == 0;
-    const uint64_t Hl = H >> lane;
-    const uint32_t h = lane + ctz64(Hl);
-    const uint32_t ph =
-        (uint32_t)__builtin_amdgcn_ds_bpermute((int)((h & 63u) << 2), (int)si.pos) - oc;
-    if (pt && Hl) tab[(g + lane - t0) / kSyncWords] = ph | ((h - lane) << 24);
-    const uint64_t nohead = ballot64(pt && !Hl);
-    if (nohead) {
-        if (!ps.k) ps.m = g + ctz64(nohead);
-        ps.k += popc64(nohead);
-    }
-    if (((meta >> 8) & 1) && ps.k) {  // chunk end inside a run
-        if (lane < ps.k) {
-            const uint32_t m = ps.m + kSyncWords * lane;
-            tab[(m - t0) / kSyncWords] = total | ((g + nv - m) << 24);
-        }
-        ps.k = 0;
-    }
 }
 
 // Copies region bytes [0, len) to out[D0 .. D0+len) (16-aligned coordinates),
@@ -742,6 +711,7 @@ __device__ __forceinline__ uint64_t scan_chunks(Smem& sm, uint32_t nc, uint32_t 
 }
 
 // One workgroup per tile (tile = blockIdx.x), 4 waves.
+template <bool SYNC>
 __global__ void __launch_bounds__(kThreads, 8)
 pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
             uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
@@ -858,7 +828,10 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                 if (s < nsteps) {
                     const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
                     si[s].meta = meta;
-                    if ((meta >> 7) & 1) pk.begin(local);
+                    if ((meta >> 7) & 1) {
+                        pk.begin(local);
+                        if (lane == 0) sm.chunk_oc[wc0 + (meta >> 9)] = (uint32_t)local;
+                    }
 #if PACK_ABLATE == 3 || PACK_ABLATE == 4
                     asm volatile("" ::"v"(cache[s]));  // timing-only: skip the arithmetic
                     pk.total += 34 * (meta & 127u) / 8;
@@ -890,7 +863,9 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                 if ((uint32_t)s < nsteps) {
                     const uint32_t meta = si[s].meta;
                     const uint32_t e = ((meta >> 8) & 1) ? 0u : ext;
-                    emit_step(cache[s], si[s], e, lane, region, sm.sel);
+                    emit_step(cache[s], si[s], e, lane, region, sm.sel, SYNC ? sm.sync : nullptr,
+                              t0, (uint32_t)__builtin_amdgcn_readlane((int)d_g, s),
+                              uniform(sm.chunk_oc[wc0 + (meta >> 9)]));
                     // ext for step s-1: absorbed here, plus later if the run
                     // covered this whole step
                     ext = ((meta >> 7) & 1) ? 0u : si[s].kin + (si[s].H == 0 ? e : 0u);
@@ -904,26 +879,9 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             if (lane < nc) sm.chunk_pos[lane] += excl;
             if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
         }
-        // record sync entries: waves 1-3 while wave 0 waits on the look-back,
-        // wave 0 after it (its look-back is not delayed)
-        if (sync) {
-            SyncPend ps;
-            uint32_t oc = 0;
-#pragma unroll
-            for (uint32_t s = 0; s < kStageSteps; s++) {
-                if (s < nsteps) {
-                    const uint32_t meta = si[s].meta;
-                    if ((meta >> 7) & 1) oc = (uint32_t)__builtin_amdgcn_readlane((int)si[s].pos, 0);
-                    const uint32_t total =
-                        (meta >> 8) & 1 ? (uint32_t)lds_u64(&sm.chunk_size[wc0 + (meta >> 9)]) : 0u;
-                    sync_step(sm.sync, t0, (uint32_t)__builtin_amdgcn_readlane((int)d_g, s), meta,
-                              si[s], oc, total, ps, lane);
-                }
-            }
-        }
         __syncthreads();
         for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
-        if (sync)
+        if constexpr (SYNC)
             for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = sm.sync[i];
 #if PACK_ABLATE == 2
         return;  // timing-only: no output stores
@@ -937,7 +895,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         if (tid == 0) TRACE(tile, 3, RT());
 #endif
     } else {
-        if (sync)
+        if constexpr (SYNC)
             for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
         run_streaming<MODE_SIZE>(in, sm.off, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
                                  region, sm.sel, outa, mis, out_cap);
@@ -985,9 +943,14 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_
     }
     hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(nchunks, tc), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(pack_kernel, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream, d_in,
-                       d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_state,
-                       d_state + ntiles, d_sync);
+    if (d_sync)
+        hipLaunchKernelGGL(pack_kernel<true>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
+                           d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_state,
+                           d_state + ntiles, d_sync);
+    else
+        hipLaunchKernelGGL(pack_kernel<false>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
+                           d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_state,
+                           d_state + ntiles, d_sync);
     return hipGetLastError();
 }
 

@@ -472,7 +472,10 @@ __device__ __forceinline__ void mark_bad(SM& S, uint32_t c, bool& marked) {
 }
 
 // Start state of segment b (starting at tile word sb): chunk, position + 1,
-// word.  An unusable entry yields the end of its chunk and marks it bad.
+// word.  The entry names the record that covers word sb; if that record
+// started in an earlier segment (d > 0: a run), it belongs to that
+// segment's walker and the segment starts after it.  An unusable entry
+// yields the end of its chunk and marks it bad.
 template <class SM>
 __device__ __forceinline__ void seg_start(SM& S, uint32_t nc, uint32_t b, uint32_t sb,
                                           uint32_t& c, uint32_t& q, uint32_t& w, bool mark,
@@ -485,14 +488,26 @@ __device__ __forceinline__ void seg_start(SM& S, uint32_t nc, uint32_t b, uint32
     }
     const uint32_t e = S.ent[b];
     const uint32_t off = e & 0xFFFFFFu, d = e >> 24;
-    if (e == kSyncNone || off > S.cp[c + 1] - S.cp[c] || sb + d > S.cw[c + 1]) {
-        if (mark) mark_bad(S, c, marked);
-        q = S.cp[c + 1] + 1u;
-        w = S.cw[c + 1];
-        return;
-    }
+    const uint32_t cpe1 = S.cp[c + 1] + 1u, cwe = S.cw[c + 1];
+    bool ok = e != kSyncNone && off < S.cp[c + 1] - S.cp[c] && sb - d >= S.cw[c] && d <= sb;
     q = S.cp[c] + off + 1u;
-    w = sb + d;
+    w = sb;
+    if (ok && d) {  // skip the run that covers sb
+        uint32_t tag, b1, b9;
+        rec_bytes(S.bytes, q, tag, b1, b9);
+        const bool isz = tag == 0, isf = tag == 0xFF;
+        const uint32_t qe = __builtin_popcount(tag) + q + (isz ? 1u : 0u) +
+                            (isf ? 8u * b9 + 1u : 0u) + 1u;
+        const uint32_t wn = sb - d + 1u + (isz ? b1 : (isf ? b9 : 0u));
+        ok = (isz || isf) && wn > sb && wn <= cwe && qe <= cpe1;
+        q = qe;
+        w = wn;
+    }
+    if (!ok) {
+        if (mark) mark_bad(S, c, marked);
+        q = cpe1;
+        w = cwe;
+    }
 }
 
 // Returns true if it marked a chunk bad.

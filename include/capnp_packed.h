@@ -136,9 +136,9 @@ capnp_status capnp_gpu_unpack_batch(capnp_ctx* ctx, const uint8_t* d_packed,
    word index m = CAPNP_SYNC_WORDS * k of the batch's word space
    (k < ceil(total_words / CAPNP_SYNC_WORDS)).
    Entry k describes the chunk c that holds word m: bits 0-23 are the
-   chunk-relative packed offset of the first record (tag) that starts at a
-   word >= m, bits 24-31 that word minus m (a run covers at most 255 words
-   after its head).  0xFFFFFFFF = not provided (chunks packed by the
+   chunk-relative packed offset of the record (tag) that covers word m,
+   bits 24-31 m minus that record's first word (a run covers at most 255
+   words after its head).  0xFFFFFFFF = not provided (chunks packed by the
    streaming path, i.e. larger than the staged tile).  The packed bytes are
    unchanged: the index is metadata, like d_out_byte_off.
    An unpack given the index (with the same word offsets as the pack, as
