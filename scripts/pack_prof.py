@@ -75,7 +75,8 @@ def main():
         print(f"iter {it}: {e0.elapsed_time(e1) * 1e3:.1f} us ok={ok} tiles={ntiles} "
               f"within-spins/tile={T[:, 5].mean():.2f} group-spins/tile={T[:, 6].mean():.2f} "
               f"windows/tile={T[:, 7].mean():.2f} pass1={us(0, 1):.1f}us "
-              f"pub->offset={us(1, 2):.1f}us offset->end={us(2, 3):.1f}us")
+              f"pub->offset={us(1, 2):.1f}us offset->end={us(2, 3):.1f}us "
+              f"life={us(0, 3):.1f}us conc={(T[:, 3] - T[:, 0]).sum() / max(T[:, 3].max() - T[:, 0].min(), 1):.0f}")
     if a.trace:
         import numpy as np
         np.save(a.trace, trace.view(ntiles, 8).cpu().numpy())
