@@ -103,8 +103,15 @@ constexpr uint64_t kFlagAgg = 1ull << 62;  // tile aggregate available
 constexpr uint64_t kFlagInc = 2ull << 62;  // tile inclusive prefix available
 constexpr uint64_t kValMask = (1ull << 62) - 1;
 
+// Compaction selectors (v_perm_b32 over hi:lo) per tag: sel[t] puts a zero
+// byte (later the tag) in byte 0 of the record's first dword and the first
+// seven non-zero bytes of the word after it; byte 7 of a 0xFF word goes
+// into the third dword separately.  sel[kSelCopy] copies the word as is (a
+// literal word inside a run), so every lane does the same two v_perms.
+constexpr uint32_t kSelCopy = 256;
+
 struct Smem {
-    uint64_t sel[256];                  // compaction selectors per tag
+    uint64_t sel[kSelCopy + 1];         // compaction selectors per tag
     uint64_t off[kMaxTileChunks + 1];   // chunk word offsets of the tile
     uint64_t chunk_size[kMaxTileChunks];
     uint64_t chunk_pos[kMaxTileChunks];
@@ -113,7 +120,9 @@ struct Smem {
     uint32_t sync[kMaxSync];            // the tile's record sync entries
     uint32_t chunk_oc[kMaxTileChunks];  // staged path: chunk start in its wave's region
     // per-wave staging region; the streaming path uses its first 4 KiB as
-    // the flush ring
+    // the flush ring.  emit_step ORs a zero into the dword before a record
+    // that starts 4-aligned, hence the pad.
+    alignas(16) uint32_t pad[4];
     alignas(16) uint8_t stage[kWaves][kRegionBytes];
 };
 
@@ -255,15 +264,10 @@ struct Packer {
             if (head && tag == 0) {
                 r0 = cnt << 8;
             } else if (head) {
-                uint32_t clo = lo, chi = hi;
-                if (tag != 0xFF) {
-                    const uint64_t s = sel[tag];
-                    clo = __builtin_amdgcn_perm(hi, lo, (uint32_t)s);
-                    chi = __builtin_amdgcn_perm(hi, lo, (uint32_t)(s >> 32));
-                }
-                r0 = tag | (clo << 8);
-                r1 = (clo >> 24) | (chi << 8);
-                r2 = (chi >> 24) | (tag == 0xFF ? cnt << 8 : 0u);
+                const uint64_t s = sel[tag];
+                r0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)s) | tag;
+                r1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(s >> 32));
+                r2 = tag == 0xFF ? __builtin_amdgcn_perm(cnt, hi, 0x0C0C0403u) : 0u;
             } else {
                 r0 = lo;
                 r1 = hi;
@@ -357,9 +361,30 @@ struct StepInfo {
     uint32_t meta;     // nvalid | first << 7 | last << 8 | chunk << 9
 };
 
+// Per lane: bit `lane` of the wave-uniform mask m ? a : b.  One VOP3
+// v_cndmask with the mask as its lane-select operand, instead of a 64-bit
+// shift and compare the compiler would emit for ((m >> lane) & 1).
+__device__ __forceinline__ uint32_t mask_sel(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
+}
+
+// The tag of a word and its popcount.  Non-zero bytes flag bit 7 of each
+// byte; v_dot4 with weights 1..128 gathers the eight flags (as tag << 7)
+// at full rate, where the multiply gather needs two quarter-rate v_mul_lo.
+__device__ __forceinline__ uint32_t word_tag_dot(uint32_t lo, uint32_t hi) {
+    const uint32_t fl = (((lo & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | lo) & 0x80808080u;
+    const uint32_t fh = (((hi & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | hi) & 0x80808080u;
+    const uint32_t t = __builtin_amdgcn_udot4(fl, 0x08040201u,
+                                              __builtin_amdgcn_udot4(fh, 0x80402010u, 0u, false),
+                                              false);
+    return t >> 7;
+}
+
 __device__ __forceinline__ void size_step(Packer& pk, uint64_t w, uint32_t nvalid, uint32_t lane,
                                           StepInfo& si) {
-    const uint32_t tag = word_tag((uint32_t)w, (uint32_t)(w >> 32));
+    const uint32_t tag = word_tag_dot((uint32_t)w, (uint32_t)(w >> 32));
     const uint32_t pop = __builtin_popcount(tag);
     const bool isz = tag == 0, isf = tag == 0xFF;
     const uint64_t V = low_mask(nvalid);
@@ -367,10 +392,10 @@ __device__ __forceinline__ void size_step(Packer& pk, uint64_t w, uint32_t nvali
     const uint64_t Lm = ballot64(pop >= 7) & V;
     const uint64_t Fm = ballot64(isf) & V;
     const StepMasks sm = resolve_step(Zm, Lm, Fm, nvalid, pk.carry);
-    const bool head = (sm.H >> lane) & 1;
-    const bool valid = lane < nvalid;
-    const uint32_t hsize = isz ? 2u : (isf ? 10u : 1u + pop);
-    const uint32_t size = head ? hsize : ((valid && !isz) ? 8u : 0u);
+    // head: 2 (Z), 10 (F), else 1 + pop; other words: 8 unless zero (lanes
+    // past nvalid hold zero words)
+    const uint32_t hsize = 1u + pop + ((0x101u >> pop) & 1u);
+    const uint32_t size = mask_sel(sm.H, hsize, isz ? 0u : 8u);
     const uint32_t incl = wave_incl_scan(size);
     si.H = sm.H;
     si.pos = (uint32_t)(pk.o_c + pk.total) + incl - size;
@@ -392,44 +417,52 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
     const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
     const uint32_t tag = si.tag;
     const uint32_t nvalid = si.meta & 127u;
-    const bool isz = tag == 0, isf = tag == 0xFF;
-    const uint64_t hsh = si.H >> lane;
-    const bool head = hsh & 1;
-    // run count of a Z/F head: words up to the next head, else to the step
-    // end plus what the run absorbs in later steps
-    const uint64_t nxt = hsh >> 1;
-    const uint32_t cnt = nxt ? ctz64(nxt) : nvalid - lane - 1 + ext;
-    const uint64_t sv = sel[tag];
-    const uint32_t clo = __builtin_amdgcn_perm(hi, lo, (uint32_t)sv);
-    const uint32_t chi = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32));
-    uint32_t r0 = isz ? (cnt << 8) : (tag | (clo << 8));
-    uint32_t r1 = (clo >> 24) | (chi << 8);
-    uint32_t r2 = (chi >> 24) | (isf ? (cnt << 8) : 0u);
-    r0 = head ? r0 : lo;
-    r1 = head ? (isz ? 0u : r1) : hi;
-    r2 = head ? (isz ? 0u : r2) : 0u;
-    // (absorbed zero words and lanes past nvalid hold w == 0: all zeros)
+    // words after this lane's record up to the next head, else to the step
+    // end plus what the run absorbs in later steps: the run count of a Z/F
+    // head; 0 for any other head (every word no run absorbs is a head)
+    const uint64_t nxt = (si.H >> 1) >> lane;
+    const uint32_t cz = (uint32_t)nxt ? (uint32_t)__builtin_ctz((uint32_t)nxt) : ~0u;
+    const uint32_t ch = (uint32_t)(nxt >> 32) ? 32u + __builtin_ctz((uint32_t)(nxt >> 32)) : ~0u;
+    const uint32_t cnt = min(min(cz, ch), nvalid - 1u - lane + ext);
+    // record dwords r2:r1:r0 = tag, compacted bytes, count byte; a literal
+    // word inside a run is copied; absorbed zero words and lanes past nvalid
+    // hold w == 0 and emit nothing
+    const uint64_t sv = sel[mask_sel(si.H, tag, kSelCopy)];
+    const uint32_t x0 = mask_sel(si.H, tag == 0 ? cnt << 8 : tag, 0u);
+    const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sv) | x0;
+    const uint32_t r1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32));
+    const uint32_t r2 = mask_sel(si.H, tag == 0xFF ? __builtin_amdgcn_perm(cnt, hi, 0x0C0C0403u) : 0u,
+                                 0u);
+    // OR (r << 8k), k = pos & 3, into the dwords from pos & ~3.  Written as
+    // alignbyte by (-pos) & 3 from the dword before ceil(pos / 4): for k = 0
+    // the first dword gets zero and the rest r0..r2 unshifted.
     const uint32_t pos = si.pos;
-    const uint32_t sh = (pos & 3) * 8;
-    const uint32_t e0 = r0 << sh;
-    const uint32_t e1 = (uint32_t)((((uint64_t)r1 << 32) | r0) >> (32 - sh));
-    const uint32_t e2 = (uint32_t)((((uint64_t)r2 << 32) | r1) >> (32 - sh));
-    const uint32_t e3 = (uint32_t)((uint64_t)r2 >> (32 - sh));
-    uint32_t* b32 = reinterpret_cast<uint32_t*>(region) + (pos >> 2);
+    const uint32_t s = 0u - pos;
+    const uint32_t e0 = __builtin_amdgcn_alignbyte(r0, 0u, s);
+    const uint32_t e1 = __builtin_amdgcn_alignbyte(r1, r0, s);
+    const uint32_t e2 = __builtin_amdgcn_alignbyte(r2, r1, s);
+    const uint32_t e3 = __builtin_amdgcn_alignbyte(0u, r2, s);
+    uint32_t* b32 = reinterpret_cast<uint32_t*>(region + ((pos + 3u) & ~3u)) - 1;
     __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 #if PACK_ABLATE != 5
     if (tab) {
-        const uint32_t hw = g + lane;
-        const uint32_t words = head ? 1u + ((isz || isf) ? cnt : 0u) : 0u;
-        uint32_t m = hw + ((t0 - hw) & (kSyncWords - 1));
-        const uint32_t rel = pos - oc;
-        if (m < hw + words) {
-            tab[(m - t0) / kSyncWords] = rel | ((m - hw) << 24);
-            for (m += kSyncWords; m < hw + words; m += kSyncWords)
-                tab[(m - t0) / kSyncWords] = rel | ((m - hw) << 24);
+        // sync points m = hw + d, d = (t0 - hw) mod 16, d <= cnt, of the
+        // record headed at word hw = g + lane; m - t0 is a multiple of 16,
+        // so its entry is the dword at byte (m - t0) / 4 of the table
+        const uint32_t d = (t0 - g - lane) & (kSyncWords - 1);
+        const uint32_t head = mask_sel(si.H, 1u, 0u);
+        if (head && d <= cnt) {
+            const uint32_t rel = pos - oc;
+            uint8_t* tb = reinterpret_cast<uint8_t*>(tab);
+            uint32_t b = (g + lane + d - t0) >> 2;
+            *reinterpret_cast<uint32_t*>(tb + b) = rel | (d << 24);
+            for (uint32_t dd = d + kSyncWords; dd <= cnt; dd += kSyncWords) {
+                b += 4;
+                *reinterpret_cast<uint32_t*>(tb + b) = rel | (dd << 24);
+            }
         }
     }
 #endif
@@ -751,17 +784,19 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     const uint64_t k1 = (uniform64(chunk_off[c1]) + kSyncWords - 1) / kSyncWords;
     const uint32_t t0 = (uint32_t)(k0 * kSyncWords - TW0);  // first sync word, tile-relative
     for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
-    // compaction selectors: byte r = index of the r-th set bit of the tag
+    // compaction selectors: byte r + 1 = index of the r-th set bit of the
+    // tag (r < 7), byte 0 zero (the tag's slot)
     {
         uint64_t s = 0x0C0C0C0C0C0C0C0Cull;
-        uint32_t r = 0;
+        uint32_t r = 1;
         for (uint32_t k = 0; k < 8; k++) {
             if (tid & (1u << k)) {
-                s = (s & ~(0xFFull << (8 * r))) | ((uint64_t)k << (8 * r));
+                if (r < 8) s = (s & ~(0xFFull << (8 * r))) | ((uint64_t)k << (8 * r));
                 r++;
             }
         }
         sm.sel[tid] = s;
+        if (tid == 0) sm.sel[kSelCopy] = 0x0706050403020100ull;
     }
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
