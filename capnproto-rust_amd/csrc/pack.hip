@@ -81,9 +81,11 @@ constexpr uint32_t kStepMax = 64 * 10 + 16;
 #endif
 constexpr uint32_t kStageSteps = PACK_STAGE_STEPS;
 constexpr uint32_t kStageWords = 64 * kStageSteps;
-// >= sum of per-chunk bounds for <= 32 chunks totalling kStageWords words,
+// >= the packed bytes of a wave's range: at most 8.5 bytes per word (a 0xFF
+// head of 10 bytes needs a word of <= 7 bytes before the next one) plus 1.5
+// per chunk, and a range holds at most kStageSteps non-empty chunks
+constexpr uint32_t kStageBytes = 8 * kStageWords + kStageWords / 2 + 2 * kStageSteps;
 // plus the 32 bytes copy_out may read past the end
-constexpr uint32_t kStageBytes = 8 * kStageWords + kStageWords / 2 + 3 * 32 + 64;
 constexpr uint32_t kRegion = (kStageBytes + 32 + 15) & ~15u;
 // per-wave LDS region: the staged bytes, or the streaming path's flush ring
 constexpr uint32_t kRegionBytes = kRegion > kRing ? kRegion : kRing;
@@ -97,27 +99,29 @@ constexpr uint32_t kRegionBytes = kRegion > kRing ? kRegion : kRing;
 // kernel does not provide (streaming path); the decoder then walks serially.
 constexpr uint32_t kSyncWords = CAPNP_SYNC_WORDS;
 constexpr uint32_t kSyncNone = 0xFFFFFFFFu;
-constexpr uint32_t kMaxSync = kWaves * 64 * kStageSteps / kSyncWords + 2;
 
 constexpr uint64_t kFlagAgg = 1ull << 62;  // tile aggregate available
 constexpr uint64_t kFlagInc = 2ull << 62;  // tile inclusive prefix available
 constexpr uint64_t kValMask = (1ull << 62) - 1;
 
-// Compaction selectors (v_perm_b32 over hi:lo) per tag: sel[t] puts a zero
-// byte (later the tag) in byte 0 of the record's first dword and the first
-// seven non-zero bytes of the word after it; byte 7 of a 0xFF word goes
-// into the third dword separately.  sel[kSelCopy] copies the word as is (a
-// literal word inside a run), so every lane does the same two v_perms.
+// Record assembly table, one entry per tag plus kSelCopy (a literal word
+// inside a run, copied as is), so every lane runs the same four ops:
+//   r0 = perm(hi, lo, s0) | ((cnt << 8 | tag) & m)
+//   r1 = perm(hi, lo, s1),  r2 = perm(cnt, hi, s2)
+// s0/s1 put a zero byte (the tag's slot) first and then the first seven
+// non-zero bytes of the word; s2 places byte 7 and the count byte of a 0xFF
+// word; m keeps the tag (0xFF), tag and count (0xFFFF, zero word) or nothing.
 constexpr uint32_t kSelCopy = 256;
+struct alignas(16) SelEntry {
+    uint32_t s0, s1, s2, m;
+};
 
 struct Smem {
-    uint64_t sel[kSelCopy + 1];         // compaction selectors per tag
-    uint64_t off[kMaxTileChunks + 1];   // chunk word offsets of the tile
+    SelEntry sel[kSelCopy + 1];         // record assembly per tag
     uint64_t chunk_size[kMaxTileChunks];
     uint64_t chunk_pos[kMaxTileChunks];
     uint64_t wave_bytes[kWaves];
     uint64_t wave_steps[kWaves];
-    uint32_t sync[kMaxSync];            // the tile's record sync entries
     uint32_t chunk_oc[kMaxTileChunks];  // staged path: chunk start in its wave's region
     // per-wave staging region; the streaming path uses its first 4 KiB as
     // the flush ring.  emit_step ORs a zero into the dword before a record
@@ -225,7 +229,7 @@ struct Packer {
     template <int MODE>
     __device__ __forceinline__ void step(uint64_t w, uint32_t nvalid, bool last, uint32_t lane,
                                          uint8_t* buf, uint8_t* __restrict__ out,
-                                         const uint64_t* sel) {
+                                         const SelEntry* sel) {
         const bool valid = lane < nvalid;
         const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
         const uint32_t tag = word_tag(lo, hi);
@@ -264,10 +268,10 @@ struct Packer {
             if (head && tag == 0) {
                 r0 = cnt << 8;
             } else if (head) {
-                const uint64_t s = sel[tag];
-                r0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)s) | tag;
-                r1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(s >> 32));
-                r2 = tag == 0xFF ? __builtin_amdgcn_perm(cnt, hi, 0x0C0C0403u) : 0u;
+                const SelEntry e = sel[tag];
+                r0 = __builtin_amdgcn_perm(hi, lo, e.s0) | tag;
+                r1 = __builtin_amdgcn_perm(hi, lo, e.s1);
+                r2 = __builtin_amdgcn_perm(cnt, hi, e.s2);
             } else {
                 r0 = lo;
                 r1 = hi;
@@ -370,6 +374,17 @@ __device__ __forceinline__ uint32_t mask_sel(uint64_t m, uint32_t a, uint32_t b)
     return r;
 }
 
+// Index of the lowest set bit, 0xFFFFFFFF for zero (v_ffbl_b32 as is).
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+__device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    return min(min(a, b), c);  // v_min3_u32
+}
+
 // The tag of a word and its popcount.  Non-zero bytes flag bit 7 of each
 // byte; v_dot4 with weights 1..128 gathers the eight flags (as tag << 7)
 // at full rate, where the multiply gather needs two quarter-rate v_mul_lo.
@@ -412,8 +427,9 @@ __device__ __forceinline__ void size_step(Packer& pk, uint64_t w, uint32_t nvali
 // words.  The head lane knows its own position and run length, so this is
 // a few VALU ops and a masked LDS store per step.
 __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32_t ext,
-                                          uint32_t lane, uint8_t* region, const uint64_t* sel,
-                                          uint32_t* tab, uint32_t t0, uint32_t g, uint32_t oc) {
+                                          uint32_t lane, uint8_t* region, const SelEntry* sel,
+                                          uint8_t* __restrict__ tab, uint32_t t0, uint32_t g,
+                                          uint32_t oc) {
     const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
     const uint32_t tag = si.tag;
     const uint32_t nvalid = si.meta & 127u;
@@ -421,18 +437,14 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
     // end plus what the run absorbs in later steps: the run count of a Z/F
     // head; 0 for any other head (every word no run absorbs is a head)
     const uint64_t nxt = (si.H >> 1) >> lane;
-    const uint32_t cz = (uint32_t)nxt ? (uint32_t)__builtin_ctz((uint32_t)nxt) : ~0u;
-    const uint32_t ch = (uint32_t)(nxt >> 32) ? 32u + __builtin_ctz((uint32_t)(nxt >> 32)) : ~0u;
-    const uint32_t cnt = min(min(cz, ch), nvalid - 1u - lane + ext);
-    // record dwords r2:r1:r0 = tag, compacted bytes, count byte; a literal
-    // word inside a run is copied; absorbed zero words and lanes past nvalid
-    // hold w == 0 and emit nothing
-    const uint64_t sv = sel[mask_sel(si.H, tag, kSelCopy)];
-    const uint32_t x0 = mask_sel(si.H, tag == 0 ? cnt << 8 : tag, 0u);
-    const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, (uint32_t)sv) | x0;
-    const uint32_t r1 = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32));
-    const uint32_t r2 = mask_sel(si.H, tag == 0xFF ? __builtin_amdgcn_perm(cnt, hi, 0x0C0C0403u) : 0u,
-                                 0u);
+    const uint32_t cnt = min3_u32(ffbl((uint32_t)nxt), ffbl((uint32_t)(nxt >> 32)) | 32u,
+                                  __builtin_elementwise_sub_sat(nvalid - 1u + ext, lane));
+    // record dwords r2:r1:r0 = tag, compacted bytes, count byte; absorbed
+    // zero words and lanes past nvalid hold w == 0 and emit nothing
+    const SelEntry se = sel[mask_sel(si.H, tag, kSelCopy)];
+    const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, se.s0) | (((cnt << 8) | tag) & se.m);
+    const uint32_t r1 = __builtin_amdgcn_perm(hi, lo, se.s1);
+    const uint32_t r2 = __builtin_amdgcn_perm(cnt, hi, se.s2);
     // OR (r << 8k), k = pos & 3, into the dwords from pos & ~3.  Written as
     // alignbyte by (-pos) & 3 from the dword before ceil(pos / 4): for k = 0
     // the first dword gets zero and the rest r0..r2 unshifted.
@@ -442,7 +454,7 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
     const uint32_t e1 = __builtin_amdgcn_alignbyte(r1, r0, s);
     const uint32_t e2 = __builtin_amdgcn_alignbyte(r2, r1, s);
     const uint32_t e3 = __builtin_amdgcn_alignbyte(0u, r2, s);
-    uint32_t* b32 = reinterpret_cast<uint32_t*>(region + ((pos + 3u) & ~3u)) - 1;
+    uint32_t* b32 = reinterpret_cast<uint32_t*>(__builtin_align_down(region + pos + 3u, 4)) - 1;
     __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
@@ -451,17 +463,20 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
     if (tab) {
         // sync points m = hw + d, d = (t0 - hw) mod 16, d <= cnt, of the
         // record headed at word hw = g + lane; m - t0 is a multiple of 16,
-        // so its entry is the dword at byte (m - t0) / 4 of the table
-        const uint32_t d = (t0 - g - lane) & (kSyncWords - 1);
-        const uint32_t head = mask_sel(si.H, 1u, 0u);
-        if (head && d <= cnt) {
+        // so its entry is the dword at byte (m - t0) / 4 of the tile's part
+        // of the index.  Other lanes get d = 512 > cnt (cnt <= 63 + ext <
+        // 512).  Every sync point is covered by exactly one record, so the
+        // entries go straight to memory.
+        const uint32_t c = t0 - g;
+        const uint32_t d = (c - lane) & (kSyncWords - 1);
+        const uint32_t dh = mask_sel(si.H, d, 512u);
+        if (dh <= cnt) {
             const uint32_t rel = pos - oc;
-            uint8_t* tb = reinterpret_cast<uint8_t*>(tab);
-            uint32_t b = (g + lane + d - t0) >> 2;
-            *reinterpret_cast<uint32_t*>(tb + b) = rel | (d << 24);
+            uint32_t b = (lane + d - c) >> 2;
+            *reinterpret_cast<uint32_t*>(tab + b) = rel | (d << 24);
             for (uint32_t dd = d + kSyncWords; dd <= cnt; dd += kSyncWords) {
                 b += 4;
-                *reinterpret_cast<uint32_t*>(tb + b) = rel | (dd << 24);
+                *reinterpret_cast<uint32_t*>(tab + b) = rel | (dd << 24);
             }
         }
     }
@@ -516,32 +531,17 @@ __device__ __forceinline__ void copy_out(const uint8_t* region, uint8_t* __restr
     if (lane < hi - b) out[b + lane] = region[(b - D0) + lane];
 }
 
-// Iterates the steps of chunks [ci, ce) of the tile in 64-word windows.
-struct RangeIter {
-    uint32_t ci, ce;
-    uint64_t base, len, woff;
-    __device__ __forceinline__ void skip(const uint64_t* off) {
-        while (ci < ce) {
-            woff = lds_u64(&off[ci]);
-            len = lds_u64(&off[ci + 1]) - woff;
-            if (base < len) break;
-            ci++;
-            base = 0;
-        }
-    }
-};
-
 // Streaming path: wave w owns chunks w, w+4, ...  MODE_SIZE fills
 // chunk_size; MODE_RING re-reads and writes at chunk_pos.
 template <int MODE>
 __device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* off,
                               uint64_t* chunk_size, const uint64_t* chunk_pos, uint32_t nc,
-                              uint32_t wave, uint32_t lane, uint8_t* ring, const uint64_t* sel,
+                              uint32_t wave, uint32_t lane, uint8_t* ring, const SelEntry* sel,
                               uint8_t* out, uint32_t mis, uint64_t out_cap) {
     Packer pk;
     for (uint32_t ci = wave; ci < nc; ci += kWaves) {
-        const uint64_t woff = lds_u64(&off[ci]);
-        const uint64_t len = lds_u64(&off[ci + 1]) - woff;
+        const uint64_t woff = uniform64(off[ci]);
+        const uint64_t len = uniform64(off[ci + 1]) - woff;
         if (len == 0) continue;
         if (MODE == MODE_RING) {
             const uint64_t pos = lds_u64(&chunk_pos[ci]);
@@ -777,7 +777,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         TRACE(tile, 4, ((uint64_t)xcc << 32) | hwid);
     }
 #endif
-    for (uint32_t i = tid; i <= nc; i += kThreads) sm.off[i] = chunk_off[c0 + i];
+    const uint64_t* __restrict__ toff = chunk_off + c0;  // the tile's chunk offsets
     // sync entries of the tile: k in [k0, k1), words 32k in [W0, W1)
     const uint64_t TW0 = uniform64(chunk_off[c0]);
     const uint64_t k0 = (TW0 + kSyncWords - 1) / kSyncWords;
@@ -795,8 +795,13 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                 r++;
             }
         }
-        sm.sel[tid] = s;
-        if (tid == 0) sm.sel[kSelCopy] = 0x0706050403020100ull;
+        SelEntry e;
+        e.s0 = (uint32_t)s;
+        e.s1 = (uint32_t)(s >> 32);
+        e.s2 = tid == 0xFF ? 0x0C0C0403u : 0x0C0C0C0Cu;
+        e.m = tid == 0 ? 0xFFFFu : 0xFFu;
+        sm.sel[tid] = e;
+        if (tid == 0) sm.sel[kSelCopy] = SelEntry{0x03020100u, 0x07060504u, 0x0C0C0C0Cu, 0u};
     }
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
@@ -814,8 +819,8 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     uint32_t d_meta = 0;
     uint32_t nsteps = 0;
     for (uint32_t ci = wc0; ci < wc1; ci++) {
-        const uint64_t woff = lds_u64(&sm.off[ci]);
-        const uint64_t len = lds_u64(&sm.off[ci + 1]) - woff;
+        const uint64_t woff = uniform64(toff[ci]);
+        const uint64_t len = uniform64(toff[ci + 1]) - woff;
         const uint32_t nst = (uint32_t)((len + 63) / 64);
         const uint32_t k = lane - nsteps;
         if (lane >= nsteps && k < nst) {
@@ -898,7 +903,8 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                 if ((uint32_t)s < nsteps) {
                     const uint32_t meta = si[s].meta;
                     const uint32_t e = ((meta >> 8) & 1) ? 0u : ext;
-                    emit_step(cache[s], si[s], e, lane, region, sm.sel, SYNC ? sm.sync : nullptr,
+                    emit_step(cache[s], si[s], e, lane, region, sm.sel,
+                              SYNC ? reinterpret_cast<uint8_t*>(sync + k0) : nullptr,
                               t0, (uint32_t)__builtin_amdgcn_readlane((int)d_g, s),
                               uniform(sm.chunk_oc[wc0 + (meta >> 9)]));
                     // ext for step s-1: absorbed here, plus later if the run
@@ -916,8 +922,6 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         }
         __syncthreads();
         for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
-        if constexpr (SYNC)
-            for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = sm.sync[i];
 #if PACK_ABLATE == 2
         return;  // timing-only: no output stores
 #endif
@@ -932,7 +936,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     } else {
         if constexpr (SYNC)
             for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
-        run_streaming<MODE_SIZE>(in, sm.off, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
+        run_streaming<MODE_SIZE>(in, toff, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
                                  region, sm.sel, outa, mis, out_cap);
         __syncthreads();
         if (wave == 0) {
@@ -947,7 +951,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 #if PACK_ABLATE == 2
         return;
 #endif
-        run_streaming<MODE_RING>(in, sm.off, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
+        run_streaming<MODE_RING>(in, toff, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
                                  region, sm.sel, outa, mis, out_cap);
     }
 }

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--chunk-words", type=int, default=128)
     ap.add_argument("--pz", type=int, default=1288490189)
     ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--rounds", type=int, default=4)
     a = ap.parse_args()
     import torch
     from capnp_amd import Context, tile_chunks_for
@@ -38,9 +39,10 @@ def main():
     oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
     sync = torch.empty(ctx.sync_entries(n * cw), dtype=torch.int32, device="cuda")
     tc = tile_chunks_for(n * cw, n)
+    vp, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
+    libs = []
     for path in a.libs:
         L = C.CDLL(os.path.abspath(path))
-        vp, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
         L.capnp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int)]
         L.capnp_ctx_create.restype = vp
         L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, u32, vp]
@@ -49,29 +51,37 @@ def main():
         st = C.c_int(0)
         h = vp(L.capnp_ctx_create(0, C.byref(st)))
         L.capnp_ctx_reserve(h, n)
+        libs.append((path, L, h))
+    times = {}
+    oks = {}
+    # rounds interleave the libraries so clock drift hits all of them alike
+    for rnd in range(a.rounds):
+        for path, L, h in libs:
+            for use_sync in (False, True):
+                for it in range(a.iters + 1):
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    if use_sync:
+                        r = L.capnp_gpu_pack_batch_sync_tuned(
+                            h, P(words.data_ptr()), P(offs.data_ptr()), n, P(out.data_ptr()), cap,
+                            P(oo.data_ptr()), P(sync.data_ptr()), tc, P(stream.cuda_stream))
+                    else:
+                        r = L.capnp_gpu_pack_batch_tuned(
+                            h, P(words.data_ptr()), P(offs.data_ptr()), n, P(out.data_ptr()), cap,
+                            P(oo.data_ptr()), tc, P(stream.cuda_stream))
+                    e1.record(stream)
+                    e1.synchronize()
+                    assert r == 0, r
+                    if it:
+                        times.setdefault((path, use_sync), []).append(e0.elapsed_time(e1) * 1e3)
+                ok = torch.equal(oo, ref_off) and torch.equal(out[:ref.numel()], ref)
+                oks[(path, use_sync)] = oks.get((path, use_sync), True) and ok
+    for path, _, _ in libs:
         for use_sync in (False, True):
-            ts = []
-            for it in range(a.iters + 1):
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                if use_sync:
-                    r = L.capnp_gpu_pack_batch_sync_tuned(h, P(words.data_ptr()), P(offs.data_ptr()),
-                                                          n, P(out.data_ptr()), cap,
-                                                          P(oo.data_ptr()), P(sync.data_ptr()), tc,
-                                                          P(stream.cuda_stream))
-                else:
-                    r = L.capnp_gpu_pack_batch_tuned(h, P(words.data_ptr()), P(offs.data_ptr()),
-                                                     n, P(out.data_ptr()), cap, P(oo.data_ptr()),
-                                                     tc, P(stream.cuda_stream))
-                e1.record(stream)
-                e1.synchronize()
-                assert r == 0, r
-                if it:
-                    ts.append(e0.elapsed_time(e1) * 1e3)
-            ok = torch.equal(oo, ref_off) and torch.equal(out[:ref.numel()], ref)
-            print(f"{os.path.basename(path)} sync={int(use_sync)}: pack {min(ts):.1f} us "
-                  f"(mean {sum(ts) / len(ts):.1f}) ok={ok}", flush=True)
+            ts = sorted(times[(path, use_sync)])
+            print(f"{os.path.basename(path)} sync={int(use_sync)}: pack {ts[0]:.1f} us "
+                  f"(median {ts[len(ts) // 2]:.1f}) ok={oks[(path, use_sync)]}", flush=True)
 
 
 if __name__ == "__main__":
