@@ -116,6 +116,36 @@ struct alignas(16) SelEntry {
     uint32_t s0, s1, s2, m;
 };
 
+struct SelTable {
+    SelEntry e[kSelCopy + 1];
+};
+
+// The table, built at compile time; each tile copies it to LDS (one 16-byte
+// load and store per thread).
+constexpr SelTable make_sel_table() {
+    SelTable t{};
+    for (uint32_t tag = 0; tag < 256; tag++) {
+        uint64_t s = 0x0C0C0C0C0C0C0C0Cull;
+        uint32_t r = 1;  // byte r + 1 = index of the r-th set bit (r < 7)
+        for (uint32_t k = 0; k < 8; k++) {
+            if (tag & (1u << k)) {
+                if (r < 8) s = (s & ~(0xFFull << (8 * r))) | ((uint64_t)k << (8 * r));
+                r++;
+            }
+        }
+        t.e[tag].s0 = (uint32_t)s;
+        t.e[tag].s1 = (uint32_t)(s >> 32);
+        t.e[tag].s2 = tag == 0xFF ? 0x0C0C0403u : 0x0C0C0C0Cu;
+        t.e[tag].m = tag == 0 ? 0xFFFFu : 0xFFu;
+    }
+    t.e[kSelCopy].s0 = 0x03020100u;
+    t.e[kSelCopy].s1 = 0x07060504u;
+    t.e[kSelCopy].s2 = 0x0C0C0C0Cu;
+    t.e[kSelCopy].m = 0u;
+    return t;
+}
+__device__ constexpr SelTable kSelTable = make_sel_table();
+
 struct Smem {
     SelEntry sel[kSelCopy + 1];         // record assembly per tag
     uint64_t chunk_size[kMaxTileChunks];
@@ -438,7 +468,7 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
     // head; 0 for any other head (every word no run absorbs is a head)
     const uint64_t nxt = (si.H >> 1) >> lane;
     const uint32_t cnt = min3_u32(ffbl((uint32_t)nxt), ffbl((uint32_t)(nxt >> 32)) | 32u,
-                                  __builtin_elementwise_sub_sat(nvalid - 1u + ext, lane));
+                                  __builtin_elementwise_sub_sat(nvalid + ext, lane + 1u));
     // record dwords r2:r1:r0 = tag, compacted bytes, count byte; absorbed
     // zero words and lanes past nvalid hold w == 0 and emit nothing
     const SelEntry se = sel[mask_sel(si.H, tag, kSelCopy)];
@@ -744,8 +774,12 @@ __device__ __forceinline__ uint64_t scan_chunks(Smem& sm, uint32_t nc, uint32_t 
 }
 
 // One workgroup per tile (tile = blockIdx.x), 4 waves.
+#ifndef PACK_MIN_WAVES
+#define PACK_MIN_WAVES 6  // per SIMD: 7 (the LDS limit) spills VGPRs to scratch
+#endif
+
 template <bool SYNC>
-__global__ void __launch_bounds__(kThreads, 8)
+__global__ void __launch_bounds__(kThreads, PACK_MIN_WAVES)
 pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
             uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
             uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts,
@@ -754,7 +788,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-    const uint64_t ntiles = (nchunks + tc - 1) / tc;
+    const uint64_t ntiles = gridDim.x;  // = ceil(nchunks / tc), set by the launch
     const uint64_t tile = blockIdx.x;
     LookbackArgs LA;
     LA.ts = ts;
@@ -784,25 +818,11 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     const uint64_t k1 = (uniform64(chunk_off[c1]) + kSyncWords - 1) / kSyncWords;
     const uint32_t t0 = (uint32_t)(k0 * kSyncWords - TW0);  // first sync word, tile-relative
     for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
-    // compaction selectors: byte r + 1 = index of the r-th set bit of the
-    // tag (r < 7), byte 0 zero (the tag's slot)
-    {
-        uint64_t s = 0x0C0C0C0C0C0C0C0Cull;
-        uint32_t r = 1;
-        for (uint32_t k = 0; k < 8; k++) {
-            if (tid & (1u << k)) {
-                if (r < 8) s = (s & ~(0xFFull << (8 * r))) | ((uint64_t)k << (8 * r));
-                r++;
-            }
-        }
-        SelEntry e;
-        e.s0 = (uint32_t)s;
-        e.s1 = (uint32_t)(s >> 32);
-        e.s2 = tid == 0xFF ? 0x0C0C0403u : 0x0C0C0C0Cu;
-        e.m = tid == 0 ? 0xFFFFu : 0xFFu;
-        sm.sel[tid] = e;
-        if (tid == 0) sm.sel[kSelCopy] = SelEntry{0x03020100u, 0x07060504u, 0x0C0C0C0Cu, 0u};
-    }
+    // record assembly table: one 16-byte entry per thread (+ the copy entry)
+    reinterpret_cast<uint4*>(sm.sel)[tid] = reinterpret_cast<const uint4*>(kSelTable.e)[tid];
+    if (tid == 0)
+        reinterpret_cast<uint4*>(sm.sel)[kSelCopy] =
+            reinterpret_cast<const uint4*>(kSelTable.e)[kSelCopy];
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
     uint8_t* const outa = out - mis;
@@ -840,16 +860,23 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     staged = __builtin_amdgcn_readfirstlane((int)staged) != 0;
 
     if (staged) {
-        // load every step of the range into registers, zero the region
+        // Load every step of the range into registers and zero the region.
+        // All kStageSteps steps run unconditionally: a step past nsteps has
+        // meta 0 (no valid words, no chunk edges) and is a no-op, so the
+        // compiler sees a straight line and counts the loads' waits exactly.
+        // The loads go through a buffer descriptor over the tile's words (<=
+        // 16 KiB here): a lane past nvalid reads out of range and gets 0.
+        const uint32_t tile_bytes = (uint32_t)((uniform64(toff[nc]) - TW0) * 8);
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
         uint64_t cache[kStageSteps];
 #pragma unroll
         for (uint32_t s = 0; s < kStageSteps; s++) {
-            cache[s] = 0;
-            if (s < nsteps) {
-                const uint64_t src = readlane64(d_src, s);
-                const uint32_t nv = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s) & 127u;
-                if (lane < nv) cache[s] = in[src + lane];
-            }
+            const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)d_g, s);
+            const uint32_t nv = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s) & 127u;
+            const uint32_t vo = lane < nv ? (g + lane) * 8u : 0x80000000u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vo, 0, 0);
+            cache[s] = ((uint64_t)v[1] << 32) | v[0];
         }
         for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
             *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
@@ -860,28 +887,25 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             uint64_t local = 0;
 #pragma unroll
             for (uint32_t s = 0; s < kStageSteps; s++) {
+                const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
+                si[s].meta = meta;
+                if ((meta >> 7) & 1) {
+                    pk.begin(local);
+                    if (lane == 0) sm.chunk_oc[wc0 + (meta >> 9)] = (uint32_t)local;
+                }
+#if PACK_ABLATE == 3 || PACK_ABLATE == 4
+                asm volatile("" ::"v"(cache[s]));  // timing-only: skip the arithmetic
+                pk.total += 34 * (meta & 127u) / 8;
                 si[s].H = 0;
                 si[s].kin = 0;
-                si[s].meta = 0;
                 si[s].pos = 0;
                 si[s].tag = 0;
-                if (s < nsteps) {
-                    const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
-                    si[s].meta = meta;
-                    if ((meta >> 7) & 1) {
-                        pk.begin(local);
-                        if (lane == 0) sm.chunk_oc[wc0 + (meta >> 9)] = (uint32_t)local;
-                    }
-#if PACK_ABLATE == 3 || PACK_ABLATE == 4
-                    asm volatile("" ::"v"(cache[s]));  // timing-only: skip the arithmetic
-                    pk.total += 34 * (meta & 127u) / 8;
 #else
-                    size_step(pk, cache[s], meta & 127u, lane, si[s]);
+                size_step(pk, cache[s], meta & 127u, lane, si[s]);
 #endif
-                    if ((meta >> 8) & 1) {
-                        if (lane == 0) sm.chunk_size[wc0 + (meta >> 9)] = pk.total;
-                        local += pk.total;
-                    }
+                if ((meta >> 8) & 1) {
+                    if (lane == 0) sm.chunk_size[wc0 + (meta >> 9)] = pk.total;
+                    local += pk.total;
                 }
             }
             if (lane == 0) sm.wave_bytes[wave] = local;
@@ -900,17 +924,15 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             uint32_t ext = 0;  // words the run open at the step end absorbs later
 #pragma unroll
             for (int s = (int)kStageSteps - 1; s >= 0; s--) {
-                if ((uint32_t)s < nsteps) {
-                    const uint32_t meta = si[s].meta;
-                    const uint32_t e = ((meta >> 8) & 1) ? 0u : ext;
-                    emit_step(cache[s], si[s], e, lane, region, sm.sel,
-                              SYNC ? reinterpret_cast<uint8_t*>(sync + k0) : nullptr,
-                              t0, (uint32_t)__builtin_amdgcn_readlane((int)d_g, s),
-                              uniform(sm.chunk_oc[wc0 + (meta >> 9)]));
-                    // ext for step s-1: absorbed here, plus later if the run
-                    // covered this whole step
-                    ext = ((meta >> 7) & 1) ? 0u : si[s].kin + (si[s].H == 0 ? e : 0u);
-                }
+                const uint32_t meta = si[s].meta;
+                const uint32_t e = ((meta >> 8) & 1) ? 0u : ext;
+                emit_step(cache[s], si[s], e, lane, region, sm.sel,
+                          SYNC ? reinterpret_cast<uint8_t*>(sync + k0) : nullptr, t0,
+                          (uint32_t)__builtin_amdgcn_readlane((int)d_g, s),
+                          uniform(sm.chunk_oc[(wc0 + (meta >> 9)) & (kMaxTileChunks - 1)]));
+                // ext for step s-1: absorbed here, plus later if the run
+                // covered this whole step
+                ext = ((meta >> 7) & 1) ? 0u : si[s].kin + (si[s].H == 0 ? e : 0u);
             }
         }
 #endif
