@@ -391,8 +391,8 @@ struct StepInfo {
     uint64_t H;        // heads of the step
     uint32_t pos;      // this lane's byte position in the region (per lane)
     uint32_t tag;      // this lane's tag (per lane)
-    uint32_t kin;      // words absorbed by the run carried into the step
-    uint32_t meta;     // nvalid | first << 7 | last << 8 | chunk << 9
+    uint32_t meta;     // nvalid | first << 7 | last << 8 | chunk << 9 | kin << 16,
+                       // kin = words absorbed by the run carried into the step
 };
 
 // Per lane: bit `lane` of the wave-uniform mask m ? a : b.  One VOP3
@@ -427,7 +427,21 @@ __device__ __forceinline__ uint32_t word_tag_dot(uint32_t lo, uint32_t hi) {
     return t >> 7;
 }
 
-__device__ __forceinline__ void size_step(Packer& pk, uint64_t w, uint32_t nvalid, uint32_t lane,
+// Staged path: packing state of the chunk in progress (region-local, so
+// 32 bits suffice).
+struct StageState {
+    Carry carry;
+    uint32_t total;  // packed bytes of the chunk so far
+    uint32_t o_c;    // chunk start in the wave's region
+    __device__ __forceinline__ void begin(uint32_t oc) {
+        carry.type = 0;
+        carry.rem = 0;
+        total = 0;
+        o_c = oc;
+    }
+};
+
+__device__ __forceinline__ void size_step(StageState& pk, uint64_t w, uint32_t nvalid, uint32_t lane,
                                           StepInfo& si) {
     const uint32_t tag = word_tag_dot((uint32_t)w, (uint32_t)(w >> 32));
     const uint32_t pop = __builtin_popcount(tag);
@@ -443,9 +457,9 @@ __device__ __forceinline__ void size_step(Packer& pk, uint64_t w, uint32_t nvali
     const uint32_t size = mask_sel(sm.H, hsize, isz ? 0u : 8u);
     const uint32_t incl = wave_incl_scan(size);
     si.H = sm.H;
-    si.pos = (uint32_t)(pk.o_c + pk.total) + incl - size;
+    si.pos = pk.o_c + pk.total + incl - size;
     si.tag = tag;
-    si.kin = sm.absorbed_carry;
+    si.meta |= sm.absorbed_carry << 16;
     pk.carry = sm.next;
     pk.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
 }
@@ -504,6 +518,8 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
             const uint32_t rel = pos - oc;
             uint32_t b = (lane + d - c) >> 2;
             *reinterpret_cast<uint32_t*>(tab + b) = rel | (d << 24);
+            // (runs of > 16 words: rare; kept a plain loop so it costs no registers)
+#pragma clang loop unroll(disable) vectorize(disable)
             for (uint32_t dd = d + kSyncWords; dd <= cnt; dd += kSyncWords) {
                 b += 4;
                 *reinterpret_cast<uint32_t*>(tab + b) = rel | (dd << 24);
@@ -883,8 +899,9 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         // pass 1: sizes and positions
         StepInfo si[kStageSteps];
         {
-            Packer pk;
-            uint64_t local = 0;
+            StageState pk;
+            pk.begin(0);
+            uint32_t local = 0;
 #pragma unroll
             for (uint32_t s = 0; s < kStageSteps; s++) {
                 const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
@@ -897,7 +914,6 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                 asm volatile("" ::"v"(cache[s]));  // timing-only: skip the arithmetic
                 pk.total += 34 * (meta & 127u) / 8;
                 si[s].H = 0;
-                si[s].kin = 0;
                 si[s].pos = 0;
                 si[s].tag = 0;
 #else
@@ -929,10 +945,10 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                 emit_step(cache[s], si[s], e, lane, region, sm.sel,
                           SYNC ? reinterpret_cast<uint8_t*>(sync + k0) : nullptr, t0,
                           (uint32_t)__builtin_amdgcn_readlane((int)d_g, s),
-                          uniform(sm.chunk_oc[(wc0 + (meta >> 9)) & (kMaxTileChunks - 1)]));
+                          uniform(sm.chunk_oc[(wc0 + ((meta >> 9) & 63u)) & (kMaxTileChunks - 1)]));
                 // ext for step s-1: absorbed here, plus later if the run
                 // covered this whole step
-                ext = ((meta >> 7) & 1) ? 0u : si[s].kin + (si[s].H == 0 ? e : 0u);
+                ext = ((meta >> 7) & 1) ? 0u : (meta >> 16) + (si[s].H == 0 ? e : 0u);
             }
         }
 #endif
