@@ -94,7 +94,7 @@ constexpr uint32_t kRegionBytes = kRegion > kRing ? kRegion : kRing;
 // m = 16k, for the chunk that holds word m: the chunk-relative packed offset of
 // the record that covers word m (24 bits) and m minus that record's first
 // word (8 bits; a run covers at most 255 words after its head, so it fits).  An
-// unpack that has the index walks 16-word segments in parallel and checks that
+// unpack that has the index walks CAPNP_SYNC_WORDS-word segments in parallel and checks that
 // consecutive segments meet (unpack.hip).  kSyncNone marks an entry the
 // kernel does not provide (streaming path); the decoder then walks serially.
 constexpr uint32_t kSyncWords = CAPNP_SYNC_WORDS;
@@ -506,9 +506,9 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
 #if PACK_ABLATE != 5
     if (tab) {
         // sync points m = hw + d, d = (t0 - hw) mod 16, d <= cnt, of the
-        // record headed at word hw = g + lane; m - t0 is a multiple of 16,
-        // so its entry is the dword at byte (m - t0) / 4 of the tile's part
-        // of the index.  Other lanes get d = 512 > cnt (cnt <= 63 + ext <
+        // record headed at word hw = g + lane; m - t0 is a multiple of
+        // kSyncWords, so its entry is dword (m - t0) / kSyncWords of the
+        // tile's part of the index.  Other lanes get d = 512 > cnt (cnt <= 63 + ext <
         // 512).  Every sync point is covered by exactly one record, so the
         // entries go straight to memory.
         const uint32_t c = t0 - g;
@@ -516,9 +516,9 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
         const uint32_t dh = mask_sel(si.H, d, 512u);
         if (dh <= cnt) {
             const uint32_t rel = pos - oc;
-            uint32_t b = (lane + d - c) >> 2;
+            uint32_t b = ((lane + d - c) / kSyncWords) * 4u;
             *reinterpret_cast<uint32_t*>(tab + b) = rel | (d << 24);
-            // (runs of > 16 words: rare; kept a plain loop so it costs no registers)
+            // (runs longer than kSyncWords words: rare; a plain loop costs no registers)
 #pragma clang loop unroll(disable) vectorize(disable)
             for (uint32_t dd = d + kSyncWords; dd <= cnt; dd += kSyncWords) {
                 b += 4;

@@ -455,7 +455,7 @@ __device__ __forceinline__ void walk_wave(SM& S, uint32_t p, uint32_t pe, uint32
 
 // ---------------------------------------------------------------------------
 // Sync walk: with the record sync index the tile's words split into segments
-// at every multiple of 32 (global word index); lane b of the walker wave(s)
+// at every multiple of kSyncWords (global word index); lane b of the walkers
 // walks segment b from the record the index names, across chunk ends, until
 // its word reaches the segment end.  The walks are exact if they meet: lane
 // b's end state (position, word) must equal the start lane b+1 derives from
@@ -674,7 +674,7 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
     UPROF_T(t0);
     const uint32_t nbytes = (uint32_t)(B1 - B0) + off0;
     const uint32_t Wt = (uint32_t)(W1 - W0);
-    // sync segments: [0, 32 kf - W0), then 32-word blocks up to Wt
+    // sync segments: [0, kSyncWords kf - W0), then kSyncWords-word blocks up to Wt
     const uint64_t kf = W0 / kSyncWords + 1;
     const uint32_t nseg =
         W1 > W0 ? 1u + (uint32_t)((W1 - 1) / kSyncWords + 1 - kf) : 0u;
@@ -712,7 +712,8 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
                     for (uint32_t bb = blo; bb < bhi; bb++) S.segc[bb] = (uint8_t)tid;
                 }
             }
-            if (tid >= 1 && tid < nseg) S.ent[tid] = sync[kf + tid - 1];
+            for (uint32_t b = tid; b < nseg; b += kThreads)
+                if (b >= 1) S.ent[b] = sync[kf + b - 1];
             if (tid < kStageChunks) S.badc[tid] = 0;
         }
 #pragma unroll
@@ -734,13 +735,13 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
 #endif
     if constexpr (SYNC) {
         const uint32_t wrel = (wave - walker) & (kWaves - 1);
-        const uint32_t b = wrel * CAPNP_WAVE + lane;
         bool marked = false;
-        if (b < nseg) {
+        // (one pass unless the segments outnumber the threads: kSyncWords < 16)
+        for (uint32_t b = wrel * CAPNP_WAVE + lane; b < nseg; b += kThreads) {
             const uint32_t sb = b == 0 ? 0u : (uint32_t)((kf + b - 1) * kSyncWords - W0);
             const bool last = b + 1 == nseg;
             const uint32_t eb = last ? Wt : (uint32_t)((kf + b) * kSyncWords - W0);
-            marked = walk_segment(S, nc, b, sb, eb, last);
+            marked |= walk_segment(S, nc, b, sb, eb, last);
         }
         const bool anybad = __syncthreads_or(marked);
         if (tid < nc) {
@@ -810,7 +811,7 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
 // Sync kernel (the record sync index is given): every wave is autonomous.  A
 // sub-tile = `tc` consecutive chunks of about kSubWords output words; wave w
 // of workgroup g takes sub-tile 4 g + w, stages its packed bytes in its own
-// LDS region, walks its 16-word segments (walk_segment, one lane each),
+// LDS region, walks its kSyncWords-word segments (walk_segment, one lane each),
 // re-walks chunks whose segments did not meet, and expands - with no
 // workgroup barrier after the selector table, so the 16-32 resident waves of
 // a CU overlap each other's load latency, walks and expansions freely.

@@ -146,7 +146,9 @@ capnp_status capnp_gpu_unpack_batch(capnp_ctx* ctx, const uint8_t* d_packed,
    that consecutive segments meet exactly; any mismatch (a corrupt or
    foreign index) falls back to the serial walk for that chunk, so results
    and statuses are always those of capnp_gpu_unpack_batch. */
-#define CAPNP_SYNC_WORDS 16
+#ifndef CAPNP_SYNC_WORDS /* (overridable for diagnostic builds only) */
+#define CAPNP_SYNC_WORDS 8
+#endif
 size_t capnp_sync_index_entries(size_t total_words);
 capnp_status capnp_gpu_pack_batch_sync(capnp_ctx* ctx, const uint64_t* d_words,
                                        const uint64_t* d_chunk_word_off, size_t nchunks,
