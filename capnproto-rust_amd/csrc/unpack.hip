@@ -39,7 +39,10 @@
 #define UNPACK_GROUPS 2  // expansion groups in flight per wave
 #endif
 #ifndef UNPACK_MIN_WAVES
-#define UNPACK_MIN_WAVES 7  // __launch_bounds__ waves per SIMD of the tile kernel (8 spills)
+#define UNPACK_MIN_WAVES 8  // __launch_bounds__ waves per SIMD of the tile kernel
+#endif
+#ifndef UNPACK_HOPIF
+#define UNPACK_HOPIF 1  // phase A hop under an exec mask (0: branch-free selects)
 #endif
 #ifndef UNPACK_PHASEA_UNROLL
 #define UNPACK_PHASEA_UNROLL 1
@@ -264,6 +267,7 @@ constexpr uint16_t kRaw = 0x8000;
 // w, whose run covers words w+1 .. w+n (n <= 255).
 template <class SM>
 __device__ __forceinline__ void lit_entries(SM& S, uint32_t w, uint32_t p, uint32_t n) {
+#pragma clang loop unroll(disable) vectorize(disable)
     for (uint32_t i = 0; i < n; i++) S.dpos[w + 1 + i] = (uint16_t)(kRaw | (p + 10 + 8 * i));
 }
 
@@ -323,13 +327,26 @@ union USmem {
 // address is a misaligned LDS access: replayed, and SQ_LDS_UNALIGNED_STALL
 // was half of this kernel's LDS cycles.  The tag is extracted from its
 // aligned dword instead (32-bit reads are never misaligned).
+// UNPACK_RECB=1: three ds_read_u8 kept apart by volatile (a byte read is
+// never misaligned): all three share q's address register through the
+// offset field, so the hop spends no VALU on addressing.
+#ifndef UNPACK_RECB
+#define UNPACK_RECB 0  // measured slower (volatile pins the reads' order): 427 vs 403 us
+#endif
 __device__ __forceinline__ void rec_bytes(const uint8_t* B, uint32_t q, uint32_t& tag,
                                           uint32_t& b1, uint32_t& b9) {
+#if UNPACK_RECB
+    const volatile uint8_t* V = B;
+    tag = V[q - 1u];
+    b1 = V[q];
+    b9 = V[q + 8u];
+#else
     const uint32_t p = q - 1u;
     const uint32_t dw = *reinterpret_cast<const uint32_t*>(B + (p & ~3u));
     tag = __builtin_amdgcn_ubfe(dw, (p & 3u) * 8u, 8u);
     b1 = B[q];
     b9 = B[q + 8];
+#endif
 }
 
 // Exact status of a record that failed the fast check in walk_chunk, in the
@@ -540,6 +557,37 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     // word, so a lane reaches stopw within kSyncWords hops; a lane already
     // there only sends its store to the dummy slot).  Phase B below handles
     // chunk ends and whatever is left.
+#if UNPACK_HOPIF
+    // (UNPACK_HOPIF: the hop runs under the exec mask of the lanes still
+    // below stopw, so the state updates need no selects and the record
+    // checks collect in a wave mask)
+    uint64_t errm = 0;
+#pragma unroll UNPACK_PHASEA_UNROLL
+    for (uint32_t it = 0; it < kSyncWords; it++) {
+        if (w < stopw) {
+            const bool isz = tag == 0, isf = tag == 0xFF;
+            const uint32_t fx = isf ? 8u * b9 + 1u : 0u;
+            const uint32_t qe = __builtin_popcount(tag) + q + (isz ? 1u : 0u) + fx + 1u;
+            const uint32_t qn = qe < cpe1 ? qe : cpe1;
+            uint32_t ntag, nb1, nb9;
+            rec_bytes(B, qn, ntag, nb1, nb9);
+            const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+            const uint32_t wn0 = w + 1u + cnt;
+            errm |= ballot64(qe > cpe1 || wn0 > cwe);
+            const uint32_t wn = wn0 < cwe ? wn0 : cwe;
+            S.dpos[w] = (uint16_t)(q - 1u);
+            if (ballot64(isf && wn > w + 1)) {  // literal-run words (rare)
+                if (isf) lit_entries(S, w, q - 1u, wn - w - 1);
+            }
+            q = qn;
+            w = wn;
+            tag = ntag;
+            b1 = nb1;
+            b9 = nb9;
+        }
+    }
+    err = (errm >> lane_id()) & 1;
+#else
 #pragma unroll UNPACK_PHASEA_UNROLL
     for (uint32_t it = 0; it < kSyncWords; it++) {
         const bool hop = w < stopw;
@@ -563,6 +611,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
         b1 = hop ? nb1 : b1;
         b9 = hop ? nb9 : b9;
     }
+#endif
     for (;;) {
 #if UNPACK_PROF
         iters++;
