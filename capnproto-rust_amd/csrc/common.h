@@ -21,7 +21,7 @@ __host__ __device__ __forceinline__ uint32_t word_tag(uint32_t lo, uint32_t hi) 
 
 // Byte k of the result is bit k of `tag` (0/1).  Done per nibble: the
 // multiply by 0x00204081 puts bit j at 8j with no colliding terms.
-__host__ __device__ __forceinline__ uint64_t spread_bits(uint32_t tag) {
+__host__ __device__ __forceinline__ constexpr uint64_t spread_bits(uint32_t tag) {
     uint32_t lo = ((tag & 15u) * 0x00204081u) & 0x01010101u;
     uint32_t hi = (((tag >> 4) & 15u) * 0x00204081u) & 0x01010101u;
     return ((uint64_t)hi << 32) | lo;
@@ -30,7 +30,7 @@ __host__ __device__ __forceinline__ uint64_t spread_bits(uint32_t tag) {
 // v_perm_b32 selector (two dwords, 8 bytes) that scatters the `pop` packed
 // bytes of a tag back to their word positions: output byte k = bit k ?
 // rank_k : 0x0C (zero), rank_k = number of set bits below k.
-__host__ __device__ __forceinline__ uint64_t expand_selector(uint32_t tag) {
+__host__ __device__ __forceinline__ constexpr uint64_t expand_selector(uint32_t tag) {
     uint64_t t8 = spread_bits(tag);
     uint64_t incl = t8 * 0x0101010101010101ull;     // inclusive prefix per byte
     uint64_t rank = incl - t8;                       // exclusive prefix

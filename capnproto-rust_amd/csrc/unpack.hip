@@ -271,6 +271,18 @@ __device__ __forceinline__ void lit_entries(SM& S, uint32_t w, uint32_t p, uint3
     for (uint32_t i = 0; i < n; i++) S.dpos[w + 1 + i] = (uint16_t)(kRaw | (p + 10 + 8 * i));
 }
 
+// expand_selector for every tag, built at compile time: each tile copies it
+// into LDS with one 8-byte load and store per thread.
+struct ExpandTable {
+    uint64_t s[256];
+};
+constexpr ExpandTable make_expand_table() {
+    ExpandTable t{};
+    for (uint32_t tag = 0; tag < 256; tag++) t.s[tag] = expand_selector(tag);
+    return t;
+}
+__device__ constexpr ExpandTable kExpandTable = make_expand_table();
+
 // Rebuilds one output word from its descriptor (sel = expand selectors).
 __device__ __forceinline__ uint64_t expand_desc(const uint8_t* B, const uint64_t* sel,
                                                 uint32_t d) {
@@ -744,7 +756,7 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
         uint4* dd = reinterpret_cast<uint4*>(S.dpos);
         const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
         for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
-        S.sel[tid] = expand_selector(tid);
+        S.sel[tid] = kExpandTable.s[tid];
         if constexpr (SYNC) {
             // chunk tables and the tile's sync entries (segment b >= 1 starts
             // at global word 32 (kf + b - 1))
@@ -900,7 +912,7 @@ unpack_sync_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ 
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-    sm.sel[tid] = expand_selector(tid);
+    sm.sel[tid] = kExpandTable.s[tid];
     __syncthreads();
     const uint64_t ca = ((uint64_t)blockIdx.x * kWaves + wave) * tc;
     if (ca >= nchunks) return;
