@@ -470,8 +470,9 @@ __device__ __forceinline__ void size_step(StageState& pk, uint64_t w, uint32_t n
 // start in the region); usually none or one, more only for runs of > 16
 // words.  The head lane knows its own position and run length, so this is
 // a few VALU ops and a masked LDS store per step.
+template <bool SYNC>
 __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32_t ext,
-                                          uint32_t lane, uint8_t* region, const SelEntry* sel,
+                                          uint32_t lane, uint8_t* region_m1, const SelEntry* sel,
                                           uint8_t* __restrict__ tab, uint32_t t0, uint32_t g,
                                           uint32_t oc) {
     const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
@@ -498,25 +499,28 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
     const uint32_t e1 = __builtin_amdgcn_alignbyte(r1, r0, s);
     const uint32_t e2 = __builtin_amdgcn_alignbyte(r2, r1, s);
     const uint32_t e3 = __builtin_amdgcn_alignbyte(0u, r2, s);
-    uint32_t* b32 = reinterpret_cast<uint32_t*>(__builtin_align_down(region + pos + 3u, 4)) - 1;
+    // (region_m1 = region - 1, region 16-aligned: align_down(region - 1 + pos)
+    // = region + ceil(pos / 4) * 4 - 4)
+    uint32_t* b32 = reinterpret_cast<uint32_t*>(__builtin_align_down(region_m1 + pos, 4));
     __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 #if PACK_ABLATE != 5
-    if (tab) {
-        // sync points m = hw + d, d = (t0 - hw) mod 16, d <= cnt, of the
-        // record headed at word hw = g + lane; m - t0 is a multiple of
+    if constexpr (SYNC) {
+        // sync points m = hw + d, d = (t0 - hw) mod kSyncWords, d <= cnt, of
+        // the record headed at word hw = g + lane; m - t0 is a multiple of
         // kSyncWords, so its entry is dword (m - t0) / kSyncWords of the
-        // tile's part of the index.  Other lanes get d = 512 > cnt (cnt <= 63 + ext <
-        // 512).  Every sync point is covered by exactly one record, so the
-        // entries go straight to memory.
+        // tile's part of the index.  Other lanes get d = ~0 > cnt.  Every
+        // sync point is covered by exactly one record, so the entries go
+        // straight to memory.
         const uint32_t c = t0 - g;
         const uint32_t d = (c - lane) & (kSyncWords - 1);
-        const uint32_t dh = mask_sel(si.H, d, 512u);
+        const uint32_t dh = mask_sel(si.H, d, ~0u);
         if (dh <= cnt) {
             const uint32_t rel = pos - oc;
-            uint32_t b = ((lane + d - c) / kSyncWords) * 4u;
+            // (lane + d - c is a multiple of kSyncWords)
+            uint32_t b = (lane + d - c) / (kSyncWords / 4u);
             *reinterpret_cast<uint32_t*>(tab + b) = rel | (d << 24);
             // (runs longer than kSyncWords words: rare; a plain loop costs no registers)
 #pragma clang loop unroll(disable) vectorize(disable)
@@ -934,6 +938,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             if (lane == 0) TRACE(tile, 1, RT());
         }
         // pass 2: assemble the bytes (the look-back loads are in flight)
+        uint8_t* const region_m1 = region - 1;
 #if PACK_ABLATE != 3 && PACK_ABLATE != 4
         wave_lds_sync();
         {
@@ -942,7 +947,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             for (int s = (int)kStageSteps - 1; s >= 0; s--) {
                 const uint32_t meta = si[s].meta;
                 const uint32_t e = ((meta >> 8) & 1) ? 0u : ext;
-                emit_step(cache[s], si[s], e, lane, region, sm.sel,
+                emit_step<SYNC>(cache[s], si[s], e, lane, region_m1, sm.sel,
                           SYNC ? reinterpret_cast<uint8_t*>(sync + k0) : nullptr, t0,
                           (uint32_t)__builtin_amdgcn_readlane((int)d_g, s),
                           uniform(sm.chunk_oc[(wc0 + ((meta >> 9) & 63u)) & (kMaxTileChunks - 1)]));
