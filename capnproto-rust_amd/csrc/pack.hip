@@ -787,6 +787,15 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
 
 // Wave 0: exclusive scan of the tile's chunk sizes (<= 64) into chunk_pos
 // (tile-relative); returns the tile aggregate.
+// Staged path: the tile's packed bytes fit 32 bits (<= 4 regions), so the
+// scan is the DPP wave scan.
+__device__ __forceinline__ uint64_t scan_chunks32(Smem& sm, uint32_t nc, uint32_t lane) {
+    const uint32_t v = lane < nc ? (uint32_t)sm.chunk_size[lane] : 0u;
+    const uint32_t incl = wave_incl_scan(v);
+    if (lane < nc) sm.chunk_pos[lane] = incl - v;
+    return (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+}
+
 __device__ __forceinline__ uint64_t scan_chunks(Smem& sm, uint32_t nc, uint32_t lane) {
     const uint64_t v = lane < nc ? sm.chunk_size[lane] : 0;
     uint64_t s = v;
@@ -938,7 +947,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         __syncthreads();
         uint64_t agg = 0;
         if (wave == 0) {
-            agg = scan_chunks(sm, nc, lane);
+            agg = scan_chunks32(sm, nc, lane);
             publish(LA, tile, agg, lane);
             if (lane == 0) TRACE(tile, 1, RT());
         }

@@ -47,6 +47,9 @@
 #ifndef UNPACK_PHASEA_UNROLL
 #define UNPACK_PHASEA_UNROLL 1
 #endif
+#ifndef UNPACK_EXP3
+#define UNPACK_EXP3 1  // expand reads three aligned dwords (0: two aligned qwords)
+#endif
 #ifndef UNPACK_EXP
 #define UNPACK_EXP 0  // diagnostic variants of the segment walk (scripts/uvar.py)
 #endif
@@ -293,6 +296,14 @@ __device__ __forceinline__ uint64_t expand_desc(const uint8_t* B, const uint64_t
     // off 8-byte alignment is replayed at 64 LDS cycles, MI355X_MICROARCH.md
     // §LDS, and was half the LDS time of this kernel)
     const uint32_t src = raw ? pos : pos + 1;
+#if UNPACK_EXP3
+    // three naturally aligned dwords from src & ~3 (never misaligned) and a
+    // funnel shift by src & 3 (alignbyte reads only the low two bits)
+    const uint32_t* q4 = reinterpret_cast<const uint32_t*>(B + (src & ~3u));
+    const uint32_t x0 = q4[0], x1 = q4[1], x2 = q4[2];
+    const uint64_t v = ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, src) << 32) |
+                       __builtin_amdgcn_alignbyte(x1, x0, src);
+#else
     const uint64_t* q8 = reinterpret_cast<const uint64_t*>(B + (src & ~7u));
     const uint64_t a = q8[0], b = q8[1];
     const uint32_t o = src & 7u, sh = o & 3u;
@@ -302,6 +313,7 @@ __device__ __forceinline__ uint64_t expand_desc(const uint8_t* B, const uint64_t
     const uint32_t x0 = up ? a1 : a0, x1 = up ? b0 : a1, x2 = up ? b1 : b0;
     const uint64_t v = ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sh) << 32) |
                        __builtin_amdgcn_alignbyte(x1, x0, sh);
+#endif
     const uint32_t t = none ? 0u : (raw ? 0xFFu : tag);
     const uint64_t sv = sel[t];
     const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
