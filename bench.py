@@ -283,6 +283,25 @@ def end_to_end(ctx, torch, words, offs, n, cw, tc, dev):
                "roundtrip_GiBps": round(U / (t2 - t0) / GiB, 3),
                "note": "pinned host -> H2D -> kernel -> D2H, sequential (no overlap)"}
     assert torch.equal(h_back, h_words)
+    # streaming host batch (capnp_stream_*): copy in, kernel and copy out of
+    # consecutive slices overlap on three streams
+    h_poffs = torch.empty(n + 1, dtype=torch.int64, pin_memory=True)
+    h_offs = offs.cpu().pin_memory()
+    h_status = torch.empty(n, dtype=torch.int32, pin_memory=True)
+    slice_words = 4 << 20
+    for rep in range(3):
+        h_back.zero_()
+        t0 = time.perf_counter()
+        P = ctx.stream_pack(h_words, h_offs, h_packed, h_poffs, slice_words=slice_words)
+        t1 = time.perf_counter()
+        ctx.stream_unpack(h_packed, h_poffs, h_offs, h_back, h_status, slice_words=slice_words)
+        t2 = time.perf_counter()
+        res["stream_encode_GiBps"] = round(U / (t1 - t0) / GiB, 3)
+        res["stream_decode_GiBps"] = round(U / (t2 - t1) / GiB, 3)
+        res["stream_roundtrip_GiBps"] = round(U / (t2 - t0) / GiB, 3)
+    assert torch.equal(h_back, h_words) and int(h_status.sum()) == 0
+    res["stream_note"] = (f"capnp_stream_pack_batch / capnp_stream_unpack_batch, "
+                          f"{slice_words} words per slice, pinned host buffers")
     return res
 
 

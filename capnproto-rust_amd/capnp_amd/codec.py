@@ -149,6 +149,27 @@ class Context:
                                chunks_per_tile)
         return words[:total], status[:n], consumed[:n]
 
+    # ---- streaming host batch (host buffers; pinned for overlap) ---------
+    def stream_pack(self, words, chunk_word_off, out, out_off, slice_words=0):
+        """capnp_stream_pack_batch on host tensors (CPU torch tensors, ideally
+        pinned): words int64, chunk_word_off int64[n+1], out uint8,
+        out_off int64[n+1].  Returns the packed total."""
+        n = chunk_word_off.numel() - 1
+        st = _lib.lib().capnp_stream_pack_batch(self._h, _ptr(words), _ptr(chunk_word_off), n,
+                                                _ptr(out), out.numel(), _ptr(out_off),
+                                                int(slice_words))
+        _check(st, self._h)
+        return int(out_off[n]) if n else 0
+
+    def stream_unpack(self, packed, in_byte_off, out_word_off, words, status, consumed=None,
+                      slice_words=0):
+        """capnp_stream_unpack_batch on host tensors (see stream_pack)."""
+        n = in_byte_off.numel() - 1
+        st = _lib.lib().capnp_stream_unpack_batch(self._h, _ptr(packed), _ptr(in_byte_off), n,
+                                                  _ptr(words), _ptr(out_word_off), _ptr(status),
+                                                  _ptr(consumed), int(slice_words))
+        _check(st, self._h)
+
     def gen_batch(self, words, offs, kind=0, pz_thresh=0, kinds=None, id0=0, stream=None):
         n = offs.numel() - 1
         st = _lib.lib().capnp_gpu_gen_batch(self._h, _ptr(words), _ptr(offs), n, int(id0),

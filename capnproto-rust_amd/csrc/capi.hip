@@ -53,6 +53,14 @@ struct capnp_ctx {
     size_t body_cap = 0;
     FrameResult* d_frame = nullptr;
     FrameResult* h_frame = nullptr;  // pinned
+    // streaming host batch (capnp_stream_*): copy-in, compute and copy-out
+    // streams, two device staging slots and their events
+    hipStream_t sstream[3] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev_in[2] = {}, ev_comp[2] = {}, ev_off[2] = {}, ev_out[2] = {};
+    uint8_t* d_slot[2] = {nullptr, nullptr};
+    size_t slot_cap = 0;
+    uint64_t* h_slot_off[2] = {nullptr, nullptr};  // pinned: a slice's packed offsets
+    size_t h_slot_off_cap = 0;
     std::string err;
 };
 
@@ -178,6 +186,57 @@ capnp_status pack_host(capnp_ctx* ctx, const uint64_t* words, const uint64_t* of
     return oo[n] > out_cap ? CAPNP_E_BUFFER_NOT_LARGE_ENOUGH : CAPNP_OK;
 }
 
+// ---- streaming host batch ------------------------------------------------
+constexpr size_t kDefaultSliceWords = size_t(4) << 20;  // 32 MiB of words (scripts/stream_sweep.py)
+constexpr size_t kSlotPad = 64;  // staging slack: the kernels read whole aligned blocks
+
+capnp_status stream_setup(capnp_ctx* ctx, size_t slot_bytes, size_t off_entries) {
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (!ctx->sstream[0]) {
+        for (int k = 0; k < 3; k++)
+            HIP_TRY(hipStreamCreateWithFlags(&ctx->sstream[k], hipStreamNonBlocking));
+        for (int k = 0; k < 2; k++) {
+            HIP_TRY(hipEventCreateWithFlags(&ctx->ev_in[k], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&ctx->ev_comp[k], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&ctx->ev_off[k], hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&ctx->ev_out[k], hipEventDisableTiming));
+        }
+    }
+    if (slot_bytes > ctx->slot_cap) {
+        for (int k = 0; k < 2; k++) {
+            if (ctx->d_slot[k]) HIP_TRY(hipFree(ctx->d_slot[k]));
+            ctx->d_slot[k] = nullptr;
+        }
+        ctx->slot_cap = 0;
+        for (int k = 0; k < 2; k++) HIP_TRY(hipMalloc(&ctx->d_slot[k], slot_bytes));
+        ctx->slot_cap = slot_bytes;
+    }
+    if (off_entries > ctx->h_slot_off_cap) {
+        for (int k = 0; k < 2; k++) {
+            if (ctx->h_slot_off[k]) HIP_TRY(hipHostFree(ctx->h_slot_off[k]));
+            ctx->h_slot_off[k] = nullptr;
+        }
+        ctx->h_slot_off_cap = 0;
+        for (int k = 0; k < 2; k++)
+            HIP_TRY(hipHostMalloc(&ctx->h_slot_off[k], off_entries * 8, 0));
+        ctx->h_slot_off_cap = off_entries;
+    }
+    return CAPNP_OK;
+}
+
+// Chunk-aligned slices of about slice_words words (at least one chunk each).
+std::vector<size_t> make_slices(const uint64_t* off, size_t n, size_t slice_words) {
+    std::vector<size_t> b{0};
+    size_t s = 0;
+    while (s < n) {
+        size_t e = s + 1;
+        while (e < n && off[e + 1] - off[s] <= slice_words) e++;
+        b.push_back(e);
+        s = e;
+    }
+    return b;
+}
+
 }  // namespace
 
 extern "C" {
@@ -236,6 +295,19 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (ctx->d_body) hipFree(ctx->d_body);
     if (ctx->d_frame) hipFree(ctx->d_frame);
     if (ctx->h_frame) hipHostFree(ctx->h_frame);
+    for (int k = 0; k < 3; k++)
+        if (ctx->sstream[k]) {
+            hipStreamSynchronize(ctx->sstream[k]);
+            hipStreamDestroy(ctx->sstream[k]);
+        }
+    for (int k = 0; k < 2; k++) {
+        if (ctx->ev_in[k]) hipEventDestroy(ctx->ev_in[k]);
+        if (ctx->ev_comp[k]) hipEventDestroy(ctx->ev_comp[k]);
+        if (ctx->ev_off[k]) hipEventDestroy(ctx->ev_off[k]);
+        if (ctx->ev_out[k]) hipEventDestroy(ctx->ev_out[k]);
+        if (ctx->d_slot[k]) hipFree(ctx->d_slot[k]);
+        if (ctx->h_slot_off[k]) hipHostFree(ctx->h_slot_off[k]);
+    }
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -426,6 +498,169 @@ capnp_status capnp_unpack(capnp_ctx* ctx, const uint8_t* in, size_t in_len, size
     *consumed = used;
     if (status == CAPNP_OK) memcpy(out, words.data(), out_len);
     return (capnp_status)status;
+}
+
+// Streaming pack: slice i+1's copy in, slice i's kernel and slice i-1's copy
+// out overlap.  The slots hold a slice's words, its (absolute) chunk offsets,
+// its packed offsets and its packed bytes; the kernel sees the words through
+// a pointer biased by the slice's first word, so the caller's offsets go
+// over unchanged.  The host waits once per slice, for the slice's packed
+// size (to place its bytes), while the next slice is already queued.
+capnp_status capnp_stream_pack_batch(capnp_ctx* ctx, const uint64_t* words,
+                                     const uint64_t* chunk_word_off, size_t nchunks,
+                                     uint8_t* out, size_t out_cap, uint64_t* out_byte_off,
+                                     size_t slice_words) {
+    if (!ctx || !chunk_word_off || !out_byte_off || (out_cap && !out))
+        return CAPNP_E_INVALID_ARGUMENT;
+    const size_t n = nchunks;
+    if (n == 0) {
+        out_byte_off[0] = 0;
+        return CAPNP_OK;
+    }
+    if (!words) return CAPNP_E_INVALID_ARGUMENT;
+    for (size_t c = 0; c < n; c++)
+        if (chunk_word_off[c + 1] < chunk_word_off[c]) return CAPNP_E_INVALID_ARGUMENT;
+    const std::vector<size_t> sl = make_slices(chunk_word_off, n, slice_words ? slice_words
+                                                                              : kDefaultSliceWords);
+    const size_t ns = sl.size() - 1;
+    size_t max_w = 0, max_n = 0, max_bound = 0;
+    for (size_t i = 0; i < ns; i++) {
+        const size_t w = chunk_word_off[sl[i + 1]] - chunk_word_off[sl[i]];
+        const size_t c = sl[i + 1] - sl[i];
+        max_w = std::max(max_w, w);
+        max_n = std::max(max_n, c);
+        max_bound = std::max(max_bound, capnp_packed_batch_bound_bytes(w, c));
+    }
+    const uint32_t tc = tile_chunks_for(chunk_word_off[n] - chunk_word_off[0], n);
+    const size_t o_off = round16(max_w * 8 + kSlotPad);
+    const size_t o_oo = o_off + round16((max_n + 1) * 8);
+    const size_t o_out = o_oo + round16((max_n + 1) * 8);
+    capnp_status st = stream_setup(ctx, o_out + max_bound + kSlotPad, max_n + 1);
+    if (st != CAPNP_OK) return st;
+    st = ensure_state(ctx, state_bytes_for(max_n, tc));
+    if (st != CAPNP_OK) return st;
+    hipStream_t s_in = ctx->sstream[0], s_comp = ctx->sstream[1], s_out = ctx->sstream[2];
+    uint64_t base = 0;
+    capnp_status result = CAPNP_OK;
+    // places slice j's bytes once its packed size is known
+    auto finalize = [&](size_t j) -> capnp_status {
+        const int k = (int)(j & 1);
+        const size_t c0 = sl[j], nj = sl[j + 1] - sl[j];
+        HIP_TRY(hipEventSynchronize(ctx->ev_off[k]));
+        const uint64_t* ho = ctx->h_slot_off[k];
+        for (size_t c = 0; c < nj; c++) out_byte_off[c0 + c] = base + ho[c];
+        const uint64_t total = ho[nj];
+        const uint64_t ncopy = base >= out_cap ? 0 : std::min<uint64_t>(total, out_cap - base);
+        if (ncopy)
+            HIP_TRY(hipMemcpyAsync(out + base, ctx->d_slot[k] + o_out, ncopy,
+                                   hipMemcpyDeviceToHost, s_out));
+        HIP_TRY(hipEventRecord(ctx->ev_out[k], s_out));
+        base += total;
+        return CAPNP_OK;
+    };
+    for (size_t i = 0; i < ns; i++) {
+        const int k = (int)(i & 1);
+        const size_t c0 = sl[i], ni = sl[i + 1] - sl[i];
+        const uint64_t w0 = chunk_word_off[c0], wi = chunk_word_off[sl[i + 1]] - w0;
+        uint8_t* d = ctx->d_slot[k];
+        if (i >= 2) HIP_TRY(hipStreamWaitEvent(s_in, ctx->ev_out[k], 0));
+        if (wi)
+            HIP_TRY(hipMemcpyAsync(d, words + w0, wi * 8, hipMemcpyHostToDevice, s_in));
+        HIP_TRY(hipMemcpyAsync(d + o_off, chunk_word_off + c0, (ni + 1) * 8,
+                               hipMemcpyHostToDevice, s_in));
+        HIP_TRY(hipEventRecord(ctx->ev_in[k], s_in));
+        HIP_TRY(hipStreamWaitEvent(s_comp, ctx->ev_in[k], 0));
+        st = pack_batch_dev(ctx, reinterpret_cast<const uint64_t*>(d) - w0,
+                            reinterpret_cast<const uint64_t*>(d + o_off), ni, d + o_out,
+                            capnp_packed_batch_bound_bytes(wi, ni),
+                            reinterpret_cast<uint64_t*>(d + o_oo), tc, s_comp);
+        if (st != CAPNP_OK) return st;
+        HIP_TRY(hipEventRecord(ctx->ev_comp[k], s_comp));
+        if (i >= 1) {
+            st = finalize(i - 1);
+            if (st != CAPNP_OK) return st;
+        }
+        HIP_TRY(hipStreamWaitEvent(s_out, ctx->ev_comp[k], 0));
+        HIP_TRY(hipMemcpyAsync(ctx->h_slot_off[k], d + o_oo, (ni + 1) * 8,
+                               hipMemcpyDeviceToHost, s_out));
+        HIP_TRY(hipEventRecord(ctx->ev_off[k], s_out));
+    }
+    st = finalize(ns - 1);
+    if (st != CAPNP_OK) return st;
+    HIP_TRY(hipStreamSynchronize(s_out));
+    out_byte_off[n] = base;
+    if (base > out_cap) result = CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;
+    return result;
+}
+
+// Streaming unpack: every slice's sizes are known from the offsets, so the
+// three streams run without any host wait until the end.
+capnp_status capnp_stream_unpack_batch(capnp_ctx* ctx, const uint8_t* packed,
+                                       const uint64_t* in_byte_off, size_t nchunks,
+                                       uint64_t* words, const uint64_t* out_word_off,
+                                       int32_t* status, uint64_t* consumed, size_t slice_words) {
+    if (!ctx || !in_byte_off || !out_word_off || !status) return CAPNP_E_INVALID_ARGUMENT;
+    const size_t n = nchunks;
+    if (n == 0) return CAPNP_OK;
+    for (size_t c = 0; c < n; c++)
+        if (in_byte_off[c + 1] < in_byte_off[c] || out_word_off[c + 1] < out_word_off[c])
+            return CAPNP_E_INVALID_ARGUMENT;
+    if ((in_byte_off[n] > in_byte_off[0] && !packed) ||
+        (out_word_off[n] > out_word_off[0] && !words))
+        return CAPNP_E_INVALID_ARGUMENT;
+    const std::vector<size_t> sl = make_slices(out_word_off, n, slice_words ? slice_words
+                                                                            : kDefaultSliceWords);
+    const size_t ns = sl.size() - 1;
+    size_t max_w = 0, max_n = 0, max_b = 0;
+    for (size_t i = 0; i < ns; i++) {
+        max_w = std::max<size_t>(max_w, out_word_off[sl[i + 1]] - out_word_off[sl[i]]);
+        max_b = std::max<size_t>(max_b, in_byte_off[sl[i + 1]] - in_byte_off[sl[i]]);
+        max_n = std::max(max_n, sl[i + 1] - sl[i]);
+    }
+    const uint64_t tw = out_word_off[n] - out_word_off[0];
+    const double mean = std::max((double)tw / (double)n, 1.0);
+    const uint32_t utc = (uint32_t)std::max(1.0, std::min((double)capnp_unpack_tile_words() /
+                                                              mean, 64.0));
+    const size_t o_in = kSlotPad;
+    const size_t o_io = o_in + round16(max_b + kSlotPad);
+    const size_t o_oo = o_io + round16((max_n + 1) * 8);
+    const size_t o_st = o_oo + round16((max_n + 1) * 8);
+    const size_t o_cs = o_st + round16(max_n * 4);
+    const size_t o_out = o_cs + round16(max_n * 8);
+    capnp_status st = stream_setup(ctx, o_out + max_w * 8 + kSlotPad, 1);
+    if (st != CAPNP_OK) return st;
+    hipStream_t s_in = ctx->sstream[0], s_comp = ctx->sstream[1], s_out = ctx->sstream[2];
+    for (size_t i = 0; i < ns; i++) {
+        const int k = (int)(i & 1);
+        const size_t c0 = sl[i], ni = sl[i + 1] - sl[i];
+        const uint64_t b0 = in_byte_off[c0], bi = in_byte_off[sl[i + 1]] - b0;
+        const uint64_t w0 = out_word_off[c0], wi = out_word_off[sl[i + 1]] - w0;
+        uint8_t* d = ctx->d_slot[k];
+        if (i >= 2) HIP_TRY(hipStreamWaitEvent(s_in, ctx->ev_out[k], 0));
+        if (bi) HIP_TRY(hipMemcpyAsync(d + o_in, packed + b0, bi, hipMemcpyHostToDevice, s_in));
+        HIP_TRY(hipMemcpyAsync(d + o_io, in_byte_off + c0, (ni + 1) * 8, hipMemcpyHostToDevice,
+                               s_in));
+        HIP_TRY(hipMemcpyAsync(d + o_oo, out_word_off + c0, (ni + 1) * 8,
+                               hipMemcpyHostToDevice, s_in));
+        HIP_TRY(hipEventRecord(ctx->ev_in[k], s_in));
+        HIP_TRY(hipStreamWaitEvent(s_comp, ctx->ev_in[k], 0));
+        HIP_TRY(capnp_launch_unpack(d + o_in - b0, reinterpret_cast<const uint64_t*>(d + o_io),
+                                    ni, utc, reinterpret_cast<uint64_t*>(d + o_out) - w0,
+                                    reinterpret_cast<const uint64_t*>(d + o_oo),
+                                    reinterpret_cast<int32_t*>(d + o_st),
+                                    reinterpret_cast<uint64_t*>(d + o_cs), nullptr, s_comp));
+        HIP_TRY(hipEventRecord(ctx->ev_comp[k], s_comp));
+        HIP_TRY(hipStreamWaitEvent(s_out, ctx->ev_comp[k], 0));
+        if (wi)
+            HIP_TRY(hipMemcpyAsync(words + w0, d + o_out, wi * 8, hipMemcpyDeviceToHost, s_out));
+        HIP_TRY(hipMemcpyAsync(status + c0, d + o_st, ni * 4, hipMemcpyDeviceToHost, s_out));
+        if (consumed)
+            HIP_TRY(hipMemcpyAsync(consumed + c0, d + o_cs, ni * 8, hipMemcpyDeviceToHost,
+                                   s_out));
+        HIP_TRY(hipEventRecord(ctx->ev_out[k], s_out));
+    }
+    HIP_TRY(hipStreamSynchronize(s_out));
+    return CAPNP_OK;
 }
 
 capnp_status capnp_packed_write_message(capnp_ctx* ctx, const uint64_t* const* segs,

@@ -179,6 +179,30 @@ capnp_status capnp_unpack_batch_host(capnp_ctx* ctx, const uint8_t* packed,
                                      uint64_t* words, const uint64_t* out_word_off,
                                      int32_t* status, uint64_t* consumed);
 
+/* ---- streaming host batch API ----------------------- */
+/* The same transforms and results as capnp_pack_batch_host /
+   capnp_unpack_batch_host, pipelined over slices of about slice_words words
+   (0 = 4 Mi words): the copy in of slice i+1, the kernel on slice i and the
+   copy out of slice i-1 run concurrently on three streams with
+   double-buffered device staging, so a host-to-host batch moves at the PCIe
+   rate instead of the sum of the three phases.  This is the device side of
+   the async PackedRead/PackedWrite adaptors
+   (capnp-futures/src/serialize_packed.rs:83-226, 330-521) for whole batches.
+   Host buffers should be pinned (hipHostMalloc / hipHostRegister) for the
+   copies to overlap.  Blocking: returns when every byte has landed.
+   Pack: out_byte_off (host, nchunks+1) receives the exclusive scan of packed
+   sizes; CAPNP_E_BUFFER_NOT_LARGE_ENOUGH if the total exceeds out_cap
+   (nothing at or past out_cap is written).  Unpack: per-chunk status and
+   consumed (may be NULL) as capnp_unpack_batch_host. */
+capnp_status capnp_stream_pack_batch(capnp_ctx* ctx, const uint64_t* words,
+                                     const uint64_t* chunk_word_off, size_t nchunks,
+                                     uint8_t* out, size_t out_cap, uint64_t* out_byte_off,
+                                     size_t slice_words);
+capnp_status capnp_stream_unpack_batch(capnp_ctx* ctx, const uint8_t* packed,
+                                       const uint64_t* in_byte_off, size_t nchunks,
+                                       uint64_t* words, const uint64_t* out_word_off,
+                                       int32_t* status, uint64_t* consumed, size_t slice_words);
+
 /* ---- host message API (mirrors serialize_packed) ----------------------- */
 /* serialize_packed::write_message (serialize_packed.rs:446-453 ->
    serialize.rs:574-582): packs the segment table word 0, the rest of the
