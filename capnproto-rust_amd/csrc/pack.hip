@@ -67,7 +67,10 @@ __device__ uint64_t* g_trace;
 
 namespace {
 
-constexpr int kWaves = 4;
+#ifndef PACK_WAVES
+#define PACK_WAVES 4  // waves per workgroup (tile = PACK_WAVES x kStageSteps x 64 words)
+#endif
+constexpr int kWaves = PACK_WAVES;
 constexpr int kThreads = kWaves * CAPNP_WAVE;
 constexpr uint32_t kRing = 4096;           // streaming path: per-wave ring (bytes)
 constexpr uint32_t kRingMask = kRing - 1;
@@ -657,6 +660,9 @@ __device__ uint64_t tile_aggregate(const uint64_t* __restrict__ in,
 // itself from the input (records are idempotent), so the kernel finishes with
 // the right answer under any workgroup dispatch order.
 constexpr uint32_t kGroup = 64;
+#ifndef PACK_SLEEP
+#define PACK_SLEEP 2  // s_sleep between look-back polls (x 64 cycles)
+#endif
 #ifndef PACK_GWIN
 #define PACK_GWIN 16  // measured: 64 -> 564 us, 16 -> 552, 4 -> 555, 1 -> 603
 #endif
@@ -726,7 +732,7 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
             const uint64_t a = tile_aggregate(A.in, A.chunk_off, A.nchunks, A.tc, j, lane);
             if (lane == 0) publish_agent(&A.ts[j], kFlagAgg | a);
         } else {
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(PACK_SLEEP);
         }
         st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
     }
@@ -762,7 +768,7 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
                                                    A.ntiles, jg, lane);
                 if (lane == 0) publish_agent(&A.gs[jg], kFlagAgg | a);
             } else {
-                __builtin_amdgcn_s_sleep(2);
+                __builtin_amdgcn_s_sleep(PACK_SLEEP);
             }
             continue;
         }
@@ -853,10 +859,8 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     const uint32_t t0 = (uint32_t)(k0 * kSyncWords - TW0);  // first sync word, tile-relative
     for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
     // record assembly table: one 16-byte entry per thread (+ the copy entry)
-    reinterpret_cast<uint4*>(sm.sel)[tid] = reinterpret_cast<const uint4*>(kSelTable.e)[tid];
-    if (tid == 0)
-        reinterpret_cast<uint4*>(sm.sel)[kSelCopy] =
-            reinterpret_cast<const uint4*>(kSelTable.e)[kSelCopy];
+    for (uint32_t i = tid; i <= kSelCopy; i += kThreads)
+        reinterpret_cast<uint4*>(sm.sel)[i] = reinterpret_cast<const uint4*>(kSelTable.e)[i];
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
     uint8_t* const outa = out - mis;

@@ -51,12 +51,13 @@ def main():
         st = C.c_int(0)
         h = vp(L.capnp_ctx_create(0, C.byref(st)))
         L.capnp_ctx_reserve(h, n)
-        libs.append((path, L, h))
+        L.capnp_pack_tile_words.restype = u32
+        libs.append((path, L, h, tile_chunks_for(n * cw, n, lib=L)))
     times = {}
     oks = {}
     # rounds interleave the libraries so clock drift hits all of them alike
     for rnd in range(a.rounds):
-        for path, L, h in libs:
+        for path, L, h, tc in libs:
             for use_sync in (False, True):
                 for it in range(a.iters + 1):
                     e0 = torch.cuda.Event(enable_timing=True)
@@ -77,7 +78,7 @@ def main():
                         times.setdefault((path, use_sync), []).append(e0.elapsed_time(e1) * 1e3)
                 ok = torch.equal(oo, ref_off) and torch.equal(out[:ref.numel()], ref)
                 oks[(path, use_sync)] = oks.get((path, use_sync), True) and ok
-    for path, _, _ in libs:
+    for path, _, _, _ in libs:
         for use_sync in (False, True):
             ts = sorted(times[(path, use_sync)])
             print(f"{os.path.basename(path)} sync={int(use_sync)}: pack {ts[0]:.1f} us "

@@ -61,7 +61,8 @@ def main():
         sync = torch.empty(int(L.capnp_sync_index_entries(n * cw)), dtype=torch.int32,
                            device="cuda")
         utc = unpack_tile_chunks_for(n * cw, n, lib=L, sync=True)
-        libs.append((path, L, h, sync, utc))
+        L.capnp_pack_tile_words.restype = u32
+        libs.append((path, L, h, sync, utc, tile_chunks_for(n * cw, n, lib=L)))
     tp, tu, oks = {}, {}, {}
 
     def timed(fn):
@@ -75,7 +76,7 @@ def main():
         return e0.elapsed_time(e1) * 1e3
 
     for rnd in range(a.rounds):
-        for path, L, h, sync, utc in libs:
+        for path, L, h, sync, utc, tc in libs:
             for it in range(a.iters + 1):
                 t = timed(lambda: L.capnp_gpu_pack_batch_sync_tuned(
                     h, P(words.data_ptr()), P(offs.data_ptr()), n, P(out.data_ptr()), cap,
@@ -92,7 +93,7 @@ def main():
             ok = torch.equal(back, words) and int((status != 0).sum()) == 0
             oks[path] = oks.get(path, True) and ok
             back.zero_()
-    for path, _, _, _, utc in libs:
+    for path, _, _, _, utc, _ in libs:
         p, u = sorted(tp[path]), sorted(tu[path])
         print(f"{os.path.basename(path)}: pack {p[0]:.1f} (med {p[len(p) // 2]:.1f}) "
               f"unpack {u[0]:.1f} (med {u[len(u) // 2]:.1f}) sum {p[0] + u[0]:.1f} us "
