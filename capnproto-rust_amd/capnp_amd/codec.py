@@ -149,6 +149,28 @@ class Context:
                                chunks_per_tile)
         return words[:total], status[:n], consumed[:n]
 
+    def write_messages(self, words, seg_word_off, msg_seg_off, out=None, stream=None):
+        """serialize_packed::write_message for a batch of messages on the
+        device (capnp_gpu_write_messages): int64 device tensors `words`
+        (segments back to back), `seg_word_off` (segments + 1) and
+        `msg_seg_off` (messages + 1).  Returns (packed uint8 trimmed,
+        msg_byte_off int64)."""
+        import torch
+        nmsg = msg_seg_off.numel() - 1
+        nseg = seg_word_off.numel() - 1
+        total_words = int(seg_word_off[-1].item() - seg_word_off[0].item()) if nseg else 0
+        if out is None:
+            cap = self.batch_bound_bytes(total_words + 2 * nmsg + nseg // 2, 2 * nmsg + nseg)
+            out = torch.empty(max(cap, 1), dtype=torch.uint8, device=words.device)
+        mo = torch.empty(nmsg + 1, dtype=torch.int64, device=words.device)
+        st = _lib.lib().capnp_gpu_write_messages(self._h, _ptr(words), _ptr(seg_word_off),
+                                                 _ptr(msg_seg_off), nmsg, nseg, total_words,
+                                                 _ptr(out), out.numel(), _ptr(mo),
+                                                 self._stream(stream))
+        _check(st, self._h)
+        total = int(mo[-1].item())
+        return out[:total], mo
+
     # ---- streaming host batch (host buffers; pinned for overlap) ---------
     def stream_pack(self, words, chunk_word_off, out, out_off, slice_words=0):
         """capnp_stream_pack_batch on host tensors (CPU torch tensors, ideally

@@ -24,6 +24,13 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t*, const uint64_t*, uint64
                                         uint8_t*, uint64_t, uint64_t*, uint64_t*, uint32_t*,
                                         hipStream_t);
 extern "C" uint32_t capnp_pack_tile_words(void);
+extern "C" hipError_t capnp_msg_scan_bytes(uint64_t, size_t*);
+extern "C" hipError_t capnp_launch_msg_prepare(const uint64_t*, const uint64_t*, const uint64_t*,
+                                               uint64_t, uint64_t*, uint64_t*, uint64_t*,
+                                               uint64_t*, void*, size_t, uint64_t*, uint64_t*,
+                                               hipStream_t);
+extern "C" hipError_t capnp_launch_msg_offsets(const uint64_t*, const uint64_t*, uint64_t,
+                                               uint64_t*, hipStream_t);
 extern "C" size_t capnp_pack_state_bytes(uint64_t, uint32_t);
 extern "C" hipError_t capnp_launch_unpack(const uint8_t*, const uint64_t*, uint64_t, uint32_t,
                                           uint64_t*, const uint64_t*, int32_t*, uint64_t*,
@@ -61,6 +68,8 @@ struct capnp_ctx {
     size_t slot_cap = 0;
     uint64_t* h_slot_off[2] = {nullptr, nullptr};  // pinned: a slice's packed offsets
     size_t h_slot_off_cap = 0;
+    uint8_t* d_msg = nullptr;  // batch message framing: staging words and tables
+    size_t msg_cap = 0;
     std::string err;
 };
 
@@ -295,6 +304,7 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (ctx->d_body) hipFree(ctx->d_body);
     if (ctx->d_frame) hipFree(ctx->d_frame);
     if (ctx->h_frame) hipHostFree(ctx->h_frame);
+    if (ctx->d_msg) hipFree(ctx->d_msg);
     for (int k = 0; k < 3; k++)
         if (ctx->sstream[k]) {
             hipStreamSynchronize(ctx->sstream[k]);
@@ -660,6 +670,54 @@ capnp_status capnp_stream_unpack_batch(capnp_ctx* ctx, const uint8_t* packed,
         HIP_TRY(hipEventRecord(ctx->ev_out[k], s_out));
     }
     HIP_TRY(hipStreamSynchronize(s_out));
+    return CAPNP_OK;
+}
+
+// Batch write_message on the device (msgbatch.hip): layout, scans and
+// assembly into a staging array, one stream synchronisation for the totals,
+// then the batch pack of the chunks and the message offsets.
+capnp_status capnp_gpu_write_messages(capnp_ctx* ctx, const uint64_t* d_words,
+                                      const uint64_t* d_seg_word_off,
+                                      const uint64_t* d_msg_seg_off, size_t nmsg,
+                                      size_t total_segs, size_t total_words, uint8_t* d_out,
+                                      size_t out_cap, uint64_t* d_msg_byte_off, void* stream) {
+    if (!ctx || !d_msg_byte_off || (nmsg && (!d_seg_word_off || !d_msg_seg_off)))
+        return CAPNP_E_INVALID_ARGUMENT;
+    hipStream_t s = pick(ctx, stream);
+    if (nmsg == 0) {
+        HIP_TRY(hipMemsetAsync(d_msg_byte_off, 0, sizeof(uint64_t), s));
+        return CAPNP_OK;
+    }
+    if (total_segs < nmsg || (total_words && !d_words)) return CAPNP_E_INVALID_ARGUMENT;
+    // bounds: table words <= nmsg + total_segs / 2 + nmsg, chunks <= 2 nmsg + total_segs
+    const size_t max_words = total_words + 2 * nmsg + total_segs / 2 + 1;
+    const size_t max_chunks = 2 * nmsg + total_segs;
+    size_t scan_bytes = 0;
+    HIP_TRY(capnp_msg_scan_bytes(nmsg + 1, &scan_bytes));
+    const size_t o_cw = 0;
+    const size_t o_cc = o_cw + round16((nmsg + 1) * 8);
+    const size_t o_wofs = o_cc + round16((nmsg + 1) * 8);
+    const size_t o_cofs = o_wofs + round16((nmsg + 1) * 8);
+    const size_t o_tmp = o_cofs + round16((nmsg + 1) * 8);
+    const size_t o_coff = o_tmp + round16(scan_bytes + 16);
+    const size_t o_cboff = o_coff + round16((max_chunks + 1) * 8);
+    const size_t o_stage = o_cboff + round16((max_chunks + 1) * 8);
+    capnp_status st = ensure_buf(ctx, &ctx->d_msg, &ctx->msg_cap, o_stage + max_words * 8 + 64);
+    if (st != CAPNP_OK) return st;
+    uint8_t* d = ctx->d_msg;
+    auto U = [&](size_t o) { return reinterpret_cast<uint64_t*>(d + o); };
+    HIP_TRY(capnp_launch_msg_prepare(d_words, d_seg_word_off, d_msg_seg_off, nmsg, U(o_cw),
+                                     U(o_cc), U(o_wofs), U(o_cofs), d + o_tmp, scan_bytes,
+                                     U(o_stage), U(o_coff), s));
+    uint64_t tot[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&tot[0], U(o_wofs) + nmsg, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&tot[1], U(o_cofs) + nmsg, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (tot[0] > max_words || tot[1] > max_chunks) return CAPNP_E_INVALID_ARGUMENT;
+    st = pack_batch_dev(ctx, U(o_stage), U(o_coff), tot[1], d_out, out_cap, U(o_cboff),
+                        tile_chunks_for(tot[0], tot[1]), s);
+    if (st != CAPNP_OK) return st;
+    HIP_TRY(capnp_launch_msg_offsets(U(o_cofs), U(o_cboff), nmsg, d_msg_byte_off, s));
     return CAPNP_OK;
 }
 

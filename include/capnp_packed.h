@@ -203,6 +203,25 @@ capnp_status capnp_stream_unpack_batch(capnp_ctx* ctx, const uint8_t* packed,
                                        uint64_t* words, const uint64_t* out_word_off,
                                        int32_t* status, uint64_t* consumed, size_t slice_words);
 
+/* ---- device batch message framing ------------------ */
+/* serialize_packed::write_message for nmsg messages at once
+   (serialize_packed.rs:446-453 -> serialize.rs:574-679).  Message m owns
+   segments [d_msg_seg_off[m], d_msg_seg_off[m+1]) (at least one), segment s
+   is words [d_seg_word_off[s], d_seg_word_off[s+1]) of d_words, and a
+   message's segments are consecutive in d_words.  The packed messages go
+   back to back into d_out, message m at d_msg_byte_off[m] (nmsg+1 entries,
+   the last is the total): each is exactly the byte stream write_message
+   produces (the segment table's word 0, the rest of the table, then every
+   segment, each packed by its own write_all).  total_segs and total_words
+   are the batch's segment count and segment words (host-side sizes for the
+   staging).  Synchronises the stream once (to size the pack); out_cap as in
+   capnp_gpu_pack_batch. */
+capnp_status capnp_gpu_write_messages(capnp_ctx* ctx, const uint64_t* d_words,
+                                      const uint64_t* d_seg_word_off,
+                                      const uint64_t* d_msg_seg_off, size_t nmsg,
+                                      size_t total_segs, size_t total_words, uint8_t* d_out,
+                                      size_t out_cap, uint64_t* d_msg_byte_off, void* stream);
+
 /* ---- host message API (mirrors serialize_packed) ----------------------- */
 /* serialize_packed::write_message (serialize_packed.rs:446-453 ->
    serialize.rs:574-582): packs the segment table word 0, the rest of the

@@ -1,0 +1,104 @@
+"""GPU parity of the device batch message framing (capnp_gpu_write_messages,
+SURVEY §8f row 1): every message of the batch must be byte-identical to the
+oracle's serialize_packed::write_message (oracle/packed_oracle.c, pinned by
+the reference's golden vectors), the message offsets must be the running
+sum of their sizes, and every message must read back (oracle read_message).
+"""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from capnp_amd import Context
+    return Context(0)
+
+
+def _segment(rng, n):
+    w = np.zeros(n, np.uint64)
+    b = w.view(np.uint8)
+    mode = rng.random()
+    for i in range(n):
+        r = rng.random()
+        if mode < 0.3:
+            if r < 0.1:
+                b[8 * i:8 * i + 8] = [rng.randrange(256) for _ in range(8)]
+        elif mode < 0.6:
+            vals = [rng.randrange(1, 256) for _ in range(8)]
+            if r < 0.2:
+                vals[rng.randrange(8)] = 0
+            b[8 * i:8 * i + 8] = vals
+        elif r > 0.3:
+            b[8 * i:8 * i + 8] = [rng.randrange(256) if rng.random() < 0.56 else 0
+                                  for _ in range(8)]
+    return w
+
+
+def _check_messages(ctx, msgs):
+    seg_lens = [len(s) for m in msgs for s in m]
+    seg_off = np.concatenate([[0], np.cumsum(seg_lens)]).astype(np.int64)
+    msg_seg_off = np.concatenate([[0], np.cumsum([len(m) for m in msgs])]).astype(np.int64)
+    words = (np.concatenate([s for m in msgs for s in m]) if seg_off[-1] else
+             np.zeros(1, np.uint64))
+    dw = torch.from_numpy(words.view(np.int64).copy()).cuda()
+    packed, mo = ctx.write_messages(dw, torch.from_numpy(seg_off).cuda(),
+                                    torch.from_numpy(msg_seg_off).cuda())
+    torch.cuda.synchronize()
+    got = packed.cpu().numpy().tobytes()
+    mo = mo.cpu().numpy()
+    pos = 0
+    for i, m in enumerate(msgs):
+        st, ref = O.write_message(m)
+        assert st == 0
+        assert mo[i] == pos, i
+        assert got[pos:pos + len(ref)] == ref, (i, [len(s) for s in m])
+        st2, segs, used = O.read_message(got[pos:pos + len(ref)], limit=None,
+                                         body_cap=sum(len(s) for s in m) + 16)
+        assert st2 == 0 and used == len(ref)
+        assert len(segs) == len(m) and all(np.array_equal(a, b) for a, b in zip(segs, m))
+        pos += len(ref)
+    assert mo[-1] == pos == len(got)
+
+
+def test_write_messages_random(ctx):
+    rng = random.Random(7)
+    msgs = []
+    for _ in range(300):
+        nseg = rng.choice([1, 1, 2, 3, 4, 5, 8, 17])
+        msgs.append([_segment(rng, rng.choice([0, 1, 2, 63, 64, 65, 128, 300]))
+                     for _ in range(nseg)])
+    _check_messages(ctx, msgs)
+
+
+def test_write_messages_edges(ctx):
+    rng = random.Random(3)
+    msgs = [
+        [np.zeros(0, np.uint64)],                        # one empty segment
+        [np.zeros(300, np.uint64)],                      # one long zero run
+        [np.full(600, 0x0102030405060708, np.uint64)],   # literal run > 255
+        [np.zeros(0, np.uint64)] * 6,                     # empty segments only
+        [_segment(rng, 5) for _ in range(511)],          # the most segments a reader takes
+        [_segment(rng, 1000)],
+    ]
+    _check_messages(ctx, msgs)
+    _check_messages(ctx, msgs[:1])
+
+
+def test_write_messages_carsales_like_batch(ctx):
+    # many single-segment 1 KiB messages (the config-2 shape) plus a few
+    # multi-segment ones
+    rng = random.Random(9)
+    msgs = [[_segment(rng, 128)] for _ in range(2000)]
+    for k in range(0, 2000, 97):
+        msgs[k] = [_segment(rng, 60), _segment(rng, 68)]
+    _check_messages(ctx, msgs)
