@@ -201,13 +201,16 @@ class Context:
 
 
 def tile_chunks_for(total_words, nchunks, lib=None):
-    """Chunks per 256-thread pack workgroup: about capnp_pack_tile_words()
-    words per tile, i.e. one staged range per wave (pack.hip kStageSteps)."""
+    """Chunks per pack workgroup: the staged path holds
+    capnp_pack_tile_words() / 64 steps of 64 words per tile and a chunk
+    takes whole steps, so the budget is counted in steps of the mean chunk
+    (pack.hip kStageSteps; the same rule as capi.hip)."""
+    import math
     if nchunks <= 0:
         return 16
     tw = (lib or _lib.lib()).capnp_pack_tile_words()
-    mean = max(total_words / nchunks, 1.0)
-    return int(max(1, min(64, tw // mean)))
+    steps = max(1, math.ceil(total_words / nchunks / 64.0))
+    return int(max(1, min(64, (tw // 64) // steps)))
 
 
 def unpack_tile_chunks_for(total_words, nchunks, lib=None, sync=False):

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <string>
+#include <cmath>
 #include <vector>
 
 #include "../../include/capnp_packed.h"
@@ -151,10 +152,14 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
     return CAPNP_OK;
 }
 
+// Chunks per pack tile: the staged path holds capnp_pack_tile_words() / 64
+// steps of 64 words per tile, and a chunk takes whole steps, so the budget
+// is counted in steps of the mean chunk (a 32-word chunk still takes one).
 uint32_t tile_chunks_for(uint64_t total_words, size_t n) {
     if (n == 0) return kDefaultTileChunks;
     const double mean = (double)total_words / (double)n;
-    double t = (double)capnp_pack_tile_words() / std::max(mean, 1.0);  // staged path size
+    const double steps = std::max(1.0, std::ceil(mean / 64.0));
+    double t = (double)(capnp_pack_tile_words() / 64) / steps;
     uint32_t tc = (uint32_t)std::max(1.0, std::min(t, (double)kMaxTileChunks));
     return tc;
 }
