@@ -32,6 +32,7 @@ EXPORTS = [
     "capnp_gpu_unpack_batch_sync", "capnp_gpu_pack_batch_sync_tuned",
     "capnp_gpu_unpack_batch_sync_tuned", "capnp_unpack_sync_tile_words",
     "capnp_stream_pack_batch", "capnp_stream_unpack_batch", "capnp_gpu_write_messages",
+    "capnp_gpu_read_messages",
 ]
 
 
@@ -103,6 +104,8 @@ def lib():
     L.capnp_stream_pack_batch.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz]
     L.capnp_stream_unpack_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, sz]
     L.capnp_gpu_write_messages.argtypes = [vp, vp, vp, vp, sz, sz, sz, vp, sz, vp, vp]
+    L.capnp_gpu_read_messages.argtypes = [vp, vp, vp, sz, C.POINTER(ReaderOptionsC), i32, vp, sz,
+                                          vp, vp, sz, vp, vp, vp, vp]
     L.capnp_packed_write_message.argtypes = [vp, vp, vp, u32, vp, sz, C.POINTER(C.c_size_t)]
     L.capnp_packed_read_message.argtypes = [vp, vp, sz, C.POINTER(ReaderOptionsC), i32, vp, sz,
                                             vp, C.POINTER(C.c_uint32), C.POINTER(C.c_size_t)]

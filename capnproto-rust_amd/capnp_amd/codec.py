@@ -171,6 +171,30 @@ class Context:
         total = int(mo[-1].item())
         return out[:total], mo
 
+    def read_messages(self, packed, msg_byte_off, words_cap, segs_cap, try_mode=False,
+                      limit=8 * 1024 * 1024, stream=None):
+        """serialize_packed::read_message for a batch of messages on the
+        device (capnp_gpu_read_messages).  Returns (words, msg_word_off,
+        seg_words, msg_seg_off, status, consumed) as device tensors; limit
+        None = no traversal limit."""
+        import torch
+        nmsg = msg_byte_off.numel() - 1
+        dev = msg_byte_off.device
+        words = torch.empty(max(words_cap, 1), dtype=torch.int64, device=dev)
+        mwo = torch.empty(nmsg + 1, dtype=torch.int64, device=dev)
+        segs = torch.empty(max(segs_cap, 1), dtype=torch.int64, device=dev)
+        mso = torch.empty(nmsg + 1, dtype=torch.int64, device=dev)
+        status = torch.empty(max(nmsg, 1), dtype=torch.int32, device=dev)
+        consumed = torch.empty(max(nmsg, 1), dtype=torch.int64, device=dev)
+        o = _lib.ReaderOptionsC(int(limit or 0), 1 if limit is not None else 0, 64)
+        st = _lib.lib().capnp_gpu_read_messages(self._h, _ptr(packed), _ptr(msg_byte_off), nmsg,
+                                                C.byref(o), int(bool(try_mode)), _ptr(words),
+                                                int(words_cap), _ptr(mwo), _ptr(segs),
+                                                int(segs_cap), _ptr(mso), _ptr(status),
+                                                _ptr(consumed), self._stream(stream))
+        _check(st, self._h)
+        return words, mwo, segs, mso, status[:nmsg], consumed[:nmsg]
+
     # ---- streaming host batch (host buffers; pinned for overlap) ---------
     def stream_pack(self, words, chunk_word_off, out, out_off, slice_words=0):
         """capnp_stream_pack_batch on host tensors (CPU torch tensors, ideally

@@ -32,6 +32,17 @@ extern "C" hipError_t capnp_launch_msg_prepare(const uint64_t*, const uint64_t*,
                                                hipStream_t);
 extern "C" hipError_t capnp_launch_msg_offsets(const uint64_t*, const uint64_t*, uint64_t,
                                                uint64_t*, hipStream_t);
+extern "C" hipError_t capnp_launch_msg_frame(const uint8_t*, const uint64_t*, uint64_t, int,
+                                             uint64_t, int, uint64_t*, uint64_t*, int32_t*,
+                                             uint64_t*, void*, size_t, uint64_t*, uint64_t*,
+                                             hipStream_t);
+extern "C" hipError_t capnp_launch_msg_segs(const uint8_t*, const uint64_t*, uint64_t, int,
+                                            uint64_t, int, const int32_t*, const uint64_t*,
+                                            const uint64_t*, const uint64_t*, uint64_t*,
+                                            uint64_t*, uint64_t*, hipStream_t);
+extern "C" hipError_t capnp_launch_msg_status(uint64_t, const int32_t*, const uint64_t*,
+                                              const int32_t*, const uint64_t*, int32_t*,
+                                              uint64_t*, hipStream_t);
 extern "C" size_t capnp_pack_state_bytes(uint64_t, uint32_t);
 extern "C" hipError_t capnp_launch_unpack(const uint8_t*, const uint64_t*, uint64_t, uint32_t,
                                           uint64_t*, const uint64_t*, int32_t*, uint64_t*,
@@ -723,6 +734,70 @@ capnp_status capnp_gpu_write_messages(capnp_ctx* ctx, const uint64_t* d_words,
                         tile_chunks_for(tot[0], tot[1]), s);
     if (st != CAPNP_OK) return st;
     HIP_TRY(capnp_launch_msg_offsets(U(o_cofs), U(o_cboff), nmsg, d_msg_byte_off, s));
+    return CAPNP_OK;
+}
+
+// Batch read_message on the device (msgbatch.hip): table decode per
+// message, scans into the caller's offset arrays, one synchronisation for
+// the totals (capacity check), segment lengths and the interleaved chunk
+// tables, the batch unpack of the bodies, then the per-message status.
+capnp_status capnp_gpu_read_messages(capnp_ctx* ctx, const uint8_t* d_packed,
+                                     const uint64_t* d_msg_byte_off, size_t nmsg,
+                                     const capnp_reader_options* opts, int try_mode,
+                                     uint64_t* d_words, size_t words_cap,
+                                     uint64_t* d_msg_word_off, uint64_t* d_seg_words,
+                                     size_t segs_cap, uint64_t* d_msg_seg_off,
+                                     int32_t* d_status, uint64_t* d_consumed, void* stream) {
+    if (!ctx || !d_msg_word_off || !d_msg_seg_off ||
+        (nmsg && (!d_msg_byte_off || !d_status)))
+        return CAPNP_E_INVALID_ARGUMENT;
+    hipStream_t s = pick(ctx, stream);
+    if (nmsg == 0) {
+        HIP_TRY(hipMemsetAsync(d_msg_word_off, 0, 8, s));
+        HIP_TRY(hipMemsetAsync(d_msg_seg_off, 0, 8, s));
+        return CAPNP_OK;
+    }
+    const capnp_reader_options o = opts ? *opts : capnp_default_reader_options();
+    size_t scan_bytes = 0;
+    HIP_TRY(capnp_msg_scan_bytes(nmsg + 1, &scan_bytes));
+    const size_t n1 = nmsg + 1, n2 = 2 * nmsg + 1;
+    const size_t o_nseg = 0;
+    const size_t o_words = o_nseg + round16(n1 * 8);
+    const size_t o_tst = o_words + round16(n1 * 8);
+    const size_t o_tused = o_tst + round16(n1 * 4);
+    const size_t o_tmp = o_tused + round16(n1 * 8);
+    const size_t o_in2 = o_tmp + round16(scan_bytes + 16);
+    const size_t o_out2 = o_in2 + round16(n2 * 8);
+    const size_t o_cst = o_out2 + round16(n2 * 8);
+    const size_t o_ccons = o_cst + round16(n2 * 4);
+    const size_t o_end = o_ccons + round16(n2 * 8);
+    capnp_status st = ensure_buf(ctx, &ctx->d_msg, &ctx->msg_cap, o_end + 64);
+    if (st != CAPNP_OK) return st;
+    uint8_t* d = ctx->d_msg;
+    auto U = [&](size_t off) { return reinterpret_cast<uint64_t*>(d + off); };
+    auto I = [&](size_t off) { return reinterpret_cast<int32_t*>(d + off); };
+    const uint64_t limit = o.traversal_limit_in_words;
+    const int has_limit = o.has_traversal_limit != 0;
+    HIP_TRY(capnp_launch_msg_frame(d_packed, d_msg_byte_off, nmsg, try_mode, limit, has_limit,
+                                   U(o_nseg), U(o_words), I(o_tst), U(o_tused), d + o_tmp,
+                                   scan_bytes, d_msg_seg_off, d_msg_word_off, s));
+    uint64_t tot[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&tot[0], d_msg_word_off + nmsg, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&tot[1], d_msg_seg_off + nmsg, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (tot[0] > words_cap || tot[1] > segs_cap || (tot[0] && !d_words) ||
+        (tot[1] && !d_seg_words))
+        return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;
+    HIP_TRY(capnp_launch_msg_segs(d_packed, d_msg_byte_off, nmsg, try_mode, limit, has_limit,
+                                  I(o_tst), U(o_tused), d_msg_seg_off, d_msg_word_off,
+                                  d_seg_words, U(o_in2), U(o_out2), s));
+    const double mean = std::max((double)tot[0] / (double)(2 * nmsg), 1.0);
+    const uint32_t utc = (uint32_t)std::max(1.0, std::min((double)capnp_unpack_tile_words() /
+                                                              mean, 64.0));
+    HIP_TRY(capnp_launch_unpack(d_packed, U(o_in2), 2 * nmsg, utc, d_words, U(o_out2),
+                                I(o_cst), U(o_ccons), nullptr, s));
+    HIP_TRY(capnp_launch_msg_status(nmsg, I(o_tst), U(o_tused), I(o_cst), U(o_ccons), d_status,
+                                    d_consumed, s));
     return CAPNP_OK;
 }
 

@@ -129,3 +129,212 @@ extern "C" hipError_t capnp_launch_msg_offsets(const uint64_t* cofs,
                        msg_byte_off);
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Batch read_message / try_read_message on the device (serialize_packed.rs:
+// 233-255 -> serialize.rs:287-325, 448-524), messages delimited by a
+// side-band byte index (as capnp_gpu_write_messages writes it).  Per
+// message: the 8-byte first read unit, the rest of the table as one read
+// unit (serialize.rs:476-496), then the body as one read_exact.  The table
+// read units are decoded by one lane per message with PackedRead semantics
+// (serialize_packed.rs:80-228), streaming the decoded bytes into a sink, so
+// no per-message table buffer is needed; the bodies then go through the
+// batch UNPACK kernel as chunks interleaved with zero-word "table" chunks
+// (so that consecutive chunks stay contiguous in the packed stream).
+namespace {
+
+enum : int32_t {
+    MST_OK = 0, MST_NONE = 1, MST_PREMATURE = 2, MST_NOT_CLEAN = 3, MST_FAILED_FILL = 4,
+    MST_EOF = 5, MST_BAD_NSEG = 6, MST_TOO_LARGE = 8,
+};
+
+// One PackedRead::read of out_len bytes over in[0..in_len), the decoded
+// bytes handed to sink(i, byte) in order (frame.hip serial_read with a sink).
+template <class Sink>
+__device__ int32_t read_unit(const uint8_t* in, uint64_t in_len, uint64_t out_len, Sink sink,
+                             uint64_t* used, uint64_t* nread) {
+    *used = 0;
+    *nread = 0;
+    if (out_len == 0 || in_len == 0) return MST_OK;
+    uint64_t ip = 0, op = 0;
+    while (op < out_len) {
+        if (ip == in_len) return MST_PREMATURE;
+        const uint32_t tag = in[ip++];
+        for (int k = 0; k < 8; k++) {
+            if (tag & (1u << k)) {
+                if (ip == in_len) return MST_PREMATURE;
+                sink(op++, in[ip++]);
+            } else {
+                sink(op++, 0);
+            }
+        }
+        if (tag == 0 || tag == 0xFF) {
+            if (ip == in_len) return MST_PREMATURE;
+            const uint64_t run = 8ull * in[ip++];
+            if (run > out_len - op) return MST_NOT_CLEAN;
+            if (tag == 0) {
+                for (uint64_t i = 0; i < run; i++) sink(op++, 0);
+            } else {
+                if (in_len - ip < run) { *used = in_len; return MST_FAILED_FILL; }
+                for (uint64_t i = 0; i < run; i++) sink(op++, in[ip++]);
+            }
+        }
+    }
+    *used = ip;
+    *nread = out_len;
+    return MST_OK;
+}
+
+// The segment table of the message in in[0..in_len): status, segment count,
+// body words and the packed bytes the table used; seg (may be null) receives
+// the segment lengths.
+__device__ int32_t read_table(const uint8_t* in, uint64_t in_len, int try_mode, uint64_t limit,
+                              int has_limit, uint32_t* nseg_out, uint64_t* words_out,
+                              uint64_t* used_out, uint64_t* seg) {
+    *nseg_out = 0;
+    *words_out = 0;
+    *used_out = 0;
+    uint32_t w0[2] = {0, 0};
+    uint64_t used = 0, nread = 0;
+    int32_t st = read_unit(in, in_len, 8,
+                           [&](uint64_t i, uint32_t b) { w0[i >> 2] |= b << (8 * (i & 3)); },
+                           &used, &nread);
+    if (st != MST_OK) return st;
+    if (nread == 0) return try_mode ? MST_NONE : MST_EOF;
+    const uint32_t nseg = w0[0] + 1u;
+    if (nseg >= 512u || nseg == 0) return MST_BAD_NSEG;
+    uint64_t total = w0[1];
+    if (seg) seg[0] = w0[1];
+    uint64_t pos = used;
+    if (nseg > 1) {
+        const uint64_t rest = nseg < 4 ? 8 : (uint64_t)(nseg & ~1u) * 4;
+        uint32_t acc = 0;
+        st = read_unit(in + pos, in_len - pos, rest,
+                       [&](uint64_t i, uint32_t b) {
+                           acc |= b << (8 * (i & 3));
+                           if ((i & 3) == 3) {
+                               const uint64_t k = (i >> 2) + 1;  // segment index
+                               if (k < nseg) {
+                                   total += acc;
+                                   if (seg) seg[k] = acc;
+                               }
+                               acc = 0;
+                           }
+                       },
+                       &used, &nread);
+        if (st == MST_OK && nread != rest) st = MST_FAILED_FILL;  // read_exact (io.rs:16-31)
+        if (st != MST_OK) return st;
+        pos += used;
+    }
+    if (has_limit && total > limit) return MST_TOO_LARGE;
+    *nseg_out = nseg;
+    *words_out = total;
+    *used_out = pos;
+    return MST_OK;
+}
+
+__global__ void msg_frame(const uint8_t* __restrict__ in, const uint64_t* __restrict__ msg_off,
+                          uint64_t nmsg, int try_mode, uint64_t limit, int has_limit,
+                          uint64_t* __restrict__ nseg, uint64_t* __restrict__ words,
+                          int32_t* __restrict__ st, uint64_t* __restrict__ tused) {
+    const uint64_t m = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (m > nmsg) return;
+    if (m == nmsg) {
+        nseg[m] = 0;
+        words[m] = 0;
+        return;
+    }
+    const uint64_t a = msg_off[m], b = msg_off[m + 1];
+    uint32_t ns = 0;
+    uint64_t w = 0, u = 0;
+    const int32_t s = read_table(in + a, b - a, try_mode, limit, has_limit, &ns, &w, &u, nullptr);
+    st[m] = s;
+    nseg[m] = s == MST_OK ? ns : 0;
+    words[m] = s == MST_OK ? w : 0;
+    tused[m] = s == MST_OK ? u : 0;
+}
+
+// Segment lengths into seg[sofs[m] ..], and the interleaved chunk tables of
+// the body unpack: chunk 2m = message m's table bytes (no output words),
+// chunk 2m + 1 = its body (words[m] words; a failed table gets none).
+__global__ void msg_segs(const uint8_t* __restrict__ in, const uint64_t* __restrict__ msg_off,
+                         uint64_t nmsg, int try_mode, uint64_t limit, int has_limit,
+                         const int32_t* __restrict__ st, const uint64_t* __restrict__ tused,
+                         const uint64_t* __restrict__ sofs, const uint64_t* __restrict__ wofs,
+                         uint64_t* __restrict__ seg, uint64_t* __restrict__ in_off,
+                         uint64_t* __restrict__ out_off) {
+    const uint64_t m = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (m > nmsg) return;
+    if (m == nmsg) {
+        in_off[2 * m] = msg_off[m];
+        out_off[2 * m] = wofs[m];
+        return;
+    }
+    const uint64_t a = msg_off[m], b = msg_off[m + 1];
+    in_off[2 * m] = a;
+    out_off[2 * m] = wofs[m];
+    out_off[2 * m + 1] = wofs[m];
+    if (st[m] == MST_OK) {
+        uint32_t ns;
+        uint64_t w, u;
+        read_table(in + a, b - a, try_mode, limit, has_limit, &ns, &w, &u, seg + sofs[m]);
+        in_off[2 * m + 1] = a + tused[m];
+    } else {
+        in_off[2 * m + 1] = b;  // the whole range is "table"; the body chunk is empty
+    }
+}
+
+// Per message: the table's status, else the body's; bytes consumed.
+__global__ void msg_status(uint64_t nmsg, const int32_t* __restrict__ tst,
+                           const uint64_t* __restrict__ tused, const int32_t* __restrict__ cst,
+                           const uint64_t* __restrict__ ccons, int32_t* __restrict__ status,
+                           uint64_t* __restrict__ consumed) {
+    const uint64_t m = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (m >= nmsg) return;
+    const bool ok = tst[m] == MST_OK;
+    status[m] = ok ? cst[2 * m + 1] : tst[m];
+    if (consumed) consumed[m] = ok ? tused[m] + ccons[2 * m + 1] : 0;
+}
+
+}  // namespace
+
+extern "C" hipError_t capnp_launch_msg_frame(const uint8_t* in, const uint64_t* msg_off,
+                                             uint64_t nmsg, int try_mode, uint64_t limit,
+                                             int has_limit, uint64_t* nseg, uint64_t* words,
+                                             int32_t* st, uint64_t* tused, void* tmp,
+                                             size_t tmp_bytes, uint64_t* sofs, uint64_t* wofs,
+                                             hipStream_t s) {
+    const uint32_t g = (uint32_t)((nmsg + 1 + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(msg_frame, dim3(g), dim3(kThreads), 0, s, in, msg_off, nmsg, try_mode,
+                       limit, has_limit, nseg, words, st, tused);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    size_t tb = tmp_bytes;
+    e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, nseg, sofs, (int)(nmsg + 1), s);
+    if (e != hipSuccess) return e;
+    tb = tmp_bytes;
+    return hipcub::DeviceScan::ExclusiveSum(tmp, tb, words, wofs, (int)(nmsg + 1), s);
+}
+
+extern "C" hipError_t capnp_launch_msg_segs(const uint8_t* in, const uint64_t* msg_off,
+                                            uint64_t nmsg, int try_mode, uint64_t limit,
+                                            int has_limit, const int32_t* st,
+                                            const uint64_t* tused, const uint64_t* sofs,
+                                            const uint64_t* wofs, uint64_t* seg,
+                                            uint64_t* in_off, uint64_t* out_off, hipStream_t s) {
+    const uint32_t g = (uint32_t)((nmsg + 1 + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(msg_segs, dim3(g), dim3(kThreads), 0, s, in, msg_off, nmsg, try_mode,
+                       limit, has_limit, st, tused, sofs, wofs, seg, in_off, out_off);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t capnp_launch_msg_status(uint64_t nmsg, const int32_t* tst,
+                                              const uint64_t* tused, const int32_t* cst,
+                                              const uint64_t* ccons, int32_t* status,
+                                              uint64_t* consumed, hipStream_t s) {
+    const uint32_t g = (uint32_t)((nmsg + kThreads - 1) / kThreads);
+    if (g)
+        hipLaunchKernelGGL(msg_status, dim3(g), dim3(kThreads), 0, s, nmsg, tst, tused, cst,
+                           ccons, status, consumed);
+    return hipGetLastError();
+}

@@ -222,6 +222,30 @@ capnp_status capnp_gpu_write_messages(capnp_ctx* ctx, const uint64_t* d_words,
                                       size_t total_segs, size_t total_words, uint8_t* d_out,
                                       size_t out_cap, uint64_t* d_msg_byte_off, void* stream);
 
+/* serialize_packed::read_message / try_read_message (serialize_packed.rs:
+   233-255 -> serialize.rs:287-325, 448-524) for nmsg messages at once, the
+   messages delimited by a side-band byte index: message m is packed bytes
+   [d_msg_byte_off[m], d_msg_byte_off[m+1]) of d_packed (as
+   capnp_gpu_write_messages writes it).  Per message: the table's read units
+   (8 bytes, then the rest of the table as one unit) with the reference's
+   checks (segment count, traversal limit of opts, NULL = defaults;
+   try_mode: an empty message yields CAPNP_NONE), then the body as one
+   read_exact.  Outputs (device): the bodies back to back in d_words
+   (message m's segments at words [d_msg_word_off[m], d_msg_word_off[m+1]),
+   nmsg+1 entries), the segment lengths in d_seg_words (message m's at
+   [d_msg_seg_off[m], d_msg_seg_off[m+1])), d_status[m] and d_consumed[m]
+   (may be NULL; packed bytes the message used).  A message whose table
+   fails gets no words and no segments.  Synchronises the stream once (the
+   totals are checked against words_cap and segs_cap:
+   CAPNP_E_BUFFER_NOT_LARGE_ENOUGH, with only the offset arrays written). */
+capnp_status capnp_gpu_read_messages(capnp_ctx* ctx, const uint8_t* d_packed,
+                                     const uint64_t* d_msg_byte_off, size_t nmsg,
+                                     const capnp_reader_options* opts, int try_mode,
+                                     uint64_t* d_words, size_t words_cap,
+                                     uint64_t* d_msg_word_off, uint64_t* d_seg_words,
+                                     size_t segs_cap, uint64_t* d_msg_seg_off,
+                                     int32_t* d_status, uint64_t* d_consumed, void* stream);
+
 /* ---- host message API (mirrors serialize_packed) ----------------------- */
 /* serialize_packed::write_message (serialize_packed.rs:446-453 ->
    serialize.rs:574-582): packs the segment table word 0, the rest of the

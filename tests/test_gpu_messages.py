@@ -102,3 +102,85 @@ def test_write_messages_carsales_like_batch(ctx):
     for k in range(0, 2000, 97):
         msgs[k] = [_segment(rng, 60), _segment(rng, 68)]
     _check_messages(ctx, msgs)
+
+
+# ------------------------------------------------------------ batch read side
+def _read_back(ctx, packed_bytes, msg_off, words_cap, segs_cap, try_mode=False,
+               limit=8 * 1024 * 1024):
+    pk = torch.from_numpy(np.frombuffer(packed_bytes, np.uint8).copy()).cuda() \
+        if len(packed_bytes) else torch.zeros(1, dtype=torch.uint8, device="cuda")
+    mo = torch.from_numpy(np.asarray(msg_off, np.int64)).cuda()
+    w, mwo, sg, mso, st, cons = ctx.read_messages(pk, mo, words_cap, segs_cap,
+                                                  try_mode=try_mode, limit=limit)
+    torch.cuda.synchronize()
+    return (w.cpu().numpy().view(np.uint64), mwo.cpu().numpy(), sg.cpu().numpy(),
+            mso.cpu().numpy(), st.cpu().numpy(), cons.cpu().numpy())
+
+
+def _oracle_read(buf, try_mode, limit):
+    cap = 8 * len(buf) * 32 + 64  # (zero runs expand 2040x at most per 2 bytes)
+    return O.read_message(buf, try_mode=try_mode, limit=limit, body_cap=cap)
+
+
+def test_read_messages_round_trip(ctx):
+    rng = random.Random(21)
+    msgs = []
+    for _ in range(400):
+        nseg = rng.choice([1, 1, 2, 3, 4, 7, 33])
+        msgs.append([_segment(rng, rng.choice([0, 1, 5, 64, 65, 129, 300]))
+                     for _ in range(nseg)])
+    seg_lens = [len(s) for m in msgs for s in m]
+    seg_off = np.concatenate([[0], np.cumsum(seg_lens)]).astype(np.int64)
+    msg_seg_off = np.concatenate([[0], np.cumsum([len(m) for m in msgs])]).astype(np.int64)
+    words = np.concatenate([s for m in msgs for s in m])
+    packed, mo = ctx.write_messages(torch.from_numpy(words.view(np.int64).copy()).cuda(),
+                                    torch.from_numpy(seg_off).cuda(),
+                                    torch.from_numpy(msg_seg_off).cuda())
+    w, mwo, sg, mso, st, cons = ctx.read_messages(packed, mo, len(words), len(seg_lens))
+    torch.cuda.synchronize()
+    assert (st.cpu().numpy() == 0).all()
+    assert np.array_equal(cons.cpu().numpy(), np.diff(mo.cpu().numpy()))
+    assert np.array_equal(mso.cpu().numpy(), msg_seg_off)
+    assert np.array_equal(sg.cpu().numpy()[:len(seg_lens)], seg_lens)
+    assert np.array_equal(mwo.cpu().numpy(), [0] + list(np.cumsum([sum(len(s) for s in m)
+                                                                   for m in msgs])))
+    assert np.array_equal(w.cpu().numpy().view(np.uint64)[:len(words)], words)
+
+
+def test_read_messages_errors_vs_oracle(ctx):
+    """Truncated, corrupted and empty messages, segment counts >= 512, the
+    traversal limit: status, consumed bytes and (for OK messages) the
+    segments must equal the oracle's read_message on each message alone."""
+    rng = random.Random(5)
+    bufs = []
+    for i in range(300):
+        m = [_segment(rng, rng.choice([0, 2, 40, 130])) for _ in range(rng.choice([1, 2, 5]))]
+        st, b = O.write_message(m)
+        b = bytearray(b)
+        r = rng.random()
+        if r < 0.2 and len(b) > 1:
+            b = b[:rng.randrange(len(b))]                     # truncated
+        elif r < 0.35 and len(b) > 2:
+            b[rng.randrange(len(b))] = rng.choice([0, 0xFF, rng.randrange(256)])  # corrupted
+        elif r < 0.4:
+            b = bytearray()                                    # empty
+        bufs.append(bytes(b))
+    # a table claiming 600 segments, and one over the traversal limit
+    bufs.append(bytes([0x0F, 0x57, 0x02, 0x00, 0x00, 0x00]))
+    big = [np.full(100, 1, np.uint64)]
+    bufs.append(O.write_message(big)[1])
+    msg_off = np.concatenate([[0], np.cumsum([len(b) for b in bufs])]).astype(np.int64)
+    allb = b"".join(bufs)
+    for try_mode, limit in ((False, 8 * 1024 * 1024), (True, 8 * 1024 * 1024), (False, 64),
+                            (True, None)):
+        ref = [_oracle_read(b, try_mode, limit) for b in bufs]
+        tw = sum(sum(len(s) for s in r[1]) for r in ref if r[0] == 0) + 1000000
+        w, mwo, sg, mso, st, cons = _read_back(ctx, allb, msg_off, tw, 100000, try_mode, limit)
+        for i, (rst, rsegs, rused) in enumerate(ref):
+            assert st[i] == rst, (i, try_mode, limit, st[i], rst)
+            if rst == 0:
+                assert cons[i] == rused, i
+                lens = sg[mso[i]:mso[i + 1]]
+                assert list(lens) == [len(s) for s in rsegs], i
+                body = w[mwo[i]:mwo[i + 1]]
+                assert np.array_equal(body, np.concatenate(rsegs) if rsegs else body[:0]), i
