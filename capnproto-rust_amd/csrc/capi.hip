@@ -24,7 +24,15 @@
 extern "C" hipError_t capnp_launch_pack(const uint64_t*, const uint64_t*, uint64_t, uint32_t,
                                         uint8_t*, uint64_t, uint64_t*, uint64_t*, uint32_t*,
                                         hipStream_t);
+extern "C" hipError_t capnp_launch_pack_gap(const uint64_t*, const uint64_t*, uint64_t, uint32_t,
+                                            uint8_t*, uint64_t, uint64_t*, uint64_t*,
+                                            const uint32_t*, hipStream_t);
 extern "C" uint32_t capnp_pack_tile_words(void);
+extern "C" hipError_t capnp_launch_msg_gap(const uint64_t*, const uint64_t*, uint64_t, uint64_t,
+                                           uint32_t*, uint32_t*, hipStream_t);
+extern "C" hipError_t capnp_launch_msg_tables(const uint64_t*, const uint64_t*, uint64_t,
+                                              const uint64_t*, uint8_t*, uint64_t, uint64_t*,
+                                              hipStream_t);
 extern "C" hipError_t capnp_msg_scan_bytes(uint64_t, size_t*);
 extern "C" hipError_t capnp_launch_msg_prepare(const uint64_t*, const uint64_t*, const uint64_t*,
                                                uint64_t, uint64_t*, uint64_t*, uint64_t*,
@@ -705,6 +713,37 @@ capnp_status capnp_gpu_write_messages(capnp_ctx* ctx, const uint64_t* d_words,
         return CAPNP_OK;
     }
     if (total_segs < nmsg || (total_words && !d_words)) return CAPNP_E_INVALID_ARGUMENT;
+    // Gap path: the segments are packed in place as the chunks, each
+    // message's first chunk preceded by a gap of its packed table's size, and
+    // the tables are written into the gaps afterwards.  Messages without
+    // segments (or offsets that do not span the batch) take the staging path.
+    {
+        const size_t g_gap = 0;
+        const size_t g_cboff = g_gap + round16(total_segs * 4);
+        const size_t g_flag = g_cboff + round16((total_segs + 1) * 8);
+        capnp_status st = ensure_buf(ctx, &ctx->d_msg, &ctx->msg_cap, g_flag + 64);
+        if (st != CAPNP_OK) return st;
+        uint8_t* d = ctx->d_msg;
+        uint32_t* gap = reinterpret_cast<uint32_t*>(d + g_gap);
+        uint64_t* cboff = reinterpret_cast<uint64_t*>(d + g_cboff);
+        uint32_t* flag = reinterpret_cast<uint32_t*>(d + g_flag);
+        HIP_TRY(capnp_launch_msg_gap(d_seg_word_off, d_msg_seg_off, nmsg, total_segs, gap, flag,
+                                     s));
+        uint32_t h_flag = 1;
+        HIP_TRY(hipMemcpyAsync(&h_flag, flag, 4, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (h_flag == 0) {
+            const uint32_t tc = tile_chunks_for(total_words, total_segs);
+            st = ensure_state(ctx, state_bytes_for(total_segs, tc));
+            if (st != CAPNP_OK) return st;
+            HIP_TRY(capnp_launch_pack_gap(d_words, d_seg_word_off, total_segs, tc, d_out, out_cap,
+                                          cboff, reinterpret_cast<uint64_t*>(ctx->d_state), gap,
+                                          s));
+            HIP_TRY(capnp_launch_msg_tables(d_seg_word_off, d_msg_seg_off, nmsg, cboff, d_out,
+                                            out_cap, d_msg_byte_off, s));
+            return CAPNP_OK;
+        }
+    }
     // bounds: table words <= nmsg + total_segs / 2 + nmsg, chunks <= 2 nmsg + total_segs
     const size_t max_words = total_words + 2 * nmsg + total_segs / 2 + 1;
     const size_t max_chunks = 2 * nmsg + total_segs;

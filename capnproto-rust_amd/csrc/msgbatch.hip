@@ -86,7 +86,131 @@ __global__ void msg_offsets(const uint64_t* __restrict__ cofs,
     if (m <= nmsg) msg_byte_off[m] = chunk_byte_off[cofs[m]];
 }
 
+// ---- gap path: segments packed in place, tables written into the gaps ----
+// Word i of message m's segment table (serialize.rs:211-253): word 0 =
+// (nseg - 1, len 0), then the other lengths as u32 pairs, zero padded.
+__device__ __forceinline__ uint64_t table_word(const uint64_t* __restrict__ seg_off, uint64_t s0,
+                                               uint64_t nseg, uint64_t i) {
+    auto len = [&](uint64_t k) -> uint64_t {
+        return k < nseg ? (uint32_t)(seg_off[s0 + k + 1] - seg_off[s0 + k]) : 0u;
+    };
+    if (i == 0) return (uint64_t)(uint32_t)(nseg - 1) | (len(0) << 32);
+    return len(2 * i - 1) | (len(2 * i) << 32);
+}
+
+// PackedWrite::write_all of table words [i0, i1) (serialize_packed.rs:
+// 304-439, the oracle's pack_into): the bytes go to emit(byte) in order;
+// returns their count.
+template <class Emit>
+__device__ uint32_t pack_table_words(const uint64_t* __restrict__ seg_off, uint64_t s0,
+                                     uint64_t nseg, uint64_t i0, uint64_t i1, Emit emit) {
+    uint32_t n = 0;
+    uint64_t i = i0;
+    while (i < i1) {
+        const uint64_t w = table_word(seg_off, s0, nseg, i++);
+        uint32_t tag = 0;
+        for (int k = 0; k < 8; k++) tag |= (((w >> (8 * k)) & 0xFF) != 0) << k;
+        emit(n++, tag);
+        for (int k = 0; k < 8; k++)
+            if ((w >> (8 * k)) & 0xFF) emit(n++, (uint32_t)(w >> (8 * k)) & 0xFF);
+        if (tag == 0 || tag == 0xFF) {
+            const uint64_t lim = (i1 - i) < 255 ? i1 - i : 255;
+            uint64_t r = 0;
+            while (r < lim) {
+                const uint64_t v = table_word(seg_off, s0, nseg, i + r);
+                if (tag == 0 ? v != 0 : __builtin_popcount(word_tag((uint32_t)v,
+                                                                  (uint32_t)(v >> 32))) < 7)
+                    break;
+                r++;
+            }
+            emit(n++, (uint32_t)r);
+            if (tag == 0xFF)
+                for (uint64_t j = 0; j < r; j++) {
+                    const uint64_t v = table_word(seg_off, s0, nseg, i + j);
+                    for (int k = 0; k < 8; k++) emit(n++, (uint32_t)(v >> (8 * k)) & 0xFF);
+                }
+            i += r;
+        }
+    }
+    return n;
+}
+
+// write_message packs the table as two write_all calls: word 0, then the
+// rest (when nseg > 1; serialize.rs:605-679).
+template <class Emit>
+__device__ uint32_t pack_table(const uint64_t* __restrict__ seg_off, uint64_t s0, uint64_t nseg,
+                               Emit emit) {
+    const uint32_t a = pack_table_words(seg_off, s0, nseg, 0, 1, emit);
+    if (nseg < 2) return a;
+    return a + pack_table_words(seg_off, s0, nseg, 1, 1 + nseg / 2,
+                                [&](uint32_t k, uint32_t b) { emit(a + k, b); });
+}
+
+// One thread per message: the packed table size into gap[first segment]
+// (gap is zeroed beforehand).  flag bit 0: a message without segments, or
+// message segment offsets that do not span [0, total_segs) -> staging path.
+__global__ void msg_gap(const uint64_t* __restrict__ seg_off,
+                        const uint64_t* __restrict__ msg_seg_off, uint64_t nmsg,
+                        uint64_t total_segs, uint32_t* __restrict__ gap,
+                        uint32_t* __restrict__ flag) {
+    const uint64_t m = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (m >= nmsg) return;
+    const uint64_t s0 = msg_seg_off[m], s1 = msg_seg_off[m + 1];
+    bool bad = s1 <= s0 || s1 > total_segs;
+    if (m == 0) bad |= s0 != 0;
+    if (m + 1 == nmsg) bad |= s1 != total_segs;
+    if (bad) {
+        atomicOr(flag, 1u);
+        return;
+    }
+    gap[s0] = pack_table(seg_off, s0, s1 - s0, [](uint32_t, uint32_t) {});
+}
+
+// After the gap pack: the table bytes into each message's gap and the
+// message byte offsets (the gap starts).
+__global__ void msg_tables(const uint64_t* __restrict__ seg_off,
+                           const uint64_t* __restrict__ msg_seg_off, uint64_t nmsg,
+                           const uint64_t* __restrict__ chunk_byte_off, uint8_t* __restrict__ out,
+                           uint64_t out_cap, uint64_t* __restrict__ msg_byte_off) {
+    const uint64_t m = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (m > nmsg) return;
+    const uint64_t s0 = msg_seg_off[m];
+    const uint64_t p = chunk_byte_off[s0];
+    msg_byte_off[m] = p;
+    if (m == nmsg) return;
+    const uint64_t nseg = msg_seg_off[m + 1] - s0;
+    const uint32_t g = pack_table(seg_off, s0, nseg, [](uint32_t, uint32_t) {});
+    if (p + g > out_cap) return;  // the caller sees the size and reports it
+    uint8_t* dst = out + p;
+    pack_table(seg_off, s0, nseg, [&](uint32_t k, uint32_t b) { dst[k] = (uint8_t)b; });
+}
+
 }  // namespace
+
+extern "C" hipError_t capnp_launch_msg_gap(const uint64_t* d_seg_off,
+                                           const uint64_t* d_msg_seg_off, uint64_t nmsg,
+                                           uint64_t total_segs, uint32_t* d_gap,
+                                           uint32_t* d_flag, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(d_gap, 0, total_segs * 4, s);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(d_flag, 0, 4, s);
+    if (e != hipSuccess) return e;
+    const uint32_t g = (uint32_t)((nmsg + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(msg_gap, dim3(g), dim3(kThreads), 0, s, d_seg_off, d_msg_seg_off, nmsg,
+                       total_segs, d_gap, d_flag);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t capnp_launch_msg_tables(const uint64_t* d_seg_off,
+                                              const uint64_t* d_msg_seg_off, uint64_t nmsg,
+                                              const uint64_t* d_chunk_byte_off, uint8_t* d_out,
+                                              uint64_t out_cap, uint64_t* d_msg_byte_off,
+                                              hipStream_t s) {
+    const uint32_t g = (uint32_t)((nmsg + 1 + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(msg_tables, dim3(g), dim3(kThreads), 0, s, d_seg_off, d_msg_seg_off, nmsg,
+                       d_chunk_byte_off, d_out, out_cap, d_msg_byte_off);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t capnp_msg_scan_bytes(uint64_t n, size_t* bytes) {
     *bytes = 0;

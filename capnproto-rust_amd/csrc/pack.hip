@@ -88,8 +88,11 @@ constexpr uint32_t kStageWords = 64 * kStageSteps;
 // head of 10 bytes needs a word of <= 7 bytes before the next one) plus 1.5
 // per chunk, and a range holds at most kStageSteps non-empty chunks
 constexpr uint32_t kStageBytes = 8 * kStageWords + kStageWords / 2 + 2 * kStageSteps;
+// Leading gaps (capnp_launch_pack_gap): a wave's range stays staged while
+// its gaps total at most kGapSlack bytes.
+constexpr uint32_t kGapSlack = 128;
 // plus the 32 bytes copy_out may read past the end
-constexpr uint32_t kRegion = (kStageBytes + 32 + 15) & ~15u;
+constexpr uint32_t kRegion = (kStageBytes + kGapSlack + 32 + 15) & ~15u;
 // per-wave LDS region: the staged bytes, or the streaming path's flush ring
 constexpr uint32_t kRegionBytes = kRegion > kRing ? kRegion : kRing;
 
@@ -156,6 +159,7 @@ struct Smem {
     uint64_t wave_bytes[kWaves];
     uint64_t wave_steps[kWaves];
     uint32_t chunk_oc[kMaxTileChunks];  // staged path: chunk start in its wave's region
+    uint32_t chunk_gap[kMaxTileChunks];  // leading gap bytes of each chunk (GAP kernels)
     // per-wave staging region; the streaming path uses its first 4 KiB as
     // the flush ring.  emit_step ORs a zero into the dword before a record
     // that starts 4-aligned, hence the pad.
@@ -590,16 +594,21 @@ template <int MODE>
 __device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* off,
                               uint64_t* chunk_size, const uint64_t* chunk_pos, uint32_t nc,
                               uint32_t wave, uint32_t lane, uint8_t* ring, const SelEntry* sel,
-                              uint8_t* out, uint32_t mis, uint64_t out_cap) {
+                              uint8_t* out, uint32_t mis, uint64_t out_cap,
+                              const uint32_t* cgap) {
     Packer pk;
     for (uint32_t ci = wave; ci < nc; ci += kWaves) {
         const uint64_t woff = uniform64(off[ci]);
         const uint64_t len = uniform64(off[ci + 1]) - woff;
-        if (len == 0) continue;
+        const uint32_t g = cgap ? uniform(cgap[ci]) : 0u;  // leading gap bytes
+        if (len == 0) {
+            if (MODE == MODE_SIZE && lane == 0) chunk_size[ci] = g;
+            continue;
+        }
         if (MODE == MODE_RING) {
             const uint64_t pos = lds_u64(&chunk_pos[ci]);
             if (pos + lds_u64(&chunk_size[ci]) > out_cap) continue;  // does not fit
-            pk.begin(pos + mis);
+            pk.begin(pos + g + mis);
         } else {
             pk.begin(0);
         }
@@ -613,7 +622,7 @@ __device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* o
             pk.step<MODE>(w, nvalid, last, lane, ring, out, sel);
             if (last) break;
         }
-        if (MODE == MODE_SIZE && lane == 0) chunk_size[ci] = pk.total;
+        if (MODE == MODE_SIZE && lane == 0) chunk_size[ci] = pk.total + g;
     }
 }
 
@@ -621,7 +630,8 @@ __device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* o
 // fallback below; normally never executed).
 __device__ uint64_t tile_aggregate(const uint64_t* __restrict__ in,
                                    const uint64_t* __restrict__ chunk_off, uint64_t nchunks,
-                                   uint32_t tc, uint64_t j, uint32_t lane) {
+                                   uint32_t tc, const uint32_t* __restrict__ gap, uint64_t j,
+                                   uint32_t lane) {
     const uint64_t c0 = j * tc;
     const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
     uint64_t total = 0;
@@ -635,7 +645,7 @@ __device__ uint64_t tile_aggregate(const uint64_t* __restrict__ in,
             const uint64_t w = lane < nvalid ? in[woff + base + lane] : 0;
             pk.step<MODE_SIZE>(w, nvalid, base + 64 >= len, lane, nullptr, nullptr, nullptr);
         }
-        total += pk.total;
+        total += pk.total + (gap ? gap[ci] : 0u);
     }
     return total;
 }
@@ -671,14 +681,15 @@ constexpr uint32_t kSpinLimit = 4096;
 
 __device__ uint64_t group_aggregate(uint64_t* __restrict__ ts, const uint64_t* __restrict__ in,
                                     const uint64_t* __restrict__ chunk_off, uint64_t nchunks,
-                                    uint32_t tc, uint64_t ntiles, uint64_t g, uint32_t lane) {
+                                    uint32_t tc, const uint32_t* __restrict__ gap,
+                                    uint64_t ntiles, uint64_t g, uint32_t lane) {
     const uint64_t t0 = g * kGroup;
     const uint64_t tn = (t0 + kGroup < ntiles) ? kGroup : ntiles - t0;
     uint64_t st = lane < tn ? poll_agent(&ts[t0 + lane]) : kFlagAgg;
     uint64_t miss = ballot64((st >> 62) == 0);
     while (miss) {
         const uint32_t k = ctz64(miss);
-        const uint64_t a = tile_aggregate(in, chunk_off, nchunks, tc, t0 + k, lane);
+        const uint64_t a = tile_aggregate(in, chunk_off, nchunks, tc, gap, t0 + k, lane);
         if (lane == 0) publish_agent(&ts[t0 + k], kFlagAgg | a);
         if (lane == k) st = kFlagAgg | a;
         miss &= miss - 1;
@@ -696,6 +707,7 @@ struct LookbackArgs {
     const uint64_t* chunk_off;
     uint64_t nchunks;
     uint32_t tc;
+    const uint32_t* gap;
 };
 
 // Wave 0: publishes tile t's aggregate.
@@ -729,7 +741,7 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
         if (++spins >= kSpinLimit) {
             if (lane == 0) PROF_ADD(2, 1);
             const uint64_t j = g * kGroup + ctz64(miss);
-            const uint64_t a = tile_aggregate(A.in, A.chunk_off, A.nchunks, A.tc, j, lane);
+            const uint64_t a = tile_aggregate(A.in, A.chunk_off, A.nchunks, A.tc, A.gap, j, lane);
             if (lane == 0) publish_agent(&A.ts[j], kFlagAgg | a);
         } else {
             __builtin_amdgcn_s_sleep(PACK_SLEEP);
@@ -764,7 +776,7 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
 #endif
             if (++spins >= kSpinLimit) {
                 const uint64_t jg = (uint64_t)(idx - (int64_t)ctz64(missing));
-                const uint64_t a = group_aggregate(A.ts, A.in, A.chunk_off, A.nchunks, A.tc,
+                const uint64_t a = group_aggregate(A.ts, A.in, A.chunk_off, A.nchunks, A.tc, A.gap,
                                                    A.ntiles, jg, lane);
                 if (lane == 0) publish_agent(&A.gs[jg], kFlagAgg | a);
             } else {
@@ -818,12 +830,17 @@ __device__ __forceinline__ uint64_t scan_chunks(Smem& sm, uint32_t nc, uint32_t 
 #define PACK_MIN_WAVES 6  // per SIMD: 7 (the LDS limit) spills VGPRs to scratch
 #endif
 
-template <bool SYNC>
+// GAP: chunk c is preceded by gap[c] bytes of the output that the kernel
+// leaves zero (out_off[c] is the gap's start; capnp_gpu_write_messages puts
+// each message's segment table there).
+template <bool SYNC, bool GAP>
 __global__ void __launch_bounds__(kThreads, PACK_MIN_WAVES)
 pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
             uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
             uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts,
-            uint64_t* __restrict__ gs, uint32_t* __restrict__ sync) {
+            uint64_t* __restrict__ gs, uint32_t* __restrict__ sync,
+            const uint32_t* __restrict__ gap) {
+    static_assert(!(SYNC && GAP), "the sync index is not written with gaps");
     __shared__ Smem sm;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -838,6 +855,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     LA.chunk_off = chunk_off;
     LA.nchunks = nchunks;
     LA.tc = tc;
+    LA.gap = GAP ? gap : nullptr;
 
     const uint64_t c0 = tile * tc;
     const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
@@ -858,6 +876,8 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     const uint64_t k1 = (uniform64(chunk_off[c1]) + kSyncWords - 1) / kSyncWords;
     const uint32_t t0 = (uint32_t)(k0 * kSyncWords - TW0);  // first sync word, tile-relative
     for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
+    if constexpr (GAP)
+        for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_gap[i] = gap[c0 + i];
     // record assembly table: one 16-byte entry per thread (+ the copy entry)
     for (uint32_t i = tid; i <= kSelCopy; i += kThreads)
         reinterpret_cast<uint4*>(sm.sel)[i] = reinterpret_cast<const uint4*>(kSelTable.e)[i];
@@ -876,10 +896,15 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     uint32_t d_g = 0;  // tile-relative word of the step's lane 0
     uint32_t d_meta = 0;
     uint32_t nsteps = 0;
+    uint32_t gsum = 0;  // GAP: the range's gap bytes; an empty chunk with a gap streams
     for (uint32_t ci = wc0; ci < wc1; ci++) {
         const uint64_t woff = uniform64(toff[ci]);
         const uint64_t len = uniform64(toff[ci + 1]) - woff;
         const uint32_t nst = (uint32_t)((len + 63) / 64);
+        if constexpr (GAP) {
+            const uint32_t g = uniform(sm.chunk_gap[ci]);
+            gsum += (len == 0 && g) ? kGapSlack + 1 : g;
+        }
         const uint32_t k = lane - nsteps;
         if (lane >= nsteps && k < nst) {
             const uint64_t rest = len - 64ull * k;
@@ -890,7 +915,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         }
         nsteps += nst;
     }
-    if (lane == 0) sm.wave_steps[wave] = nsteps;
+    if (lane == 0) sm.wave_steps[wave] = (GAP && gsum > kGapSlack) ? kStageSteps + 1 : nsteps;
     __syncthreads();
     bool staged = true;
 #pragma unroll
@@ -929,6 +954,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                 const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
                 si[s].meta = meta;
                 if ((meta >> 7) & 1) {
+                    if constexpr (GAP) local += uniform(sm.chunk_gap[wc0 + (meta >> 9)]);
                     pk.begin(local);
                     if (lane == 0) sm.chunk_oc[wc0 + (meta >> 9)] = (uint32_t)local;
                 }
@@ -942,7 +968,9 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                 size_step(pk, cache[s], meta & 127u, lane, si[s]);
 #endif
                 if ((meta >> 8) & 1) {
-                    if (lane == 0) sm.chunk_size[wc0 + (meta >> 9)] = pk.total;
+                    if (lane == 0)
+                        sm.chunk_size[wc0 + (meta >> 9)] =
+                            pk.total + (GAP ? uniform(sm.chunk_gap[wc0 + (meta >> 9)]) : 0u);
                     local += pk.total;
                 }
             }
@@ -998,7 +1026,8 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         if constexpr (SYNC)
             for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
         run_streaming<MODE_SIZE>(in, toff, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
-                                 region, sm.sel, outa, mis, out_cap);
+                                 region, sm.sel, outa, mis, out_cap,
+                                 GAP ? sm.chunk_gap : nullptr);
         __syncthreads();
         if (wave == 0) {
             const uint64_t agg = scan_chunks(sm, nc, lane);
@@ -1013,7 +1042,8 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         return;
 #endif
         run_streaming<MODE_RING>(in, toff, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
-                                 region, sm.sel, outa, mis, out_cap);
+                                 region, sm.sel, outa, mis, out_cap,
+                                 GAP ? sm.chunk_gap : nullptr);
     }
 }
 
@@ -1044,13 +1074,32 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_
     hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(nchunks, tc), stream);
     if (e != hipSuccess) return e;
     if (d_sync)
-        hipLaunchKernelGGL(pack_kernel<true>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
-                           d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_state,
-                           d_state + ntiles, d_sync);
+        hipLaunchKernelGGL((pack_kernel<true, false>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
+                           stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
+                           d_state, d_state + ntiles, d_sync, nullptr);
     else
-        hipLaunchKernelGGL(pack_kernel<false>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
-                           d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_state,
-                           d_state + ntiles, d_sync);
+        hipLaunchKernelGGL((pack_kernel<false, false>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
+                           stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
+                           d_state, d_state + ntiles, d_sync, nullptr);
+    return hipGetLastError();
+}
+
+// Pack with a leading gap of d_gap[c] bytes before every chunk c: out_off[c]
+// is the gap's start, the chunk's bytes follow the gap, the gap bytes are
+// written as zeros.
+extern "C" hipError_t capnp_launch_pack_gap(const uint64_t* d_in, const uint64_t* d_chunk_off,
+                                            uint64_t nchunks, uint32_t tc, uint8_t* d_out,
+                                            uint64_t out_cap, uint64_t* d_out_off,
+                                            uint64_t* d_state, const uint32_t* d_gap,
+                                            hipStream_t stream) {
+    if (tc == 0 || tc > kMaxTileChunks || !d_gap) return hipErrorInvalidValue;
+    const uint64_t ntiles = (nchunks + tc - 1) / tc;
+    if (nchunks == 0) return hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), stream);
+    hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(nchunks, tc), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((pack_kernel<false, true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
+                       stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_state,
+                       d_state + ntiles, nullptr, d_gap);
     return hipGetLastError();
 }
 

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Throughput of capnp_gpu_write_messages on config-2-shaped batches (1 Mi
+"""Throughput of capnp_gpu_write_messages / capnp_gpu_read_messages on config-2-shaped batches (1 Mi
 single-segment 1 KiB messages), next to the plain chunk batch pack of the
 same words (diagnostic).
 
@@ -31,8 +31,13 @@ def main():
     ctx.gen_batch(words, seg_off, pz_thresh=1288490189)
     msg_off = torch.arange(0, (nm + 1) * sp, sp, dtype=torch.int64, device="cuda")
     U = words.numel() * 8
+    packed, mo = ctx.write_messages(words, seg_off, msg_off)
+    pk, po = ctx.pack_batch(words, seg_off)
+    torch.cuda.synchronize()
     for name, fn in (("write_messages", lambda: ctx.write_messages(words, seg_off, msg_off)),
-                     ("pack_batch (chunks only)", lambda: ctx.pack_batch(words, seg_off))):
+                     ("pack_batch (chunks only)", lambda: ctx.pack_batch(words, seg_off)),
+                     ("read_messages", lambda: ctx.read_messages(packed, mo, words.numel(), nseg)),
+                     ("unpack_batch (chunks only)", lambda: ctx.unpack_batch(pk, po, seg_off))):
         fn()
         torch.cuda.synchronize()
         ts = []
@@ -41,6 +46,10 @@ def main():
             fn()
             torch.cuda.synchronize()
             ts.append(time.perf_counter() - t0)
+        if name == "read_messages":
+            r = fn()
+            torch.cuda.synchronize()
+            assert int((r[4] != 0).sum()) == 0 and torch.equal(r[0][:words.numel()], words)
         print(f"{name}: {min(ts) * 1e3:.3f} ms, {U / min(ts) / GiB:.1f} GiB/s of segment words",
               flush=True)
 

@@ -104,6 +104,29 @@ def test_write_messages_carsales_like_batch(ctx):
     _check_messages(ctx, msgs)
 
 
+def test_write_messages_staging_path(ctx):
+    """Message offsets that do not span the batch (a segment before the first
+    message and one after the last) take the staging path; the messages must
+    still match the oracle byte for byte."""
+    rng = random.Random(13)
+    msgs = [[_segment(rng, rng.choice([0, 3, 64, 200])) for _ in range(rng.choice([1, 2, 3]))]
+            for _ in range(50)]
+    segs = [_segment(rng, 7)] + [s for m in msgs for s in m] + [_segment(rng, 9)]
+    seg_off = np.concatenate([[0], np.cumsum([len(x) for x in segs])]).astype(np.int64)
+    msg_seg_off = (1 + np.concatenate([[0], np.cumsum([len(m) for m in msgs])])).astype(np.int64)
+    words = np.concatenate(segs)
+    packed, mo = ctx.write_messages(torch.from_numpy(words.view(np.int64).copy()).cuda(),
+                                    torch.from_numpy(seg_off).cuda(),
+                                    torch.from_numpy(msg_seg_off).cuda())
+    got = packed.cpu().numpy().tobytes()
+    mo = mo.cpu().numpy()
+    base = mo[0]
+    for i, m in enumerate(msgs):
+        ref = O.write_message(m)[1]
+        assert got[mo[i]:mo[i + 1]] == ref, i
+    assert mo[-1] - base == sum(len(O.write_message(m)[1]) for m in msgs)
+
+
 # ------------------------------------------------------------ batch read side
 def _read_back(ctx, packed_bytes, msg_off, words_cap, segs_cap, try_mode=False,
                limit=8 * 1024 * 1024):
