@@ -213,9 +213,12 @@ capnp_status capnp_stream_unpack_batch(capnp_ctx* ctx, const uint8_t* packed,
    the last is the total): each is exactly the byte stream write_message
    produces (the segment table's word 0, the rest of the table, then every
    segment, each packed by its own write_all).  total_segs and total_words
-   are the batch's segment count and segment words (host-side sizes for the
-   staging).  Synchronises the stream once (to size the pack); out_cap as in
-   capnp_gpu_pack_batch. */
+   are the batch's segment count and segment words (host-side sizes).  The
+   segments are packed in place with a gap before each message's first
+   segment that then receives the packed table; a batch whose message offsets
+   do not span [0, total_segs) goes through a staging copy instead.
+   Synchronises the stream once (to choose the path, or to size the staging
+   pack); out_cap as in capnp_gpu_pack_batch. */
 capnp_status capnp_gpu_write_messages(capnp_ctx* ctx, const uint64_t* d_words,
                                       const uint64_t* d_seg_word_off,
                                       const uint64_t* d_msg_seg_off, size_t nmsg,
