@@ -32,7 +32,8 @@ EXPORTS = [
     "capnp_gpu_unpack_batch_sync", "capnp_gpu_pack_batch_sync_tuned",
     "capnp_gpu_unpack_batch_sync_tuned", "capnp_unpack_sync_tile_words",
     "capnp_stream_pack_batch", "capnp_stream_unpack_batch", "capnp_gpu_write_messages",
-    "capnp_gpu_read_messages",
+    "capnp_gpu_read_messages", "capnp_gpu_unpack_batch_resync", "capnp_resync_stats",
+    "capnp_resync_block_bytes",
 ]
 
 
@@ -93,6 +94,10 @@ def lib():
     L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, u32, vp]
     L.capnp_gpu_unpack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, u32, vp]
     L.capnp_ctx_reserve.argtypes = [vp, sz]
+    L.capnp_gpu_unpack_batch_resync.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
+    L.capnp_resync_stats.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+    L.capnp_resync_block_bytes.argtypes = []
+    L.capnp_resync_block_bytes.restype = u32
     L.capnp_pack_tile_words.argtypes = []
     L.capnp_pack_tile_words.restype = C.c_uint32
     L.capnp_unpack_tile_words.argtypes = []

@@ -122,6 +122,22 @@ class Context:
                 self._stream(stream))
         _check(st, self._h)
 
+    def unpack_batch_resync_into(self, packed, in_byte_off, out_word_off, words, status,
+                                 consumed=None, stream=None):
+        """Index-free UNPACK of chunks of any length (capnp_gpu_unpack_batch_resync):
+        results identical to unpack_batch_into; blocks until done.  Returns
+        (fix passes, 1 if the batch went to the serial batch unpack)."""
+        import ctypes as C
+        n = in_byte_off.numel() - 1
+        L = _lib.lib()
+        st = L.capnp_gpu_unpack_batch_resync(
+            self._h, _ptr(packed), _ptr(in_byte_off), n, _ptr(words), _ptr(out_word_off),
+            _ptr(status), _ptr(consumed), self._stream(stream))
+        _check(st, self._h)
+        passes, serial = C.c_int(0), C.c_int(0)
+        _check(L.capnp_resync_stats(self._h, C.byref(passes), C.byref(serial)), self._h)
+        return passes.value, serial.value
+
     def pack_batch(self, words, chunk_word_off, chunks_per_tile=0):
         """Returns (packed uint8 tensor trimmed to size, out_byte_off int64).
         Synchronises the stream once to read the total size."""

@@ -57,6 +57,12 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t*, const uint64_t*, uint6
                                           const uint32_t*, hipStream_t);
 extern "C" hipError_t capnp_launch_gen(uint64_t*, const uint64_t*, uint64_t, uint64_t,
                                        const uint8_t*, uint32_t, uint32_t, hipStream_t);
+extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes);
+extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d_in_off, uint64_t n,
+                                          uint64_t total_bytes, uint64_t* d_out,
+                                          const uint64_t* d_out_off, int32_t* d_status,
+                                          uint64_t* d_consumed, void* d_ws, size_t ws_bytes,
+                                          hipStream_t s, int* passes, int* serial);
 extern "C" hipError_t capnp_launch_frame(const uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t,
                                          uint32_t, uint64_t, FrameResult*, hipStream_t);
 
@@ -90,6 +96,9 @@ struct capnp_ctx {
     size_t h_slot_off_cap = 0;
     uint8_t* d_msg = nullptr;  // batch message framing: staging words and tables
     size_t msg_cap = 0;
+    uint8_t* d_resync = nullptr;  // index-free decode: per-block chain state
+    size_t resync_cap = 0;
+    int resync_passes = 0, resync_serial = 0;  // last capnp_gpu_unpack_batch_resync
     std::string err;
 };
 
@@ -329,6 +338,7 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (ctx->d_frame) hipFree(ctx->d_frame);
     if (ctx->h_frame) hipHostFree(ctx->h_frame);
     if (ctx->d_msg) hipFree(ctx->d_msg);
+    if (ctx->d_resync) hipFree(ctx->d_resync);
     for (int k = 0; k < 3; k++)
         if (ctx->sstream[k]) {
             hipStreamSynchronize(ctx->sstream[k]);
@@ -446,6 +456,37 @@ capnp_status capnp_gpu_unpack_batch_sync_tuned(capnp_ctx* ctx, const uint8_t* d_
     if (!d_sync) return CAPNP_E_INVALID_ARGUMENT;
     return unpack_batch_dev(ctx, d_packed, d_in_byte_off, nchunks, d_words, d_out_word_off,
                             d_status, d_consumed, chunks_per_tile, stream, d_sync);
+}
+
+capnp_status capnp_gpu_unpack_batch_resync(capnp_ctx* ctx, const uint8_t* d_packed,
+                                           const uint64_t* d_in_byte_off, size_t nchunks,
+                                           uint64_t* d_words, const uint64_t* d_out_word_off,
+                                           int32_t* d_status, uint64_t* d_consumed,
+                                           void* stream) {
+    if (!ctx || (nchunks && (!d_in_byte_off || !d_out_word_off || !d_status)))
+        return CAPNP_E_INVALID_ARGUMENT;
+    ctx->resync_passes = ctx->resync_serial = 0;
+    if (nchunks == 0) return CAPNP_OK;
+    hipStream_t s = pick(ctx, stream);
+    uint64_t ends[2];
+    HIP_TRY(hipMemcpyAsync(&ends[0], d_in_byte_off, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(&ends[1], d_in_byte_off + nchunks, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (ends[1] < ends[0]) return CAPNP_E_INVALID_ARGUMENT;
+    const size_t ws = capnp_resync_ws_bytes(nchunks, ends[1] - ends[0]);
+    capnp_status st = ensure_buf(ctx, &ctx->d_resync, &ctx->resync_cap, ws);
+    if (st != CAPNP_OK) return st;
+    HIP_TRY(capnp_resync_unpack(d_packed, d_in_byte_off, nchunks, ends[1] - ends[0], d_words,
+                                d_out_word_off, d_status, d_consumed, ctx->d_resync,
+                                ctx->resync_cap, s, &ctx->resync_passes, &ctx->resync_serial));
+    return CAPNP_OK;
+}
+
+capnp_status capnp_resync_stats(capnp_ctx* ctx, int* passes, int* serial) {
+    if (!ctx) return CAPNP_E_INVALID_ARGUMENT;
+    if (passes) *passes = ctx->resync_passes;
+    if (serial) *serial = ctx->resync_serial;
+    return CAPNP_OK;
 }
 
 capnp_status capnp_gpu_gen_batch(capnp_ctx* ctx, uint64_t* d_words, const uint64_t* d_offs,

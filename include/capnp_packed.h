@@ -160,6 +160,24 @@ capnp_status capnp_gpu_unpack_batch_sync(capnp_ctx* ctx, const uint8_t* d_packed
                                          const uint32_t* d_sync, int32_t* d_status,
                                          uint64_t* d_consumed, void* stream);
 
+/* ---- index-free decode of long read units ---------- */
+/* The same transform, statuses and consumed counts as capnp_gpu_unpack_batch
+   (PackedRead::read under read_exact, serialize_packed.rs:76-229, io.rs:16-31)
+   for batches that carry no record sync index and whose chunks may be of any
+   length (a foreign stream: a 64 KiB segment, or a whole message body read
+   as one unit by read_message, serialize.rs:514-524).  Each chunk's packed
+   bytes are split into fixed blocks decoded in parallel: a block's tag chain
+   is walked speculatively from its first byte and resynchronised against
+   its predecessor's exit (csrc/resync.hip).  A chunk whose chain does not
+   end exactly at its packed end with exactly its word count makes the call
+   re-decode the whole batch with capnp_gpu_unpack_batch, so every result is
+   that function's.  Blocking: synchronises `stream` (typically twice). */
+capnp_status capnp_gpu_unpack_batch_resync(capnp_ctx* ctx, const uint8_t* d_packed,
+                                           const uint64_t* d_in_byte_off, size_t nchunks,
+                                           uint64_t* d_words, const uint64_t* d_out_word_off,
+                                           int32_t* d_status, uint64_t* d_consumed,
+                                           void* stream);
+
 /* ---- host single-unit API (blocking; runs the same kernels) ------------ */
 /* PackedWrite::write_all of one chunk (serialize_packed.rs:304-439) into a
    caller buffer; *written = packed length.  len must be a multiple of 8. */

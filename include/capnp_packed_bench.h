@@ -65,6 +65,13 @@ uint32_t capnp_unpack_tile_words(void);
  * words); chunks_per_tile ~ this / mean chunk words. */
 uint32_t capnp_pack_tile_words(void);
 
+/* Diagnostics of the last capnp_gpu_unpack_batch_resync on ctx: fix passes
+ * run, and 1 if the batch went to the serial batch unpack. */
+capnp_status capnp_resync_stats(capnp_ctx* ctx, int* passes, int* serial);
+
+/* Packed bytes per lane of the index-free decode. */
+uint32_t capnp_resync_block_bytes(void);
+
 /* Pre-sizes the context workspace for batches of up to max_chunks chunks so
  * that later calls allocate nothing (required before HIP graph capture). */
 capnp_status capnp_ctx_reserve(capnp_ctx* ctx, size_t max_chunks);
