@@ -34,8 +34,10 @@
 //   check  lane per chunk: the chain must end exactly at the chunk's packed
 //          end with exactly the chunk's word count (then no record ran short,
 //          and no run overran the output: the word count is monotone).
-//   expand lane per block walks its records from its true entry and writes
-//          the words.
+//   decode each resolved block is a read unit of its own (its records run
+//          from its entry to its exit): the blocks go to the batch unpack
+//          kernel as a batch of ~120-word units (staged LDS tiles, coalesced
+//          stores).
 //
 // Any chunk that fails the check (a malformed stream, or a valid unit
 // followed by spare bytes in its range) makes the call re-decode the batch
@@ -63,6 +65,8 @@ constexpr uint32_t kThreads = 256;
 constexpr uint64_t kGroup = 8;  // blocks per fix lane
 constexpr int kMaxPasses = 512;  // fix passes before giving up to the serial path
 constexpr int kPassBatch = 8;    // fix passes enqueued per flag read-back
+constexpr uint64_t kShortChunk = 2 * kBlock;  // mean packed bytes per chunk below which
+                                              // the batch goes straight to the batch unpack
 
 // One record hop from p (< b, the chunk's packed end): p moves past the
 // record, w counts its words.  A record cut short by the chunk end leaves p
@@ -229,55 +233,29 @@ k_check(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __restr
     }
 }
 
-__device__ __forceinline__ uint64_t load_bytes(const uint8_t* __restrict__ base, uint64_t pos,
-                                               uint32_t len) {
-    const uint64_t a = pos & ~7ull;
-    const uint32_t s = (uint32_t)(pos & 7);
-    const uint64_t* q = reinterpret_cast<const uint64_t*>(base + a);
-    uint64_t v = q[0] >> (8 * s);
-    if (s + len > 8) v |= q[1] << (64 - 8 * s);
-    return v;
-}
-
-__device__ __forceinline__ uint64_t expand_word(uint32_t tag, uint64_t packed) {
-    const uint64_t sel = expand_selector(tag);
-    const uint32_t lo = (uint32_t)packed, hi = (uint32_t)(packed >> 32);
-    const uint32_t rlo = __builtin_amdgcn_perm(hi, lo, (uint32_t)sel);
-    const uint32_t rhi = __builtin_amdgcn_perm(hi, lo, (uint32_t)(sel >> 32));
-    return ((uint64_t)rhi << 32) | rlo;
-}
-
+// Each block, resolved, is a read unit of its own: the records that start in
+// it run from its entry to its exit and decode to exactly its word count.
+// Lane k writes block k's packed start and first output word, so the blocks
+// tile the batch's packed bytes and words contiguously (a block inside a
+// literal run is an empty unit; a chunk of 0 words keeps its blocks empty,
+// since read() of an empty buffer consumes nothing).
 __global__ void __launch_bounds__(kThreads)
-k_expand(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
-         const uint64_t* __restrict__ out_off, const uint64_t* __restrict__ bstart,
-         const uint64_t* __restrict__ exit, const uint64_t* __restrict__ wbase,
-         const int32_t* __restrict__ ok, uint64_t* __restrict__ out) {
+k_blocks(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __restrict__ out_off,
+         const uint64_t* __restrict__ bstart, const uint64_t* __restrict__ exit,
+         const uint64_t* __restrict__ wbase, uint64_t* __restrict__ blk_in,
+         uint64_t* __restrict__ blk_out) {
     const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (k >= bstart[n]) return;
-    const uint64_t c = chunk_of(bstart, n, k);
-    if (!ok[c]) return;
-    const uint64_t a = in_off[c], b = in_off[c + 1];
-    const uint64_t f = bstart[c];
-    const uint64_t s = a + (k - f) * kBlock;
-    const uint64_t end = s + kBlock < b ? s + kBlock : b;
-    uint64_t p = k == f ? a : exit[k - 1];
-    uint64_t* o = out + out_off[c] + (wbase[k] - wbase[f]);
-    while (p < end) {
-        const uint32_t tag = in[p];
-        const uint32_t pop = __builtin_popcount(tag);
-        *o++ = pop ? expand_word(tag, load_bytes(in, p + 1, pop)) : 0ull;
-        p += 1 + pop;
-        if (tag == 0u) {
-            const uint32_t r = in[p];
-            p += 1;
-            for (uint32_t i = 0; i < r; i++) *o++ = 0ull;
-        } else if (tag == 0xFFu) {
-            const uint32_t r = in[p];
-            p += 1;
-            for (uint32_t i = 0; i < r; i++) *o++ = load_bytes(in, p + 8ull * i, 8);
-            p += 8ull * r;
-        }
+    const uint64_t nb = bstart[n];
+    if (k > nb) return;
+    if (k == nb) {
+        blk_in[k] = in_off[n];
+        blk_out[k] = out_off[n];
+        return;
     }
+    const uint64_t c = chunk_of(bstart, n, k);
+    const uint64_t f = bstart[c];
+    blk_in[k] = k == f ? in_off[c] : exit[k - 1];
+    blk_out[k] = out_off[c] + (out_off[c + 1] == out_off[c] ? 0 : wbase[k] - wbase[f]);
 }
 
 size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes) {
@@ -326,7 +304,9 @@ extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes) {
 }
 
 // Blocking (the fix passes read a flag back).  On return, *passes = fix passes
-// run and *serial = 1 if the batch was re-decoded by the serial batch unpack.
+// run and *serial = 1 if the batch was re-decoded by the serial batch unpack
+// (a chunk failed its check), 2 if its chunks were short enough to go there
+// directly.
 extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d_in_off, uint64_t n,
                                           uint64_t total_bytes, uint64_t* d_out,
                                           const uint64_t* d_out_off, int32_t* d_status,
@@ -335,13 +315,22 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
     if (passes) *passes = 0;
     if (serial) *serial = 0;
     if (n == 0) return hipSuccess;
+    hipError_t e;
+    if (total_bytes < n * kShortChunk) {
+        // chunks this short are parallel enough as they are: the batch unpack
+        // (one walker per chunk) is faster than resolving blocks
+        if (serial) *serial = 2;
+        if ((e = capnp_launch_unpack(d_in, d_in_off, n, 0, d_out, d_out_off, d_status, d_consumed,
+                                     nullptr, s)) != hipSuccess)
+            return e;
+        return hipStreamSynchronize(s);
+    }
     const uint64_t nbb = blocks_bound(n, total_bytes);
     const uint64_t m = nbb > n + 1 ? nbb : n + 1;
     Ws w;
     uint8_t* base = (uint8_t*)(((uintptr_t)d_ws + 255) & ~uintptr_t(255));
     if (carve(&w, base, n, nbb, scan_tmp_bytes(m)) + (base - (uint8_t*)d_ws) > ws_bytes)
         return hipErrorInvalidValue;
-    hipError_t e;
     int32_t hflags[2] = {0, 0};
     if ((e = hipMemsetAsync(w.flags, 0, 4 * (2 + kMaxPasses), s)) != hipSuccess) return e;
     k_count<<<grid(n + 1), kThreads, 0, s>>>(d_in_off, n, w.nblk);
@@ -380,11 +369,24 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
             return e;
         k_check<<<grid(n), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit, w.words,
                                              w.wbase, w.ok, d_status, d_consumed, w.flags);
-        k_expand<<<grid(nbb), kThreads, 0, s>>>(d_in, d_in_off, n, d_out_off, w.bstart, w.exit,
-                                                w.wbase, w.ok, d_out);
+        uint64_t nb = 0;
         if ((e = hipMemcpyAsync(hflags, w.flags, 8, hipMemcpyDeviceToHost, s)) != hipSuccess)
             return e;
+        if ((e = hipMemcpyAsync(&nb, w.bstart + n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess)
+            return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (!hflags[1]) {
+            // every chunk resolved: decode the blocks as independent read
+            // units with the batch unpack (staged LDS tiles, coalesced stores)
+            uint64_t* blk_in = w.spec_exit;  // (spec state is dead by now)
+            uint64_t* blk_out = w.entry;
+            int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
+            k_blocks<<<grid(nbb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit,
+                                                        w.wbase, blk_in, blk_out);
+            if ((e = capnp_launch_unpack(d_in, blk_in, nb, 0, d_out, blk_out, blk_status, nullptr,
+                                         nullptr, s)) != hipSuccess)
+                return e;
+        }
     }
     if (hflags[1]) {
         if (serial) *serial = 1;

@@ -185,3 +185,13 @@ def test_resync_config4_round_trip(ctx):
     assert serial == 0
     assert (st == 0).all().item()
     assert torch.equal(back, words)
+
+
+def test_resync_short_chunks_dispatch(ctx):
+    """Batches of short chunks (config-2 shape) go straight to the batch
+    unpack; results are the same either way."""
+    words, offs, packed, poffs = packed_batch([128] * 2000, [0] * 2000, id0=31)
+    g, st, used, passes, serial = resync(ctx, packed, poffs, offs)
+    assert serial == 2 and passes == 0
+    assert (st == 0).all() and np.array_equal(used, np.diff(poffs))
+    assert np.array_equal(g, words)
