@@ -16,7 +16,8 @@ STATUS_NAMES = {
     3: "PackedInputDidNotEndCleanlyOnASegmentBoundary", 4: "FailedToFillTheWholeBuffer",
     5: "PrematureEndOfFile", 6: "InvalidNumberOfSegments", 7: "MessageSizeOverflow",
     8: "MessageTooLarge", 9: "BufferNotLargeEnough", 10: "UnalignedSegment",
-    11: "MisalignedLength", 64: "InvalidArgument", 65: "NoDevice", 66: "HipError",
+    11: "MisalignedLength", 12: "MessageEndsPrematurely", 13: "EmptySlice",
+    14: "MessageNotAlignedBy8BytesBoundary", 64: "InvalidArgument", 65: "NoDevice", 66: "HipError",
     67: "OutOfMemory",
 }
 
@@ -33,7 +34,7 @@ EXPORTS = [
     "capnp_gpu_unpack_batch_sync_tuned", "capnp_unpack_sync_tile_words",
     "capnp_stream_pack_batch", "capnp_stream_unpack_batch", "capnp_gpu_write_messages",
     "capnp_gpu_read_messages", "capnp_gpu_unpack_batch_resync", "capnp_resync_stats",
-    "capnp_resync_block_bytes",
+    "capnp_resync_block_bytes", "capnp_gpu_read_flat_messages",
 ]
 
 
@@ -111,6 +112,8 @@ def lib():
     L.capnp_gpu_write_messages.argtypes = [vp, vp, vp, vp, sz, sz, sz, vp, sz, vp, vp]
     L.capnp_gpu_read_messages.argtypes = [vp, vp, vp, sz, C.POINTER(ReaderOptionsC), i32, vp, sz,
                                           vp, vp, sz, vp, vp, vp, vp]
+    L.capnp_gpu_read_flat_messages.argtypes = [vp, vp, vp, sz, C.POINTER(ReaderOptionsC), i32,
+                                               vp, sz, vp, vp, vp, vp, vp]
     L.capnp_packed_write_message.argtypes = [vp, vp, vp, u32, vp, sz, C.POINTER(C.c_size_t)]
     L.capnp_packed_read_message.argtypes = [vp, vp, sz, C.POINTER(ReaderOptionsC), i32, vp, sz,
                                             vp, C.POINTER(C.c_uint32), C.POINTER(C.c_size_t)]

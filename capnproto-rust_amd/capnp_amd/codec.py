@@ -211,6 +211,30 @@ class Context:
         _check(st, self._h)
         return words, mwo, segs, mso, status[:nmsg], consumed[:nmsg]
 
+    def read_flat_messages(self, buf, slice_off, segs_cap, no_alloc=False,
+                           limit=8 * 1024 * 1024, stream=None):
+        """serialize::read_message_from_flat_slice (or its _no_alloc twin)
+        for a batch of unpacked messages on the device
+        (capnp_gpu_read_flat_messages): message m is read from the slice
+        buf[slice_off[m]:slice_off[m+1]].  Returns (seg_words int32,
+        msg_seg_off, status, body_off, consumed) as device tensors; limit
+        None = no traversal limit."""
+        import torch
+        nmsg = slice_off.numel() - 1
+        dev = slice_off.device
+        segs = torch.empty(max(segs_cap, 1), dtype=torch.int32, device=dev)
+        mso = torch.empty(nmsg + 1, dtype=torch.int64, device=dev)
+        status = torch.empty(max(nmsg, 1), dtype=torch.int32, device=dev)
+        body_off = torch.empty(max(nmsg, 1), dtype=torch.int64, device=dev)
+        consumed = torch.empty(max(nmsg, 1), dtype=torch.int64, device=dev)
+        o = _lib.ReaderOptionsC(int(limit or 0), 1 if limit is not None else 0, 64)
+        st = _lib.lib().capnp_gpu_read_flat_messages(
+            self._h, _ptr(buf), _ptr(slice_off), nmsg, C.byref(o), int(bool(no_alloc)),
+            _ptr(segs), int(segs_cap), _ptr(mso), _ptr(status), _ptr(body_off), _ptr(consumed),
+            self._stream(stream))
+        _check(st, self._h)
+        return segs, mso, status[:nmsg], body_off[:nmsg], consumed[:nmsg]
+
     # ---- streaming host batch (host buffers; pinned for overlap) ---------
     def stream_pack(self, words, chunk_word_off, out, out_off, slice_words=0):
         """capnp_stream_pack_batch on host tensors (CPU torch tensors, ideally

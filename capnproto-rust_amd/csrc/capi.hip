@@ -51,6 +51,12 @@ extern "C" hipError_t capnp_launch_msg_segs(const uint8_t*, const uint64_t*, uin
 extern "C" hipError_t capnp_launch_msg_status(uint64_t, const int32_t*, const uint64_t*,
                                               const int32_t*, const uint64_t*, int32_t*,
                                               uint64_t*, hipStream_t);
+extern "C" hipError_t capnp_launch_flat_frame(const uint8_t*, const uint64_t*, uint64_t, int,
+                                              uint64_t, int, uint64_t*, int32_t*, uint64_t*,
+                                              uint64_t*, void*, size_t, uint64_t*, hipStream_t);
+extern "C" hipError_t capnp_launch_flat_segs(const uint8_t*, const uint64_t*, uint64_t, int,
+                                             uint64_t, int, const int32_t*, const uint64_t*,
+                                             uint32_t*, hipStream_t);
 extern "C" size_t capnp_pack_state_bytes(uint64_t, uint32_t);
 extern "C" hipError_t capnp_launch_unpack(const uint8_t*, const uint64_t*, uint64_t, uint32_t,
                                           uint64_t*, const uint64_t*, int32_t*, uint64_t*,
@@ -878,6 +884,44 @@ capnp_status capnp_gpu_read_messages(capnp_ctx* ctx, const uint8_t* d_packed,
                                 I(o_cst), U(o_ccons), nullptr, s));
     HIP_TRY(capnp_launch_msg_status(nmsg, I(o_tst), U(o_tused), I(o_cst), U(o_ccons), d_status,
                                     d_consumed, s));
+    return CAPNP_OK;
+}
+
+capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf,
+                                          const uint64_t* d_slice_off, size_t nmsg,
+                                          const capnp_reader_options* opts, int no_alloc,
+                                          uint32_t* d_seg_words, size_t segs_cap,
+                                          uint64_t* d_msg_seg_off, int32_t* d_status,
+                                          uint64_t* d_body_off, uint64_t* d_consumed,
+                                          void* stream) {
+    if (!ctx || !d_msg_seg_off || (nmsg && (!d_buf || !d_slice_off || !d_status)))
+        return CAPNP_E_INVALID_ARGUMENT;
+    hipStream_t s = pick(ctx, stream);
+    if (nmsg == 0) {
+        HIP_TRY(hipMemsetAsync(d_msg_seg_off, 0, 8, s));
+        return CAPNP_OK;
+    }
+    const capnp_reader_options o = opts ? *opts : capnp_default_reader_options();
+    size_t scan_bytes = 0;
+    HIP_TRY(capnp_msg_scan_bytes(nmsg + 1, &scan_bytes));
+    const size_t o_nseg = 0;
+    const size_t o_tmp = o_nseg + round16((nmsg + 1) * 8);
+    const size_t o_end = o_tmp + round16(scan_bytes + 16);
+    capnp_status st = ensure_buf(ctx, &ctx->d_msg, &ctx->msg_cap, o_end + 64);
+    if (st != CAPNP_OK) return st;
+    uint8_t* d = ctx->d_msg;
+    const uint64_t limit = o.traversal_limit_in_words;
+    const int has_limit = o.has_traversal_limit != 0;
+    HIP_TRY(capnp_launch_flat_frame(d_buf, d_slice_off, nmsg, no_alloc, limit, has_limit,
+                                    reinterpret_cast<uint64_t*>(d + o_nseg), d_status,
+                                    d_body_off, d_consumed, d + o_tmp, scan_bytes,
+                                    d_msg_seg_off, s));
+    uint64_t tot = 0;
+    HIP_TRY(hipMemcpyAsync(&tot, d_msg_seg_off + nmsg, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (tot > segs_cap || (tot && !d_seg_words)) return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;
+    HIP_TRY(capnp_launch_flat_segs(d_buf, d_slice_off, nmsg, no_alloc, limit, has_limit,
+                                   d_status, d_msg_seg_off, d_seg_words, s));
     return CAPNP_OK;
 }
 

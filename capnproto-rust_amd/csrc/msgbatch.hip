@@ -420,6 +420,108 @@ __global__ void msg_status(uint64_t nmsg, const int32_t* __restrict__ tst,
     if (consumed) consumed[m] = ok ? tused[m] + ccons[2 * m + 1] : 0;
 }
 
+// ---- unpacked flat-slice framing -------------------------
+// One thread per message: the segment table is at most 2 KiB and almost
+// always one word, so the pass is a handful of loads per message (the batch
+// is bound by the 8-64 B of table each message reads plus its output rows).
+// Status values are capnp_status codes.
+enum : int32_t {
+    FST_OK = 0, FST_FAILED_FILL = 4, FST_BAD_NSEG = 6, FST_TOO_LARGE = 8,
+    FST_ENDS_PREMATURELY = 12, FST_EMPTY = 13, FST_NOT_ALIGNED = 14,
+};
+
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+           ((uint32_t)p[3] << 24);
+}
+
+// read_message_from_flat_slice (serialize.rs:53-78 over read_segment_table
+// :448-510 on a &[u8]) or NoAllocSliceSegments::from_slice
+// (no_alloc_buffer_segments.rs:22-92).  seg (nullable) receives the lengths.
+__device__ int32_t flat_table(const uint8_t* p, uint64_t len, int no_alloc, uint64_t limit,
+                              int has_limit, uint32_t* nseg_out, uint64_t* table_out,
+                              uint64_t* words_out, uint32_t* seg) {
+    uint64_t total = 0, pos, nseg;
+    if (!no_alloc) {
+        if (len == 0) return FST_EMPTY;                       // serialize.rs:60-62
+        if (len < 8) return FST_FAILED_FILL;                  // read_exact, :458-463
+        const uint32_t n32 = ld_u32(p) + 1u;                  // wrapping_add(1)
+        if (n32 >= 512u || n32 == 0) return FST_BAD_NSEG;     // :467-473
+        nseg = n32;
+        total = ld_u32(p + 4);
+        if (seg) seg[0] = (uint32_t)total;
+        pos = 8;
+        if (nseg > 1) {
+            const uint64_t rest = nseg < 4 ? 8 : (nseg & ~1ull) * 4;  // :476-496
+            if (len - pos < rest) return FST_FAILED_FILL;
+            for (uint64_t i = 0; i + 1 < nseg; i++) {
+                const uint32_t l = ld_u32(p + pos + 4 * i);
+                if (seg) seg[i + 1] = l;
+                total += l;
+            }
+            pos += rest;
+        }
+        if (has_limit && total > limit) return FST_TOO_LARGE;           // :501-507
+        if (total > (len - pos) / 8) return FST_ENDS_PREMATURELY;       // :66-70
+    } else {
+        if (((uintptr_t)p) & 7) return FST_NOT_ALIGNED;                 // :234-248
+        if (len < 4) return FST_ENDS_PREMATURELY;                       // read_u32_le
+        nseg = (uint64_t)ld_u32(p) + 1;                                 // :268-279
+        if (nseg >= 512) return FST_BAD_NSEG;                           // :31-35
+        pos = 4;
+        for (uint64_t i = 0; i < nseg; i++) {                           // :38-45
+            if (len - pos < 4) return FST_ENDS_PREMATURELY;
+            const uint32_t l = ld_u32(p + pos);
+            if (seg) seg[i] = l;
+            total += l;
+            pos += 4;
+        }
+        if (has_limit && total > limit) return FST_TOO_LARGE;           // :50-57
+        if (!(nseg & 1)) {                                              // padding :61-63
+            if (len - pos < 4) return FST_ENDS_PREMATURELY;
+            pos += 4;
+        }
+        if (len - pos < total * 8) return FST_ENDS_PREMATURELY;         // :84-89
+    }
+    *nseg_out = (uint32_t)nseg;
+    *table_out = pos;
+    *words_out = total;
+    return FST_OK;
+}
+
+__global__ void flat_frame(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+                           uint64_t nmsg, int no_alloc, uint64_t limit, int has_limit,
+                           uint64_t* __restrict__ nseg, int32_t* __restrict__ status,
+                           uint64_t* __restrict__ body_off, uint64_t* __restrict__ consumed) {
+    const uint64_t m = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (m > nmsg) return;
+    if (m == nmsg) {
+        nseg[m] = 0;
+        return;
+    }
+    const uint64_t a = off[m], b = off[m + 1];
+    uint32_t ns = 0;
+    uint64_t t = 0, w = 0;
+    const int32_t s = flat_table(buf + a, b - a, no_alloc, limit, has_limit, &ns, &t, &w, nullptr);
+    const bool ok = s == FST_OK;
+    status[m] = s;
+    nseg[m] = ok ? ns : 0;
+    if (body_off) body_off[m] = a + (ok ? t : 0);
+    if (consumed) consumed[m] = ok ? t + 8 * w : 0;
+}
+
+__global__ void flat_segs(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,
+                          uint64_t nmsg, int no_alloc, uint64_t limit, int has_limit,
+                          const int32_t* __restrict__ status, const uint64_t* __restrict__ sofs,
+                          uint32_t* __restrict__ seg) {
+    const uint64_t m = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (m >= nmsg || status[m] != FST_OK) return;
+    const uint64_t a = off[m], b = off[m + 1];
+    uint32_t ns;
+    uint64_t t, w;
+    flat_table(buf + a, b - a, no_alloc, limit, has_limit, &ns, &t, &w, seg + sofs[m]);
+}
+
 }  // namespace
 
 extern "C" hipError_t capnp_launch_msg_frame(const uint8_t* in, const uint64_t* msg_off,
@@ -460,5 +562,31 @@ extern "C" hipError_t capnp_launch_msg_status(uint64_t nmsg, const int32_t* tst,
     if (g)
         hipLaunchKernelGGL(msg_status, dim3(g), dim3(kThreads), 0, s, nmsg, tst, tused, cst,
                            ccons, status, consumed);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t capnp_launch_flat_frame(const uint8_t* buf, const uint64_t* off,
+                                              uint64_t nmsg, int no_alloc, uint64_t limit,
+                                              int has_limit, uint64_t* nseg, int32_t* status,
+                                              uint64_t* body_off, uint64_t* consumed, void* tmp,
+                                              size_t tmp_bytes, uint64_t* sofs, hipStream_t s) {
+    const uint32_t g = (uint32_t)((nmsg + 1 + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(flat_frame, dim3(g), dim3(kThreads), 0, s, buf, off, nmsg, no_alloc,
+                       limit, has_limit, nseg, status, body_off, consumed);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    size_t tb = tmp_bytes;
+    return hipcub::DeviceScan::ExclusiveSum(tmp, tb, nseg, sofs, (int)(nmsg + 1), s);
+}
+
+extern "C" hipError_t capnp_launch_flat_segs(const uint8_t* buf, const uint64_t* off,
+                                             uint64_t nmsg, int no_alloc, uint64_t limit,
+                                             int has_limit, const int32_t* status,
+                                             const uint64_t* sofs, uint32_t* seg,
+                                             hipStream_t s) {
+    const uint32_t g = (uint32_t)((nmsg + kThreads - 1) / kThreads);
+    if (g)
+        hipLaunchKernelGGL(flat_segs, dim3(g), dim3(kThreads), 0, s, buf, off, nmsg, no_alloc,
+                           limit, has_limit, status, sofs, seg);
     return hipGetLastError();
 }

@@ -61,6 +61,16 @@ typedef enum capnp_status {
     /* Replaces the panic "PackedRead reads must be word-aligned."
        (serialize_packed.rs:86) and non-word-multiple write_all input. */
     CAPNP_E_MISALIGNED_LEN = 11,
+    /* ErrorKind::MessageEndsPrematurely (lib.rs:361): a flat slice shorter
+       than its segment table claims (serialize.rs:66-70,
+       no_alloc_buffer_segments.rs:253-258, :84-89). */
+    CAPNP_E_MESSAGE_ENDS_PREMATURELY = 12,
+    /* ErrorKind::EmptySlice (lib.rs:247): read_message_from_flat_slice on an
+       empty slice (serialize.rs:60-62). */
+    CAPNP_E_EMPTY_SLICE = 13,
+    /* ErrorKind::MessageNotAlignedBy8BytesBoundary (lib.rs:370): the no-alloc
+       flat reader's alignment check (no_alloc_buffer_segments.rs:234-248). */
+    CAPNP_E_NOT_ALIGNED = 14,
     /* Library-level errors (no counterpart in the reference). */
     CAPNP_E_INVALID_ARGUMENT = 64,
     CAPNP_E_NO_DEVICE = 65,
@@ -266,6 +276,29 @@ capnp_status capnp_gpu_read_messages(capnp_ctx* ctx, const uint8_t* d_packed,
                                      uint64_t* d_msg_word_off, uint64_t* d_seg_words,
                                      size_t segs_cap, uint64_t* d_msg_seg_off,
                                      int32_t* d_status, uint64_t* d_consumed, void* stream);
+
+/* Unpacked flat-slice framing for nmsg messages at once:
+   serialize::read_message_from_flat_slice (serialize.rs:53-78) when
+   no_alloc == 0, read_message_from_flat_slice_no_alloc /
+   NoAllocSliceSegments::from_slice (serialize.rs:88-96,
+   no_alloc_buffer_segments.rs:22-92, :152-162) when no_alloc != 0.  Message
+   m is read from the slice d_buf[d_slice_off[m] .. d_slice_off[m+1]) (the
+   slice may extend past the message, as in the reference).  Zero copy:
+   nothing is moved, only the framing is validated and described.  Outputs
+   (device): d_status[m]; d_body_off[m] the byte offset in d_buf of the first
+   segment (slice start + table bytes); d_consumed[m] table + body bytes (the
+   reference's `*slice` advance); segment lengths in words in d_seg_words,
+   message m's at [d_msg_seg_off[m], d_msg_seg_off[m+1]) (nmsg+1 entries; a
+   failed message has none).  d_body_off / d_consumed may be NULL.
+   Synchronises the stream once (segment total against segs_cap:
+   CAPNP_E_BUFFER_NOT_LARGE_ENOUGH, with only d_msg_seg_off written). */
+capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf,
+                                          const uint64_t* d_slice_off, size_t nmsg,
+                                          const capnp_reader_options* opts, int no_alloc,
+                                          uint32_t* d_seg_words, size_t segs_cap,
+                                          uint64_t* d_msg_seg_off, int32_t* d_status,
+                                          uint64_t* d_body_off, uint64_t* d_consumed,
+                                          void* stream);
 
 /* ---- host message API (mirrors serialize_packed) ----------------------- */
 /* serialize_packed::write_message (serialize_packed.rs:446-453 ->

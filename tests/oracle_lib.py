@@ -48,6 +48,9 @@ def lib():
         L.oracle_read_message_no_alloc.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_int,
                                                    C.c_int, C.c_void_p, C.c_size_t,
                                                    C.POINTER(C.c_uint32), szp, szp, szp]
+        L.oracle_read_flat_message.argtypes = [C.c_void_p, C.c_size_t, C.c_uint64, C.c_int,
+                                               C.c_int, C.c_void_p, C.POINTER(C.c_uint32),
+                                               szp, szp]
         L.oracle_pack_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
                                         C.c_size_t, C.c_void_p, C.c_int]
         L.oracle_unpack_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
@@ -205,3 +208,16 @@ def gen_fill(offs, kinds=None, kind0=0, pz=PZ30, id0=0):
     lib().gen_fill(words.ctypes.data, offs.ctypes.data, 0, n, id0,
                    k.ctypes.data if k is not None else None, kind0, pz)
     return words[:int(offs[-1])]
+
+
+def read_flat_message(buf, off, length, no_alloc=False, limit=DEFAULT_TRAVERSAL_LIMIT):
+    """serialize::read_message_from_flat_slice(_no_alloc) on buf[off:off+length]
+    (buf an 8-byte aligned np.uint8 array, so off % 8 is the slice's
+    alignment).  -> (status, [segment lengths], table_bytes, consumed)."""
+    seg = np.zeros(512, np.uint32)
+    nseg, tb, used = C.c_uint32(0), C.c_size_t(0), C.c_size_t(0)
+    st = lib().oracle_read_flat_message(buf.ctypes.data + off, length,
+                                        limit if limit is not None else 0, limit is not None,
+                                        int(no_alloc), seg.ctypes.data, C.byref(nseg),
+                                        C.byref(tb), C.byref(used))
+    return st, [int(x) for x in seg[:nseg.value]], tb.value, used.value
