@@ -894,7 +894,8 @@ capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf,
                                           uint64_t* d_msg_seg_off, int32_t* d_status,
                                           uint64_t* d_body_off, uint64_t* d_consumed,
                                           void* stream) {
-    if (!ctx || !d_msg_seg_off || (nmsg && (!d_buf || !d_slice_off || !d_status)))
+    // d_buf may be NULL when every slice is empty (an empty tensor has no storage)
+    if (!ctx || !d_msg_seg_off || (nmsg && (!d_slice_off || !d_status)))
         return CAPNP_E_INVALID_ARGUMENT;
     hipStream_t s = pick(ctx, stream);
     if (nmsg == 0) {

@@ -121,3 +121,32 @@ def test_flat_write_messages_layout_round_trip(ctx):
     assert (used == np.diff(starts)).all()
     assert int(mso[-1]) == int(nsegs.sum())
     assert (body.cpu().numpy() == starts[:-1] + 8 * (nsegs // 2 + 1)).all()
+
+
+def test_host_mirror_reference_cases(ctx):
+    """The reference's flat-slice tests through the host mirror
+    (capnp_amd.serialize): serialize.rs:1063-1115 and
+    no_alloc_buffer_segments.rs:505-544."""
+    from capnp_amd import CapnpError
+    from capnp_amd import serialize as S
+    segs = [[123, 0, 0, 0, 0, 0, 0, 0], [4, 0, 0, 0, 0, 0, 0, 0, 5, 0, 0, 0, 0, 0, 0, 0]]
+    extra = bytes([9, 9, 9, 9, 9, 9, 9, 9, 8, 7, 6, 5, 4, 3, 2, 1])
+    data = flat_message(segs) + extra
+    dev = torch.tensor(list(data), dtype=torch.uint8, device="cuda")
+    for fn in (S.read_message_from_flat_slice, S.read_message_from_flat_slice_no_alloc):
+        got, rest = fn(dev)
+        assert [g.cpu().tolist() for g in got] == segs
+        assert bytes(rest.cpu().tolist()) == extra
+    short = flat_message([[1, 0, 0, 0, 0, 0, 0, 0], [2, 0, 0, 0, 0, 0, 0, 0, 3, 0, 0, 0, 0, 0, 0, 0]])
+    dshort = torch.tensor(list(short), dtype=torch.uint8, device="cuda")
+    for k in range(len(short)):
+        for fn in (S.read_message_from_flat_slice, S.read_message_from_flat_slice_no_alloc):
+            with pytest.raises(CapnpError):
+                fn(dshort[:k])
+    with pytest.raises(CapnpError) as e:
+        S.read_message_from_flat_slice(dshort[:0])
+    assert e.value.kind == "EmptySlice"
+    bad = torch.tensor([255, 255, 255, 255], dtype=torch.uint8, device="cuda")
+    with pytest.raises(CapnpError) as e:
+        S.read_message_from_flat_slice_no_alloc(bad)
+    assert e.value.kind == "InvalidNumberOfSegments"
