@@ -1,16 +1,25 @@
 #!/usr/bin/env python3
 """Benchmark: packed encode+decode of device-resident Cap'n Proto segments.
 
-Workload (BASELINE.json configs[1]): 1 Mi segments x 1 KiB (128 words) per
-GPU, ~30 % zero words (SURVEY.md §8d config 2 generator), resident in HBM.
-One step = PACK the whole batch (capnp_gpu_pack_batch) and UNPACK it back
-(capnp_gpu_unpack_batch) — the encode+decode round trip of the metric.
-value = unpacked GiB per step (all ranks) / step time.
+Workloads (--workload; SURVEY.md §8d, BASELINE.json configs):
+  config2   (default, configs[1]) 1 Mi segments x 1 KiB per GPU, ~30 % zero
+            words (seeded splitmix64 generator)
+  config3   the same shape at >= 80 % zero words (configs[2]; --chunks
+            23400000 for the 4 GiB-packed size)
+  carsales  1 Mi x 1 KiB carsales-shaped segments: the reference benchmark's
+            request stream (benchmark/carsales.rs:84-150 on FastRand,
+            common.rs:22-70) cut into 128-word chunks (north_star workload)
+  config4   mixed 64 B - 64 KiB segments, ~1 GiB (configs[3])
+  config5   8 Mi x 1 KiB per GPU = 8 GiB (configs[4]: 64 GiB over 8 GPUs)
+One step = PACK the whole batch (capnp_gpu_pack_batch_sync) and UNPACK it
+back (capnp_gpu_unpack_batch_sync): the encode+decode round trip of the
+metric.  value = unpacked GiB per step (all ranks) / step time.
 
-Multi-GPU: one process per GPU (torch.distributed.run); every rank packs
-and unpacks its own shard of independent segments (chunk ids offset by
-rank), no data-path collective; scaling is weak.  RCCL is used only for the
-barrier and the max-over-ranks of the timing.
+Multi-GPU: `--gpus N` (N > 1) started as a plain process re-launches itself
+under torch.distributed.run with N ranks (a child process, before any GPU
+call); one process per GPU, each rank packs and unpacks its own shard of
+independent segments, no data-path collective; scaling is weak.  The
+collectives are the barrier and the max-over-ranks of the timing only.
 
 The JSON line also carries
   roofline      the dominant kernel's algorithmic bytes per launch / its mean
@@ -21,6 +30,8 @@ The JSON line also carries
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,40 +41,81 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HBM_MEASURED_COPY_GBS = 6290.0  # measured float4 copy (same source)
-PZ = {"config2": 1288490189, "config3": 3435973837}
+PZ = {"config2": 1288490189, "config3": 3435973837, "config5": 1288490189,
+      "config4": 1288490189}
 METRIC = "GiB/s packed encode+decode, device-resident segments; % HBM roofline"
 GiB = float(1 << 30)
+CARSALES_RANK_STRIDE = 100_000  # rank r's requests start at r x this (~90 k per GiB)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--chunks", type=int, default=1 << 20, help="segments per GPU")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="segments per GPU (0 = the workload's size)")
     ap.add_argument("--chunk-words", type=int, default=128)
-    ap.add_argument("--workload", default="config2", choices=["config2", "config3"])
-    ap.add_argument("--cpu-sample-chunks", type=int, default=1 << 18)
-    ap.add_argument("--cpu-reps", type=int, default=4)
+    ap.add_argument("--workload", default="config2",
+                    choices=["config2", "config3", "carsales", "config4", "config5"])
+    ap.add_argument("--cpu-sample-words", type=int, default=1 << 25)
+    ap.add_argument("--cpu-reps", type=int, default=3)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--e2e", action="store_true", help="also time host->device->host")
     ap.add_argument("--no-sync", action="store_true",
                     help="pack without the record sync index; unpack walks whole chunks")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rendezvous / reporting only, no GPU (gloo; tests)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(args):
-    """Oracle pack + unpack of the first `cpu_sample_chunks` segments of the
-    same workload on this host's cores."""
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(args):
+    """--gpus N from a plain process: run this script under
+    torch.distributed.run with N ranks as a child process (nothing here has
+    touched the GPU) and exit with its status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "16")
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_threads(args):
+    """Threads for the CPU baseline: the host share this process may use
+    (OMP_NUM_THREADS, set to the box's 16-CPU share on the GPU pool, else the
+    affinity mask)."""
+    if args.cpu_threads:
+        return args.cpu_threads
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 0
+    return env or aff or (os.cpu_count() or 1)
+
+
+def cpu_baseline(args, threads):
+    """The CPU oracle on a bounded sample of the same workload on this host:
+    chunk-level pack + unpack (all workloads), and for carsales the
+    reference benchmark's per-request write_message + read_message."""
     import numpy as np
     import oracle_lib as O
-    n, cw = args.cpu_sample_chunks, args.chunk_words
-    threads = args.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or \
-        min(16, os.cpu_count() or 1)
+    cw = args.chunk_words
+    n = max(1, args.cpu_sample_words // cw)
     offs = np.arange(0, (n + 1) * cw, cw, dtype=np.uint64)
-    words = O.gen_fill(offs, kind0=0, pz=PZ[args.workload])
+    if args.workload == "carsales":
+        words, msg_off, _ = O.carsales_stream(n * cw)
+    else:
+        words = O.gen_fill(offs, kind0=0, pz=PZ.get(args.workload, PZ["config2"]))
 
     def timed(nn, thr, reps):
         w, o = words[:nn * cw], offs[:nn + 1]
@@ -82,28 +134,89 @@ def cpu_baseline(args):
     best = timed(n, threads, args.cpu_reps)
     n1 = max(1, n // 16)
     one = timed(n1, 1, 2)
-    u = n * cw * 8
-    u1 = n1 * cw * 8
-    return {
+    u, u1 = n * cw * 8, n1 * cw * 8
+    res = {
         "value": round(u / best[0] / GiB, 3),
         "unit": "GiB/s",
         "cores": threads,
+        "host_cpus": os.cpu_count(),
         "kind": "port",
-        "sample": f"{n} segments x {cw * 8} B ({u / GiB:.3f} GiB) of the same generator, "
-                  f"pack+unpack, best of {args.cpu_reps}, {threads} threads "
-                  f"(oracle/packed_oracle.c, gcc -O3)",
+        "sample": f"{n} segments x {cw * 8} B ({u / GiB:.3f} GiB) of the same workload, "
+                  f"pack+unpack per segment, best of {args.cpu_reps}, {threads} threads "
+                  f"(oracle/packed_oracle.c, gcc -O3; cores = threads used: the GPU box's "
+                  f"CPU share, OMP_NUM_THREADS; host_cpus = os.cpu_count())",
         "pack_gibps": round(u / best[1] / GiB, 3),
         "unpack_gibps": round(u / best[2] / GiB, 3),
         "single_thread_gibps": round(u1 / one[0] / GiB, 3),
     }
+    if args.workload == "carsales":
+        # benchmark carsales bytes reuse packed: write_message + read_message
+        # of each whole request (benchmark.rs:235-241), the codec part of it
+        m = len(msg_off) - 2  # requests complete in the sample
+        mo = msg_off[:m + 1]
+        ww = words[:int(mo[-1])]
+        um = 8 * len(ww)
+        bm = min(O.messages_roundtrip_mt(ww, mo, threads)[:2], key=sum)
+        m1 = max(1, m // 16)
+        b1 = O.messages_roundtrip_mt(words[:int(msg_off[m1])], msg_off[:m1 + 1], 1)
+        res["carsales_messages"] = {
+            "requests": int(m), "threads": threads,
+            "roundtrip_gibps": round(um / sum(bm) / GiB, 3),
+            "write_gibps": round(um / bm[0] / GiB, 3), "read_gibps": round(um / bm[1] / GiB, 3),
+            "single_thread_roundtrip_gibps": round(8 * int(msg_off[m1]) / sum(b1[:2]) / GiB, 3),
+            "note": "oracle write_message + read_message per carsales request "
+                    "(benchmark/carsales.rs bytes reuse packed, codec calls only)"}
+    return res
+
+
+def make_workload(args, ctx, torch, dev, rank):
+    """-> (words, chunk_word_off, n, description) resident in HBM."""
+    import numpy as np
+    cw = args.chunk_words
+    wl = args.workload
+    if wl == "config4":
+        rng = np.random.default_rng(4 + rank)
+        target = (1 << 30) // 8
+        sizes, total = [], 0
+        while total < target:
+            s = int(np.exp(rng.uniform(np.log(8), np.log(8193))))
+            sizes.append(s)
+            total += s
+        n = len(sizes)
+        kinds = rng.choice(3, size=n, p=[0.8, 0.1, 0.1]).astype(np.uint8)
+        offs_h = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        offs = torch.from_numpy(offs_h).to(dev)
+        words = torch.empty(total, dtype=torch.int64, device=dev)
+        ctx.gen_batch(words, offs, pz_thresh=PZ[wl], kinds=torch.from_numpy(kinds).to(dev),
+                      id0=rank * 10_000_000)
+        return words, offs, n, (f"config4: {n} segments, 64 B - 64 KiB log-uniform, "
+                                f"{8 * total / GiB:.3f} GiB per GPU (80 % ~30 %-zero words, "
+                                "10 % long zero runs, 10 % long literal runs)")
+    n = args.chunks or {"config5": 8 << 20}.get(wl, 1 << 20)
+    offs = torch.arange(0, (n + 1) * cw, cw, dtype=torch.int64, device=dev)
+    words = torch.empty(n * cw, dtype=torch.int64, device=dev)
+    if wl == "carsales":
+        req = ctx.gen_carsales(words, skip_requests=rank * CARSALES_RANK_STRIDE)
+        desc = (f"carsales: {n} segments x {cw * 8} B per GPU cut from {len(req) - 1} "
+                f"carsales requests (benchmark/carsales.rs, FastRand chain from request "
+                f"{rank * CARSALES_RANK_STRIDE})")
+    else:
+        ctx.gen_batch(words, offs, pz_thresh=PZ[wl], id0=rank * n)
+        desc = (f"{wl}: {n} segments x {cw * 8} B per GPU, "
+                f"{'~80' if wl == 'config3' else '~30'} % zero words")
+    return words, offs, n, desc
 
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args))
+    if args.dry_run:
+        return dry_run(args, world)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -114,11 +227,8 @@ def main():
 
     from capnp_amd import Context, tile_chunks_for, unpack_tile_chunks_for
     ctx = Context(local)
-    n, cw = args.chunks, args.chunk_words
-    total_words = n * cw
-    offs = torch.arange(0, (n + 1) * cw, cw, dtype=torch.int64, device=dev)
-    words = torch.empty(total_words, dtype=torch.int64, device=dev)
-    ctx.gen_batch(words, offs, pz_thresh=PZ[args.workload], id0=rank * n)
+    words, offs, n, desc = make_workload(args, ctx, torch, dev, rank)
+    total_words = words.numel()
     cap = ctx.batch_bound_bytes(total_words, n)
     packed = torch.empty(cap, dtype=torch.uint8, device=dev)
     poffs = torch.empty(n + 1, dtype=torch.int64, device=dev)
@@ -179,28 +289,46 @@ def main():
     # and consumed arrays)
     pack_bytes = U + P + 2 * offs_bytes + sync_bytes
     unpack_bytes = P + U + 2 * offs_bytes + 4 * n + 8 * n + sync_bytes
-    kernels = {
-        "pack": {"ms": round(pack_ms, 4), "alg_bytes": pack_bytes,
-                 "GBps": round(pack_bytes / (pack_ms * 1e-3) / 1e9, 1),
-                 "unpacked_GiBps": round(U / (pack_ms * 1e-3) / GiB, 2)},
-        "unpack": {"ms": round(unpack_ms, 4), "alg_bytes": unpack_bytes,
-                   "GBps": round(unpack_bytes / (unpack_ms * 1e-3) / 1e9, 1),
-                   "unpacked_GiBps": round(U / (unpack_ms * 1e-3) / GiB, 2)},
-    }
+
+    def kern(ms, nbytes):
+        return {"ms": round(ms, 4), "alg_bytes": nbytes,
+                "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1),
+                "frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "unpacked_GiBps": round(U / (ms * 1e-3) / GiB, 2)}
+
+    kernels = {"pack": kern(pack_ms, pack_bytes), "unpack": kern(unpack_ms, unpack_bytes)}
+    if sync is not None:
+        # the reference-compatible decode (a stream with no side-band index),
+        # timed after the headline loop on the same packed batch
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        reps = max(3, args.steps // 4)
+        ctx.unpack_batch_into(packed, poffs, offs, back, status, consumed,
+                              chunks_per_tile=unpack_tile_chunks_for(total_words, n))
+        e[0].record(stream)
+        for _ in range(reps):
+            ctx.unpack_batch_into(packed, poffs, offs, back, status, consumed,
+                                  chunks_per_tile=unpack_tile_chunks_for(total_words, n))
+        e[1].record(stream)
+        torch.cuda.synchronize()
+        ok_ns = bool(torch.equal(back, words)) and int((status != 0).sum()) == 0
+        kernels["unpack_nosync"] = kern(e[0].elapsed_time(e[1]) / reps,
+                                        P + U + 2 * offs_bytes + 12 * n)
+        kernels["unpack_nosync"]["roundtrip_ok"] = ok_ns
+        ok = ok and ok_ns
     dom = "pack" if pack_ms >= unpack_ms else "unpack"
     achieved = kernels[dom]["GBps"]
     traffic = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        key = f"{args.workload}:{n}x{cw}" + (":sync" if sync is not None else "")
+        key = f"{args.workload}:{n}x{args.chunk_words}" + (":sync" if sync is not None else "")
         traffic = tj.get(key, {}).get(dom)
     except (OSError, ValueError):
         pass
 
     e2e = None
     if args.e2e and rank == 0:
-        e2e = end_to_end(ctx, torch, words, offs, n, cw, tc, dev)
+        e2e = end_to_end(ctx, torch, words, offs, n, tc, dev)
 
     ms_per_step = elapsed / args.steps * 1e3
     value = world * U / GiB / (elapsed / args.steps)
@@ -217,12 +345,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (seeded splitmix64 generator, SURVEY §8d)",
+            "data": ("synthetic: the reference benchmark's carsales requests (FastRand chain)"
+                     if args.workload == "carsales" else
+                     "synthetic (seeded splitmix64 generator, SURVEY §8d)"),
             "config": {
-                "workload": f"{args.workload}: {n} segments x {cw * 8} B per GPU, "
-                            f"{'~30' if args.workload == 'config2' else '~80'} % zero words, "
-                            "pack+unpack round trip",
-                "segments_per_gpu": n, "segment_bytes": cw * 8,
+                "workload": desc + ", pack+unpack round trip",
+                "segments_per_gpu": n, "unpacked_bytes_per_gpu": U,
                 "global_unpacked_bytes": world * U, "parallelism": f"shard{world}",
             },
             "roofline": {
@@ -230,6 +358,12 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
             },
+            "roundtrip_frac_of_hbm": round((pack_bytes + unpack_bytes) /
+                                           ((pack_ms + unpack_ms) * 1e-3) / 1e9 /
+                                           HBM_PEAK_GBS, 4),
+            "aggregate_frac_of_hbm": round(world * (pack_bytes + unpack_bytes) /
+                                           (elapsed / args.steps) / 1e9 /
+                                           (world * HBM_PEAK_GBS), 4),
             "kernels": kernels,
             "packed_ratio": round(P / U, 4),
             "sync_index": sync is not None,
@@ -238,7 +372,7 @@ def main():
         if e2e:
             line["e2e"] = e2e
         if not args.no_cpu:
-            line["cpu_baseline"] = cpu_baseline(args)
+            line["cpu_baseline"] = cpu_baseline(args, cpu_threads(args))
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -246,21 +380,43 @@ def main():
         sys.exit(3)
 
 
-def end_to_end(ctx, torch, words, offs, n, cw, tc, dev):
+def dry_run(args, world):
+    """The launcher path without a GPU: each rank joins a gloo group, the
+    max over ranks of a per-rank stand-in time is taken, rank 0 reports."""
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        from capnp_amd import shard
+        elapsed = shard.max_over_ranks(0.01 * (rank + 1))
+        dist.barrier()
+        dist.destroy_process_group()
+    else:
+        elapsed = 0.01
+    print(json.dumps({"dry_run": True, "rank": rank, "world": world}), file=sys.stderr,
+          flush=True)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world,
+                          "dry_run": True, "max_elapsed": elapsed, "steps": args.steps,
+                          "warmup": args.warmup}), flush=True)
+
+
+def end_to_end(ctx, torch, words, offs, n, tc, dev):
     """Host pinned buffer -> H2D -> pack -> D2H and back (PCIe-bound).
     Reported in DESIGN.md only; never the headline value."""
     from capnp_amd import unpack_tile_chunks_for
-    U = n * cw * 8
-    h_words = torch.empty(n * cw, dtype=torch.int64, pin_memory=True)
+    total = words.numel()
+    U = total * 8
+    h_words = torch.empty(total, dtype=torch.int64, pin_memory=True)
     h_words.copy_(words)
-    cap = ctx.batch_bound_bytes(n * cw, n)
+    cap = ctx.batch_bound_bytes(total, n)
     d_words = torch.empty_like(words)
     d_packed = torch.empty(cap, dtype=torch.uint8, device=dev)
     d_poffs = torch.empty(n + 1, dtype=torch.int64, device=dev)
     h_packed = torch.empty(cap, dtype=torch.uint8, pin_memory=True)
     d_back = torch.empty_like(words)
     status = torch.empty(n, dtype=torch.int32, device=dev)
-    h_back = torch.empty(n * cw, dtype=torch.int64, pin_memory=True)
+    h_back = torch.empty(total, dtype=torch.int64, pin_memory=True)
     res = {}
     for rep in range(3):
         torch.cuda.synchronize()
@@ -274,7 +430,7 @@ def end_to_end(ctx, torch, words, offs, n, cw, tc, dev):
         t1 = time.perf_counter()
         d_packed[:P].copy_(h_packed[:P], non_blocking=True)
         ctx.unpack_batch_into(d_packed, d_poffs, offs, d_back, status,
-                              chunks_per_tile=unpack_tile_chunks_for(n * cw, n))
+                              chunks_per_tile=unpack_tile_chunks_for(total, n))
         h_back.copy_(d_back, non_blocking=True)
         torch.cuda.synchronize()
         t2 = time.perf_counter()
@@ -292,7 +448,7 @@ def end_to_end(ctx, torch, words, offs, n, cw, tc, dev):
     for rep in range(3):
         h_back.zero_()
         t0 = time.perf_counter()
-        P = ctx.stream_pack(h_words, h_offs, h_packed, h_poffs, slice_words=slice_words)
+        ctx.stream_pack(h_words, h_offs, h_packed, h_poffs, slice_words=slice_words)
         t1 = time.perf_counter()
         ctx.stream_unpack(h_packed, h_poffs, h_offs, h_back, h_status, slice_words=slice_words)
         t2 = time.perf_counter()

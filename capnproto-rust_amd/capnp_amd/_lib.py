@@ -34,7 +34,7 @@ EXPORTS = [
     "capnp_gpu_unpack_batch_sync_tuned", "capnp_unpack_sync_tile_words",
     "capnp_stream_pack_batch", "capnp_stream_unpack_batch", "capnp_gpu_write_messages",
     "capnp_gpu_read_messages", "capnp_gpu_unpack_batch_resync", "capnp_resync_stats",
-    "capnp_resync_block_bytes", "capnp_gpu_read_flat_messages",
+    "capnp_resync_block_bytes", "capnp_gpu_read_flat_messages", "capnp_gpu_gen_carsales",
 ]
 
 
@@ -86,6 +86,9 @@ def lib():
     L.capnp_gpu_unpack_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.capnp_gpu_unpack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, C.c_uint32, vp]
     L.capnp_gpu_gen_batch.argtypes = [vp, vp, vp, sz, u64, vp, u32, u32, vp]
+    L.capnp_gpu_gen_carsales.argtypes = [vp, vp, u64, u64, vp, sz, C.POINTER(C.c_size_t), vp]
+    L.capnp_carsales_plan.argtypes = [vp, u64, u64, vp, vp, u64]
+    L.capnp_carsales_plan.restype = u64
     L.capnp_unpack_sync_tile_words.argtypes = []
     L.capnp_unpack_sync_tile_words.restype = u32
     L.capnp_sync_index_entries.argtypes = [sz]

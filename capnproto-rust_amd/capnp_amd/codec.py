@@ -263,6 +263,35 @@ class Context:
                                             self._stream(stream))
         _check(st, self._h)
 
+    def gen_carsales(self, words, skip_requests=0, stream=None):
+        """Fill `words` (int64, HBM) with the reference benchmark's carsales
+        request stream (capnp_gpu_gen_carsales) -> host list of request word
+        offsets (nreq + 1 entries; the last request may be cut at
+        words.numel())."""
+        import numpy as np
+        total = words.numel()
+        cap = total // 3 + 2
+        offs = np.zeros(cap + 1, np.uint64)
+        nreq = C.c_size_t(0)
+        st = _lib.lib().capnp_gpu_gen_carsales(
+            self._h, _ptr(words), total, int(skip_requests),
+            C.c_void_p(offs.ctypes.data), cap, C.byref(nreq), self._stream(stream))
+        _check(st, self._h)
+        return offs[:nreq.value + 1]
+
+
+def carsales_plan(total_words, skip_requests=0):
+    """Host walk of the carsales FastRand chain (no device needed):
+    -> (states uint32[nreq, 4], request word offsets uint64[nreq + 1])."""
+    import numpy as np
+    cap = total_words // 3 + 2
+    seed = np.array([0x1d2acd47, 0x58ca3e14, 0xf563f232, 0x0bc76199], np.uint32)
+    states = np.zeros((cap, 4), np.uint32)
+    offs = np.zeros(cap + 1, np.uint64)
+    m = _lib.lib().capnp_carsales_plan(seed.ctypes.data, int(skip_requests), int(total_words),
+                                       states.ctypes.data, offs.ctypes.data, cap)
+    return states[:m], offs[:m + 1]
+
 
 def tile_chunks_for(total_words, nchunks, lib=None):
     """Chunks per pack workgroup: the staged path holds

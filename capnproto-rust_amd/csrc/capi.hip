@@ -63,6 +63,10 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t*, const uint64_t*, uint6
                                           const uint32_t*, hipStream_t);
 extern "C" hipError_t capnp_launch_gen(uint64_t*, const uint64_t*, uint64_t, uint64_t,
                                        const uint8_t*, uint32_t, uint32_t, hipStream_t);
+extern "C" uint64_t capnp_carsales_plan(const uint32_t*, uint64_t, uint64_t, uint32_t*, uint64_t*,
+                                        uint64_t);
+extern "C" hipError_t capnp_launch_gen_carsales(uint64_t*, uint64_t, const uint32_t*,
+                                                const uint64_t*, uint64_t, hipStream_t);
 extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes);
 extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d_in_off, uint64_t n,
                                           uint64_t total_bytes, uint64_t* d_out,
@@ -501,6 +505,34 @@ capnp_status capnp_gpu_gen_batch(capnp_ctx* ctx, uint64_t* d_words, const uint64
     if (!ctx) return CAPNP_E_INVALID_ARGUMENT;
     HIP_TRY(capnp_launch_gen(d_words, d_offs, nchunks, id0, d_kinds, kind0, pz_thresh,
                              pick(ctx, stream)));
+    return CAPNP_OK;
+}
+
+capnp_status capnp_gpu_gen_carsales(capnp_ctx* ctx, uint64_t* d_words, uint64_t total_words,
+                                    uint64_t skip_requests, uint64_t* h_req_off,
+                                    size_t max_req, size_t* nreq, void* stream) {
+    if (!ctx || (total_words && !d_words)) return CAPNP_E_INVALID_ARGUMENT;
+    // a request has at least 3 words: this many requests always cover it
+    const uint64_t cap = std::min<uint64_t>(total_words / 3 + 2, max_req ? max_req : ~0ull);
+    std::vector<uint32_t> states(4 * cap);
+    std::vector<uint64_t> off(cap + 1);
+    static const uint32_t seed[4] = {0x1d2acd47u, 0x58ca3e14u, 0xf563f232u, 0x0bc76199u};
+    const uint64_t m = capnp_carsales_plan(seed, skip_requests, total_words, states.data(),
+                                           off.data(), cap);
+    if (nreq) *nreq = m;
+    if (h_req_off) memcpy(h_req_off, off.data(), (m + 1) * 8);
+    if (m == 0) return CAPNP_OK;
+    const size_t o_off = round16(m * 16);
+    capnp_status st = ensure_stage(ctx, o_off + (m + 1) * 8);
+    if (st != CAPNP_OK) return st;
+    hipStream_t s = pick(ctx, stream);
+    HIP_TRY(hipMemcpyAsync(ctx->d_stage, states.data(), m * 16, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ctx->d_stage + o_off, off.data(), (m + 1) * 8, hipMemcpyHostToDevice,
+                           s));
+    HIP_TRY(capnp_launch_gen_carsales(d_words, total_words,
+                                      reinterpret_cast<uint32_t*>(ctx->d_stage),
+                                      reinterpret_cast<uint64_t*>(ctx->d_stage + o_off), m, s));
+    HIP_TRY(hipStreamSynchronize(s));  // the staging buffer is reused by later calls
     return CAPNP_OK;
 }
 

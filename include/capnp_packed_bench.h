@@ -22,6 +22,20 @@ capnp_status capnp_gpu_gen_batch(capnp_ctx* ctx, uint64_t* d_words, const uint64
                                  size_t nchunks, uint64_t id0, const uint8_t* d_kinds,
                                  uint32_t kind0, uint32_t pz_thresh, void* stream);
 
+/* Fills d_words[0 .. total_words) with the carsales request stream of the
+ * reference benchmark (BASELINE.json configs[0]; benchmark/carsales.rs:84-150
+ * on benchmark/common.rs:22-70's FastRand from its default seed, one
+ * generator for the whole run): the single segments of requests
+ * skip_requests, skip_requests + 1, ... back to back, the last one cut at
+ * total_words.  Bit-identical to oracle/carsales_oracle.c's carsales_stream.
+ * *nreq = requests started; h_req_off (optional, host, nreq + 1 entries) =
+ * each request's first word, then the end of the last one in full.  The
+ * chain is walked on the host (serial by construction); the words are
+ * written on the device, then the call synchronises `stream`. */
+capnp_status capnp_gpu_gen_carsales(capnp_ctx* ctx, uint64_t* d_words, uint64_t total_words,
+                                    uint64_t skip_requests, uint64_t* h_req_off,
+                                    size_t max_req, size_t* nreq, void* stream);
+
 /* capnp_gpu_pack_batch with an explicit tile size (chunks per 256-thread
  * workgroup, 1..64; 0 = default).  Pick ~1024 / mean_chunk_words. */
 capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,

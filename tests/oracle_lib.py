@@ -62,6 +62,19 @@ def lib():
         L.gen_word.restype = C.c_uint64
         L.gen_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_size_t, C.c_uint64,
                                C.c_void_p, C.c_int, C.c_uint32]
+        L.oracle_write_messages_mt.argtypes = [
+            C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+            C.c_int]
+        L.oracle_read_messages_mt.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.carsales_seed.argtypes = [C.c_void_p]
+        L.carsales_request.argtypes = [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)]
+        L.carsales_request.restype = C.c_size_t
+        L.carsales_value.argtypes = [C.c_void_p, C.c_size_t]
+        L.carsales_value.restype = C.c_uint64
+        L.carsales_stream.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
+                                      C.c_void_p, C.c_size_t]
+        L.carsales_stream.restype = C.c_size_t
         _lib = L
     return _lib
 
@@ -221,3 +234,72 @@ def read_flat_message(buf, off, length, no_alloc=False, limit=DEFAULT_TRAVERSAL_
                                         int(no_alloc), seg.ctypes.data, C.byref(nseg),
                                         C.byref(tb), C.byref(used))
     return st, [int(x) for x in seg[:nseg.value]], tb.value, used.value
+
+
+# ---- carsales (oracle/carsales_oracle.c; BASELINE.json configs[0]) --------
+
+CARSALES_MAX_WORDS = 3 + 15 * 199
+
+
+def carsales_seed():
+    """FastRand's default state (benchmark/common.rs:30-39) as uint32[4]."""
+    st = np.zeros(4, np.uint32)
+    lib().carsales_seed(st.ctypes.data)
+    return st
+
+
+def carsales_request(st):
+    """setup_request on the chain state `st` (advanced in place) ->
+    (request segment words, expected total value)."""
+    seg = np.zeros(CARSALES_MAX_WORDS, np.uint64)
+    exp = C.c_uint64(0)
+    nw = lib().carsales_request(st.ctypes.data, seg.ctypes.data, C.byref(exp))
+    return seg[:nw].copy(), exp.value
+
+
+def carsales_value(seg):
+    seg = np.ascontiguousarray(seg, np.uint64)
+    return int(lib().carsales_value(seg.ctypes.data, len(seg)))
+
+
+def carsales_stream(target_words, skip=0, st=None, max_msgs=None):
+    """Request segments of the benchmark's chain back to back, cut at
+    target_words -> (words, msg_off[nmsgs + 1], state after)."""
+    if st is None:
+        st = carsales_seed()
+    if max_msgs is None:
+        max_msgs = target_words // 3 + 2
+    words = np.zeros(max(target_words, 1), np.uint64)
+    offs = np.zeros(max_msgs + 1, np.uint64)
+    m = lib().carsales_stream(st.ctypes.data, skip, words.ctypes.data, target_words,
+                              offs.ctypes.data, max_msgs)
+    return words[:target_words], offs[:m + 1], st
+
+
+def messages_roundtrip_mt(words, msg_off, threads=1):
+    """One-segment messages words[msg_off[m]:msg_off[m+1]] through
+    write_message then read_message (the carsales benchmark's codec calls) on
+    `threads` threads -> (seconds write, seconds read, packed bytes, ok)."""
+    import time
+    words = np.ascontiguousarray(words, np.uint64)
+    msg_off = np.ascontiguousarray(msg_off, np.uint64)
+    n = len(msg_off) - 1
+    lens = np.diff(msg_off).astype(np.int64)
+    slot = np.zeros(n + 1, np.uint64)
+    slot[1:] = np.cumsum(8 * lens + (lens + 1) // 2 + 48)
+    out = np.zeros(int(slot[-1]) + 16, np.uint8)
+    sizes = np.zeros(n, np.uint64)
+    st = np.zeros(n, np.int32)
+    body = np.zeros(max(int(msg_off[-1]), 1), np.uint64)
+    out.fill(1)   # map the pages before the timed region
+    body.fill(1)
+    t0 = time.perf_counter()
+    lib().oracle_write_messages_mt(words.ctypes.data, msg_off.ctypes.data, n, out.ctypes.data,
+                                   slot.ctypes.data, sizes.ctypes.data, st.ctypes.data, threads)
+    t1 = time.perf_counter()
+    ok = bool((st == 0).all())
+    lib().oracle_read_messages_mt(out.ctypes.data, slot.ctypes.data, sizes.ctypes.data, n,
+                                  body.ctypes.data, msg_off.ctypes.data, st.ctypes.data, threads)
+    t2 = time.perf_counter()
+    ok = ok and bool((st == 0).all()) and np.array_equal(body[:len(words)], words)
+    return t1 - t0, t2 - t1, int(sizes.sum()), ok
