@@ -241,15 +241,20 @@ constexpr uint32_t kMaxTileChunks = kWaves * CAPNP_WAVE;
 // ---------------------------------------------------------------------------
 // Staged path.
 
-// Tile tables sized for UNPACK_TILE_WORDS output words (~4.5 packed bytes per
-// word of capacity: P/U up to 0.56).  The walk and the expansion are latency
+// Tile tables sized for UNPACK_TILE_WORDS output words (~5.8 packed bytes per
+// word of capacity: P/U up to 0.72; a tile with more is cut into sub-tiles).  The walk and the expansion are latency
 // chains, so throughput scales with resident workgroups: smaller tiles, more
 // of them per CU (2048 words: ~16 KB of LDS, 9 workgroups per CU).
 #ifndef UNPACK_TILE_WORDS
 #define UNPACK_TILE_WORDS 2048
 #endif
 constexpr uint32_t kTileWords = UNPACK_TILE_WORDS;   // descriptor capacity (output words)
-constexpr uint32_t kTileBytes = kTileWords * 9 / 2;  // LDS capacity for packed bytes
+// LDS capacity for packed bytes: 5.8 bytes per word of capacity (carsales
+// segments pack to 5.6), what is left of 20 KiB per workgroup (8 per CU)
+#ifndef UNPACK_TILE_BYTES
+#define UNPACK_TILE_BYTES (kTileWords * 93 / 16)
+#endif
+constexpr uint32_t kTileBytes = UNPACK_TILE_BYTES;
 // The global path (tiles that do not fit) runs on as many waves as the
 // staged tables' LDS can hold descriptor tables for (8 KiB each).
 constexpr uint32_t kGlobalWaves = kTileWords >= 4096 ? 4 : 2;
@@ -714,36 +719,22 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     return marked;
 }
 
+// One staged sub-tile: chunks [ca, cb) whose packed bytes, output words and
+// count fit the LDS tables (stage, walk, expand).  All threads of the
+// workgroup call it; it ends after its last LDS access of the expansion.
 template <bool SYNC>
-__global__ void __launch_bounds__(kThreads, UNPACK_MIN_WAVES)
-unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-              uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
-              const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
-              uint64_t* __restrict__ consumed, const uint32_t* __restrict__ sync) {
-    __shared__ USmem sm;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-    const uint64_t ca = (uint64_t)blockIdx.x * tc;
-    const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
+__device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __restrict__ in,
+                                              const uint64_t* __restrict__ in_off, uint64_t ca,
+                                              uint64_t cb, uint64_t* __restrict__ out,
+                                              const uint64_t* __restrict__ out_off,
+                                              int32_t* __restrict__ status,
+                                              uint64_t* __restrict__ consumed,
+                                              const uint32_t* __restrict__ sync, uint32_t tid,
+                                              uint32_t lane, uint32_t wave) {
     const uint32_t nc = (uint32_t)(cb - ca);
     const uint64_t B0 = uniform64(in_off[ca]), B1 = uniform64(in_off[cb]);
     const uint64_t W0 = uniform64(out_off[ca]), W1 = uniform64(out_off[cb]);
     const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
-    const bool fits = nc <= kStageChunks && B1 - B0 <= kTileBytes - off0 &&
-                      W1 - W0 <= kTileWords;
-    if (!fits) {
-#if UNPACK_PROF
-        if (tid == 0 && g_utrace) g_utrace[blockIdx.x * 8 + 4] = 1;
-#endif
-        if (wave >= kGlobalWaves) return;
-        for (uint64_t c0 = ca + (uint64_t)wave * CAPNP_WAVE; c0 < cb;
-             c0 += (uint64_t)kGlobalWaves * CAPNP_WAVE)
-            unpack_global<CAPNP_WAVE>(in, in_off, c0, cb, out, out_off, status, consumed,
-                                      sm.desc[wave], lane);
-        return;
-    }
-    StageSmem& S = sm.st;
     UPROF_T(t0);
     const uint32_t nbytes = (uint32_t)(B1 - B0) + off0;
     const uint32_t Wt = (uint32_t)(W1 - W0);
@@ -768,7 +759,6 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
         uint4* dd = reinterpret_cast<uint4*>(S.dpos);
         const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
         for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
-        S.sel[tid] = kExpandTable.s[tid];
         if constexpr (SYNC) {
             // chunk tables and the tile's sync entries (segment b >= 1 starts
             // at global word 32 (kf + b - 1))
@@ -802,7 +792,7 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
 #define UNPACK_ROTATE_WALKER 1
 #endif
 #if UNPACK_ROTATE_WALKER
-    const uint32_t walker = blockIdx.x & (kWaves - 1);
+    const uint32_t walker = (blockIdx.x + (uint32_t)ca) & (kWaves - 1);
 #else
     const uint32_t walker = 0;
 #endif
@@ -878,6 +868,74 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
         tr[3] = t3;
     }
 #endif
+}
+
+// One workgroup per tile of `tc` chunks.  The tile is cut into sub-tiles
+// that fit the LDS tables (normally one: the whole tile), each staged,
+// walked and expanded in turn; a single chunk too large for the tables
+// takes the global path.
+template <bool SYNC>
+__global__ void __launch_bounds__(kThreads, UNPACK_MIN_WAVES)
+unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+              uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
+              const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
+              uint64_t* __restrict__ consumed, const uint32_t* __restrict__ sync) {
+    __shared__ USmem sm;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint64_t ca = (uint64_t)blockIdx.x * tc;
+    const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
+    sm.st.sel[tid] = kExpandTable.s[tid];  // (read only by the staged expansions)
+    {
+        // the usual case, kept straight-line: the whole tile fits
+        const uint64_t B0 = uniform64(in_off[ca]), W0 = uniform64(out_off[ca]);
+        const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
+        if (cb - ca <= kStageChunks && uniform64(in_off[cb]) - B0 <= kTileBytes - off0 &&
+            uniform64(out_off[cb]) - W0 <= kTileWords) {
+            unpack_staged<SYNC>(sm.st, in, in_off, ca, cb, out, out_off, status, consumed, sync,
+                                tid, lane, wave);
+            return;
+        }
+    }
+    bool first = true, resel = false;
+    for (uint64_t lo = ca; lo < cb;) {
+        // the longest prefix of [lo, cb) that fits: <= kStageChunks chunks,
+        // <= kTileWords words, <= kTileBytes bytes from lo's 16-byte block
+        // (the fit is monotone in the prefix, so it is a ballot count)
+        const uint64_t B0 = uniform64(in_off[lo]), W0 = uniform64(out_off[lo]);
+        const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
+        uint32_t k;
+        if (cb - lo <= kStageChunks && uniform64(in_off[cb]) - B0 <= kTileBytes - off0 &&
+            uniform64(out_off[cb]) - W0 <= kTileWords) {
+            k = (uint32_t)(cb - lo);  // the usual case: the rest of the tile fits (scalar loads)
+        } else {
+            const uint64_t c = lo + 1 + lane;
+            const bool fit = c <= cb && in_off[c < cb ? c : cb] - B0 <= kTileBytes - off0 &&
+                             out_off[c < cb ? c : cb] - W0 <= kTileWords;
+            k = (uint32_t)__builtin_popcountll(ballot64(fit));
+        }
+        if (!first) __syncthreads();  // the previous sub-tile is done with LDS
+        first = false;
+        if (k == 0) {  // chunk lo alone does not fit: global walk (wave 0)
+#if UNPACK_PROF
+            if (tid == 0 && g_utrace) g_utrace[blockIdx.x * 8 + 4] = 1;
+#endif
+            if (wave == 0)
+                unpack_global<CAPNP_WAVE>(in, in_off, lo, lo + 1, out, out_off, status, consumed,
+                                          sm.desc[0], lane);
+            resel = true;
+            lo += 1;
+            continue;
+        }
+        if (resel) {  // the global path's descriptor table overlaid the selectors
+            sm.st.sel[tid] = kExpandTable.s[tid];
+            resel = false;
+        }
+        unpack_staged<SYNC>(sm.st, in, in_off, lo, lo + k, out, out_off, status, consumed, sync,
+                            tid, lane, wave);
+        lo += k;
+    }
 }
 
 // ---------------------------------------------------------------------------
