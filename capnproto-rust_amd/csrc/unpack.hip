@@ -30,6 +30,7 @@
 // literal run's bytes are missing (:195-205 + io.rs:26-28) or the input is
 // empty (read() returns 0, io.rs:26-28).
 #include "common.h"
+#include <stdlib.h>
 #include "../../include/capnp_packed.h"
 
 #ifndef UNPACK_SYNC_WAVES
@@ -830,8 +831,13 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
         const uint64_t ow = out_off[c], oe = out_off[c + 1];
         int32_t st;
         uint32_t used;
+#ifndef UNPACK_WALK_PRIO
+#define UNPACK_WALK_PRIO 0  // s_setprio of the walker wave (its hops are a latency chain)
+#endif
+        if (UNPACK_WALK_PRIO) __builtin_amdgcn_s_setprio(UNPACK_WALK_PRIO);
         walk_wave(S, (uint32_t)(gp - B0) + off0, (uint32_t)(ge - B0) + off0,
                   (uint32_t)(ow - W0), (uint32_t)(oe - ow), st, used);
+        if (UNPACK_WALK_PRIO) __builtin_amdgcn_s_setprio(0);
         status[c] = st;
         if (consumed) consumed[c] = used;
     }
@@ -1103,12 +1109,35 @@ extern "C" uint32_t capnp_unpack_sync_tile_words(void) {
     return UNPACK_SYNC_WAVES ? kSubWords : kTileWords;
 }
 
+extern "C" hipError_t capnp_launch_unpack_stream(const uint8_t* d_in, const uint64_t* d_in_off,
+                                                 uint64_t nchunks, uint32_t cpw, uint64_t* d_out,
+                                                 const uint64_t* d_out_off, int32_t* d_status,
+                                                 uint64_t* d_consumed, hipStream_t stream);
+
+// Which kernel decodes a batch without the record sync index: the staged
+// tile kernel (default) or the streaming lane-per-chunk kernel (ustream.hip,
+// CAPNP_UNPACK_KERNEL=stream; measured slower: 1.11 vs 0.95 ms at config 2,
+// its per-hop instruction count is the limit).
+static bool use_stream_kernel() {
+    static const int v = [] {
+        const char* e = getenv("CAPNP_UNPACK_KERNEL");
+        return (e && e[0] == 's') ? 1 : 0;
+    }();
+    return v != 0;
+}
+
 extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d_in_off,
                                           uint64_t nchunks, uint32_t tc, uint64_t* d_out,
                                           const uint64_t* d_out_off, int32_t* d_status,
                                           uint64_t* d_consumed, const uint32_t* d_sync,
                                           hipStream_t stream) {
     if (nchunks == 0) return hipSuccess;
+    if (!d_sync && use_stream_kernel() && !(reinterpret_cast<uintptr_t>(d_out) & 15u)) {
+        // chunks per wave ~ 16 tiles' worth (tc ~ 2048 words / mean chunk)
+        const uint32_t cpw = tc ? (tc * 16 < 256 ? tc * 16 : 256) : 256;
+        return capnp_launch_unpack_stream(d_in, d_in_off, nchunks, cpw, d_out, d_out_off,
+                                          d_status, d_consumed, stream);
+    }
     if (tc == 0) tc = ((d_sync && UNPACK_SYNC_WAVES) ? kSubWords : kTileWords) / 128;
     if (tc > kMaxTileChunks) return hipErrorInvalidValue;  // global path: 4 waves x 64
     const uint64_t blocks = (nchunks + tc - 1) / tc;
