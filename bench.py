@@ -318,13 +318,17 @@ def main():
         ok = ok and ok_ns
     dom = "pack" if pack_ms >= unpack_ms else "unpack"
     achieved = kernels[dom]["GBps"]
-    traffic = None
+    traffic = traffic_rw = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
         key = f"{args.workload}:{n}x{args.chunk_words}" + (":sync" if sync is not None else "")
-        traffic = tj.get(key, {}).get(dom)
-    except (OSError, ValueError):
+        ent = tj.get(key, {}).get(dom)
+        if isinstance(ent, dict):  # per-kernel HBM bytes per launch, read / write split
+            traffic = ent["total"]
+            traffic_rw = {"read": ent["read"], "write": ent["write"],
+                          "source": "profiles/traffic.json (rocprofv3 FETCH_SIZE x 2, WRITE_SIZE)"}
+    except (OSError, ValueError, KeyError):
         pass
 
     e2e = None
@@ -357,7 +361,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
+                "traffic": traffic, "traffic_rw": traffic_rw,
             },
             "roundtrip_frac_of_hbm": round((pack_bytes + unpack_bytes) /
                                            ((pack_ms + unpack_ms) * 1e-3) / 1e9 /

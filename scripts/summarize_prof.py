@@ -1,26 +1,71 @@
 #!/usr/bin/env python3
-"""Summarise a scripts/profile.sh output dir: per-kernel mean duration and
-mean PMC counter values (one row per kernel)."""
+"""Summarise a profile output dir: per-kernel mean duration and mean PMC
+counter values (one row per kernel).
+
+Kernels are matched by their bare name (the identifier before the template
+arguments), so "pack_kernel" does not also match "unpack_kernel": round 1's
+version matched substrings and averaged the unpack launches into the pack
+row (its pack WRITE_SIZE was the mean of pack and unpack).
+
+    summarize_prof.py DIR [kernel ...] [--json OUT]   (HBM bytes per launch:
+    2 x FETCH_SIZE + WRITE_SIZE, KiB -> bytes; FETCH doubled per
+    MI355X_MICROARCH.md on gfx950)
+"""
 import collections
 import csv
 import glob
+import json
 import os
+import re
 import sys
 
-d = sys.argv[1]
-keys = sys.argv[2:] or ["pack_kernel", "unpack_kernel"]
+args = sys.argv[1:]
+out_json = None
+if "--json" in args:
+    i = args.index("--json")
+    out_json = args[i + 1]
+    del args[i:i + 2]
+d = args[0]
+keys = args[1:] or ["pack_kernel", "unpack_kernel"]
+
+
+def _strip(name):
+    return re.sub(r"^void\s+", "", name).replace("(anonymous namespace)::", "")
+
+
+def bare(name):
+    """'void (anonymous namespace)::pack_kernel<true, false>(...)' -> 'pack_kernel'"""
+    name = _strip(name)
+    m = re.search(r"([A-Za-z_][A-Za-z0-9_]*)\s*(<|\()", name)
+    return m.group(1) if m else name
+
+
+def templ(name):
+    """-> 'pack_kernel<true, false>' (one row per instantiation)"""
+    name = _strip(name)
+    m = re.search(r"([A-Za-z_][A-Za-z0-9_]*(<[^()]*>)?)\s*\(", name)
+    return m.group(1) if m else name
+
+
 stats = os.path.join(d, "trace", "run_kernel_stats.csv")
 if os.path.exists(stats):
     for r in csv.DictReader(open(stats)):
-        if any(k in r["Name"] for k in keys):
+        if bare(r["Name"]) in keys:
             print(f'{r["Name"][:60]:60s} calls={r["Calls"]} avg_us={float(r["AverageNs"])/1e3:.1f}')
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        for k in keys:
-            if k in r["Kernel_Name"]:
-                agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if bare(r["Kernel_Name"]) in keys:
+            agg[templ(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+res = {}
 for k, dct in agg.items():
     print(k)
     for c, v in sorted(dct.items()):
-        print(f"   {c:28s} {sum(v)/len(v):16.0f}")
+        print(f"   {c:28s} {sum(v)/len(v):16.0f}   (launches {len(v)})")
+    if "FETCH_SIZE" in dct and "WRITE_SIZE" in dct:
+        rd = 2 * 1024 * sum(dct["FETCH_SIZE"]) / len(dct["FETCH_SIZE"])
+        wr = 1024 * sum(dct["WRITE_SIZE"]) / len(dct["WRITE_SIZE"])
+        res[k] = {"read": int(rd), "write": int(wr), "total": int(rd + wr)}
+        print(f"   HBM per launch: read {rd/1e6:.1f} MB (2 x FETCH), write {wr/1e6:.1f} MB")
+if out_json:
+    json.dump(res, open(out_json, "w"), indent=1)

@@ -1,6 +1,7 @@
 #!/bin/bash
-# FETCH_SIZE and WRITE_SIZE passes (separate runs) over the bench workload,
-# summarised per kernel.   scripts/traffic.sh <outdir> [bench args...]
+# FETCH_SIZE and WRITE_SIZE passes (separate runs) and a kernel trace over
+# the bench workload, summarised per kernel (read / write split).
+#   scripts/traffic.sh <outdir> [bench args...]
 set -uo pipefail
 OUT=$1; shift
 ARGS=("$@")
@@ -10,4 +11,4 @@ export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o run --output-format csv -- python3 bench.py "${ARGS[@]}" > "$OUT/fetch.log" 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o run --output-format csv -- python3 bench.py "${ARGS[@]}" > "$OUT/write.log" 2>&1 || exit 1
 timeout -s KILL 120 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 bench.py "${ARGS[@]}" > "$OUT/trace.log" 2>&1 || exit 1
-python3 scripts/summarize_prof.py "$OUT" pack_kernel unpack_kernel
+python3 scripts/summarize_prof.py "$OUT" pack_kernel unpack_kernel --json "$OUT/traffic.json"
