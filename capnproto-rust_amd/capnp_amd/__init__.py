@@ -8,6 +8,7 @@ from ._lib import CapnpError, STATUS_NAMES  # noqa: F401
 from .codec import Context, default_context, tile_chunks_for, unpack_tile_chunks_for  # noqa: F401
 from . import serialize_packed  # noqa: F401
 from . import serialize  # noqa: F401
+from . import serialize_packed_async  # noqa: F401
 
-__all__ = ["CapnpError", "Context", "default_context", "serialize", "serialize_packed", "tile_chunks_for",
+__all__ = ["CapnpError", "Context", "default_context", "serialize", "serialize_packed", "serialize_packed_async", "tile_chunks_for",
            "unpack_tile_chunks_for"]

@@ -17,9 +17,15 @@ STATUS_NAMES = {
     5: "PrematureEndOfFile", 6: "InvalidNumberOfSegments", 7: "MessageSizeOverflow",
     8: "MessageTooLarge", 9: "BufferNotLargeEnough", 10: "UnalignedSegment",
     11: "MisalignedLength", 12: "MessageEndsPrematurely", 13: "EmptySlice",
-    14: "MessageNotAlignedBy8BytesBoundary", 64: "InvalidArgument", 65: "NoDevice", 66: "HipError",
-    67: "OutOfMemory",
+    14: "MessageNotAlignedBy8BytesBoundary", 15: "Pending", 64: "InvalidArgument", 65: "NoDevice", 66: "HipError",
+    67: "OutOfMemory", 68: "Io",
 }
+PENDING = 15
+IO_PENDING = -1  # CAPNP_IO_PENDING: an inner stream callback has nothing now
+
+# inner-stream callbacks of the streaming adaptors (capnp_read_fn / capnp_write_fn)
+READ_FN = C.CFUNCTYPE(C.c_ssize_t, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t)
+WRITE_FN = C.CFUNCTYPE(C.c_ssize_t, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t)
 
 EXPORTS = [
     "capnp_ctx_create", "capnp_ctx_destroy", "capnp_ctx_stream", "capnp_ctx_last_error",
@@ -35,6 +41,10 @@ EXPORTS = [
     "capnp_stream_pack_batch", "capnp_stream_unpack_batch", "capnp_gpu_write_messages",
     "capnp_gpu_read_messages", "capnp_gpu_unpack_batch_resync", "capnp_resync_stats",
     "capnp_resync_block_bytes", "capnp_gpu_read_flat_messages", "capnp_gpu_gen_carsales",
+    "capnp_packed_writer_new", "capnp_packed_writer_free", "capnp_packed_writer_write",
+    "capnp_packed_writer_flush", "capnp_packed_writer_carried", "capnp_packed_reader_new",
+    "capnp_packed_reader_free", "capnp_packed_reader_read", "capnp_packed_reader_read_exact",
+    "capnp_packed_reader_read_message", "capnp_packed_reader_buffered",
 ]
 
 
@@ -123,6 +133,23 @@ def lib():
     L.capnp_packed_read_message_no_alloc.argtypes = [
         vp, vp, sz, C.POINTER(ReaderOptionsC), i32, vp, sz, C.POINTER(C.c_uint32),
         C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]
+    L.capnp_packed_writer_new.argtypes = [vp, WRITE_FN, vp]
+    L.capnp_packed_writer_new.restype = vp
+    L.capnp_packed_writer_free.argtypes = [vp]
+    L.capnp_packed_writer_write.argtypes = [vp, vp, sz]
+    L.capnp_packed_writer_flush.argtypes = [vp]
+    L.capnp_packed_writer_carried.argtypes = [vp]
+    L.capnp_packed_writer_carried.restype = sz
+    L.capnp_packed_reader_new.argtypes = [vp, READ_FN, vp]
+    L.capnp_packed_reader_new.restype = vp
+    L.capnp_packed_reader_free.argtypes = [vp]
+    L.capnp_packed_reader_read.argtypes = [vp, vp, sz, C.POINTER(C.c_size_t)]
+    L.capnp_packed_reader_read_exact.argtypes = [vp, vp, sz, C.POINTER(C.c_size_t)]
+    L.capnp_packed_reader_read_message.argtypes = [vp, C.POINTER(ReaderOptionsC), i32, vp, sz,
+                                                   vp, C.POINTER(C.c_uint32),
+                                                   C.POINTER(C.c_uint64)]
+    L.capnp_packed_reader_buffered.argtypes = [vp]
+    L.capnp_packed_reader_buffered.restype = sz
     _lib = L
     return L
 

@@ -11,11 +11,16 @@ Same names, argument meaning and error behaviour as the reference:
     PackedWrite(inner).write_all(buf)                serialize_packed.rs:300-440
     PackedRead(inner).read(n) / read_exact(n)        serialize_packed.rs:76-229
 
-`read` is a BufRead over bytes (`SliceRead`, the `&[u8]` impl of io.rs:
-178-186): a successful read consumes exactly the bytes the message used, so
-a stream of messages is read by calling try_read_message until it returns
-None.  Errors raise CapnpError whose `.kind` is the capnp::ErrorKind name.
-Every transform runs in the HIP kernels; nothing here touches bytes.
+`read` is a BufRead (io.rs:35-38): `SliceRead` (the `&[u8]` impl), or
+`BufReader` over any raw reader, whose fill_buf() hands out one buffer at a
+time and refills after consume() — as PackedRead's refresh_buffer!
+(serialize_packed.rs:59-74) does, a read unit that runs past the current
+buffer consumes it and continues in the next one.  A successful read
+consumes exactly the bytes the message used, so a stream of messages is
+read by calling try_read_message until it returns None; a failed one leaves
+the reader where the reference leaves it (every buffer it had to look past
+consumed).  Errors raise CapnpError whose `.kind` is the capnp::ErrorKind
+name.  Every transform runs in the HIP kernels; nothing here touches bytes.
 """
 import ctypes as C
 from dataclasses import dataclass
@@ -64,6 +69,53 @@ class SliceRead:
         return self.pos >= len(self.data)
 
 
+class BufReader:
+    """std::io::BufReader over a raw reader (`.read(n) -> bytes`, b"" at the
+    end): fill_buf() returns the current buffer of up to `capacity` bytes,
+    reading the next one only once it is consumed."""
+
+    def __init__(self, raw, capacity=8192):
+        self.raw = raw
+        self.capacity = capacity
+        self.buf = b""
+        self.pos = 0
+
+    def fill_buf(self):
+        if self.pos >= len(self.buf):
+            self.buf = bytes(self.raw.read(self.capacity))
+            self.pos = 0
+        return memoryview(self.buf)[self.pos:]
+
+    def consume(self, n):
+        self.pos = min(self.pos + n, len(self.buf))
+
+
+# statuses that mean "the unit ran past the bytes in hand"
+_NEEDS_MORE = (2, 4, 5)  # PrematureEndOfPackedInput, FailedToFill, PrematureEndOfFile
+
+
+def _refilling(r, attempt):
+    """Runs attempt(data) on the reader's current buffer; while it fails for
+    lack of input and the reader has more, consumes that buffer (the
+    reference's refresh_buffer!) and retries over everything seen so far.
+    On success consumes exactly the bytes used: `attempt` returns (status,
+    used, result)."""
+    seen = b""
+    while True:
+        cur = bytes(r.fill_buf())
+        data = seen + cur
+        st, used, res = attempt(data)
+        if st in _NEEDS_MORE and len(cur) > 0:
+            r.consume(len(cur))
+            if len(r.fill_buf()) > 0:
+                seen = data
+                continue
+            return st, res  # nothing more: the failure stands over all the bytes seen
+        if st == _lib.OK:
+            r.consume(used - len(seen))
+        return st, res
+
+
 class OwnedSegments:
     """Segments of a read message (serialize.rs:170-211): one contiguous
     8-byte-aligned buffer plus (start, end) word indices."""
@@ -90,7 +142,7 @@ class OwnedSegments:
 
 
 def _as_reader(read):
-    return read if isinstance(read, SliceRead) else SliceRead(read)
+    return read if hasattr(read, "fill_buf") else SliceRead(read)
 
 
 def _np_u8(buf):
@@ -151,14 +203,17 @@ class PackedRead:
         return self._read_exact(n)
 
     def _read_exact(self, n):
-        buf = bytes(self.inner.fill_buf())
         out = np.empty(n, np.uint8)
-        used = C.c_size_t(0)
-        a = _np_u8(buf)
-        st = _lib.lib().capnp_unpack(self.ctx.handle, a.ctypes.data, len(buf), C.byref(used),
-                                     out.ctypes.data, n)
+
+        def attempt(data):
+            used = C.c_size_t(0)
+            a = _np_u8(data)
+            st = _lib.lib().capnp_unpack(self.ctx.handle, a.ctypes.data, len(data),
+                                         C.byref(used), out.ctypes.data, n)
+            return st, used.value, None
+
+        st, _ = _refilling(self.inner, attempt)
         _check(st, self.ctx)
-        self.inner.consume(used.value)
         return out.tobytes()
 
 
@@ -208,30 +263,33 @@ def write_message(write, segments, ctx=None):
 def _read(read, options, try_mode, ctx):
     ctx = ctx or default_context()
     r = _as_reader(read)
-    buf = bytes(r.fill_buf())
-    a = _np_u8(buf)
-    # a packed stream of B bytes decodes to at most ~128 words per byte;
-    # grow and retry on BufferNotLargeEnough
-    cap = max(64, 16 * len(buf))
-    while True:
-        body = np.empty(cap, np.uint64)
-        segs = np.empty(SEGMENTS_COUNT_LIMIT, np.uint32)
-        nseg, used = C.c_uint32(0), C.c_size_t(0)
-        opts = (options or DEFAULT_READER_OPTIONS)._c()
-        st = _lib.lib().capnp_packed_read_message(ctx.handle, a.ctypes.data, len(buf),
-                                                  C.byref(opts), int(try_mode),
-                                                  body.ctypes.data, cap, segs.ctypes.data,
-                                                  C.byref(nseg), C.byref(used))
-        if st == 9 and cap < 256 * (len(buf) + 1):
-            cap *= 8
-            continue
-        break
+    opts = (options or DEFAULT_READER_OPTIONS)._c()
+
+    def attempt(data):
+        a = _np_u8(data)
+        cap = 1 << 12
+        while True:
+            body = np.empty(cap, np.uint64)
+            segs = np.empty(SEGMENTS_COUNT_LIMIT, np.uint32)
+            nseg, used = C.c_uint32(0), C.c_size_t(0)
+            st = _lib.lib().capnp_packed_read_message(ctx.handle, a.ctypes.data, len(data),
+                                                      C.byref(opts), int(try_mode),
+                                                      body.ctypes.data, cap, segs.ctypes.data,
+                                                      C.byref(nseg), C.byref(used))
+            if st == 9:  # BufferNotLargeEnough: the table says how many words
+                need = int(segs[:nseg.value].astype(np.uint64).sum())
+                if need > cap:
+                    cap = need
+                    continue
+            return st, used.value, (body, segs, nseg.value)
+
+    st, res = _refilling(r, attempt)
     if st == _lib.NONE:
         return None
     _check(st, ctx)
-    r.consume(used.value)
-    total = int(segs[:nseg.value].astype(np.uint64).sum())
-    return OwnedSegments(body[:total], segs[:nseg.value])
+    body, segs, nseg = res
+    total = int(segs[:nseg].astype(np.uint64).sum())
+    return OwnedSegments(body[:total], segs[:nseg])
 
 
 def read_message(read, options=None, ctx=None):
@@ -248,19 +306,23 @@ def try_read_message(read, options=None, ctx=None):
 def _read_no_alloc(read, buffer, options, try_mode, ctx):
     ctx = ctx or default_context()
     r = _as_reader(read)
-    data = bytes(r.fill_buf())
-    a = _np_u8(data)
     nb = np.frombuffer(buffer, dtype=np.uint8) if not isinstance(buffer, np.ndarray) else \
         buffer.view(np.uint8)
-    nseg, tb, bb, used = C.c_uint32(0), C.c_size_t(0), C.c_size_t(0), C.c_size_t(0)
+    nseg, tb, bb = C.c_uint32(0), C.c_size_t(0), C.c_size_t(0)
     opts = (options or DEFAULT_READER_OPTIONS)._c()
-    st = _lib.lib().capnp_packed_read_message_no_alloc(
-        ctx.handle, a.ctypes.data, len(data), C.byref(opts), int(try_mode), nb.ctypes.data,
-        nb.nbytes, C.byref(nseg), C.byref(tb), C.byref(bb), C.byref(used))
+
+    def attempt(data):
+        a = _np_u8(data)
+        used = C.c_size_t(0)
+        st = _lib.lib().capnp_packed_read_message_no_alloc(
+            ctx.handle, a.ctypes.data, len(data), C.byref(opts), int(try_mode), nb.ctypes.data,
+            nb.nbytes, C.byref(nseg), C.byref(tb), C.byref(bb), C.byref(used))
+        return st, used.value, None
+
+    st, _ = _refilling(r, attempt)
     if st == _lib.NONE:
         return None
     _check(st, ctx)
-    r.consume(used.value)
     body = nb[tb.value:tb.value + bb.value].view(np.uint64)
     lens = []
     t = nb[:tb.value].view(np.uint32)

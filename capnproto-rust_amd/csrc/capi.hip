@@ -85,6 +85,8 @@ size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
 
 }  // namespace
 
+constexpr size_t kTablePrefixBytes = 4096;  // >= 10 bytes x (1 + 256) table words
+
 struct capnp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -999,12 +1001,18 @@ static capnp_status read_message_impl(capnp_ctx* ctx, const uint8_t* in, size_t 
                                       uint8_t** d_body_out) {
     capnp_reader_options o = opts ? *opts : capnp_default_reader_options();
     const size_t o_in = 0;
-    capnp_status st = ensure_stage(ctx, round16(in_len + 16) + 64);
+    // Only the table's read units go to the device here: a table of <= 511
+    // segments is <= 257 words, which decode from at most 10 bytes each, so
+    // a 4 KiB prefix holds it whatever the stream (the body is staged by
+    // read_body from the table's end, bounded the same way).  A call costs
+    // O(message), not O(remaining stream).
+    const size_t pre = std::min<size_t>(in_len, kTablePrefixBytes);
+    capnp_status st = ensure_stage(ctx, round16(pre + 16) + 64);
     if (st != CAPNP_OK) return st;
     uint8_t* d = ctx->d_stage;
     hipStream_t s = ctx->stream;
-    if (in_len) HIP_TRY(hipMemcpyAsync(d + o_in, in, in_len, hipMemcpyHostToDevice, s));
-    HIP_TRY(capnp_launch_frame(d + o_in, in_len, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
+    if (pre) HIP_TRY(hipMemcpyAsync(d + o_in, in, pre, hipMemcpyHostToDevice, s));
+    HIP_TRY(capnp_launch_frame(d + o_in, pre, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
                                o.traversal_limit_in_words, (uint32_t)(o.has_traversal_limit != 0),
                                buffer_len, ctx->d_frame, s));
     HIP_TRY(hipMemcpyAsync(ctx->h_frame, ctx->d_frame, sizeof(FrameResult), hipMemcpyDeviceToHost, s));
@@ -1014,29 +1022,41 @@ static capnp_status read_message_impl(capnp_ctx* ctx, const uint8_t* in, size_t 
     return CAPNP_OK;
 }
 
-// Decodes the body unit described by the device frame record into host memory.
-static capnp_status read_body(capnp_ctx* ctx, const FrameResult& fr, uint8_t* host_out,
-                              uint64_t* body_consumed) {
+// Decodes the body unit (read_exact of total_words words after the table,
+// serialize.rs:514-524) into host memory.  The stream decodes at most 10
+// bytes per word, so at most 10 * words + 16 bytes after the table are
+// staged; the result (status, consumed, words) comes back in one copy.
+static capnp_status read_body(capnp_ctx* ctx, const FrameResult& fr, const uint8_t* in,
+                              size_t in_len, uint8_t* host_out, uint64_t* body_consumed) {
     *body_consumed = 0;
     if (fr.total_words == 0) return CAPNP_OK;
-    const size_t o_st = round16(fr.total_words * 8);
-    capnp_status st = ensure_buf(ctx, &ctx->d_body, &ctx->body_cap, o_st + 64);
+    const size_t rem = in_len - std::min<size_t>(in_len, fr.table_consumed);
+    const size_t take = std::min<size_t>(rem, fr.total_words * 10 + 16);
+    const size_t o_in = 0, o_off = round16(take + 16), o_res = o_off + 32;
+    capnp_status st = ensure_stage(ctx, o_res + 64);
     if (st != CAPNP_OK) return st;
+    const size_t o_st = round16(fr.total_words * 8);
+    st = ensure_buf(ctx, &ctx->d_body, &ctx->body_cap, o_st + 64);
+    if (st != CAPNP_OK) return st;
+    uint8_t* di = ctx->d_stage;
     uint8_t* d = ctx->d_body;
     hipStream_t s = ctx->stream;
-    HIP_TRY(capnp_launch_unpack(ctx->d_stage, ctx->d_frame->body_in_off, 1, 0,
-                                reinterpret_cast<uint64_t*>(d), ctx->d_frame->body_out_off,
+    const uint64_t offs[4] = {0, take, 0, fr.total_words};
+    if (take) HIP_TRY(hipMemcpyAsync(di + o_in, in + fr.table_consumed, take,
+                                     hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(di + o_off, offs, sizeof(offs), hipMemcpyHostToDevice, s));
+    HIP_TRY(capnp_launch_unpack(di + o_in, reinterpret_cast<uint64_t*>(di + o_off), 1, 0,
+                                reinterpret_cast<uint64_t*>(d),
+                                reinterpret_cast<uint64_t*>(di + o_off + 16),
                                 reinterpret_cast<int32_t*>(d + o_st),
                                 reinterpret_cast<uint64_t*>(d + o_st + 16), nullptr, s));
-    int32_t status = 0;
-    uint64_t used = 0;
-    HIP_TRY(hipMemcpyAsync(&status, d + o_st, 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(&used, d + o_st + 16, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    if (status != CAPNP_OK) return (capnp_status)status;
+    uint64_t res[3] = {0, 0, 0};  // status (low 32 bits), pad, consumed
+    HIP_TRY(hipMemcpyAsync(res, d + o_st, 24, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(host_out, d, fr.total_words * 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    *body_consumed = used;
+    const int32_t status = (int32_t)(uint32_t)res[0];
+    if (status != CAPNP_OK) return (capnp_status)status;
+    *body_consumed = res[2];
     return CAPNP_OK;
 }
 
@@ -1053,9 +1073,14 @@ capnp_status capnp_packed_read_message(capnp_ctx* ctx, const uint8_t* in, size_t
     capnp_status st = read_message_impl(ctx, in, in_len, opts, try_mode, 0, 0, &fr, nullptr);
     if (st != CAPNP_OK) return st;
     if (fr.status != CAPNP_OK) return (capnp_status)fr.status;
-    if (fr.total_words > body_cap_words) return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;
+    if (fr.total_words > body_cap_words) {
+        // the table is read: report it, so the caller can size the body
+        memcpy(seg_words_out, fr.seg_words, fr.nseg * sizeof(uint32_t));
+        *nseg_out = fr.nseg;
+        return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;
+    }
     uint64_t used = 0;
-    st = read_body(ctx, fr, reinterpret_cast<uint8_t*>(body), &used);
+    st = read_body(ctx, fr, in, in_len, reinterpret_cast<uint8_t*>(body), &used);
     if (st != CAPNP_OK) return st;
     memcpy(seg_words_out, fr.seg_words, fr.nseg * sizeof(uint32_t));
     *nseg_out = fr.nseg;
@@ -1081,7 +1106,7 @@ capnp_status capnp_packed_read_message_no_alloc(capnp_ctx* ctx, const uint8_t* i
     if (fr.status == CAPNP_OK) memcpy(buffer, fr.table, fr.table_bytes);
     if (fr.status != CAPNP_OK) return (capnp_status)fr.status;
     uint64_t used = 0;
-    st = read_body(ctx, fr, buffer + fr.table_bytes, &used);
+    st = read_body(ctx, fr, in, in_len, buffer + fr.table_bytes, &used);
     if (st != CAPNP_OK) return st;
     *nseg_out = fr.nseg;
     *table_bytes_out = fr.table_bytes;

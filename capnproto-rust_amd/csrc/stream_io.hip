@@ -1,0 +1,402 @@
+// stream_io.hip — streaming adaptors over caller-supplied byte streams (host
+// C++ over the gfx950 kernels; no transform runs on the CPU here).
+//
+//   capnp_packed_writer   the async PackedWrite of capnp-futures
+//                         (capnp-futures/src/serialize_packed.rs:330-521):
+//                         bytes arrive in arbitrary pieces, partial words are
+//                         carried between calls (:370-393)
+//   capnp_packed_reader   the async PackedRead (:34-225) and a message reader
+//                         on top of it (capnp-futures/src/serialize.rs
+//                         read_message / try_read_message, :31-137), over a
+//                         read function that may return short reads or
+//                         "pending"
+//
+// Writer.  The async writer's output depends only on where the write calls
+// split the input: in one poll_write, a word completed from the carried
+// bytes and every whole word after it form one chunk whose runs are found in
+// that call's bytes only (WriteWord stage, :407-452: "see how long of a run
+// we can make" scans `inbuf`), and the bytes after the last whole word are
+// carried.  So a write call is one PACK chunk, exactly as a sync write_all
+// (serialize_packed.rs:300-440) of those words.  Chunks are collected and
+// packed as one batch by the GPU pack kernel (on flush, or every kBatchWords
+// words), and the packed bytes drain to the inner writer, which may accept
+// them piecemeal or report pending.
+//
+// Reader.  Packed input is pulled from the inner reader into a staging
+// buffer and decoded by the GPU unpack kernel in whole-word units
+// (PackedRead::read semantics, serialize_packed.rs:80-228); decoded bytes
+// wait in an output buffer, so reads of any size (down to one byte,
+// :186-205 of the async twin) are served from it.  A unit that ends inside a
+// run (DidNotEndCleanly) is retried larger; a unit that needs more input
+// pulls more.  At the end of the stream with a partial record left the read
+// fails with PrematureEndOfFile (the async reader's UnexpectedEof, :109-114,
+// :164-168, :207-212, which capnp maps to PrematureEndOfFile, lib.rs:481-499).
+// Divergence (documented): the async reader hands out the head word of a
+// literal run whose raw words the stream then lacks before failing; here
+// the read that would return that word fails at once.  Any read covering the
+// truncated run fails in both.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/capnp_packed.h"
+
+namespace {
+
+constexpr size_t kBatchWords = size_t(1) << 17;  // writer: pack every 1 MiB of input
+constexpr size_t kPull = size_t(1) << 16;        // reader: bytes asked of the inner reader
+
+struct Drain {
+    std::vector<uint8_t> q;
+    size_t pos = 0;
+};
+
+uint64_t get_u64(const uint8_t* p) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return v;
+}
+
+}  // namespace
+
+struct capnp_packed_writer {
+    capnp_ctx* ctx;
+    capnp_write_fn fn;
+    void* user;
+    uint8_t part[8];
+    size_t npart = 0;                   // carried bytes of an incomplete word
+    std::vector<uint64_t> words;        // chunks not yet packed, back to back
+    std::vector<uint64_t> off{0};       // their word offsets
+    Drain out;                          // packed bytes the inner writer has not taken
+};
+
+struct capnp_packed_reader {
+    capnp_ctx* ctx;
+    capnp_read_fn fn;
+    void* user;
+    std::vector<uint8_t> in;  // staged packed input
+    size_t ip = 0;            // bytes of `in` already decoded
+    bool eof = false;
+    std::vector<uint8_t> dec;  // decoded bytes not yet handed out
+    size_t dp = 0;
+};
+
+namespace {
+
+capnp_status writer_pack(capnp_packed_writer* w) {
+    const size_t n = w->off.size() - 1;
+    if (n == 0) return CAPNP_OK;
+    const uint64_t nw = w->off[n];
+    const size_t cap = capnp_packed_batch_bound_bytes(nw, n);
+    const size_t base = w->out.q.size();
+    w->out.q.resize(base + cap);
+    std::vector<uint64_t> oo(n + 1);
+    capnp_status st = capnp_pack_batch_host(w->ctx, w->words.data(), w->off.data(), n,
+                                            w->out.q.data() + base, cap, oo.data());
+    if (st != CAPNP_OK) {
+        w->out.q.resize(base);
+        return st;
+    }
+    w->out.q.resize(base + oo[n]);
+    w->words.clear();
+    w->off.assign(1, 0);
+    return CAPNP_OK;
+}
+
+// Hands queued bytes to the inner writer until it is empty or pends.
+capnp_status writer_drain(capnp_packed_writer* w) {
+    while (w->out.pos < w->out.q.size()) {
+        const ptrdiff_t r = w->fn(w->user, w->out.q.data() + w->out.pos,
+                                  w->out.q.size() - w->out.pos);
+        if (r == CAPNP_IO_PENDING) return CAPNP_PENDING;
+        if (r <= 0) return CAPNP_E_IO;  // an error, or a writer that takes nothing
+        w->out.pos += (size_t)r;
+    }
+    w->out.q.clear();
+    w->out.pos = 0;
+    return CAPNP_OK;
+}
+
+// Pulls more packed input; CAPNP_OK with bytes added, CAPNP_NONE at the end
+// of the stream, CAPNP_PENDING, or an I/O error.
+capnp_status reader_pull(capnp_packed_reader* r) {
+    if (r->eof) return CAPNP_NONE;
+    if (r->ip > 0 && r->ip * 2 >= r->in.size()) {  // drop the decoded prefix
+        r->in.erase(r->in.begin(), r->in.begin() + (ptrdiff_t)r->ip);
+        r->ip = 0;
+    }
+    const size_t base = r->in.size();
+    r->in.resize(base + kPull);
+    const ptrdiff_t got = r->fn(r->user, r->in.data() + base, kPull);
+    if (got == CAPNP_IO_PENDING) {
+        r->in.resize(base);
+        return CAPNP_PENDING;
+    }
+    if (got < 0) {
+        r->in.resize(base);
+        return CAPNP_E_IO;
+    }
+    r->in.resize(base + (size_t)got);
+    if (got == 0) {
+        r->eof = true;
+        return CAPNP_NONE;
+    }
+    return CAPNP_OK;
+}
+
+// One PackedRead::read of `nw` words at the current position, on the GPU.
+// A stream decodes at most 10 input bytes per output word (tag, 8 bytes,
+// count), so only that much of the staged input is handed to the kernel.
+capnp_status reader_unit(capnp_packed_reader* r, size_t nw, std::vector<uint8_t>& out,
+                         size_t* used, int32_t* status) {
+    const size_t avail = r->in.size() - r->ip;
+    const size_t take = std::min(avail, nw * 10 + 16);
+    out.resize(nw * 8);
+    uint64_t io[2] = {0, take}, oo[2] = {0, nw};
+    uint64_t cons = 0;
+    capnp_status st = capnp_unpack_batch_host(r->ctx, r->in.data() + r->ip, io, 1,
+                                              reinterpret_cast<uint64_t*>(out.data()), oo, status,
+                                              &cons);
+    *used = (size_t)cons;
+    return st;
+}
+
+// Decodes at least one word into r->dec (empty only at a clean end of the
+// stream).  `want` = words the caller asked for; units are at least
+// kMinUnit words (small reads are served from the decoded surplus), but an
+// inner reader that pends while the caller's own words are staged gets
+// those decoded rather than a pending answer.
+constexpr size_t kMinUnit = 256;
+
+capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
+    want = std::max<size_t>(want, 1);
+    size_t nw = std::max(want, kMinUnit);
+    std::vector<uint8_t> out;
+    for (;;) {
+        if (r->ip == r->in.size()) {
+            capnp_status p = reader_pull(r);
+            if (p == CAPNP_NONE) return CAPNP_OK;  // clean end: nothing decoded
+            if (p != CAPNP_OK) return p;
+            continue;
+        }
+        size_t used = 0;
+        int32_t st = 0;
+        capnp_status e = reader_unit(r, nw, out, &used, &st);
+        if (e != CAPNP_OK) return e;
+        if (st == CAPNP_OK) {
+            r->ip += used;
+            r->dec.swap(out);
+            r->dp = 0;
+            return CAPNP_OK;
+        }
+        if (st == CAPNP_E_DID_NOT_END_CLEANLY) {  // a run crosses the unit end
+            nw = nw * 2 + 256;
+            continue;
+        }
+        // PrematureEnd / FailedToFill: the unit needs more input
+        capnp_status p = reader_pull(r);
+        if (p == CAPNP_OK) continue;
+        if (p != CAPNP_NONE && p != CAPNP_PENDING) return p;
+        // nothing more now (pending) or ever (end of stream): the largest unit
+        // the staged bytes decode (DidNotEndCleanly = too small, PrematureEnd
+        // / FailedToFill = too large), else pending / a partial record
+        size_t lo = 1, hi = nw;
+        while (lo <= hi) {
+            const size_t mid = lo + (hi - lo) / 2;
+            e = reader_unit(r, mid, out, &used, &st);
+            if (e != CAPNP_OK) return e;
+            if (st == CAPNP_OK) {
+                r->ip += used;
+                out.resize(mid * 8);
+                r->dec.swap(out);
+                r->dp = 0;
+                return CAPNP_OK;
+            }
+            if (st == CAPNP_E_DID_NOT_END_CLEANLY) lo = mid + 1;
+            else hi = mid - 1;
+        }
+        return p == CAPNP_PENDING ? CAPNP_PENDING : CAPNP_E_PREMATURE_END_OF_FILE;  // UnexpectedEof
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+capnp_packed_writer* capnp_packed_writer_new(capnp_ctx* ctx, capnp_write_fn fn, void* user) {
+    if (!ctx || !fn) return nullptr;
+    auto* w = new capnp_packed_writer();
+    w->ctx = ctx;
+    w->fn = fn;
+    w->user = user;
+    return w;
+}
+
+void capnp_packed_writer_free(capnp_packed_writer* w) { delete w; }
+
+capnp_status capnp_packed_writer_write(capnp_packed_writer* w, const uint8_t* buf, size_t len) {
+    if (!w || (len && !buf)) return CAPNP_E_INVALID_ARGUMENT;
+    size_t k = 0;
+    const size_t w0 = w->words.size();
+    if (w->npart) {  // Start stage: complete the carried word (:370-393)
+        const size_t t = std::min(8 - w->npart, len);
+        memcpy(w->part + w->npart, buf, t);
+        w->npart += t;
+        k = t;
+        if (w->npart == 8) {
+            w->words.push_back(get_u64(w->part));
+            w->npart = 0;
+        }
+    }
+    const size_t m = (len - k) / 8;
+    if (m) {
+        const size_t b = w->words.size();
+        w->words.resize(b + m);
+        memcpy(w->words.data() + b, buf + k, m * 8);
+        k += m * 8;
+    }
+    if (k < len) {  // carry the incomplete word
+        memcpy(w->part + w->npart, buf + k, len - k);
+        w->npart += len - k;
+    }
+    if (w->words.size() > w0) w->off.push_back(w->words.size());  // this call's chunk
+    if (w->words.size() >= kBatchWords) {
+        capnp_status st = writer_pack(w);
+        if (st != CAPNP_OK) return st;
+        st = writer_drain(w);
+        if (st != CAPNP_OK && st != CAPNP_PENDING) return st;
+    }
+    return CAPNP_OK;
+}
+
+capnp_status capnp_packed_writer_flush(capnp_packed_writer* w) {
+    if (!w) return CAPNP_E_INVALID_ARGUMENT;
+    capnp_status st = writer_pack(w);
+    if (st != CAPNP_OK) return st;
+    return writer_drain(w);
+}
+
+size_t capnp_packed_writer_carried(const capnp_packed_writer* w) { return w ? w->npart : 0; }
+
+capnp_packed_reader* capnp_packed_reader_new(capnp_ctx* ctx, capnp_read_fn fn, void* user) {
+    if (!ctx || !fn) return nullptr;
+    auto* r = new capnp_packed_reader();
+    r->ctx = ctx;
+    r->fn = fn;
+    r->user = user;
+    return r;
+}
+
+void capnp_packed_reader_free(capnp_packed_reader* r) { delete r; }
+
+capnp_status capnp_packed_reader_read(capnp_packed_reader* r, uint8_t* out, size_t len,
+                                      size_t* nread) {
+    if (!r || !nread || (len && !out)) return CAPNP_E_INVALID_ARGUMENT;
+    *nread = 0;
+    if (len == 0) return CAPNP_OK;
+    if (r->dp == r->dec.size()) {
+        capnp_status st = reader_fill(r, (len + 7) / 8);
+        if (st != CAPNP_OK) return st;
+        if (r->dec.empty()) return CAPNP_OK;  // clean end of stream: Ok(0)
+    }
+    const size_t n = std::min(len, r->dec.size() - r->dp);
+    memcpy(out, r->dec.data() + r->dp, n);
+    r->dp += n;
+    if (r->dp == r->dec.size()) {
+        r->dec.clear();
+        r->dp = 0;
+    }
+    *nread = n;
+    return CAPNP_OK;
+}
+
+// read_exact (futures AsyncReadExt::read_exact): loops over reads, retrying a
+// pending inner reader; PrematureEndOfFile if the stream ends first.
+// *got (optional) = bytes delivered before an error.
+capnp_status capnp_packed_reader_read_exact(capnp_packed_reader* r, uint8_t* out, size_t len,
+                                            size_t* got) {
+    if (!r || (len && !out)) return CAPNP_E_INVALID_ARGUMENT;
+    size_t k = 0;
+    if (got) *got = 0;
+    while (k < len) {
+        size_t n = 0;
+        capnp_status st = capnp_packed_reader_read(r, out + k, len - k, &n);
+        if (st == CAPNP_PENDING) continue;
+        if (got) *got = k;
+        if (st != CAPNP_OK) return st;
+        if (n == 0) return CAPNP_E_PREMATURE_END_OF_FILE;
+        k += n;
+    }
+    if (got) *got = k;
+    return CAPNP_OK;
+}
+
+// capnp-futures serialize::try_read_message / read_message over a
+// PackedRead (capnp-futures/src/serialize_packed.rs:233-258 ->
+// capnp-futures/src/serialize.rs:31-137): the segment table (a first word,
+// then the rest of the table), then the body.  Checks as capnp's
+// read_segment_table (serialize.rs:448-510): segment count 1..511, the
+// traversal limit; the body goes to `body` (body_cap_words words; on
+// BufferNotLargeEnough *body_words holds the words needed).
+capnp_status capnp_packed_reader_read_message(capnp_packed_reader* r,
+                                              const capnp_reader_options* opts, int try_mode,
+                                              uint64_t* body, size_t body_cap_words,
+                                              uint32_t* seg_words, uint32_t* nseg_out,
+                                              uint64_t* body_words) {
+    if (!r || !seg_words || !nseg_out) return CAPNP_E_INVALID_ARGUMENT;
+    const capnp_reader_options o = opts ? *opts : capnp_default_reader_options();
+    *nseg_out = 0;
+    if (body_words) *body_words = 0;
+    uint8_t w0[8];
+    size_t got = 0;
+    capnp_status st;
+    do {  // the first read tells a clean end (Ok(0)) from a partial record
+        st = capnp_packed_reader_read(r, w0, 8, &got);
+    } while (st == CAPNP_PENDING);
+    if (st != CAPNP_OK) return st;
+    if (got == 0) return try_mode ? CAPNP_NONE : CAPNP_E_PREMATURE_END_OF_FILE;
+    if (got < 8) {
+        st = capnp_packed_reader_read_exact(r, w0 + got, 8 - got, nullptr);
+        if (st != CAPNP_OK) return st;
+    }
+    uint32_t u0, l0;
+    memcpy(&u0, w0, 4);
+    memcpy(&l0, w0 + 4, 4);
+    const uint32_t nseg = u0 + 1u;
+    if (nseg == 0 || nseg >= 512) return CAPNP_E_INVALID_NUMBER_OF_SEGMENTS;
+    seg_words[0] = l0;
+    uint64_t total = l0;
+    if (nseg > 1) {
+        const size_t rest = nseg < 4 ? 8 : (size_t)(nseg & ~1u) * 4;
+        uint8_t t[512 * 4];
+        st = capnp_packed_reader_read_exact(r, t, rest, nullptr);
+        if (st != CAPNP_OK) return st;
+        for (uint32_t i = 1; i < nseg; i++) {
+            uint32_t l;
+            memcpy(&l, t + 4 * (i - 1), 4);
+            seg_words[i] = l;
+            total += l;
+        }
+    }
+    *nseg_out = nseg;  // (the table is read: its lengths are valid from here on)
+    if (o.has_traversal_limit && total > o.traversal_limit_in_words)
+        return CAPNP_E_MESSAGE_TOO_LARGE;
+    if (body_words) *body_words = total;
+    if (total > body_cap_words || (total && !body)) return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;
+    if (total) {
+        st = capnp_packed_reader_read_exact(r, reinterpret_cast<uint8_t*>(body), total * 8,
+                                            nullptr);
+        if (st != CAPNP_OK) return st;
+    }
+    return CAPNP_OK;
+}
+
+// Bytes staged but not yet decoded, and decoded but not yet read.
+size_t capnp_packed_reader_buffered(const capnp_packed_reader* r) {
+    return r ? (r->in.size() - r->ip) + (r->dec.size() - r->dp) : 0;
+}
+
+}  // extern "C"

@@ -230,10 +230,12 @@ __device__ void unpack_global(const uint8_t* __restrict__ in, const uint64_t* __
     }
     if (have) {
         status[c] = st;
-        // bytes used: all of them when a literal run ran dry (the reference
-        // copies what is there before read_exact fails), none on other errors
+        // consumed = where the reference leaves a &[u8] reader: the bytes used
+        // on success; all of them on PrematureEnd (refresh_buffer! consumes
+        // the buffer first, serialize_packed.rs:59-74) and on FailedToFill
+        // (consume + read_exact, :195-205); none on DidNotEndCleanly
         if (consumed)
-            consumed[c] = st == ST_OK ? p - p_start : (st == ST_FAILED_FILL ? in_end - p_start : 0);
+            consumed[c] = st == ST_OK ? p - p_start : (st == ST_NOT_CLEAN ? 0 : in_end - p_start);
     }
 }
 
@@ -439,7 +441,7 @@ __device__ __forceinline__ void walk_chunk(SM& S, uint32_t p, uint32_t pe, uint3
         b1 = nb1;
         b9 = nb9;
     }
-    used = st == ST_OK ? p - p0 : (st == ST_FAILED_FILL ? pe - p0 : 0);
+    used = st == ST_OK ? p - p0 : (st == ST_NOT_CLEAN ? 0u : pe - p0);
 }
 
 // Branch-free walk of the walker wave: lane = chunk, same contract as

@@ -32,8 +32,9 @@
 // missing (:59-74, :109-145); DidNotEndCleanly when a run overruns the output
 // (:166-170, :183-187); FailedToFillTheWholeBuffer when a literal run's bytes
 // are missing (:195-205 + io.rs:26-28) or the input is empty (read() returns
-// 0).  consumed = bytes used on success, the whole chunk on FailedToFill, 0
-// otherwise (the oracle's read_exact, oracle/packed_oracle.c).
+// 0).  consumed = bytes used on success, the whole chunk on PrematureEnd and
+// FailedToFill, 0 on DidNotEndCleanly (where the reference leaves a &[u8]
+// reader; the oracle's read_exact, oracle/packed_oracle.c).
 #include "common.h"
 
 #ifndef US_D
@@ -277,7 +278,7 @@ unpack_stream_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict_
                         const uint64_t c = c_lo + dc;
                         status[c] = st;
                         if (consumed)
-                            consumed[c] = st == ST_OK ? p - p0 : (st == ST_FAILED_FILL ? pe - p0 : 0u);
+                            consumed[c] = st == ST_OK ? p - p0 : (st == ST_NOT_CLEAN ? 0u : pe - p0);
                         if (rc == dc) rc = kNone;  // stop requesting its bytes
                         dc = kNone;
                     }

@@ -71,11 +71,17 @@ typedef enum capnp_status {
     /* ErrorKind::MessageNotAlignedBy8BytesBoundary (lib.rs:370): the no-alloc
        flat reader's alignment check (no_alloc_buffer_segments.rs:234-248). */
     CAPNP_E_NOT_ALIGNED = 14,
+    /* The inner stream of a streaming adaptor has nothing now: Poll::Pending
+       (capnp-futures); call again. */
+    CAPNP_PENDING = 15,
     /* Library-level errors (no counterpart in the reference). */
     CAPNP_E_INVALID_ARGUMENT = 64,
     CAPNP_E_NO_DEVICE = 65,
     CAPNP_E_HIP = 66,
-    CAPNP_E_OUT_OF_MEMORY = 67
+    CAPNP_E_OUT_OF_MEMORY = 67,
+    /* The inner stream of a streaming adaptor reported an I/O error (an
+       io::Error, lib.rs:481-499) or took no bytes. */
+    CAPNP_E_IO = 68
 } capnp_status;
 
 /* Mirror of capnp::message::ReaderOptions (message.rs:85-120).  Only the
@@ -333,6 +339,70 @@ capnp_status capnp_packed_read_message_no_alloc(capnp_ctx* ctx, const uint8_t* i
                                                 size_t buffer_len, uint32_t* nseg_out,
                                                 size_t* table_bytes_out,
                                                 size_t* body_bytes_out, size_t* consumed);
+
+/* ---- Streaming adaptors over caller-supplied byte streams ----------------
+ * The async PackedWrite / PackedRead of capnp-futures
+ * (capnp-futures/src/serialize_packed.rs:34-225, :330-521) and its message
+ * reader (capnp-futures/src/serialize_packed.rs:233-258 ->
+ * capnp-futures/src/serialize.rs:31-137): input split at any byte, an inner
+ * stream that returns short reads / partial writes or "pending".  The inner
+ * stream is a function plus a user pointer:
+ *   read:  bytes read into buf (0 = end of stream), CAPNP_IO_PENDING when
+ *          nothing is available now, or another negative value on error;
+ *   write: bytes accepted (1..len), CAPNP_IO_PENDING, or negative on error.
+ * The transform runs in the GPU kernels (capnp_pack_batch_host /
+ * capnp_unpack_batch_host); an adaptor is used by one thread at a time. */
+#define CAPNP_IO_PENDING (-1)
+typedef ptrdiff_t (*capnp_read_fn)(void* user, uint8_t* buf, size_t len);
+typedef ptrdiff_t (*capnp_write_fn)(void* user, const uint8_t* buf, size_t len);
+typedef struct capnp_packed_writer capnp_packed_writer;
+typedef struct capnp_packed_reader capnp_packed_reader;
+
+/* PackedWrite::new(inner) (capnp-futures serialize_packed.rs:336-348). */
+capnp_packed_writer* capnp_packed_writer_new(capnp_ctx* ctx, capnp_write_fn fn, void* user);
+void capnp_packed_writer_free(capnp_packed_writer* w);
+/* poll_write (poll_write_aux, :350-504): takes all `len` bytes.  A word
+   completed from carried bytes and the whole words of this call are one
+   packed chunk (runs never reach past the call, as the reference's run scan
+   of `inbuf`); trailing bytes of an incomplete word are carried.  Packed
+   bytes are queued and handed to the inner writer on flush (or every
+   1 MiB of input). */
+capnp_status capnp_packed_writer_write(capnp_packed_writer* w, const uint8_t* buf, size_t len);
+/* poll_flush / finish_pending_writes (:506-521): packs what is queued and
+   drains it to the inner writer; CAPNP_PENDING if the inner writer pends
+   (call again).  Carried bytes of an incomplete word stay carried. */
+capnp_status capnp_packed_writer_flush(capnp_packed_writer* w);
+/* Bytes of an incomplete word carried to the next write (0..7). */
+size_t capnp_packed_writer_carried(const capnp_packed_writer* w);
+
+/* PackedRead::new(inner) (:56-70). */
+capnp_packed_reader* capnp_packed_reader_new(capnp_ctx* ctx, capnp_read_fn fn, void* user);
+void capnp_packed_reader_free(capnp_packed_reader* r);
+/* poll_read (:74-225): 1..len unpacked bytes in *nread, 0 at a clean end of
+   the stream, CAPNP_PENDING when the inner reader pends, and
+   CAPNP_E_PREMATURE_END_OF_FILE when the stream ends inside a record (the
+   reference's UnexpectedEof). */
+capnp_status capnp_packed_reader_read(capnp_packed_reader* r, uint8_t* out, size_t len,
+                                      size_t* nread);
+/* read_exact: reads until `len` bytes (retrying a pending inner reader);
+   CAPNP_E_PREMATURE_END_OF_FILE if the stream ends first; *got (may be NULL)
+   = bytes delivered. */
+capnp_status capnp_packed_reader_read_exact(capnp_packed_reader* r, uint8_t* out, size_t len,
+                                            size_t* got);
+/* try_read_message / read_message (capnp-futures serialize.rs:31-137): the
+   segment table then the body into `body`; CAPNP_NONE (try_mode) or
+   CAPNP_E_PREMATURE_END_OF_FILE at a clean end; InvalidNumberOfSegments,
+   MessageTooLarge as serialize.rs:467-507; BufferNotLargeEnough with
+   *body_words = words needed when body_cap_words is short (the table has
+   then been read and *nseg / seg_words hold it; read the body with
+   capnp_packed_reader_read_exact). */
+capnp_status capnp_packed_reader_read_message(capnp_packed_reader* r,
+                                              const capnp_reader_options* opts, int try_mode,
+                                              uint64_t* body, size_t body_cap_words,
+                                              uint32_t* seg_words, uint32_t* nseg,
+                                              uint64_t* body_words);
+/* Bytes staged (packed, not yet decoded) plus decoded bytes not yet read. */
+size_t capnp_packed_reader_buffered(const capnp_packed_reader* r);
 
 #ifdef __cplusplus
 }

@@ -51,7 +51,10 @@ def pack(data: bytes) -> bytes:
 
 
 def read(data: bytes, out_len: int):
-    """One PackedRead::read over a slice.  Returns (status, out, consumed, nread)."""
+    """One PackedRead::read over a slice.  Returns (status, out, consumed, nread);
+    consumed is where the reference leaves the &[u8] reader: all of it on
+    PrematureEnd (refresh_buffer! consumes first, :59-74) and FailedToFill,
+    nothing on DidNotEndCleanly."""
     if out_len == 0:
         return OK, b"", 0, 0
     if out_len % 8:
@@ -79,7 +82,9 @@ def read(data: bytes, out_len: int):
             run = data[ip] * 8
             ip += 1
             if run > out_len - len(out):
-                return DID_NOT_END_CLEANLY, bytes(out), ip, 0
+                # returned before any consume (serialize_packed.rs:166-170):
+                # a slice reader stays where it was
+                return DID_NOT_END_CLEANLY, bytes(out), 0, 0
             if t == 0x00:
                 out.extend(b"\0" * run)
             else:

@@ -3,7 +3,7 @@
 set -o pipefail
 TAG=${1:-us}
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_messages.py tests/test_gpu_resync.py tests/test_gpu_carsales.py -m gpu -x -v --timeout 120 --timeout-method thread \
+timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 120 --timeout-method thread \
   > gpurun_out/${TAG}_tests.log 2>&1 || { tail -60 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -3 gpurun_out/${TAG}_tests.log
 for w in config2 carsales config3; do

@@ -2,7 +2,7 @@
 reference's own tests hold for the packed codec, as data.
 
 Sources (capnproto-rust checkout, read as text):
-  * capnp/src/serialize_packed.rs:506-566   simple_packing (17 unpacked<->packed pairs)
+  * capnp/src/serialize_packed.rs:506-566   simple_packing (14 unpacked<->packed pairs)
   * capnp/src/serialize_packed.rs:468-475   premature_eof
   * capnp/src/serialize_packed.rs:596-611   did_not_end_cleanly_on_a_segment_boundary
   * capnp/src/serialize_packed.rs:613-634   premature_end_of_packed_input

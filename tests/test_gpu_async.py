@@ -1,0 +1,305 @@
+"""GPU parity of the streaming adaptors (capnp_packed_writer / _reader,
+capnp_amd.serialize_packed_async) against the reference's async tests
+(capnp-futures/src/serialize_packed.rs:560-830) and the C oracle: inputs
+split at any byte, inner streams that pend and return short reads."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden_packing.json")))
+
+
+@pytest.fixture(scope="module")
+def A():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from capnp_amd import serialize_packed_async as A
+    return A
+
+
+def check_packing_with_periods(A, rp, wp, unpacked, packed):
+    # capnp-futures serialize_packed.rs:575-600
+    w = A.BlockingWrite(wp)
+    pw = A.PackedWrite(w)
+    pw.write_all(unpacked)
+    pw.flush_blocking()
+    assert bytes(w.buf) == packed, (rp, wp, unpacked)
+    r = A.BlockingRead(packed, rp)
+    pr = A.PackedRead(r)
+    assert pr.read_exact(len(unpacked)) == unpacked
+    assert r.is_empty()  # nothing left to read
+
+
+def test_simple_packing_blocking_periods(A):
+    # simple_packing with check_packing's periods 1..9 x 1..9 (:602-671)
+    for v in GOLD["packing"]:
+        u, p = bytes(v["unpacked"]), bytes(v["packed"])
+        for ii in range(1, 10):
+            for jj in range(1, 10):
+                check_packing_with_periods(A, ii, jj, u, p)
+
+
+class _Plain:
+    def __init__(self, data):
+        self.data, self.pos = bytes(data), 0
+
+    def read(self, n):
+        b = self.data[self.pos:self.pos + n]
+        self.pos += len(b)
+        return b
+
+
+def _read_with_size(A, n, packed, unpacked):
+    # check_unpacks_with_read_size (:731-746): a plain slice reader
+    pr = A.PackedRead(_Plain(packed))
+    out = b""
+    while len(out) < len(unpacked):
+        b = pr.read(n)
+        assert len(b) > 0, "premature end of stream"
+        out += b
+    assert out == unpacked
+    assert pr.read(n) == b""
+
+
+def test_unpacks_across_partial_output_buffers(A):
+    _read_with_size(A, 1, bytes([0x81, 42, 99]), bytes([42, 0, 0, 0, 0, 0, 0, 99]))
+    _read_with_size(A, 3, bytes([0xff, 1, 3, 2, 4, 5, 7, 6, 8, 1, 8, 6, 7, 4, 5, 2, 3, 1]),
+                    bytes([1, 3, 2, 4, 5, 7, 6, 8, 8, 6, 7, 4, 5, 2, 3, 1]))
+    # a zero run split across one-byte reads (WritingZeroes stage, :150-163)
+    _read_with_size(A, 1, bytes([0, 3, 0x01, 7]), bytes(32) + bytes([7, 0, 0, 0, 0, 0, 0, 0]))
+
+
+def test_eof_cases(A):
+    from capnp_amd import CapnpError
+    # eof_mid_tag_word (:764-777) and eof_mid_message (:805-815)
+    for data in (bytes([0x81]), bytes([0xfe, 3, 3])):
+        with pytest.raises(CapnpError) as e:
+            A.try_read_message(_Plain(data))
+        assert e.value.kind == "PrematureEndOfFile"
+    # eof_mid_passthrough_run (:779-793): UnexpectedEof
+    pr = A.PackedRead(_Plain(bytes([0xff, 1, 2, 3, 4, 5, 6, 7, 8, 2, 10, 11, 12, 13])))
+    with pytest.raises(CapnpError) as e:
+        pr.read_to_end()
+    assert e.value.kind == "PrematureEndOfFile"
+    # read_empty (:795-803)
+    assert A.try_read_message(A.BlockingRead(b"", 3)) is None
+    with pytest.raises(CapnpError) as e:
+        A.read_message(A.BlockingRead(b"", 3))
+    assert e.value.kind == "PrematureEndOfFile"
+
+
+def _rand_segments(rng):
+    segs = []
+    for _ in range(rng.choice([1, 1, 2, 3, 5, 17])):
+        n = rng.choice([0, 1, 2, 7, 40, 300])
+        ws = []
+        for _ in range(n):
+            k = rng.random()
+            if k < 0.3:
+                ws.append(0)
+            elif k < 0.5:
+                ws.append(rng.getrandbits(64) | 0x0101010101010101)
+            else:
+                b = [rng.getrandbits(8) if rng.random() < 0.6 else 0 for _ in range(8)]
+                ws.append(int.from_bytes(bytes(b), "little"))
+        segs.append(np.array(ws, dtype=np.uint64))
+    return segs
+
+
+def test_round_trip_async_periods(A):
+    # round_trip / check_packed_round_trip_async (:673-729): write_message
+    # through a blocking writer, try_read_message through a blocking reader;
+    # the bytes equal the sync writer's (overflow_test.rs:65-79)
+    rng = random.Random(5)
+    cases = [[np.array([int.from_bytes(bytes([8, 14, 90, 7, 21, 13, 59, 17]), "little"),
+                        int.from_bytes(bytes([0, 31, 21, 73, 0, 54, 61, 12]), "little")],
+                       dtype=np.uint64)]]  # check_packed_round_trip_async_bug
+    cases += [_rand_segments(rng) for _ in range(40)]
+    for i, segs in enumerate(cases):
+        rp, wp = rng.randrange(1, 12), rng.randrange(1, 12)
+        w = A.BlockingWrite(wp)
+        A.write_message(w, segs)
+        st, ref = O.write_message(segs)
+        assert st == 0 and bytes(w.buf) == ref, i
+        r = A.BlockingRead(bytes(w.buf), rp)
+        got = A.try_read_message(r)
+        assert len(got) == len(segs)
+        for a, b in zip(got.segments(), segs):
+            assert np.array_equal(np.asarray(a).view(np.uint64), b)
+        assert r.is_empty()
+
+
+def _split_points(rng, n):
+    pts, k = [], 0
+    while k < n:
+        k = min(n, k + rng.choice([1, 2, 3, 5, 7, 8, 9, 15, 16, 17, 64, 1000]))
+        pts.append(k)
+    return pts
+
+
+def _async_write_model(data, pts):
+    """The async writer's chunks for write calls ending at `pts`: a word
+    completed from carried bytes plus this call's whole words, packed as one
+    write_all (serialize_packed.rs:370-452 of capnp-futures)."""
+    out, carry, a = b"", b"", 0
+    for b in pts:
+        buf = carry + data[a:b]
+        m = len(buf) // 8
+        if m:
+            st, p = O.pack(buf[:8 * m])
+            assert st == 0
+            out += p
+        carry = buf[8 * m:]
+        a = b
+    return out, carry
+
+
+def test_writes_split_at_any_byte(A):
+    rng = random.Random(11)
+    for trial in range(60):
+        segs = _rand_segments(rng)
+        data = b"".join(s.tobytes() for s in segs)
+        if not data:
+            continue
+        pts = _split_points(rng, len(data))
+        w = A.BlockingWrite(rng.randrange(1, 9))
+        pw = A.PackedWrite(w)
+        a = 0
+        for b in pts:
+            pw.write(data[a:b])
+            a = b
+        pw.flush_blocking()
+        ref, carry = _async_write_model(data, pts)
+        assert bytes(w.buf) == ref, trial
+        assert pw.carried == len(carry) == 0
+        # reads of any size give the bytes back
+        pr = A.PackedRead(A.BlockingRead(ref, rng.randrange(1, 9)))
+        out = b""
+        while True:
+            try:
+                b = pr.read(rng.choice([1, 3, 8, 13, 64, 4096]))
+            except Exception as e:
+                if getattr(e, "status", None) == 15:
+                    continue
+                raise
+            if not b:
+                break
+            out += b
+        assert out == data, trial
+
+
+def test_partial_word_carried(A):
+    w = A.BlockingWrite(1 << 30)
+    pw = A.PackedWrite(w)
+    pw.write(bytes([1, 2, 3]))
+    assert pw.carried == 3
+    pw.flush_blocking()
+    assert bytes(w.buf) == b""  # an incomplete word is not emitted
+    pw.write(bytes([4, 5, 6, 7, 8]) + bytes(16))
+    pw.flush_blocking()
+    st, ref = O.pack(bytes([1, 2, 3, 4, 5, 6, 7, 8]) + bytes(16))
+    assert bytes(w.buf) == ref and pw.carried == 0
+
+
+def test_message_stream_try_read_loop(A):
+    # a concatenated stream read message by message until try_read_message
+    # returns None (serialize.rs:310-325 via the async twin)
+    rng = random.Random(3)
+    msgs = [_rand_segments(rng) for _ in range(25)]
+    stream = b""
+    for segs in msgs:
+        st, b = O.write_message(segs)
+        stream += b
+    r = A.BlockingRead(stream, 97)
+    pr = A.PackedRead(r)
+    got = []
+    while True:
+        m = A.try_read_message(pr)
+        if m is None:
+            break
+        got.append(m)
+    assert len(got) == len(msgs)
+    for m, segs in zip(got, msgs):
+        for a, b in zip(m.segments(), segs):
+            assert np.array_equal(np.asarray(a).view(np.uint64), b)
+
+
+# ---- sync PackedRead over a BufRead that refills (io.rs:35-38,
+# refresh_buffer! serialize_packed.rs:59-74)
+
+class _Raw:
+    def __init__(self, data):
+        self.data, self.pos = bytes(data), 0
+
+    def read(self, n):
+        b = self.data[self.pos:self.pos + n]
+        self.pos += len(b)
+        return b
+
+
+def test_bufread_refill_messages():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from capnp_amd import serialize_packed as S
+    rng = random.Random(21)
+    msgs = [_rand_segments(rng) for _ in range(20)]
+    stream = b""
+    for segs in msgs:
+        st, b = O.write_message(segs)
+        stream += b
+    for cap in (7, 64, 1000, 1 << 16):
+        r = S.BufReader(_Raw(stream), capacity=cap)
+        for segs in msgs:
+            m = S.try_read_message(r)
+            assert m is not None and len(m) == len(segs), cap
+            for a, b in zip(m.segments(), segs):
+                assert np.array_equal(np.asarray(a).view(np.uint64), b), cap
+        assert S.try_read_message(r) is None, cap
+    # a message cut short: the error is the one the whole input gives
+    cut = stream[:len(stream) // 3]
+    ref_st = None
+    pos = 0
+    while True:
+        st, segs_, used = O.read_message(cut[pos:], try_mode=True)
+        if st != 0:
+            ref_st = st
+            break
+        pos += used
+    from capnp_amd import CapnpError
+    r = S.BufReader(_Raw(cut), capacity=50)
+    with pytest.raises(CapnpError) as e:
+        while S.try_read_message(r) is not None:
+            pass
+    assert e.value.status == ref_st
+
+
+def test_bufread_refill_read_exact():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from capnp_amd import serialize_packed as S
+    for v in GOLD["packing"]:
+        u, p = bytes(v["unpacked"]), bytes(v["packed"])
+        if not u:
+            continue
+        for cap in (1, 2, 3, 9, 100):
+            r = S.BufReader(_Raw(p + b"\x07\x07"), capacity=cap)
+            assert S.PackedRead(r).read_exact(len(u)) == u
+            # the bytes after the unit stay unread
+            rest = b""
+            while True:
+                b = bytes(r.fill_buf())
+                if not b:
+                    break
+                rest += b
+                r.consume(len(b))
+            assert rest == b"\x07\x07", (cap, v)

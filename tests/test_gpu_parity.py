@@ -258,7 +258,7 @@ def test_unpack_error_statuses_vs_oracle(ctx):
         torch.cuda.synchronize()
         g_st = status.cpu().numpy()
         assert np.array_equal(g_st, ref_st), (utc, np.nonzero(g_st != ref_st))
-        assert np.array_equal(consumed.cpu().numpy().view(np.uint64)[ok], ref_used[ok]), utc
+        assert np.array_equal(consumed.cpu().numpy().view(np.uint64), ref_used), utc  # error chunks too
         gw = words.cpu().numpy().view(np.uint64)
         for c in np.nonzero(ok)[0]:
             a, b = int(out_offs[c]), int(out_offs[c + 1])
@@ -495,7 +495,7 @@ def test_sync_unpack_error_statuses_vs_oracle(ctx):
             gw, g_st, g_used = _unpack_sync(ctx, pk, dev(in_offs), dev(out_offs), total, n, sv,
                                             utc)
             assert np.array_equal(g_st, ref_st), (utc, np.nonzero(g_st != ref_st))
-            assert np.array_equal(g_used[ok], ref_used[ok]), utc
+            assert np.array_equal(g_used, ref_used), utc  # error chunks too
             for c in np.nonzero(ok)[0]:
                 a, b = int(out_offs[c]), int(out_offs[c + 1])
                 assert np.array_equal(gw[a:b], ref_words[a:b]), (utc, c)

@@ -184,8 +184,34 @@ def test_unpack_garbage_never_crashes_and_matches_python():
         a = O.read_exact(d, out_len)
         b = R.read_exact(d, out_len)
         assert a[0] == b[0], (d, out_len)
+        assert a[2] == b[2], (d, out_len, a, b)  # consumed, every status
         if a[0] == 0:
-            assert a[1] == b[1] and a[2] == b[2]
+            assert a[1] == b[1]
+
+
+def test_consumed_on_errors_follows_refresh_buffer():
+    # Where the reference leaves a &[u8] reader after a failed read_exact:
+    # PrematureEndOfPackedInput consumes the whole buffer (refresh_buffer!,
+    # serialize_packed.rs:59-74, then fill_buf() is empty); FailedToFill
+    # consumes everything (consume + read_exact of the rest, :195-205, io.rs
+    # :16-31); DidNotEndCleanly returns before any consume (:166-170, :183-187);
+    # an empty input reads nothing (read() = Ok(0), :96-98).
+    cases = [
+        (bytes([0xf0, 1, 2]), 200 // 8 * 8, O.STATUS["PREMATURE_END_OF_PACKED_INPUT"], 3),
+        (bytes([0]), 8, O.STATUS["PREMATURE_END_OF_PACKED_INPUT"], 1),
+        (bytes([0xff, 1, 2, 3, 4, 5, 6, 7, 8]), 200 // 8 * 8,
+         O.STATUS["PREMATURE_END_OF_PACKED_INPUT"], 9),
+        (bytes([1, 1]), 200 // 8 * 8, O.STATUS["PREMATURE_END_OF_PACKED_INPUT"], 2),
+        (bytes([0xff, 1, 2, 3, 4, 5, 6, 7, 8, 37, 1, 2]), 8 * 2,
+         O.STATUS["DID_NOT_END_CLEANLY"], 0),
+        (bytes([0xff, 1, 2, 3, 4, 5, 6, 7, 8, 3, 1, 2, 3]), 8 * 4,
+         O.STATUS["FAILED_TO_FILL_WHOLE_BUFFER"], 13),
+        (b"", 8, O.STATUS["FAILED_TO_FILL_WHOLE_BUFFER"], 0),
+    ]
+    for data, out_len, st, used in cases:
+        for impl in (O, R):
+            got = impl.read_exact(data, out_len)
+            assert got[0] == st and got[2] == used, (impl.__name__, data, got)
 
 
 def test_message_round_trip_quickcheck_style():
