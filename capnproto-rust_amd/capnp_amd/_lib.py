@@ -45,6 +45,7 @@ EXPORTS = [
     "capnp_packed_writer_flush", "capnp_packed_writer_carried", "capnp_packed_reader_new",
     "capnp_packed_reader_free", "capnp_packed_reader_read", "capnp_packed_reader_read_exact",
     "capnp_packed_reader_read_message", "capnp_packed_reader_buffered",
+    "capnp_gpu_find_messages",
 ]
 
 
@@ -148,6 +149,7 @@ def lib():
     L.capnp_packed_reader_read_message.argtypes = [vp, C.POINTER(ReaderOptionsC), i32, vp, sz,
                                                    vp, C.POINTER(C.c_uint32),
                                                    C.POINTER(C.c_uint64)]
+    L.capnp_gpu_find_messages.argtypes = [vp, vp, sz, sz, vp, C.POINTER(C.c_size_t), vp]
     L.capnp_packed_reader_buffered.argtypes = [vp]
     L.capnp_packed_reader_buffered.restype = sz
     _lib = L

@@ -12,6 +12,8 @@ PackedRead::read_exact (capnp/src/serialize_packed.rs:304-439, :80-228).
 """
 import ctypes as C
 
+import numpy as np
+
 from . import _lib
 from ._lib import CapnpError
 
@@ -210,6 +212,57 @@ class Context:
                                                 _ptr(consumed), self._stream(stream))
         _check(st, self._h)
         return words, mwo, segs, mso, status[:nmsg], consumed[:nmsg]
+
+    def find_messages(self, packed, nbytes=None, max_msgs=None, stream=None):
+        """Message starts of a concatenated packed stream with no byte index
+        (capnp_gpu_find_messages).  -> (offs int64 device tensor of nmsg + 1
+        entries, nmsg): messages [offs[k], offs[k+1]) read completely;
+        offs[nmsg] is where the next try_read_message starts (== nbytes: a
+        clean end)."""
+        import torch
+        nb = int(packed.numel() if nbytes is None else nbytes)
+        cap = int(max_msgs if max_msgs is not None else nb // 8 + 1)
+        offs = torch.empty(cap + 1, dtype=torch.int64, device=packed.device)
+        n = C.c_size_t(0)
+        st = _lib.lib().capnp_gpu_find_messages(self._h, _ptr(packed) if nb else None, nb, cap,
+                                                _ptr(offs), C.byref(n), self._stream(stream))
+        _check(st, self._h)
+        return offs[:n.value + 1], n.value
+
+    def read_message_stream(self, packed, limit=8 * 1024 * 1024, stream=None):
+        """serialize_packed::try_read_message in a loop over one device
+        stream until it returns None or fails (serialize.rs:310-325).
+        -> (messages, end): messages = list of (segment word arrays as device
+        tensors, consumed bytes) in stream order; end = CAPNP_NONE (1) after
+        a clean end, else the status of the try_read_message that failed."""
+        import torch
+        nb = int(packed.numel())
+        offs, n = self.find_messages(packed, nb, stream=stream)
+        stop = int(offs[n].item())
+        ranges = offs if stop == nb else torch.cat(
+            [offs, torch.tensor([nb], dtype=torch.int64, device=offs.device)])
+        m = ranges.numel() - 1
+        if m == 0:
+            return [], 1
+        words_cap, segs_cap = nb * 64 // 8 + 64, m * 512
+        words, mwo, segs, mso, status, consumed = self.read_messages(
+            packed, ranges, words_cap, segs_cap, try_mode=True, limit=limit, stream=stream)
+        st = status.cpu().tolist()
+        mwo_h, mso_h = mwo.cpu().tolist(), mso.cpu().tolist()
+        seg_h = segs.cpu().numpy().view(np.uint64) if segs.numel() else np.zeros(0, np.uint64)
+        cons = consumed.cpu().tolist()
+        out, end = [], 1
+        for k in range(m):
+            if st[k] != 0:
+                end = st[k]
+                break
+            a, p = mwo_h[k], []
+            for j in range(mso_h[k], mso_h[k + 1]):
+                ln = int(seg_h[j]) & 0xFFFFFFFF
+                p.append(words[a:a + ln])
+                a += ln
+            out.append((p, cons[k]))
+        return out, end
 
     def read_flat_messages(self, buf, slice_off, segs_cap, no_alloc=False,
                            limit=8 * 1024 * 1024, stream=None):

@@ -68,6 +68,12 @@ extern "C" uint64_t capnp_carsales_plan(const uint32_t*, uint64_t, uint64_t, uin
 extern "C" hipError_t capnp_launch_gen_carsales(uint64_t*, uint64_t, const uint32_t*,
                                                 const uint64_t*, uint64_t, hipStream_t);
 extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes);
+extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t nbytes,
+                                                 uint64_t max_msgs, uint64_t* d_pos,
+                                                 uint64_t* d_words, uint64_t words_cap,
+                                                 uint64_t* nmsg, int* clean, void* d_ws,
+                                                 size_t ws_bytes, hipStream_t s,
+                                                 uint64_t* words_needed);
 extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d_in_off, uint64_t n,
                                           uint64_t total_bytes, uint64_t* d_out,
                                           const uint64_t* d_out_off, int32_t* d_status,
@@ -110,6 +116,8 @@ struct capnp_ctx {
     size_t msg_cap = 0;
     uint8_t* d_resync = nullptr;  // index-free decode: per-block chain state
     size_t resync_cap = 0;
+    uint8_t* d_stream_words = nullptr;  // message discovery: the stream decoded to words
+    size_t stream_words_cap = 0;
     int resync_passes = 0, resync_serial = 0;  // last capnp_gpu_unpack_batch_resync
     std::string err;
 };
@@ -918,6 +926,62 @@ capnp_status capnp_gpu_read_messages(capnp_ctx* ctx, const uint8_t* d_packed,
                                 I(o_cst), U(o_ccons), nullptr, s));
     HIP_TRY(capnp_launch_msg_status(nmsg, I(o_tst), U(o_tused), I(o_cst), U(o_ccons), d_status,
                                     d_consumed, s));
+    return CAPNP_OK;
+}
+
+// try_read_message in a loop over one packed stream with no byte index
+// (serialize.rs:310-325): the byte where each message starts.  Each round
+// resolves the rest of the stream as one read unit (resync.hip), decodes it,
+// follows the message chain through the segment tables and places the
+// starts; a round that stops early (max_msgs, or a resolution that did not
+// settle) is continued from where it stopped.
+capnp_status capnp_gpu_find_messages(capnp_ctx* ctx, const uint8_t* d_packed, size_t nbytes,
+                                     size_t max_msgs, uint64_t* d_msg_byte_off, size_t* nmsg,
+                                     void* stream) {
+    if (!ctx || !nmsg || !d_msg_byte_off || (nbytes && !d_packed)) return CAPNP_E_INVALID_ARGUMENT;
+    hipStream_t s = pick(ctx, stream);
+    *nmsg = 0;
+    size_t found = 0;
+    uint64_t start = 0;
+    for (;;) {
+        const uint64_t rest = nbytes - start;
+        if (rest == 0 || found == max_msgs) break;
+        const size_t ws = capnp_resync_ws_bytes(1, rest) + 8 * (max_msgs - found + 16) + 4096;
+        capnp_status st = ensure_buf(ctx, &ctx->d_resync, &ctx->resync_cap, ws);
+        if (st != CAPNP_OK) return st;
+        uint64_t words_cap = ctx->stream_words_cap / 8, need = 0, m = 0;
+        int clean = 0;
+        hipError_t e = capnp_resync_find_messages(d_packed + start, rest, max_msgs - found,
+                                                  d_msg_byte_off + found,
+                                                  reinterpret_cast<uint64_t*>(ctx->d_stream_words),
+                                                  words_cap, &m, &clean, ctx->d_resync,
+                                                  ctx->resync_cap, s, &need);
+        if (e == hipErrorInvalidValue && need > words_cap) {
+            st = ensure_buf(ctx, &ctx->d_stream_words, &ctx->stream_words_cap, need * 8 + 64);
+            if (st != CAPNP_OK) return st;
+            continue;
+        }
+        HIP_TRY(e);
+        // the round's offsets are relative to `start`
+        if (start && m + 1 > 0) {
+            std::vector<uint64_t> h(m + 1);
+            HIP_TRY(hipMemcpyAsync(h.data(), d_msg_byte_off + found, 8 * (m + 1),
+                                   hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            for (auto& v : h) v += start;
+            HIP_TRY(hipMemcpyAsync(d_msg_byte_off + found, h.data(), 8 * (m + 1),
+                                   hipMemcpyHostToDevice, s));
+        }
+        uint64_t stop = 0;
+        HIP_TRY(hipMemcpyAsync(&stop, d_msg_byte_off + found + m, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        found += m;
+        if (m == 0 || clean || stop >= nbytes) break;
+        start = stop;
+    }
+    if (found == 0) HIP_TRY(hipMemcpyAsync(d_msg_byte_off, &start, 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *nmsg = found;
     return CAPNP_OK;
 }
 

@@ -397,3 +397,253 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
     }
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Message-boundary discovery in a concatenated packed stream (SURVEY §8f row
+// 2): where successive try_read_message calls (serialize.rs:310-325,
+// :448-524; serialize_packed.rs:246-255) would start each message, with no
+// byte index.
+//
+//   1. the whole stream is resolved as one read unit (spec / fix / scan
+//      above) and decoded block by block into words;
+//   2. one lane follows the message chain in the word domain: message k
+//      starts at word u_k, its table says 1 + nseg/2 + sum(lengths) words
+//      (serialize.rs:467-510), so u_{k+1} = u_k + that; the walk stops at a
+//      table that is invalid (segment count 0 or >= 512), at a message that
+//      runs past the decoded words, or at max_msgs;
+//   3. lane per message: the packed byte where word u_k's record starts
+//      (binary search of the block word bases, then a walk from the block's
+//      entry).  A u_k inside a run (the previous message's body ended inside
+//      a record) is not a record start: the previous message is then the
+//      failing one.
+// A writer packs each message's table words and segments as separate chunks
+// (serialize.rs:595-679), so records never cross message boundaries and the
+// word-domain chain is the reference's.  For streams where they do (or that
+// are malformed), the messages up to the first failing one are still
+// exact, and the caller decodes the failing message's range to the end of
+// the stream (capnp_gpu_read_messages gives the reference's status for it).
+
+namespace {
+
+// res[0] = words before the first block the walk may not trust: one whose
+// entry is not its predecessor's exit (fix passes stopped before the fixed
+// point; the blocks before it are exact) ...
+__global__ void k_consistent(const uint64_t* __restrict__ entry, const uint64_t* __restrict__ exit_,
+                             const uint64_t* __restrict__ wbase, uint64_t nb,
+                             uint64_t* __restrict__ res) {
+    const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (k == 0 || k >= nb) return;
+    if (entry[k] != exit_[k - 1]) atomicMin((unsigned long long*)res, (unsigned long long)wbase[k]);
+}
+
+// ... or one that failed to decode (a record cut by the stream end).
+__global__ void k_valid_words(const int32_t* __restrict__ blk_status, uint64_t nb,
+                              const uint64_t* __restrict__ wbase, uint64_t* __restrict__ res) {
+    const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (k >= nb) return;
+    if (blk_status[k] != 0) atomicMin((unsigned long long*)res, (unsigned long long)wbase[k]);
+}
+
+// The last block may end in a record the stream cuts short: its unit then
+// ends after its last complete record, and only those words count.
+// tail[0] = that byte, tail[1] = the stream's complete words.
+__global__ void k_tail(const uint8_t* __restrict__ in, uint64_t nbytes,
+                       const uint64_t* __restrict__ exit_, const uint64_t* __restrict__ wbase,
+                       uint64_t nb, uint64_t* __restrict__ tail) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint64_t p = nb > 1 ? exit_[nb - 2] : 0, w = 0;
+    while (p < nbytes) {
+        uint64_t q = p, ww = w;
+        hop(in, q, ww, nbytes);
+        if (q > nbytes) break;
+        p = q;
+        w = ww;
+    }
+    tail[0] = p;
+    tail[1] = wbase[nb - 1] + w;
+}
+
+__global__ void k_set_tail(uint64_t* __restrict__ blk_in, uint64_t nb,
+                           const uint64_t* __restrict__ tail) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) blk_in[nb] = tail[0];
+}
+
+__global__ void k_msg_walk(const uint64_t* __restrict__ words, const uint64_t* __restrict__ res,
+                           uint64_t max_msgs, uint64_t* __restrict__ ustart,
+                           uint64_t* __restrict__ out) {
+    // out[0] = messages found, out[1] = word where the walk stopped
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint64_t W = res[0];
+    uint64_t u = 0, k = 0;
+    while (u < W && k < max_msgs) {
+        const uint64_t w0 = words[u];
+        const uint32_t nseg = (uint32_t)w0 + 1u;
+        if (nseg == 0 || nseg >= 512) break;
+        const uint64_t rest = nseg / 2;
+        if (u + 1 + rest > W) break;
+        uint64_t total = w0 >> 32;
+        for (uint64_t i = 1; i < nseg; i++) {
+            const uint64_t tw = words[u + 1 + (i - 1) / 2];
+            total += ((i - 1) & 1) ? (tw >> 32) : (tw & 0xFFFFFFFFull);
+        }
+        const uint64_t next = u + 1 + rest + total;
+        if (next > W || next < u) break;
+        ustart[k++] = u;
+        u = next;
+    }
+    ustart[k] = u;
+    out[0] = k;
+    out[1] = u;
+}
+
+// Packed byte of the record that starts at word u (or ~0 if u is inside a
+// record), from block j's entry.
+__device__ uint64_t word_to_byte(const uint8_t* __restrict__ in, uint64_t nbytes,
+                                 const uint64_t* __restrict__ exit_, const uint64_t* __restrict__ wbase,
+                                 uint64_t nb, uint64_t u) {
+    uint64_t lo = 0, hi = nb;  // last block with wbase <= u
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (wbase[mid] <= u) lo = mid;
+        else hi = mid;
+    }
+    uint64_t p = lo == 0 ? 0 : exit_[lo - 1], w = wbase[lo];
+    while (w < u && p < nbytes) hop(in, p, w, nbytes);
+    return w == u ? p : ~0ull;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_msg_pos(const uint8_t* __restrict__ in, uint64_t nbytes, const uint64_t* __restrict__ exit_,
+          const uint64_t* __restrict__ wbase, uint64_t nb, const uint64_t* __restrict__ ustart,
+          const uint64_t* __restrict__ out, uint64_t* __restrict__ pos,
+          uint64_t* __restrict__ bad) {
+    const uint64_t m = out[0];
+    const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (k > m) return;
+    const uint64_t p = ustart[k] == 0 ? 0 : word_to_byte(in, nbytes, exit_, wbase, nb, ustart[k]);
+    pos[k] = p;
+    if (p == ~0ull) atomicMin((unsigned long long*)bad, (unsigned long long)k);
+}
+
+}  // namespace
+
+// -> *nmsg complete messages with byte starts d_pos[0..nmsg) and
+// d_pos[nmsg] = where the walk stopped (the next message's start, or the
+// stream end); *clean = 1 if that is the end of the stream after the last
+// message, i.e. the next try_read_message returns None.  A message whose
+// start could not be placed truncates the list before the message that
+// ended inside a record.  Blocking.
+extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t nbytes,
+                                                 uint64_t max_msgs, uint64_t* d_pos,
+                                                 uint64_t* d_words, uint64_t words_cap,
+                                                 uint64_t* nmsg, int* clean, void* d_ws,
+                                                 size_t ws_bytes, hipStream_t s,
+                                                 uint64_t* words_needed) {
+    *nmsg = 0;
+    *clean = nbytes == 0;
+    if (words_needed) *words_needed = 0;
+    if (nbytes == 0) return hipMemsetAsync(d_pos, 0, 8, s);
+    hipError_t e;
+    const uint64_t n = 1;
+    const uint64_t nbb = blocks_bound(n, nbytes);
+    Ws w;
+    uint8_t* base = (uint8_t*)(((uintptr_t)d_ws + 255) & ~uintptr_t(255));
+    size_t need = carve(&w, base, n, nbb, scan_tmp_bytes(nbb > 2 ? nbb : 2)) + (base - (uint8_t*)d_ws);
+    // + in_off[2], out_off[2], res[2], walk out[2], bad, ustart[max_msgs + 1]
+    uint64_t* aux = (uint64_t*)(base + ((need - (base - (uint8_t*)d_ws) + 255) & ~size_t(255)));
+    need = (uint8_t*)(aux + 10 + max_msgs + 1) - (uint8_t*)d_ws;
+    if (need > ws_bytes) return hipErrorInvalidValue;
+    uint64_t* in_off = aux;       // [2]
+    uint64_t* out_off = aux + 2;  // [2]
+    uint64_t* res = aux + 4;      // [1]
+    uint64_t* wout = aux + 5;     // [2]
+    uint64_t* bad = aux + 7;      // [1]
+    uint64_t* ustart = aux + 10;  // [max_msgs + 1]
+    const uint64_t h_in_off[2] = {0, nbytes};
+    if ((e = hipMemcpyAsync(in_off, h_in_off, 16, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.flags, 0, 4 * (2 + kMaxPasses), s)) != hipSuccess) return e;
+    k_count<<<grid(n + 1), kThreads, 0, s>>>(in_off, n, w.nblk);
+    size_t tb = w.tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
+        hipSuccess)
+        return e;
+    k_spec<<<grid(nbb), kThreads, 0, s>>>(d_in, in_off, n, w.bstart, w.spec_exit, w.spec_words,
+                                          w.exit, w.entry, w.words);
+    int pass = 0;
+    const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
+    for (;;) {
+        if (pass >= kMaxPasses) break;  // (not converged: k_consistent bounds the walk
+                                        // to the exact prefix; the caller continues)
+        for (int i = 0; i < kPassBatch; i++, pass++)
+            k_fix<<<grid(ngroups), kThreads, 0, s>>>(d_in, in_off, n, w.bstart, w.spec_exit,
+                                                     w.spec_words, w.exit, w.entry, w.words,
+                                                     w.flags, pass);
+        int32_t last = 0;
+        if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
+            hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (!last) break;
+    }
+    uint64_t nb = 0;
+    if ((e = hipMemcpyAsync(&nb, w.bstart + n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    tb = w.tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.words, w.wbase, (int)nb, s)) != hipSuccess)
+        return e;
+    uint64_t* tail = aux + 8;  // [2]
+    k_tail<<<1, 64, 0, s>>>(d_in, nbytes, w.exit, w.wbase, nb, tail);
+    uint64_t htail[2] = {0, 0};
+    if ((e = hipMemcpyAsync(htail, tail, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    const uint64_t W = htail[1];
+    if (words_needed) *words_needed = W;
+    if (W > words_cap) return hipErrorInvalidValue;  // caller grows d_words and calls again
+    // decode every block as its own unit; a block that fails (a record cut by
+    // the stream end, or a chain the fix passes did not settle) bounds the
+    // words the walk may use
+    const uint64_t h_out_off[2] = {0, W};
+    if ((e = hipMemcpyAsync(out_off, h_out_off, 16, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return e;
+    if ((e = hipMemcpyAsync(res, &W, 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    const uint64_t none = ~0ull;
+    if ((e = hipMemcpyAsync(bad, &none, 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    k_consistent<<<grid(nb), kThreads, 0, s>>>(w.entry, w.exit, w.wbase, nb, res);
+    uint64_t* blk_in = w.spec_exit;
+    uint64_t* blk_out = w.entry;
+    int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
+    k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(in_off, n, out_off, w.bstart, w.exit, w.wbase,
+                                               blk_in, blk_out);
+    k_set_tail<<<1, 64, 0, s>>>(blk_in, nb, tail);
+    if ((e = capnp_launch_unpack(d_in, blk_in, nb, 0, d_words, blk_out, blk_status, nullptr,
+                                 nullptr, s)) != hipSuccess)
+        return e;
+    k_valid_words<<<grid(nb), kThreads, 0, s>>>(blk_status, nb, w.wbase, res);
+    k_msg_walk<<<1, 64, 0, s>>>(d_words, res, max_msgs, ustart, wout);
+    k_msg_pos<<<grid(max_msgs + 1), kThreads, 0, s>>>(d_in, nbytes, w.exit, w.wbase, nb, ustart,
+                                                      wout, d_pos, bad);
+    uint64_t hout[2] = {0, 0}, hbad = 0, hres = 0;
+    if ((e = hipMemcpyAsync(hout, wout, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(&hbad, bad, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(&hres, res, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    uint64_t m = hout[0];
+    if (hbad != ~0ull) {
+        // message hbad starts inside a record: message hbad - 1 is the one
+        // that fails; report the messages before it, and its start as the end
+        m = hbad == 0 ? 0 : hbad - 1;
+    } else if (hres == W && hout[1] == W && m > 0) {
+        // the walk consumed every word: clean end if the stream ends there
+        uint64_t pend = 0;
+        if ((e = hipMemcpyAsync(&pend, w.exit + nb - 1, 8, hipMemcpyDeviceToHost, s)) != hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (pend == nbytes) {
+            *clean = 1;
+            if ((e = hipMemcpyAsync(d_pos + m, &nbytes, 8, hipMemcpyHostToDevice, s)) != hipSuccess)
+                return e;
+        }
+    }
+    *nmsg = m;
+    return hipStreamSynchronize(s);
+}

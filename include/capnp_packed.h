@@ -340,6 +340,24 @@ capnp_status capnp_packed_read_message_no_alloc(capnp_ctx* ctx, const uint8_t* i
                                                 size_t* table_bytes_out,
                                                 size_t* body_bytes_out, size_t* consumed);
 
+/* try_read_message in a loop over one packed stream in device memory with
+   no byte index (serialize.rs:310-325, :448-524; serialize_packed.rs:246-255):
+   writes the starts of the messages the loop reads completely,
+   d_msg_byte_off[0..*nmsg), and d_msg_byte_off[*nmsg] = where the next
+   try_read_message starts (== nbytes: it returns None, a clean end; else the
+   rest of the stream is a message that fails, whose status
+   capnp_gpu_read_messages over [d_msg_byte_off[*nmsg], nbytes) gives).
+   d_msg_byte_off holds max_msgs + 1 entries; with *nmsg == max_msgs the loop
+   may go on from d_msg_byte_off[*nmsg].  The messages' bytes are
+   [d_msg_byte_off[k], d_msg_byte_off[k+1]): capnp_gpu_read_messages with
+   that index decodes them (status, segments, consumed per message).
+   Blocking.  The stream is resolved as one read unit by the speculative
+   block walk (resync), the message chain is followed through the decoded
+   segment tables on the device. */
+capnp_status capnp_gpu_find_messages(capnp_ctx* ctx, const uint8_t* d_packed, size_t nbytes,
+                                     size_t max_msgs, uint64_t* d_msg_byte_off, size_t* nmsg,
+                                     void* stream);
+
 /* ---- Streaming adaptors over caller-supplied byte streams ----------------
  * The async PackedWrite / PackedRead of capnp-futures
  * (capnp-futures/src/serialize_packed.rs:34-225, :330-521) and its message

@@ -1,0 +1,113 @@
+"""Message-boundary discovery in a concatenated packed stream with no byte
+index (capnp_gpu_find_messages + capnp_gpu_read_messages)
+against the oracle's try_read_message loop (serialize.rs:310-325,
+serialize_packed.rs:246-255): per message segments and consumed bytes, and
+how the loop ends (None after a clean end, else the failing status), on
+valid, truncated, garbage-tailed and over-limit streams."""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from capnp_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _segments(rng, big=False):
+    segs = []
+    for _ in range(rng.choice([1, 1, 1, 2, 3, 4, 7, 30])):
+        n = rng.choice([0, 1, 5, 16, 100, 600] + ([3000, 20000] if big else []))
+        kind = rng.random()
+        if kind < 0.1:  # long literal stretches
+            ws = [rng.getrandbits(64) | 0x0101010101010101 for _ in range(n)]
+        elif kind < 0.2:  # mostly zeros
+            ws = [rng.getrandbits(64) if rng.random() < 0.02 else 0 for _ in range(n)]
+        else:
+            ws = []
+            for _ in range(n):
+                b = [rng.getrandbits(8) if rng.random() < 0.56 else 0 for _ in range(8)]
+                ws.append(int.from_bytes(bytes(b), "little") if rng.random() < 0.7 else 0)
+        segs.append(np.array(ws, dtype=np.uint64))
+    return segs
+
+
+def _oracle_loop(stream, limit=O.DEFAULT_TRAVERSAL_LIMIT):
+    out, pos = [], 0
+    while True:
+        st, segs, used = O.read_message(stream[pos:], try_mode=True, limit=limit)
+        if st != 0:
+            return out, st
+        out.append((segs, used))
+        pos += used
+
+
+def _check(ctx, stream, limit=O.DEFAULT_TRAVERSAL_LIMIT):
+    import torch
+    ref, ref_end = _oracle_loop(stream, limit)
+    dev = torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).cuda() if stream else \
+        torch.zeros(0, dtype=torch.uint8, device="cuda")
+    got, end = ctx.read_message_stream(dev, limit=limit)
+    assert end == ref_end, (end, ref_end)
+    assert len(got) == len(ref), (len(got), len(ref))
+    for (gsegs, gused), (rsegs, rused) in zip(got, ref):
+        assert gused == rused
+        assert len(gsegs) == len(rsegs)
+        for a, b in zip(gsegs, rsegs):
+            assert np.array_equal(a.cpu().numpy().view(np.uint64), np.asarray(b, np.uint64))
+
+
+def _stream(rng, nmsg, big=False):
+    out = b""
+    for _ in range(nmsg):
+        st, b = O.write_message(_segments(rng, big))
+        assert st == 0
+        out += b
+    return out
+
+
+def test_valid_streams(ctx):
+    rng = random.Random(1)
+    _check(ctx, b"")
+    for nmsg in (1, 2, 5, 40, 300):
+        _check(ctx, _stream(rng, nmsg))
+    _check(ctx, _stream(rng, 30, big=True))
+
+
+def test_truncated_and_garbage_tails(ctx):
+    rng = random.Random(2)
+    for trial in range(40):
+        s = _stream(rng, rng.choice([1, 3, 20]))
+        r = rng.random()
+        if r < 0.4:
+            s = s[:rng.randrange(1, len(s))]
+        elif r < 0.7:
+            s = s + bytes(rng.randrange(256) for _ in range(rng.randrange(1, 40)))
+        else:
+            k = rng.randrange(len(s))
+            s = s[:k] + bytes([rng.choice([0, 0xFF, rng.randrange(256)])]) + s[k + 1:]
+        _check(ctx, s)
+
+
+def test_invalid_tables_and_limit(ctx):
+    rng = random.Random(3)
+    good = _stream(rng, 5)
+    # segment count 0 (u32 0xFFFFFFFF + 1) and 600 segments
+    bad0 = bytes([0x0F, 0xFF, 0xFF, 0xFF, 0xFF, 0])
+    bad600 = bytes([0x03, 0x57, 0x02]) + bytes(8)
+    _check(ctx, good + bad0 + good)
+    _check(ctx, good + bad600)
+    # a message over the traversal limit ends the loop there
+    big = _stream(rng, 3, big=True)
+    _check(ctx, good + big + good, limit=2000)
