@@ -30,6 +30,13 @@ def _ptr(t):
     return C.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def seg_words_u32(segs):
+    """Segment lengths returned in int32 storage read as the ABI's uint32
+    (a segment of 2^31 words or more would otherwise read negative)."""
+    import torch
+    return segs.to(torch.int64) & 0xFFFFFFFF
+
+
 class Context:
     """A device context bound to one gfx950 GPU."""
 
@@ -264,27 +271,46 @@ class Context:
             out.append((p, cons[k]))
         return out, end
 
-    def read_flat_messages(self, buf, slice_off, segs_cap, no_alloc=False,
+    def read_flat_messages(self, buf, slice_off, segs_cap=None, no_alloc=False,
                            limit=8 * 1024 * 1024, stream=None):
         """serialize::read_message_from_flat_slice (or its _no_alloc twin)
         for a batch of unpacked messages on the device
         (capnp_gpu_read_flat_messages): message m is read from the slice
-        buf[slice_off[m]:slice_off[m+1]].  Returns (seg_words int32,
-        msg_seg_off, status, body_off, consumed) as device tensors; limit
-        None = no traversal limit."""
+        buf[slice_off[m]:slice_off[m+1]].  Returns (seg_words, msg_seg_off,
+        status, body_off, consumed) as device tensors; seg_words holds the
+        ABI's uint32 lengths in int32 storage (read them through
+        `seg_words_u32`).  limit None = no traversal limit.  segs_cap None
+        sizes the segment array in two phases: one entry per message first,
+        then exactly msg_seg_off[nmsg] on CAPNP_E_BUFFER_NOT_LARGE_ENOUGH.
+        slice_off must be non-decreasing and end within buf (checked here,
+        CapnpError 64 otherwise)."""
         import torch
+        if buf.dtype != torch.uint8 or buf.dim() != 1 or not buf.is_contiguous():
+            raise CapnpError(64, "buf must be a contiguous 1-D uint8 tensor")
         nmsg = slice_off.numel() - 1
         dev = slice_off.device
-        segs = torch.empty(max(segs_cap, 1), dtype=torch.int32, device=dev)
+        slice_off = slice_off.to(torch.int64).contiguous()
+        if nmsg > 0:
+            bad = (slice_off[1:] < slice_off[:-1]).any() | (slice_off[0] < 0) \
+                | (slice_off[-1] > buf.numel())
+            if bool(bad):
+                raise CapnpError(64, "slice_off must be non-decreasing and within buf")
         mso = torch.empty(nmsg + 1, dtype=torch.int64, device=dev)
         status = torch.empty(max(nmsg, 1), dtype=torch.int32, device=dev)
         body_off = torch.empty(max(nmsg, 1), dtype=torch.int64, device=dev)
         consumed = torch.empty(max(nmsg, 1), dtype=torch.int64, device=dev)
         o = _lib.ReaderOptionsC(int(limit or 0), 1 if limit is not None else 0, 64)
-        st = _lib.lib().capnp_gpu_read_flat_messages(
-            self._h, _ptr(buf), _ptr(slice_off), nmsg, C.byref(o), int(bool(no_alloc)),
-            _ptr(segs), int(segs_cap), _ptr(mso), _ptr(status), _ptr(body_off), _ptr(consumed),
-            self._stream(stream))
+        cap = int(segs_cap) if segs_cap is not None else max(nmsg, 1)
+        for phase in range(2):
+            segs = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+            st = _lib.lib().capnp_gpu_read_flat_messages(
+                self._h, _ptr(buf), _ptr(slice_off), nmsg, C.byref(o), int(bool(no_alloc)),
+                _ptr(segs), cap, _ptr(mso), _ptr(status), _ptr(body_off), _ptr(consumed),
+                self._stream(stream))
+            if st == 9 and segs_cap is None and phase == 0:
+                cap = int(mso[nmsg])
+                continue
+            break
         _check(st, self._h)
         return segs, mso, status[:nmsg], body_off[:nmsg], consumed[:nmsg]
 

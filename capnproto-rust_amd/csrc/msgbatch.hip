@@ -441,7 +441,15 @@ __device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {
 __device__ int32_t flat_table(const uint8_t* p, uint64_t len, int no_alloc, uint64_t limit,
                               int has_limit, uint32_t* nseg_out, uint64_t* table_out,
                               uint64_t* words_out, uint32_t* seg) {
+    // On FST_ENDS_PREMATURELY *table_out / *words_out carry the reference's
+    // MessageEndsPrematurely(header, body) payload instead.
     uint64_t total = 0, pos, nseg;
+#define ENDS_PREMATURELY(h, b) \
+    do {                       \
+        *table_out = (h);      \
+        *words_out = (b);      \
+        return FST_ENDS_PREMATURELY; \
+    } while (0)
     if (!no_alloc) {
         if (len == 0) return FST_EMPTY;                       // serialize.rs:60-62
         if (len < 8) return FST_FAILED_FILL;                  // read_exact, :458-463
@@ -462,15 +470,15 @@ __device__ int32_t flat_table(const uint8_t* p, uint64_t len, int no_alloc, uint
             pos += rest;
         }
         if (has_limit && total > limit) return FST_TOO_LARGE;           // :501-507
-        if (total > (len - pos) / 8) return FST_ENDS_PREMATURELY;       // :66-70
+        if (total > (len - pos) / 8) ENDS_PREMATURELY(total, (len - pos) / 8);  // :66-70
     } else {
         if (((uintptr_t)p) & 7) return FST_NOT_ALIGNED;                 // :234-248
-        if (len < 4) return FST_ENDS_PREMATURELY;                       // read_u32_le
+        if (len < 4) ENDS_PREMATURELY(4, len);                          // read_u32_le
         nseg = (uint64_t)ld_u32(p) + 1;                                 // :268-279
         if (nseg >= 512) return FST_BAD_NSEG;                           // :31-35
         pos = 4;
         for (uint64_t i = 0; i < nseg; i++) {                           // :38-45
-            if (len - pos < 4) return FST_ENDS_PREMATURELY;
+            if (len - pos < 4) ENDS_PREMATURELY(4, len - pos);
             const uint32_t l = ld_u32(p + pos);
             if (seg) seg[i] = l;
             total += l;
@@ -478,11 +486,12 @@ __device__ int32_t flat_table(const uint8_t* p, uint64_t len, int no_alloc, uint
         }
         if (has_limit && total > limit) return FST_TOO_LARGE;           // :50-57
         if (!(nseg & 1)) {                                              // padding :61-63
-            if (len - pos < 4) return FST_ENDS_PREMATURELY;
+            if (len - pos < 4) ENDS_PREMATURELY(4, len - pos);
             pos += 4;
         }
-        if (len - pos < total * 8) return FST_ENDS_PREMATURELY;         // :84-89
+        if (len - pos < total * 8) ENDS_PREMATURELY(total, (len - pos) / 8);  // :84-89
     }
+#undef ENDS_PREMATURELY
     *nseg_out = (uint32_t)nseg;
     *table_out = pos;
     *words_out = total;
@@ -503,11 +512,12 @@ __global__ void flat_frame(const uint8_t* __restrict__ buf, const uint64_t* __re
     uint32_t ns = 0;
     uint64_t t = 0, w = 0;
     const int32_t s = flat_table(buf + a, b - a, no_alloc, limit, has_limit, &ns, &t, &w, nullptr);
-    const bool ok = s == FST_OK;
+    const bool ok = s == FST_OK, short_ = s == FST_ENDS_PREMATURELY;
     status[m] = s;
     nseg[m] = ok ? ns : 0;
-    if (body_off) body_off[m] = a + (ok ? t : 0);
-    if (consumed) consumed[m] = ok ? t + 8 * w : 0;
+    // MessageEndsPrematurely(header, body) rides in body_off / consumed
+    if (body_off) body_off[m] = ok ? a + t : (short_ ? t : a);
+    if (consumed) consumed[m] = ok ? t + 8 * w : (short_ ? w : 0);
 }
 
 __global__ void flat_segs(const uint8_t* __restrict__ buf, const uint64_t* __restrict__ off,

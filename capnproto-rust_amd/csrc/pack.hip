@@ -3,8 +3,9 @@
 //
 // Work decomposition
 //   * A tile = `tc` consecutive chunks; one 256-thread workgroup (4 waves)
-//     per tile; tiles are claimed through an atomic ticket so a tile only
-//     ever waits on tiles that were claimed before it (forward progress).
+//     per tile; tile = blockIdx.x (workgroups are dispatched in index
+//     order), so a tile only ever waits on lower-numbered tiles, which were
+//     dispatched before it (forward progress).
 //   * Staged path (every wave's share fits kStageSteps 64-word steps): wave
 //     w owns a contiguous run of the tile's chunks, loads all its words into
 //     registers at once, packs them into its own zeroed LDS region (offsets
@@ -97,7 +98,7 @@ constexpr uint32_t kRegion = (kStageBytes + kGapSlack + 32 + 15) & ~15u;
 constexpr uint32_t kRegionBytes = kRegion > kRing ? kRegion : kRing;
 
 // Record sync index (optional side-band): one entry per global word index
-// m = 16k, for the chunk that holds word m: the chunk-relative packed offset of
+// m = kSyncWords * k (8k), for the chunk that holds word m: the chunk-relative packed offset of
 // the record that covers word m (24 bits) and m minus that record's first
 // word (8 bits; a run covers at most 255 words after its head, so it fits).  An
 // unpack that has the index walks CAPNP_SYNC_WORDS-word segments in parallel and checks that
@@ -870,7 +871,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     }
 #endif
     const uint64_t* __restrict__ toff = chunk_off + c0;  // the tile's chunk offsets
-    // sync entries of the tile: k in [k0, k1), words 32k in [W0, W1)
+    // sync entries of the tile: k in [k0, k1), words kSyncWords * k in [W0, W1)
     const uint64_t TW0 = uniform64(chunk_off[c0]);
     const uint64_t k0 = (TW0 + kSyncWords - 1) / kSyncWords;
     const uint64_t k1 = (uniform64(chunk_off[c1]) + kSyncWords - 1) / kSyncWords;

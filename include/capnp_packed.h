@@ -295,7 +295,12 @@ capnp_status capnp_gpu_read_messages(capnp_ctx* ctx, const uint8_t* d_packed,
    segment (slice start + table bytes); d_consumed[m] table + body bytes (the
    reference's `*slice` advance); segment lengths in words in d_seg_words,
    message m's at [d_msg_seg_off[m], d_msg_seg_off[m+1]) (nmsg+1 entries; a
-   failed message has none).  d_body_off / d_consumed may be NULL.
+   failed message has none).  On CAPNP_E_MESSAGE_ENDS_PREMATURELY,
+   d_body_off[m] / d_consumed[m] carry the reference's
+   MessageEndsPrematurely(header, body) payload instead (serialize.rs:67-71,
+   no_alloc_buffer_segments.rs:77-80, :254-257).  d_slice_off must be
+   non-decreasing and end within d_buf (not checked here; the Python mirror
+   checks it).  d_body_off / d_consumed may be NULL.
    Synchronises the stream once (segment total against segs_cap:
    CAPNP_E_BUFFER_NOT_LARGE_ENOUGH, with only d_msg_seg_off written). */
 capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf,

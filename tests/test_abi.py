@@ -68,3 +68,12 @@ def test_no_cpu_fallback_without_device():
     # the host single-unit API also refuses without a context
     n = C.c_size_t(0)
     assert _lib.lib().capnp_pack(None, None, 0, None, 0, C.byref(n)) == 64
+
+
+def test_seg_words_read_unsigned():
+    """Segment lengths are uint32 in the ABI but land in int32 storage: a
+    2^31-word segment must read back as 2^31, not negative."""
+    import torch
+    from capnp_amd.codec import seg_words_u32
+    raw = torch.tensor([1, -1, -(2**31), 2**31 - 1], dtype=torch.int32)
+    assert seg_words_u32(raw).tolist() == [1, 2**32 - 1, 2**31, 2**31 - 1]

@@ -75,6 +75,8 @@ def test_flat_batch_matches_oracle(ctx, no_alloc, limit):
         if est == 0:
             n_ok += 1
             assert body[m] == a + etb and used[m] == eused, m
+        elif est == 12:  # MessageEndsPrematurely(header, body) payload
+            assert (body[m], used[m]) == (etb, eused), m
         else:
             assert used[m] == 0, m
     assert n_ok > nmsg // (50 if limit == 2 else 10)  # the batch is not all errors
@@ -150,3 +152,37 @@ def test_host_mirror_reference_cases(ctx):
     with pytest.raises(CapnpError) as e:
         S.read_message_from_flat_slice_no_alloc(bad)
     assert e.value.kind == "InvalidNumberOfSegments"
+
+
+def test_serialize_batch_two_phase_cap_and_checks(ctx):
+    """The public batch entry point sizes the segment array exactly (no
+    511-per-message default): 200k one-segment messages need 200k entries.
+    Bad slice offsets, strided tensors and short caps raise instead of
+    reading out of bounds."""
+    from capnp_amd import CapnpError
+    from capnp_amd import serialize as S
+    nmsg = 200_000
+    one = np.frombuffer(flat_message([bytes(8)] * 3), np.uint8)  # 3 segments, 40 bytes
+    buf = torch.from_numpy(np.tile(one, nmsg).copy()).cuda()
+    off = torch.arange(nmsg + 1, dtype=torch.int64, device="cuda") * one.size
+    segs, mso, st, body, used = S.read_flat_messages(buf, off)
+    assert segs.numel() == 3 * nmsg and int(mso[-1]) == 3 * nmsg
+    assert bool((st == 0).all()) and bool((used == one.size).all())
+    for bad in ([0, 40, 20], [0, 40, 10**9], [-8, 40]):
+        with pytest.raises(CapnpError):
+            S.read_flat_messages(buf, torch.tensor(bad, dtype=torch.int64, device="cuda"))
+    with pytest.raises(CapnpError):
+        S.read_flat_messages(buf[::2], off[:2])
+    with pytest.raises(CapnpError):
+        S.read_message_from_flat_slice(buf[::2])
+
+
+def test_message_ends_prematurely_payload(ctx):
+    """capnp/tests/buffer_size_too_small.rs: one segment claiming 2 words with
+    1 word of body is MessageEndsPrematurely(2, 1); the pair comes back in
+    body_off / consumed."""
+    data = np.array([0, 0, 0, 0, 2, 0, 0, 0] + [0] * 8, np.uint8)
+    d = torch.from_numpy(data).cuda()
+    off = torch.tensor([0, 16], dtype=torch.int64, device="cuda")
+    segs, mso, st, body, used = ctx.read_flat_messages(d, off)
+    assert (int(st[0]), int(body[0]), int(used[0])) == (12, 2, 1)

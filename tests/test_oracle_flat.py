@@ -37,7 +37,8 @@ def aligned(data, pad=0):
 
 
 def py_flat(data, no_alloc, limit=O.DEFAULT_TRAVERSAL_LIMIT, align=0):
-    """Independent restatement -> (status, lens, table_bytes, consumed)."""
+    """Independent restatement -> (status, lens, table_bytes, consumed); on
+    MessageEndsPrematurely the last two are its (header, body) payload."""
     n = len(data)
     u32 = lambda p: struct.unpack_from("<I", data, p)[0]
     if not no_alloc:
@@ -59,29 +60,29 @@ def py_flat(data, no_alloc, limit=O.DEFAULT_TRAVERSAL_LIMIT, align=0):
         if limit is not None and sum(lens) > limit:
             return TOO_LARGE, [], 0, 0
         if sum(lens) > (n - pos) // 8:
-            return ENDS, [], 0, 0
+            return ENDS, [], sum(lens), (n - pos) // 8
     else:
         if align % 8:
             return NOT_ALIGNED, [], 0, 0
         if n < 4:
-            return ENDS, [], 0, 0
+            return ENDS, [], 4, n
         cnt = u32(0) + 1
         if cnt >= 512:
             return NSEG, [], 0, 0
         pos, lens = 4, []
         for _ in range(cnt):
             if n - pos < 4:
-                return ENDS, [], 0, 0
+                return ENDS, [], 4, n - pos
             lens.append(u32(pos))
             pos += 4
         if limit is not None and sum(lens) > limit:
             return TOO_LARGE, [], 0, 0
         if cnt % 2 == 0:
             if n - pos < 4:
-                return ENDS, [], 0, 0
+                return ENDS, [], 4, n - pos
             pos += 4
         if n - pos < 8 * sum(lens):
-            return ENDS, [], 0, 0
+            return ENDS, [], sum(lens), (n - pos) // 8
     return OK, lens, pos, pos + 8 * sum(lens)
 
 
@@ -148,3 +149,14 @@ def test_round_trip_property_and_restatement():
             assert got == py_flat(data, na, limit, pad), (it, na)
             if got[0] == OK and mode >= 0.5:
                 assert got[1] == [len(s) // 8 for s in segs]
+
+
+def test_message_ends_prematurely_payload():
+    """capnp/tests/buffer_size_too_small.rs:5-20: one segment claiming 2 words
+    over 1 word of body is MessageEndsPrematurely(2, 1); the no-alloc reader
+    reads the same bytes as a 1-segment table of length 2 (u32 count 0, u32
+    length 2) and reports the same pair (no_alloc_buffer_segments.rs:77-80)."""
+    data = bytes([0, 0, 0, 0, 2, 0, 0, 0]) + bytes(8)
+    for na in (False, True):
+        assert oracle(data, na) == (ENDS, [], 2, 1)
+    assert oracle(bytes(3), True) == (ENDS, [], 4, 3)  # read_u32_le :254-257
