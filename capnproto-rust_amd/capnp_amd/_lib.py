@@ -150,6 +150,8 @@ def lib():
                                                    vp, C.POINTER(C.c_uint32),
                                                    C.POINTER(C.c_uint64)]
     L.capnp_gpu_find_messages.argtypes = [vp, vp, sz, sz, vp, C.POINTER(C.c_size_t), vp]
+    L.capnp_unpack_wt_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    L.capnp_unpack_wt_stats.restype = C.c_int
     L.capnp_packed_reader_buffered.argtypes = [vp]
     L.capnp_packed_reader_buffered.restype = sz
     _lib = L

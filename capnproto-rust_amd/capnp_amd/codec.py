@@ -372,6 +372,9 @@ def carsales_plan(total_words, skip_requests=0):
     return states[:m], offs[:m + 1]
 
 
+WORD_TILE_MEAN = 512  # capi.hip kWordTileMean
+
+
 def tile_chunks_for(total_words, nchunks, lib=None):
     """Chunks per pack workgroup: the staged path holds
     capnp_pack_tile_words() / 64 steps of 64 words per tile and a chunk
@@ -380,6 +383,8 @@ def tile_chunks_for(total_words, nchunks, lib=None):
     import math
     if nchunks <= 0:
         return 16
+    if total_words / nchunks >= WORD_TILE_MEAN:
+        return 0  # word tiles (pack.hip pack_wt_kernel): chunks of any length
     tw = (lib or _lib.lib()).capnp_pack_tile_words()
     steps = max(1, math.ceil(total_words / nchunks / 64.0))
     return int(max(1, min(64, (tw // 64) // steps)))
@@ -389,12 +394,16 @@ def unpack_tile_chunks_for(total_words, nchunks, lib=None, sync=False):
     """Chunks per unpack tile: about capnp_unpack_tile_words() output words
     per 256-thread tile (the staged path's descriptor capacity, unpack.hip),
     or capnp_unpack_sync_tile_words() per wave sub-tile when the record sync
-    index is used."""
+    index is used.  With the index and a mean chunk of WORD_TILE_MEAN words or
+    more: 0, the library's word tiles (chunks of any length, unpack.hip
+    unpack_wt_kernel)."""
     L = lib or _lib.lib()
     tw = L.capnp_unpack_sync_tile_words() if sync else L.capnp_unpack_tile_words()
     if nchunks <= 0:
         return max(1, tw // 128)
     mean = max(total_words / nchunks, 1.0)
+    if sync and mean >= WORD_TILE_MEAN:
+        return 0
     return int(max(1, min(64, tw // mean)))
 
 

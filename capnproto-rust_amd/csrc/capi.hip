@@ -68,6 +68,16 @@ extern "C" uint64_t capnp_carsales_plan(const uint32_t*, uint64_t, uint64_t, uin
 extern "C" hipError_t capnp_launch_gen_carsales(uint64_t*, uint64_t, const uint32_t*,
                                                 const uint64_t*, uint64_t, hipStream_t);
 extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes);
+extern "C" size_t capnp_unpack_wt_ws_bytes(uint64_t wlo, uint64_t whi);
+extern "C" uint64_t capnp_pack_wt_tiles(uint64_t wlo, uint64_t whi);
+extern "C" size_t capnp_pack_wt_ws_bytes(uint64_t wlo, uint64_t whi);
+extern "C" hipError_t capnp_launch_pack_wt(const uint64_t*, const uint64_t*, uint64_t, uint8_t*,
+                                           uint64_t, uint64_t*, uint64_t*, void*, size_t,
+                                           uint32_t*, uint64_t, uint64_t, hipStream_t);
+extern "C" hipError_t capnp_launch_unpack_wt(const uint8_t*, const uint64_t*, uint64_t, uint64_t*,
+                                             const uint64_t*, int32_t*, uint64_t*,
+                                             const uint32_t*, uint64_t, uint64_t, void*, size_t,
+                                             hipStream_t);
 extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t nbytes,
                                                  uint64_t max_msgs, uint64_t* d_pos,
                                                  uint64_t* d_words, uint64_t words_cap,
@@ -116,6 +126,10 @@ struct capnp_ctx {
     size_t msg_cap = 0;
     uint8_t* d_resync = nullptr;  // index-free decode: per-block chain state
     size_t resync_cap = 0;
+    uint8_t* d_wt = nullptr;  // word-tile unpack: per-tile plans and piece flags
+    size_t wt_cap = 0;
+    uint8_t* d_pwt = nullptr;  // word-tile pack: range map and tile offsets
+    size_t pwt_cap = 0;
     uint8_t* d_stream_words = nullptr;  // message discovery: the stream decoded to words
     size_t stream_words_cap = 0;
     int resync_passes = 0, resync_serial = 0;  // last capnp_gpu_unpack_batch_resync
@@ -185,21 +199,6 @@ size_t state_bytes_for(size_t nchunks, uint32_t tc) {
     return capnp_pack_state_bytes(nchunks, tc) + 16;
 }
 
-capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint64_t* d_off,
-                            size_t n, uint8_t* d_out, size_t cap, uint64_t* d_out_off,
-                            uint32_t tc, hipStream_t s, uint32_t* d_sync = nullptr) {
-    if (tc == 0) tc = kDefaultTileChunks;
-    if (tc > kMaxTileChunks) return CAPNP_E_INVALID_ARGUMENT;
-    if (n > 0 && !d_off) return CAPNP_E_INVALID_ARGUMENT;
-    if (!d_out_off) return CAPNP_E_INVALID_ARGUMENT;
-    const size_t sb = state_bytes_for(n, tc);
-    capnp_status st = ensure_state(ctx, sb);
-    if (st != CAPNP_OK) return st;
-    HIP_TRY(capnp_launch_pack(d_words, d_off, n, tc, d_out, cap, d_out_off,
-                              reinterpret_cast<uint64_t*>(ctx->d_state), d_sync, s));
-    return CAPNP_OK;
-}
-
 // Chunks per pack tile: the staged path holds capnp_pack_tile_words() / 64
 // steps of 64 words per tile, and a chunk takes whole steps, so the budget
 // is counted in steps of the mean chunk (a 32-word chunk still takes one).
@@ -210,6 +209,49 @@ uint32_t tile_chunks_for(uint64_t total_words, size_t n) {
     double t = (double)(capnp_pack_tile_words() / 64) / steps;
     uint32_t tc = (uint32_t)std::max(1.0, std::min(t, (double)kMaxTileChunks));
     return tc;
+}
+
+// Batches whose mean chunk is at least this many words pack (and, with the
+// record sync index, unpack) in word tiles.
+constexpr uint64_t kWordTileMean = 512;
+
+// tc == 0: the launch is sized from the batch's word range (one
+// synchronisation to read it): word tiles (capnp_launch_pack_wt: chunks of
+// any length) for a mean chunk of at least kWordTileMean words, else chunk
+// tiles of about capnp_pack_tile_words() words.
+capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint64_t* d_off,
+                            size_t n, uint8_t* d_out, size_t cap, uint64_t* d_out_off,
+                            uint32_t tc, hipStream_t s, uint32_t* d_sync = nullptr) {
+    if (n > 0 && !d_off) return CAPNP_E_INVALID_ARGUMENT;
+    if (!d_out_off) return CAPNP_E_INVALID_ARGUMENT;
+    if (tc == 0 && n > 0) {
+        uint64_t wr[2];
+        HIP_TRY(hipMemcpyAsync(&wr[0], d_off, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&wr[1], d_off + n, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
+        const uint64_t words = wr[1] - wr[0];
+        if (words && words / n >= kWordTileMean) {
+            const uint64_t ntiles = capnp_pack_wt_tiles(wr[0], wr[1]);
+            capnp_status st = ensure_state(ctx, capnp_pack_state_bytes(ntiles, 1) + 16);
+            if (st != CAPNP_OK) return st;
+            st = ensure_buf(ctx, &ctx->d_pwt, &ctx->pwt_cap, capnp_pack_wt_ws_bytes(wr[0], wr[1]));
+            if (st != CAPNP_OK) return st;
+            HIP_TRY(capnp_launch_pack_wt(d_words, d_off, n, d_out, cap, d_out_off,
+                                         reinterpret_cast<uint64_t*>(ctx->d_state), ctx->d_pwt,
+                                         ctx->pwt_cap, d_sync, wr[0], wr[1], s));
+            return CAPNP_OK;
+        }
+        tc = tile_chunks_for(words, n);
+    }
+    if (tc == 0) tc = kDefaultTileChunks;
+    if (tc > kMaxTileChunks) return CAPNP_E_INVALID_ARGUMENT;
+    const size_t sb = state_bytes_for(n, tc);
+    capnp_status st = ensure_state(ctx, sb);
+    if (st != CAPNP_OK) return st;
+    HIP_TRY(capnp_launch_pack(d_words, d_off, n, tc, d_out, cap, d_out_off,
+                              reinterpret_cast<uint64_t*>(ctx->d_state), d_sync, s));
+    return CAPNP_OK;
 }
 
 // Host batch pack through the staging buffer.  Returns the needed size in
@@ -233,7 +275,8 @@ capnp_status pack_host(capnp_ctx* ctx, const uint64_t* words, const uint64_t* of
     HIP_TRY(hipMemcpyAsync(d + o_off, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
     st = pack_batch_dev(ctx, reinterpret_cast<uint64_t*>(d + o_words),
                         reinterpret_cast<uint64_t*>(d + o_off), n, d + o_out, bound,
-                        reinterpret_cast<uint64_t*>(d + o_oo), tile_chunks_for(nw, n), s);
+                        reinterpret_cast<uint64_t*>(d + o_oo),
+                        (n && nw / n >= kWordTileMean) ? 0u : tile_chunks_for(nw, n), s);
     if (st != CAPNP_OK) return st;
     std::vector<uint64_t> oo(n + 1);
     HIP_TRY(hipMemcpyAsync(oo.data(), d + o_oo, (n + 1) * 8, hipMemcpyDeviceToHost, s));
@@ -359,6 +402,8 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (ctx->h_frame) hipHostFree(ctx->h_frame);
     if (ctx->d_msg) hipFree(ctx->d_msg);
     if (ctx->d_resync) hipFree(ctx->d_resync);
+    if (ctx->d_wt) hipFree(ctx->d_wt);
+    if (ctx->d_pwt) hipFree(ctx->d_pwt);
     for (int k = 0; k < 3; k++)
         if (ctx->sstream[k]) {
             hipStreamSynchronize(ctx->sstream[k]);
@@ -391,7 +436,7 @@ capnp_status capnp_gpu_pack_batch(capnp_ctx* ctx, const uint64_t* d_words,
                                   void* stream) {
     if (!ctx) return CAPNP_E_INVALID_ARGUMENT;
     return pack_batch_dev(ctx, d_words, d_chunk_word_off, nchunks, d_out, out_cap,
-                          d_out_byte_off, kDefaultTileChunks, pick(ctx, stream));
+                          d_out_byte_off, 0, pick(ctx, stream));
 }
 
 capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
@@ -404,6 +449,12 @@ capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
                           d_out_byte_off, chunks_per_tile, pick(ctx, stream));
 }
 
+// With the record sync index and chunks_per_tile == 0 the launch is sized
+// from the batch's word range (one synchronisation to read it): batches whose
+// mean chunk is at least kWordTileMean words decode in word tiles
+// (capnp_launch_unpack_wt: chunks of any length, cut at sync points), others
+// in chunk tiles of about capnp_unpack_tile_words() words.
+
 static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
                                      const uint64_t* d_in_byte_off, size_t nchunks,
                                      uint64_t* d_words, const uint64_t* d_out_word_off,
@@ -412,6 +463,27 @@ static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
     if (!ctx || (nchunks && (!d_in_byte_off || !d_out_word_off || !d_status)))
         return CAPNP_E_INVALID_ARGUMENT;
     if (tc > 256) return CAPNP_E_INVALID_ARGUMENT;
+    if (d_sync && tc == 0 && nchunks) {
+        hipStream_t s = pick(ctx, stream);
+        uint64_t wr[2];
+        HIP_TRY(hipMemcpyAsync(&wr[0], d_out_word_off, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipMemcpyAsync(&wr[1], d_out_word_off + nchunks, 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
+        const uint64_t words = wr[1] - wr[0];
+        if (words && words / nchunks >= kWordTileMean) {
+            const size_t ws = capnp_unpack_wt_ws_bytes(wr[0], wr[1]);
+            capnp_status st = ensure_buf(ctx, &ctx->d_wt, &ctx->wt_cap, ws);
+            if (st != CAPNP_OK) return st;
+            HIP_TRY(capnp_launch_unpack_wt(d_packed, d_in_byte_off, nchunks, d_words,
+                                           d_out_word_off, d_status, d_consumed, d_sync, wr[0],
+                                           wr[1], ctx->d_wt, ctx->wt_cap, s));
+            return CAPNP_OK;
+        }
+        const uint64_t mean = words / nchunks ? words / nchunks : 1;
+        const uint64_t t = capnp_unpack_tile_words() / mean;
+        tc = (uint32_t)(t < 1 ? 1 : (t > 64 ? 64 : t));
+    }
     HIP_TRY(capnp_launch_unpack(d_packed, d_in_byte_off, nchunks, tc, d_words, d_out_word_off,
                                 d_status, d_consumed, d_sync, pick(ctx, stream)));
     return CAPNP_OK;
@@ -444,7 +516,7 @@ capnp_status capnp_gpu_pack_batch_sync(capnp_ctx* ctx, const uint64_t* d_words,
                                        uint32_t* d_sync, void* stream) {
     if (!ctx || !d_sync) return CAPNP_E_INVALID_ARGUMENT;
     return pack_batch_dev(ctx, d_words, d_chunk_word_off, nchunks, d_out, out_cap,
-                          d_out_byte_off, kDefaultTileChunks, pick(ctx, stream), d_sync);
+                          d_out_byte_off, 0, pick(ctx, stream), d_sync);
 }
 
 capnp_status capnp_gpu_unpack_batch_sync(capnp_ctx* ctx, const uint8_t* d_packed,

@@ -627,12 +627,202 @@ __device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* o
     }
 }
 
+// ---------------------------------------------------------------------------
+// Word tiles (batches of long chunks): the batch is one word stream in which
+// every chunk start is a forced record head, cut into tiles of kWtTile words
+// and wave ranges of kWtRange words wherever those boundaries fall.  A range
+// that starts inside a record needs the run state there (carry_into), and a
+// run left open at its end needs the words it goes on to absorb (run_ext);
+// both come from the words around the boundary.
+constexpr uint32_t kWtRange = 64 * kStageSteps;  // words per wave range
+constexpr uint32_t kWtTile = kWaves * kWtRange;  // words per tile
+
+struct LookbackArgs {
+    uint64_t* ts;
+    uint64_t* gs;
+    uint64_t ntiles;
+    const uint64_t* in;
+    const uint64_t* chunk_off;
+    uint64_t nchunks;
+    uint32_t tc;
+    const uint32_t* gap;
+    // word tiles: the batch's words [wlo, whi), tile t = global tile g0 + t
+    uint32_t wt;
+    uint64_t wlo, whi, g0;
+    const uint64_t* map;  // first chunk starting at or after each wave range
+};
+
+// Run segmentation of one step with forced heads S (chunk starts) and
+// `nvalid` valid words: the heads, the words the carried run absorbs, and
+// the run state after the step's last valid word.  As resolve_step, plus:
+// no run absorbs a chunk start (zero runs: Z' & (Z' << 1) & ~S; literal runs:
+// the L runs are cut before every chunk start, and a 0xFF head at a chunk
+// start opens its run at the next word).
+__device__ __forceinline__ StepMasks resolve_step_s(uint64_t Zm, uint64_t Lm, uint64_t Fm,
+                                                    uint64_t Sm, uint32_t nvalid, Carry c) {
+    StepMasks r;
+    uint64_t AC = 0;
+    uint32_t k = 0;
+    if (c.type != 0) {
+        const uint32_t lead = ctz64(~(c.type == 1 ? Zm : Lm));
+        const uint32_t cut = ctz64(Sm);
+        k = min(min(lead, c.rem), cut);
+        AC = low_mask(k);
+    }
+    const uint64_t Z2 = Zm & ~AC;
+    const uint64_t AZ = Z2 & (Z2 << 1) & ~Sm;
+    const uint64_t L2 = Lm & ~AC & ~Sm;
+    const uint64_t F2 = Fm & ~AC;
+    const uint64_t F3 = (F2 & ~Sm) | (((F2 & Sm) << 1) & L2);
+    const uint64_t filled = ((L2 ^ (L2 + F3)) & L2) | F2;
+    const uint64_t AF = filled & (filled << 1) & ~Sm;
+    const uint64_t H = low_mask(nvalid) & ~(AC | AZ | AF);
+    r.H = H;
+    r.absorbed_carry = k;
+    if (H == 0) {
+        r.next.type = c.type;
+        r.next.rem = c.rem - nvalid;  // the carry covered the valid words
+    } else {
+        const uint32_t h = 63u - (uint32_t)__builtin_clzll(H);
+        const uint64_t hb = 1ull << h;
+        r.next.type = (Zm & hb) ? 1u : ((Fm & hb) ? 2u : 0u);
+        r.next.rem = r.next.type ? 255u - (nvalid - 1u - h) : 0u;
+    }
+    return r;
+}
+
+// Word i (after its chunk's first word) is a record head whatever came
+// before when: it is zero after a non-zero word, or non-zero after a zero
+// word (a zero run absorbs only zero words, a 0xFF run only words with at
+// most one zero byte); it has 2..7 zero bytes (nothing absorbs it); or it has
+// at most one zero byte after a word with 2..7 zero bytes (a head that opens
+// no run).
+__device__ __forceinline__ bool sure_head(uint32_t tag, uint32_t ptag) {
+    const uint32_t pop = __builtin_popcount(tag), ppop = __builtin_popcount(ptag);
+    const bool z = tag == 0, pz = ptag == 0;
+    const bool brk = !z && pop <= 6, pbrk = !pz && ppop <= 6;
+    return z != pz || brk || (pop >= 7 && pbrk);
+}
+
+__device__ __forceinline__ uint32_t tag_of(uint64_t w) {
+    return word_tag_dot((uint32_t)w, (uint32_t)(w >> 32));
+}
+
+// Run state entering word R of the chunk starting at cs (cs < R): from the
+// last sure head s before R, heads fall every 256 words while the words are
+// all zero or all 0xFF-tagged; otherwise the steps from s are resolved.
+__device__ Carry carry_into(const uint64_t* __restrict__ in, uint64_t cs, uint64_t R,
+                            uint32_t lane) {
+    uint64_t s = cs;
+    bool allz = true, allf = true;  // over [s, R)
+    for (uint64_t hi = R; hi > cs;) {
+        const uint64_t lo = hi - cs > 64 ? hi - 64 : cs;
+        const uint64_t i = lo + lane;
+        const bool v = i < hi;
+        const uint32_t tag = v ? tag_of(in[i]) : 0u;
+        const uint32_t ptag = (v && i > cs) ? tag_of(in[i - 1]) : 0u;
+        const uint64_t G = ballot64(v && (i == cs || sure_head(tag, ptag)));
+        const uint32_t j = G ? 63u - (uint32_t)__builtin_clzll(G) : 0u;
+        const bool mine = v && lane >= j;
+        allz = allz && ballot64(mine && tag != 0) == 0;
+        allf = allf && ballot64(mine && tag != 0xFF) == 0;
+        if (G) {
+            s = lo + j;
+            break;
+        }
+        hi = lo;
+    }
+    if (allz || allf) {
+        const uint64_t h = s + (R - 1 - s) / 256 * 256;  // the last head before R
+        return Carry{allz ? 1u : 2u, (uint32_t)(255u - (R - 1 - h))};
+    }
+    Carry c{0, 0};
+    for (uint64_t p = s; p < R; p += 64) {
+        const uint32_t nv = (uint32_t)(R - p < 64 ? R - p : 64);
+        const uint32_t tag = lane < nv ? tag_of(in[p + lane]) : 0u;
+        const uint32_t pop = __builtin_popcount(tag);
+        const uint64_t V = low_mask(nv);
+        const StepMasks sm = resolve_step_s(ballot64(tag == 0) & V, ballot64(pop >= 7) & V,
+                                            ballot64(tag == 0xFF) & V, 0, nv, c);
+        c = sm.next;
+    }
+    return c;
+}
+
+// Words from R on (up to the chunk end ce) that the open run c absorbs.
+__device__ uint32_t run_ext(const uint64_t* __restrict__ in, uint64_t R, uint64_t ce, Carry c,
+                            uint32_t lane) {
+    if (c.type == 0 || c.rem == 0) return 0;
+    uint32_t ext = 0;
+    for (uint64_t p = R; p < ce && ext < c.rem; p += 64) {
+        const uint32_t nv = (uint32_t)(ce - p < 64 ? ce - p : 64);
+        const uint32_t tag = lane < nv ? tag_of(in[p + lane]) : 0u;
+        const bool cls = c.type == 1 ? tag == 0 : __builtin_popcount(tag) >= 7;
+        const uint32_t lead = ctz64(~ballot64(lane < nv && cls));
+        ext += lead;
+        if (lead < 64) break;
+    }
+    return ext < c.rem ? ext : c.rem;
+}
+
+__device__ __forceinline__ void wt_tile_bounds(const LookbackArgs& A, uint64_t t, uint64_t& Ta,
+                                               uint64_t& Tb) {
+    const uint64_t g = A.g0 + t;
+    Ta = g * kWtTile > A.wlo ? g * kWtTile : A.wlo;
+    Tb = (g + 1) * kWtTile < A.whi ? (g + 1) * kWtTile : A.whi;
+}
+
+// Packed bytes of words [R0, R1) (one wave; the look-back fallback).
+__device__ uint64_t wt_range_size(const LookbackArgs& A, uint64_t R0, uint64_t R1, uint64_t cA,
+                                  uint32_t lane) {
+    const uint64_t* off = A.chunk_off;
+    Carry c{0, 0};
+    if (uniform64(off[cA]) != R0) c = carry_into(A.in, uniform64(off[cA - 1]), R0, lane);
+    uint64_t total = 0, cp = cA;
+    for (uint64_t p = R0; p < R1; p += 64) {
+        const uint32_t nv = (uint32_t)(R1 - p < 64 ? R1 - p : 64);
+        uint64_t S = 0;
+        while (cp <= A.nchunks && uniform64(off[cp]) < p + nv) {
+            S |= 1ull << (uniform64(off[cp]) - p);
+            cp++;
+        }
+        const uint32_t tag = lane < nv ? tag_of(A.in[p + lane]) : 0u;
+        const uint32_t pop = __builtin_popcount(tag);
+        const uint64_t V = low_mask(nv);
+        const StepMasks sm = resolve_step_s(ballot64(tag == 0) & V, ballot64(pop >= 7) & V,
+                                            ballot64(tag == 0xFF) & V, S, nv, c);
+        const bool head = (sm.H >> lane) & 1;
+        const uint32_t size = lane >= nv ? 0u : head ? 1u + pop + ((0x101u >> pop) & 1u)
+                                                     : (tag ? 8u : 0u);
+        uint64_t v = size;
+        for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        total += v;
+        c = sm.next;
+    }
+    return total;
+}
+
+__device__ uint64_t wt_tile_size(const LookbackArgs& A, uint64_t t, uint32_t lane) {
+    uint64_t Ta, Tb, total = 0;
+    wt_tile_bounds(A, t, Ta, Tb);
+    for (uint32_t w = 0; w < kWaves; w++) {
+        const uint64_t R0 = Ta + (uint64_t)w * kWtRange;
+        if (R0 >= Tb) break;
+        const uint64_t R1 = R0 + kWtRange < Tb ? R0 + kWtRange : Tb;
+        total += wt_range_size(A, R0, R1, uniform64(A.map[t * kWaves + w]), lane);
+    }
+    return total;
+}
+
 // Packed size of tile j computed by one wave from the input (the look-back
 // fallback below; normally never executed).
-__device__ uint64_t tile_aggregate(const uint64_t* __restrict__ in,
-                                   const uint64_t* __restrict__ chunk_off, uint64_t nchunks,
-                                   uint32_t tc, const uint32_t* __restrict__ gap, uint64_t j,
-                                   uint32_t lane) {
+__device__ uint64_t tile_aggregate(const LookbackArgs& A, uint64_t j, uint32_t lane) {
+    if (A.wt) return wt_tile_size(A, j, lane);
+    const uint64_t* __restrict__ in = A.in;
+    const uint64_t* __restrict__ chunk_off = A.chunk_off;
+    const uint64_t nchunks = A.nchunks;
+    const uint32_t tc = A.tc;
+    const uint32_t* __restrict__ gap = A.gap;
     const uint64_t c0 = j * tc;
     const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
     uint64_t total = 0;
@@ -680,17 +870,16 @@ constexpr uint32_t kGroup = 64;
 constexpr uint32_t kGroupWindow = PACK_GWIN;  // group records per poll
 constexpr uint32_t kSpinLimit = 4096;
 
-__device__ uint64_t group_aggregate(uint64_t* __restrict__ ts, const uint64_t* __restrict__ in,
-                                    const uint64_t* __restrict__ chunk_off, uint64_t nchunks,
-                                    uint32_t tc, const uint32_t* __restrict__ gap,
-                                    uint64_t ntiles, uint64_t g, uint32_t lane) {
+__device__ uint64_t group_aggregate(const LookbackArgs& A, uint64_t g, uint32_t lane) {
+    uint64_t* __restrict__ ts = A.ts;
+    const uint64_t ntiles = A.ntiles;
     const uint64_t t0 = g * kGroup;
     const uint64_t tn = (t0 + kGroup < ntiles) ? kGroup : ntiles - t0;
     uint64_t st = lane < tn ? poll_agent(&ts[t0 + lane]) : kFlagAgg;
     uint64_t miss = ballot64((st >> 62) == 0);
     while (miss) {
         const uint32_t k = ctz64(miss);
-        const uint64_t a = tile_aggregate(in, chunk_off, nchunks, tc, gap, t0 + k, lane);
+        const uint64_t a = tile_aggregate(A, t0 + k, lane);
         if (lane == 0) publish_agent(&ts[t0 + k], kFlagAgg | a);
         if (lane == k) st = kFlagAgg | a;
         miss &= miss - 1;
@@ -699,17 +888,6 @@ __device__ uint64_t group_aggregate(uint64_t* __restrict__ ts, const uint64_t* _
     for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
 }
-
-struct LookbackArgs {
-    uint64_t* ts;
-    uint64_t* gs;
-    uint64_t ntiles;
-    const uint64_t* in;
-    const uint64_t* chunk_off;
-    uint64_t nchunks;
-    uint32_t tc;
-    const uint32_t* gap;
-};
 
 // Wave 0: publishes tile t's aggregate.
 __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint64_t agg,
@@ -742,7 +920,7 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
         if (++spins >= kSpinLimit) {
             if (lane == 0) PROF_ADD(2, 1);
             const uint64_t j = g * kGroup + ctz64(miss);
-            const uint64_t a = tile_aggregate(A.in, A.chunk_off, A.nchunks, A.tc, A.gap, j, lane);
+            const uint64_t a = tile_aggregate(A, j, lane);
             if (lane == 0) publish_agent(&A.ts[j], kFlagAgg | a);
         } else {
             __builtin_amdgcn_s_sleep(PACK_SLEEP);
@@ -777,8 +955,7 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
 #endif
             if (++spins >= kSpinLimit) {
                 const uint64_t jg = (uint64_t)(idx - (int64_t)ctz64(missing));
-                const uint64_t a = group_aggregate(A.ts, A.in, A.chunk_off, A.nchunks, A.tc, A.gap,
-                                                   A.ntiles, jg, lane);
+                const uint64_t a = group_aggregate(A, jg, lane);
                 if (lane == 0) publish_agent(&A.gs[jg], kFlagAgg | a);
             } else {
                 __builtin_amdgcn_s_sleep(PACK_SLEEP);
@@ -857,6 +1034,9 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     LA.nchunks = nchunks;
     LA.tc = tc;
     LA.gap = GAP ? gap : nullptr;
+    LA.wt = 0;
+    LA.wlo = LA.whi = LA.g0 = 0;
+    LA.map = nullptr;
 
     const uint64_t c0 = tile * tc;
     const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
@@ -1048,6 +1228,273 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     }
 }
 
+// ---------------------------------------------------------------------------
+// Word-tile pack kernel.  Tile t = words [Ta, Tb) of the batch (kWtTile words
+// at global multiples of kWtTile), wave w = range [Ta + w kWtRange, ...): the
+// staged path of pack_kernel with steps of 64 consecutive words of the range,
+// chunk starts as forced heads (resolve_step_s), the run state at the range
+// start from carry_into and the words its last run goes on to absorb from
+// run_ext.  Record bytes land as in the chunk tiles; a chunk's offset is the
+// position of its first word's record.  Sync entries are written by the lane
+// of the sync point's word: the covering record's position minus its
+// chunk's, both tile-relative; for the chunk the tile starts inside of, the
+// chunk's own start is unknown here, so the entry holds the record's position
+// relative to the tile (24-bit two's complement) and pack_wt_fix_sync adds
+// tile offset - chunk offset once every tile is placed.
+struct WtSmem {
+    uint64_t smask[kWaves][kStageSteps];   // chunk starts per step
+    uint16_t wpos[kWaves][kWtRange];       // region position of chunk-start words
+    uint32_t lastcs[kWaves];               // region position of the last chunk start
+    uint64_t excl;
+};
+
+__device__ __forceinline__ void size_step_s(StageState& pk, uint64_t w, uint32_t nvalid,
+                                            uint64_t Sm, uint32_t lane, StepInfo& si) {
+    const uint32_t tag = word_tag_dot((uint32_t)w, (uint32_t)(w >> 32));
+    const uint32_t pop = __builtin_popcount(tag);
+    const bool isz = tag == 0, isf = tag == 0xFF;
+    const uint64_t V = low_mask(nvalid);
+    const uint64_t Zm = ballot64(isz) & V;
+    const uint64_t Lm = ballot64(pop >= 7) & V;
+    const uint64_t Fm = ballot64(isf) & V;
+    const StepMasks sm = resolve_step_s(Zm, Lm, Fm, Sm, nvalid, pk.carry);
+    const uint32_t hsize = 1u + pop + ((0x101u >> pop) & 1u);
+    const uint32_t size = mask_sel(sm.H, hsize, isz ? 0u : 8u);
+    const uint32_t incl = wave_incl_scan(size);
+    si.H = sm.H;
+    si.pos = pk.o_c + pk.total + incl - size;
+    si.tag = tag;
+    si.meta = nvalid | (sm.absorbed_carry << 16);
+    pk.carry = sm.next;
+    pk.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+}
+
+template <bool SYNC>
+__global__ void __launch_bounds__(kThreads, PACK_MIN_WAVES)
+pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
+               uint64_t nchunks, uint8_t* __restrict__ out, uint64_t out_cap,
+               uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts, uint64_t* __restrict__ gs,
+               uint32_t* __restrict__ sync, const uint64_t* __restrict__ map,
+               uint64_t* __restrict__ tile_off, uint64_t wlo, uint64_t whi, uint64_t g0) {
+    __shared__ Smem sm;
+    __shared__ WtSmem wm;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint64_t tile = blockIdx.x;
+    LookbackArgs LA;
+    LA.ts = ts;
+    LA.gs = gs;
+    LA.ntiles = gridDim.x;
+    LA.in = in;
+    LA.chunk_off = chunk_off;
+    LA.nchunks = nchunks;
+    LA.tc = 0;
+    LA.gap = nullptr;
+    LA.wt = 1;
+    LA.wlo = wlo;
+    LA.whi = whi;
+    LA.g0 = g0;
+    LA.map = map;
+    uint64_t Ta, Tb;
+    wt_tile_bounds(LA, tile, Ta, Tb);
+    const uint64_t R0 = Ta + (uint64_t)wave * kWtRange;
+    const bool have = R0 < Tb;
+    const uint64_t R1 = !have ? R0 : (R0 + kWtRange < Tb ? R0 + kWtRange : Tb);
+    const uint32_t nw = (uint32_t)(R1 - R0);
+    const bool lastr = have && R1 == whi;
+    for (uint32_t i = tid; i <= kSelCopy; i += kThreads)
+        reinterpret_cast<uint4*>(sm.sel)[i] = reinterpret_cast<const uint4*>(kSelTable.e)[i];
+    if (lane < kStageSteps) wm.smask[wave][lane] = 0;
+    uint8_t* region = sm.stage[wave];
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
+    uint8_t* const outa = out - mis;
+    // the range's words
+    uint64_t cache[kStageSteps];
+#pragma unroll
+    for (uint32_t s = 0; s < kStageSteps; s++) {
+        const uint32_t i = 64u * s + lane;
+        cache[s] = i < nw ? in[R0 + i] : 0ull;
+    }
+    for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
+        *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
+    wave_lds_sync();
+    // chunk starts in the range: [cA, cB) (plus, in the batch's last range,
+    // the empty chunks at its end)
+    const uint64_t cA = have ? uniform64(map[tile * kWaves + wave]) : nchunks;
+    uint64_t cB = cA;
+    if (have) {
+        for (uint64_t c0 = cA;; c0 += 64) {
+            const uint64_t c = c0 + lane;
+            const uint64_t st = c < nchunks ? chunk_off[c] : ~0ull;
+            const bool inr = c < nchunks && (st < R1 || (lastr && st == R1));
+            if (inr && st < R1) {
+                const uint32_t r = (uint32_t)(st - R0);
+                atomicOr(reinterpret_cast<unsigned long long*>(&wm.smask[wave][r >> 6]),
+                         1ull << (r & 63u));
+            }
+            const uint64_t m = ballot64(inr);
+            cB = c0 + popc64(m);
+            if (m != ~0ull) break;
+        }
+    }
+    Carry cin{0, 0};
+    if (have && uniform64(chunk_off[cA < nchunks ? cA : nchunks]) != R0)
+        cin = carry_into(in, uniform64(chunk_off[cA - 1]), R0, lane);
+    __syncthreads();
+    // pass 1: sizes and positions
+    StepInfo si[kStageSteps];
+    uint64_t smk[kStageSteps];
+    StageState pk;
+    pk.begin(0);
+    pk.carry = cin;
+    uint32_t lastcs = ~0u;
+#pragma unroll
+    for (uint32_t s = 0; s < kStageSteps; s++) {
+        const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
+        smk[s] = uniform64(wm.smask[wave][s]);
+        size_step_s(pk, cache[s], nv, smk[s], lane, si[s]);
+        if ((smk[s] >> lane) & 1) wm.wpos[wave][64u * s + lane] = (uint16_t)si[s].pos;
+        if (smk[s])
+            lastcs = (uint32_t)__builtin_amdgcn_readlane((int)si[s].pos,
+                                                         63 - __builtin_clzll(smk[s]));
+    }
+    uint32_t rext = 0;
+    if (have && !lastr) {
+        const uint64_t ce = uniform64(chunk_off[cB]);  // end of the chunk holding word R1 - 1
+        rext = run_ext(in, R1, ce, pk.carry, lane);
+    }
+    if (lane == 0) {
+        sm.wave_bytes[wave] = pk.total;
+        wm.lastcs[wave] = lastcs;
+    }
+    __syncthreads();
+    uint32_t woff = 0, agg = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+        const uint32_t b = (uint32_t)lds_u64(&sm.wave_bytes[w]);
+        woff += w < (int)wave ? b : 0u;
+        agg += b;
+    }
+    if (wave == 0) publish(LA, tile, agg, lane);
+    // pass 2: the bytes
+    wave_lds_sync();
+    {
+        uint8_t* const region_m1 = region - 1;
+        uint32_t ext = rext;
+#pragma unroll
+        for (int s = (int)kStageSteps - 1; s >= 0; s--) {
+            const uint32_t e = ext;
+            emit_step<false>(cache[s], si[s], e, lane, region_m1, sm.sel, nullptr, 0, 0, 0);
+            ext = (si[s].meta >> 16) + (si[s].H == 0 ? e : 0u);
+        }
+    }
+    if constexpr (SYNC) {
+        // the chunk open at R0 started at tile position oc (0: before the tile)
+        uint32_t oc = 0;
+        for (int w = (int)wave - 1; w >= 0; w--) {
+            const uint32_t l = uniform(wm.lastcs[w]);
+            if (l != ~0u) {
+                uint32_t o = 0;
+                for (int v = 0; v < w; v++) o += (uint32_t)lds_u64(&sm.wave_bytes[v]);
+                oc = o + l;
+                break;
+            }
+        }
+        // the record open at R0 (a run from before it): its head word and
+        // tile position (its head bytes and literal words precede R0's bytes)
+        const uint32_t before = cin.type == 2 ? 255u - cin.rem : 0u;
+        uint32_t hp = woff - (cin.type == 1 ? 2u : 10u + 8u * before);
+        uint64_t hw = R0 - (255u - cin.rem) - 1u;
+#pragma unroll
+        for (uint32_t s = 0; s < kStageSteps; s++) {
+            const uint32_t nv = si[s].meta & 127u;
+            const uint64_t base = R0 + 64u * s;
+            const uint64_t H = si[s].H, Sm = smk[s];
+            const uint32_t tpos = woff + si[s].pos;
+            const uint64_t below = low_mask(lane + 1);
+            const uint64_t sb = Sm & below, hb = H & below;
+            const uint32_t js = sb ? 63u - (uint32_t)__builtin_clzll(sb) : 0u;
+            const uint32_t jh = hb ? 63u - (uint32_t)__builtin_clzll(hb) : 0u;
+            const uint32_t pjs = (uint32_t)__shfl((int)tpos, (int)js, 64);
+            const uint32_t pjh = (uint32_t)__shfl((int)tpos, (int)jh, 64);
+            const uint64_t gw = base + lane;
+            if (lane < nv && (gw & (kSyncWords - 1)) == 0) {
+                const uint32_t myoc = sb ? pjs : oc;
+                const uint32_t myhp = hb ? pjh : hp;
+                const uint32_t d = (uint32_t)(gw - (hb ? base + jh : hw));
+                sync[gw / kSyncWords] = ((myhp - myoc) & 0xFFFFFFu) | (d << 24);
+            }
+            if (Sm) oc = (uint32_t)__builtin_amdgcn_readlane((int)tpos, 63 - __builtin_clzll(Sm));
+            if (H) {
+                const uint32_t h = 63u - (uint32_t)__builtin_clzll(H);
+                hp = (uint32_t)__builtin_amdgcn_readlane((int)tpos, (int)h);
+                hw = base + h;
+            }
+        }
+    }
+    if (wave == 0) {
+        const uint64_t excl = lookback(LA, tile, agg, lane);
+        if (lane == 0) {
+            wm.excl = excl;
+            tile_off[tile] = excl;
+            if (Tb == whi) out_off[nchunks] = excl + agg;
+        }
+    }
+    __syncthreads();
+    const uint64_t excl = lds_u64(&wm.excl);
+    for (uint64_t c = cA + lane; c < cB; c += CAPNP_WAVE) {
+        const uint64_t st = chunk_off[c];
+        out_off[c] = st < R1 ? excl + woff + wm.wpos[wave][st - R0] : excl + agg;
+    }
+    if (have)
+        copy_out(region, outa, excl + woff + mis, lds_u64(&sm.wave_bytes[wave]), out_cap + mis,
+                 lane);
+}
+
+// First chunk starting at or after each wave range's first word.
+__global__ void __launch_bounds__(256)
+pack_wt_map(const uint64_t* __restrict__ chunk_off, uint64_t nchunks, uint64_t wlo, uint64_t whi,
+            uint64_t g0, uint64_t nranges, uint64_t* __restrict__ map) {
+    const uint64_t r = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= nranges) return;
+    const uint64_t g = g0 + r / kWaves;
+    const uint64_t Ta = g * kWtTile > wlo ? g * kWtTile : wlo;
+    const uint64_t R0 = Ta + (r % kWaves) * kWtRange;
+    uint64_t lo = 0, hi = nchunks;  // in [0, nchunks]
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (chunk_off[mid] < R0) lo = mid + 1;
+        else hi = mid;
+    }
+    map[r] = R0 < whi ? lo : nchunks;
+}
+
+// Sync entries of each tile's first chunk when it started before the tile:
+// tile-relative record positions become chunk-relative.
+__global__ void __launch_bounds__(64)
+pack_wt_fix_sync(const uint64_t* __restrict__ chunk_off, const uint64_t* __restrict__ out_off,
+                 const uint64_t* __restrict__ map, const uint64_t* __restrict__ tile_off,
+                 uint32_t* __restrict__ sync, uint64_t wlo, uint64_t whi, uint64_t g0) {
+    const uint64_t t = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t g = g0 + t;
+    const uint64_t Ta = g * kWtTile > wlo ? g * kWtTile : wlo;
+    const uint64_t Tb = (g + 1) * kWtTile < whi ? (g + 1) * kWtTile : whi;
+    const uint64_t cA = map[t * kWaves];
+    if (chunk_off[cA] == Ta) return;  // the tile starts a chunk
+    const uint64_t c = cA - 1;
+    const int64_t delta = (int64_t)(tile_off[t] - out_off[c]);
+    const uint64_t end = chunk_off[cA] < Tb ? chunk_off[cA] : Tb;
+    const uint64_t k0 = (Ta + kSyncWords - 1) / kSyncWords, k1 = (end + kSyncWords - 1) / kSyncWords;
+    for (uint64_t k = k0 + lane; k < k1; k += 64) {
+        const uint32_t v = sync[k];
+        const int32_t rel = (int32_t)(v << 8) >> 8;  // 24-bit two's complement
+        const int64_t f = (int64_t)rel + delta;
+        sync[k] = (f < 0 || f >= (1 << 24)) ? kSyncNone : ((uint32_t)f | (v & 0xFF000000u));
+    }
+}
+
 }  // namespace
 
 // Words per tile the staged path is sized for (kWaves waves x kStageSteps
@@ -1101,6 +1548,50 @@ extern "C" hipError_t capnp_launch_pack_gap(const uint64_t* d_in, const uint64_t
     hipLaunchKernelGGL((pack_kernel<false, true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
                        stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_state,
                        d_state + ntiles, nullptr, d_gap);
+    return hipGetLastError();
+}
+
+// Word tiles (batches of long chunks): workspace = map (first chunk of every
+// wave range) + tile offsets; the look-back records live in d_state
+// (capnp_pack_state_bytes(ntiles, 1), uncached).  [wlo, whi) = the batch's
+// words, read by the caller (the grid is sized by them).
+extern "C" uint64_t capnp_pack_wt_tiles(uint64_t wlo, uint64_t whi) {
+    return whi > wlo ? (whi + kWtTile - 1) / kWtTile - wlo / kWtTile : 0;
+}
+
+extern "C" size_t capnp_pack_wt_ws_bytes(uint64_t wlo, uint64_t whi) {
+    return capnp_pack_wt_tiles(wlo, whi) * (kWaves + 1) * 8 + 64;
+}
+
+extern "C" uint32_t capnp_pack_wt_words(void) { return kWtTile; }
+
+extern "C" hipError_t capnp_launch_pack_wt(const uint64_t* d_in, const uint64_t* d_chunk_off,
+                                           uint64_t nchunks, uint8_t* d_out, uint64_t out_cap,
+                                           uint64_t* d_out_off, uint64_t* d_state, void* d_ws,
+                                           size_t ws_bytes, uint32_t* d_sync, uint64_t wlo,
+                                           uint64_t whi, hipStream_t stream) {
+    const uint64_t ntiles = capnp_pack_wt_tiles(wlo, whi);
+    if (nchunks == 0 || ntiles == 0 || ws_bytes < capnp_pack_wt_ws_bytes(wlo, whi))
+        return hipErrorInvalidValue;
+    const uint64_t g0 = wlo / kWtTile;
+    uint64_t* map = reinterpret_cast<uint64_t*>(d_ws);
+    uint64_t* toff = map + ntiles * kWaves;
+    hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(ntiles, 1), stream);
+    if (e != hipSuccess) return e;
+    const uint64_t nr = ntiles * kWaves;
+    hipLaunchKernelGGL(pack_wt_map, dim3((uint32_t)((nr + 255) / 256)), dim3(256), 0, stream,
+                       d_chunk_off, nchunks, wlo, whi, g0, nr, map);
+    if (d_sync) {
+        hipLaunchKernelGGL(pack_wt_kernel<true>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
+                           d_in, d_chunk_off, nchunks, d_out, out_cap, d_out_off, d_state,
+                           d_state + ntiles, d_sync, map, toff, wlo, whi, g0);
+        hipLaunchKernelGGL(pack_wt_fix_sync, dim3((uint32_t)ntiles), dim3(64), 0, stream,
+                           d_chunk_off, d_out_off, map, toff, d_sync, wlo, whi, g0);
+    } else {
+        hipLaunchKernelGGL(pack_wt_kernel<false>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
+                           d_in, d_chunk_off, nchunks, d_out, out_cap, d_out_off, d_state,
+                           d_state + ntiles, d_sync, map, toff, wlo, whi, g0);
+    }
     return hipGetLastError();
 }
 

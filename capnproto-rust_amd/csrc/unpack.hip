@@ -67,6 +67,27 @@ __device__ unsigned long long g_uprof[8];
 #define UPROF_T(v)
 #endif
 
+#ifndef UNPACK_WT_DEBUG
+#define UNPACK_WT_DEBUG 0
+#endif
+#if UNPACK_WT_DEBUG
+__device__ unsigned long long g_wt_ev_n;
+__device__ uint32_t g_wt_ev[64 * 12];
+__device__ __forceinline__ void wt_event(uint32_t kind, uint32_t b, uint32_t c, uint32_t q,
+                                         uint32_t w, uint32_t c2, uint32_t q2, uint32_t w2,
+                                         uint32_t err, uint32_t x, uint32_t y) {
+    const unsigned long long k = atomicAdd(&g_wt_ev_n, 1ull);
+    if (k < 64) {
+        uint32_t* e = g_wt_ev + 12 * k;
+        e[0] = blockIdx.x; e[1] = kind; e[2] = b; e[3] = c; e[4] = q; e[5] = w;
+        e[6] = c2; e[7] = q2; e[8] = w2; e[9] = err; e[10] = x; e[11] = y;
+    }
+}
+#define WT_EVENT(...) wt_event(__VA_ARGS__)
+#else
+#define WT_EVENT(...) ((void)0)
+#endif
+
 namespace {
 
 constexpr int kWaves = 4;
@@ -343,6 +364,10 @@ struct StageSmem {
     uint32_t cp[kStageChunks + 1];  // sync walk: chunk packed offsets (LDS positions)
     uint32_t ent[kMaxSeg];          // sync walk: entry of segment b (b >= 1)
     uint8_t segc[kMaxSeg];          // sync walk: chunk that holds segment b's first word
+    // word tiles (unpack_wt_kernel): walk start of segment 0 (position + 1,
+    // word), the state the last walker must reach at the tile end when the
+    // last chunk continues, words of the first chunk before the tile, flags
+    uint32_t wt_q0, wt_w0, wt_qB, wt_wB, wt_pre, wt_pl;
     alignas(16) uint8_t bytes[kTileBytes + 16];
     alignas(16) uint16_t dpos[kTileWords + 2 * CAPNP_WAVE];  // [kTileWords + 2 lane]: dummy slots
 };
@@ -525,20 +550,32 @@ __device__ __forceinline__ void mark_bad(SM& S, uint32_t c, bool& marked) {
 // started in an earlier segment (d > 0: a run), it belongs to that
 // segment's walker and the segment starts after it.  An unusable entry
 // yields the end of its chunk and marks it bad.
-template <class SM>
+//
+// WT (word tiles): segment 0 starts where the tile's plan put it (mid-chunk
+// after the run that covers the tile's first word), and a run may have its
+// head in the first chunk before the tile (wt_pre words of it lie there).
+template <class SM, bool WT = false>
 __device__ __forceinline__ void seg_start(SM& S, uint32_t nc, uint32_t b, uint32_t sb,
                                           uint32_t& c, uint32_t& q, uint32_t& w, bool mark,
                                           bool& marked) {
     c = S.segc[b];
     if (b == 0) {
-        q = S.cp[c] + 1u;
-        w = 0;
+        if constexpr (WT) {
+            q = S.wt_q0;
+            w = S.wt_w0;
+        } else {
+            q = S.cp[c] + 1u;
+            w = 0;
+        }
         return;
     }
     const uint32_t e = S.ent[b];
     const uint32_t off = e & 0xFFFFFFu, d = e >> 24;
     const uint32_t cpe1 = S.cp[c + 1] + 1u, cwe = S.cw[c + 1];
-    bool ok = e != kSyncNone && off < S.cp[c + 1] - S.cp[c] && sb - d >= S.cw[c] && d <= sb;
+    // the run's head word sb - d must lie in chunk c
+    uint32_t pre = 0;
+    if constexpr (WT) pre = c == 0 ? S.wt_pre : 0u;
+    bool ok = e != kSyncNone && off < S.cp[c + 1] - S.cp[c] && d <= sb - S.cw[c] + pre;
     q = S.cp[c] + off + 1u;
     w = sb;
     if (ok && d) {  // skip the run that covers sb
@@ -553,6 +590,7 @@ __device__ __forceinline__ void seg_start(SM& S, uint32_t nc, uint32_t b, uint32
         w = wn;
     }
     if (!ok) {
+        if constexpr (WT) if (mark) WT_EVENT(4, b, c, q, w, e, off, d, 0, sb, cwe);
         if (mark) mark_bad(S, c, marked);
         q = cpe1;
         w = cwe;
@@ -566,12 +604,17 @@ __device__ __forceinline__ void seg_start(SM& S, uint32_t nc, uint32_t b, uint32
 // (rare, wave-uniform) stop branch, which moves a lane at a chunk end to the
 // next chunk or retires it.  Record checks accumulate into a sticky error
 // flag (a failed record ends its chunk; the chunk is re-walked exactly).
-template <class SM>
+//
+// WT: the last chunk may continue past the tile (wt_pl): its runs may reach
+// past the tile end (their literal entries stop at wlim = the tile's words)
+// and the last walker must end in the state the tile plan derived from the
+// entry at the tile end.
+template <class SM, bool WT = false>
 __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uint32_t sb,
-                                             uint32_t eb, bool last) {
+                                             uint32_t eb, bool last, uint32_t wlim = 0) {
     bool marked = false;
     uint32_t c, q, w;
-    seg_start(S, nc, b, sb, c, q, w, true, marked);
+    seg_start<SM, WT>(S, nc, b, sb, c, q, w, true, marked);
     const uint8_t* B = S.bytes;
     const uint32_t dummy = SM::kDummy + 2u * lane_id();
     uint32_t cwe = S.cw[c + 1], cpe1 = S.cp[c + 1] + 1u;
@@ -609,7 +652,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
             const uint32_t wn = wn0 < cwe ? wn0 : cwe;
             S.dpos[w] = (uint16_t)(q - 1u);
             if (ballot64(isf && wn > w + 1)) {  // literal-run words (rare)
-                if (isf) lit_entries(S, w, q - 1u, wn - w - 1);
+                if (isf) lit_entries(S, w, q - 1u, (WT && wn > wlim ? wlim : wn) - w - 1);
             }
             q = qn;
             w = wn;
@@ -635,7 +678,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
         const uint32_t wn = wn0 < cwe ? wn0 : cwe;
         S.dpos[hop ? w : dummy] = (uint16_t)(q - 1u);
         if (ballot64(hop && isf && wn > w + 1)) {  // literal-run words (rare)
-            if (hop && isf) lit_entries(S, w, q - 1u, wn - w - 1);
+            if (hop && isf) lit_entries(S, w, q - 1u, (WT && wn > wlim ? wlim : wn) - w - 1);
         }
         q = hop ? qn : q;
         w = hop ? wn : w;
@@ -654,7 +697,10 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
             if (!hop && !((done >> lane_id()) & 1)) {
                 if (w == cwe) {
                     // a non-empty chunk must end exactly at its packed end
-                    if (err || (S.cw[c] < cwe && q != cpe1)) mark_bad(S, c, marked);
+                    if (err || (S.cw[c] < cwe && q != cpe1)) {
+                        if constexpr (WT) WT_EVENT(5, b, c, q, w, cpe1, cwe, S.cw[c], err, sb, eb);
+                        mark_bad(S, c, marked);
+                    }
                     err = false;
                     c++;
                     while (c < nc && S.cw[c + 1] == w) c++;  // empty chunks: status OK
@@ -691,7 +737,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
 #if UNPACK_EXP != 1  // 1: timing only, no descriptors
         S.dpos[hop ? w : dummy] = (uint16_t)(q - 1u);
         if (ballot64(hop && isf && wn > w + 1)) {  // literal-run words (rare)
-            if (hop && isf) lit_entries(S, w, q - 1u, wn - w - 1);
+            if (hop && isf) lit_entries(S, w, q - 1u, (WT && wn > wlim ? wlim : wn) - w - 1);
         }
 #endif
         q = hop ? qn : q;
@@ -708,13 +754,27 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
 #endif
     // the walks must meet
     if (last) {
-        if (c < nc) mark_bad(S, c, marked);
+        bool pl = false;
+        if constexpr (WT) pl = S.wt_pl != 0;
+        if (pl) {
+            if constexpr (WT)
+                // (c == nc: the walk reached the chunk's end exactly, just past
+                // the tile, and passed its end check)
+                if (c + 1 < nc || q != S.wt_qB || w != S.wt_wB || err) {
+                    WT_EVENT(1, b, c, q, w, nc, S.wt_qB, S.wt_wB, err, sb, eb);
+                    mark_bad(S, nc - 1, marked);
+                }
+        } else if (c < nc) {
+            if constexpr (WT) WT_EVENT(2, b, c, q, w, nc, 0, 0, err, sb, eb);
+            mark_bad(S, c, marked);
+        }
     } else {
         uint32_t c2, q2, w2;
-        seg_start(S, nc, b + 1, eb, c2, q2, w2, false, marked);
+        seg_start<SM, WT>(S, nc, b + 1, eb, c2, q2, w2, false, marked);
         // (positions and words decide: "end of chunk c" and "start of chunk
         // c+1" are the same state)
         if (q2 != q || w2 != w || err) {
+            if constexpr (WT) WT_EVENT(3, b, c, q, w, c2, q2, w2, err, sb, eb);
             if (c < nc) mark_bad(S, c, marked);
             mark_bad(S, c2, marked);
         }
@@ -947,6 +1007,372 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
 }
 
 // ---------------------------------------------------------------------------
+// Word tiles: batches of long chunks with the record sync index.
+//
+// Chunk tiles (unpack_kernel) hold whole chunks, so a chunk longer than a
+// tile falls to the lane-per-chunk global walk.  Word tiles cut the batch's
+// output words at every multiple of kWtWords instead (a multiple of
+// kSyncWords, so the index has an entry at every cut): tile s decodes words
+// [Wa, Wb) whatever chunks they belong to.
+//   * A chunk that starts before Wa (the tile's first chunk, "partial
+//     first") is entered through the entry at Wa: its walk starts at the
+//     record that covers Wa, or after it when that record is a run that began
+//     earlier (a literal run's words in the tile are listed up front).
+//   * A chunk that continues past Wb ("partial last") is walked up to Wb,
+//     where the last walker must reach the state the entry at Wb names.
+//   * Every segment boundary inside the tile is checked as in the chunk
+//     tiles, so the pieces of a chunk are exact when every check passes.
+// Chunks inside the tile get their status here.  A partial chunk's pieces
+// report to flags[] (bit 0: the tile's first chunk failed, bit 1: its last),
+// and unpack_wt_finish gives the chunk its status from all of them: OK, or an
+// exact serial decode of the chunk when any piece failed or a tile could not
+// be planned (an unusable index entry, more than kStageChunks chunks, or
+// bytes beyond the LDS table).  unpack_wt_plan (one thread per tile) resolves
+// the tile's chunks and both ends from global memory up front.
+#ifndef UNPACK_WT_WORDS
+#define UNPACK_WT_WORDS 1024
+#endif
+constexpr uint32_t kWtWords = UNPACK_WT_WORDS;
+static_assert(kWtWords % kSyncWords == 0 && kWtWords <= kTileWords, "word tile size");
+// plan flags
+constexpr uint32_t kWtPf = 1, kWtPl = 2, kWtFallback = 4;
+
+// Diagnostics (capnp_unpack_wt_stats): [0] tiles planned as fallback, [1]
+// pieces that failed in a tile, [2] chunks the finish kernel decoded serially.
+__device__ unsigned long long g_wt_stats[4];
+// first failing tiles: tile id, badc mask (UNPACK_WT_DEBUG builds)
+__device__ unsigned long long g_wt_dbg[2 * 256];
+
+struct alignas(16) WtPlan {
+    uint64_t ca, cb;  // chunks [ca, cb) overlap the tile
+    uint64_t bs;      // first staged byte (global)
+    uint32_t span;    // staged bytes from bs
+    uint32_t flags;   // kWtPf | kWtPl | kWtFallback
+    uint32_t q0, w0;  // segment 0 start: position after bs + 1, tile word
+    uint32_t qB, wB;  // state at the tile end (partial last): position after bs + 1, tile word
+    uint32_t pre;     // words of the first chunk before the tile
+    uint32_t litp;    // partial first inside a literal run: position after bs of
+    uint32_t litn;    // tile word 0's raw word, and the tile words the run covers
+    uint32_t pad;
+};
+static_assert(sizeof(WtPlan) == 64, "plan record");
+
+__device__ __forceinline__ void wt_bounds(uint64_t s, uint64_t g0, uint64_t wlo, uint64_t whi,
+                                          uint64_t& Wa, uint64_t& Wb) {
+    const uint64_t g = g0 + s;
+    Wa = g * kWtWords > wlo ? g * kWtWords : wlo;
+    Wb = (g + 1) * kWtWords < whi ? (g + 1) * kWtWords : whi;
+}
+
+// The record that covers global word W of chunk c, from its sync entry:
+// false if the entry is unusable.  h = the record's first byte; for a run that
+// started before W (d > 0): its end (qe), its word count and whether literal.
+__device__ bool wt_entry(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                         const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ sync,
+                         uint64_t c, uint64_t W, uint64_t& h, uint32_t& d, uint64_t& qe,
+                         uint32_t& cnt, bool& lit) {
+    const uint64_t cs = in_off[c], ce = in_off[c + 1];
+    const uint32_t e = sync[W / kSyncWords];
+    const uint32_t off = e & 0xFFFFFFu;
+    d = e >> 24;
+    if (e == kSyncNone || ce < cs || off >= ce - cs || d > W - out_off[c]) return false;
+    h = cs + off;
+    cnt = 0;
+    lit = false;
+    qe = h;
+    if (d == 0) return true;
+    const uint32_t tag = in[h];
+    if (tag != 0 && tag != 0xFF) return false;
+    lit = tag == 0xFF;
+    const uint64_t cpos = h + (lit ? 9u : 1u);
+    if (cpos >= ce) return false;
+    cnt = in[cpos];
+    qe = cpos + 1 + (lit ? 8ull * cnt : 0ull);
+    return cnt >= d && qe <= ce;
+}
+
+__global__ void __launch_bounds__(256)
+unpack_wt_plan(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
+               const uint64_t* __restrict__ out_off, const uint32_t* __restrict__ sync,
+               uint64_t wlo, uint64_t whi, uint64_t g0, uint64_t ntiles,
+               WtPlan* __restrict__ plan) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= ntiles) return;
+    uint64_t Wa, Wb;
+    wt_bounds(s, g0, wlo, whi, Wa, Wb);
+    const uint32_t Wt = (uint32_t)(Wb - Wa);
+    // first chunk: the one holding Wa, else the first to start at Wa
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (out_off[mid] < Wa) lo = mid + 1;
+        else hi = mid;
+    }
+    const uint64_t ca = (lo > 0 && out_off[lo] > Wa) ? lo - 1 : lo;
+    uint64_t cb = ca + 1;
+    if (Wb == whi) cb = n;  // the last tile takes the empty chunks at the end
+    else
+        while (cb < n && out_off[cb] < Wb) cb++;
+    WtPlan P = {};
+    P.ca = ca;
+    P.cb = cb;
+    const bool pf = out_off[ca] < Wa, pl = Wb < whi && out_off[cb] > Wb;
+    bool ok = cb - ca <= kStageChunks;
+    uint64_t bs = in_off[ca], be = in_off[cb];
+    P.q0 = 1;
+    if (ok && pf) {
+        uint64_t h, qe;
+        uint32_t d, cnt;
+        bool lit;
+        ok = wt_entry(in, in_off, out_off, sync, ca, Wa, h, d, qe, cnt, lit);
+        if (ok) {
+            bs = h;
+            P.pre = (uint32_t)(Wa - out_off[ca]);
+            if (d) {  // a run from before the tile covers its first words
+                P.q0 = (uint32_t)(qe - h) + 1u;
+                P.w0 = cnt - d + 1u;
+                if (lit) {
+                    P.litp = 10u + 8u * (d - 1u);
+                    P.litn = P.w0 < Wt ? P.w0 : Wt;
+                }
+            }
+        }
+    }
+    if (ok && pl) {
+        const uint64_t cl = cb - 1;
+        uint64_t h, qe;
+        uint32_t d, cnt;
+        bool lit;
+        ok = wt_entry(in, in_off, out_off, sync, cl, Wb, h, d, qe, cnt, lit) && h >= bs;
+        if (ok) {
+            if (d == 0) {
+                P.qB = (uint32_t)(h - bs) + 1u;
+                P.wB = Wt;
+                be = h;
+            } else {
+                P.qB = (uint32_t)(qe - bs) + 1u;
+                P.wB = Wt - d + 1u + cnt;
+                be = lit ? h + 10 + 8ull * (d - 1) : h + 2;
+            }
+        }
+    }
+    const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + bs) & 15u);
+    ok = ok && be >= bs && be - bs <= kTileBytes - off0;
+    P.bs = bs;
+    P.span = ok ? (uint32_t)(be - bs) : 0u;
+    P.flags = (pf ? kWtPf : 0u) | (pl ? kWtPl : 0u) | (ok ? 0u : kWtFallback);
+    plan[s] = P;
+}
+
+// Exact decode of one chunk by one lane from global memory, the reference's
+// order of checks (as unpack_global): the word-tile path's fallback.
+__device__ void serial_chunk(const uint8_t* __restrict__ in, uint64_t p0, uint64_t pe,
+                             uint64_t* __restrict__ out, uint64_t n, int32_t& st,
+                             uint64_t& used) {
+    uint64_t p = p0, w = 0;
+    st = ST_OK;
+    if (n > 0 && p == pe) st = ST_FAILED_FILL;
+    while (st == ST_OK && w < n) {
+        if (p >= pe) { st = ST_PREMATURE; break; }
+        const uint32_t tag = in[p];
+        const uint32_t pop = __builtin_popcount(tag);
+        if (p + 1 + pop > pe) { st = ST_PREMATURE; break; }
+        uint64_t word = 0;
+        for (uint32_t k = 0, r = 0; k < 8; k++)
+            if (tag & (1u << k)) word |= (uint64_t)in[p + 1 + r++] << (8 * k);
+        out[w++] = word;
+        uint64_t q = p + 1 + pop;
+        if (tag == 0 || tag == 0xFF) {
+            if (q >= pe) { st = ST_PREMATURE; break; }
+            const uint64_t cnt = in[q++];
+            if (cnt > n - w) { st = ST_NOT_CLEAN; break; }
+            if (tag == 0) {
+                for (uint64_t i = 0; i < cnt; i++) out[w++] = 0;
+            } else {
+                if (pe - q < 8 * cnt) { st = ST_FAILED_FILL; break; }
+                for (uint64_t i = 0; i < cnt; i++, q += 8) out[w++] = load_bytes(in, q, 8);
+            }
+        }
+        p = q;
+    }
+    used = st == ST_OK ? p - p0 : (st == ST_NOT_CLEAN ? 0 : pe - p0);
+}
+
+__device__ __forceinline__ void serial_chunk_at(const uint8_t* __restrict__ in,
+                                                const uint64_t* __restrict__ in_off,
+                                                uint64_t* __restrict__ out,
+                                                const uint64_t* __restrict__ out_off,
+                                                int32_t* __restrict__ status,
+                                                uint64_t* __restrict__ consumed, uint64_t c) {
+    int32_t st;
+    uint64_t used;
+    const uint64_t ow = out_off[c];
+    serial_chunk(in, in_off[c], in_off[c + 1], out + ow, out_off[c + 1] - ow, st, used);
+    status[c] = st;
+    if (consumed) consumed[c] = used;
+}
+
+__global__ void __launch_bounds__(kThreads, UNPACK_MIN_WAVES)
+unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                 uint64_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                 int32_t* __restrict__ status, uint64_t* __restrict__ consumed,
+                 const uint32_t* __restrict__ sync, const WtPlan* __restrict__ plan,
+                 uint32_t* __restrict__ flags, uint64_t wlo, uint64_t whi, uint64_t g0) {
+    __shared__ USmem sm;
+    StageSmem& S = sm.st;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t s = blockIdx.x;
+    uint64_t Wa, Wb;
+    wt_bounds(s, g0, wlo, whi, Wa, Wb);
+    const uint32_t Wt = (uint32_t)(Wb - Wa);
+    const WtPlan* Pp = plan + s;
+    const uint64_t ca = uniform64(Pp->ca), cb = uniform64(Pp->cb);
+    const uint32_t pf_ = uniform(Pp->flags);
+    const bool pf = pf_ & kWtPf, pl = pf_ & kWtPl;
+    if (pf_ & kWtFallback) {  // exact serial decode of the chunks inside the tile
+        for (uint64_t c = ca + tid; c < cb; c += kThreads)
+            if (!((pf && c == ca) || (pl && c + 1 == cb)))
+                serial_chunk_at(in, in_off, out, out_off, status, consumed, c);
+        if (tid == 0) {
+            flags[s] = 3u;
+            atomicAdd(&g_wt_stats[0], 1ull);
+        }
+        return;
+    }
+    const uint32_t nc = (uint32_t)(cb - ca);
+    const uint64_t Bs = uniform64(Pp->bs);
+    const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + Bs) & 15u);
+    const uint32_t nbytes = uniform(Pp->span) + off0;
+    // segments as in the chunk tiles: [0, kSyncWords kf - Wa), then blocks
+    // at global multiples of kSyncWords (Wa is one except for a batch that
+    // starts unaligned, whose first tile starts a chunk)
+    const uint64_t kf = Wa / kSyncWords + 1;
+    const uint32_t nseg = 1u + (uint32_t)((Wb - 1) / kSyncWords + 1 - kf);
+    const uint32_t r0 = (uint32_t)(Wa % kSyncWords);
+    S.sel[tid] = kExpandTable.s[tid];
+    {
+        constexpr uint32_t kLoads = (kTileBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
+        const uint4* src = reinterpret_cast<const uint4*>(in + Bs - off0);
+        uint4* dst = reinterpret_cast<uint4*>(S.bytes);
+        const uint32_t nblk = (nbytes + 15) / 16;
+        uint4 r[kLoads];
+#pragma unroll
+        for (uint32_t k = 0; k < kLoads; k++) {
+            const uint32_t idx = tid + k * kThreads;
+            r[k] = nblk ? src[idx < nblk ? idx : nblk - 1] : make_uint4(0, 0, 0, 0);
+        }
+        // descriptors: none, or the raw words of a literal run carried in
+        const uint32_t litn = uniform(Pp->litn), litp = uniform(Pp->litp) + off0;
+        if (litn == 0) {
+            uint4* dd = reinterpret_cast<uint4*>(S.dpos);
+            const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
+            for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
+        } else {
+            for (uint32_t i = tid; i < ((Wt + 7) & ~7u); i += kThreads)
+                S.dpos[i] = i < litn ? (uint16_t)(kRaw | (litp + 8 * i)) : kNone;
+        }
+        if (tid <= nc) {
+            const uint64_t wo = out_off[ca + tid];
+            const uint32_t wa = wo < Wa ? 0u : (uint32_t)(wo - Wa);
+            S.cw[tid] = wa;  // (the end of a partial last chunk lies past Wt)
+            S.cp[tid] = (uint32_t)(in_off[ca + tid] - Bs) + off0;  // (wraps for a partial first)
+            if (tid < nc) {
+                const uint64_t wn = out_off[ca + tid + 1];
+                const uint32_t wz = wn - Wa < Wt ? (uint32_t)(wn - Wa) : Wt;
+                if (wz > wa) {
+                    const uint32_t blo = wa == 0 ? 0u : (wa + r0 + kSyncWords - 1) / kSyncWords;
+                    const uint32_t bhi = (wz + r0 + kSyncWords - 1) / kSyncWords;
+                    for (uint32_t bb = blo; bb < bhi; bb++) S.segc[bb] = (uint8_t)tid;
+                }
+            }
+        }
+        for (uint32_t b = tid; b < nseg; b += kThreads)
+            if (b >= 1) S.ent[b] = sync[kf + b - 1];
+        if (tid < kStageChunks) S.badc[tid] = 0;
+        if (tid == 0) {
+            S.wt_q0 = uniform(Pp->q0) + off0;
+            S.wt_w0 = uniform(Pp->w0);
+            S.wt_qB = uniform(Pp->qB) + off0;
+            S.wt_wB = uniform(Pp->wB);
+            S.wt_pre = uniform(Pp->pre);
+            S.wt_pl = pl ? 1u : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kLoads; k++)
+            if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
+    }
+    __syncthreads();
+    bool marked = false;
+    for (uint32_t b = tid; b < nseg; b += kThreads) {
+        const uint32_t sb = b == 0 ? 0u : (uint32_t)((kf + b - 1) * kSyncWords - Wa);
+        const bool last = b + 1 == nseg;
+        const uint32_t eb = last ? Wt : (uint32_t)((kf + b) * kSyncWords - Wa);
+        marked |= walk_segment<StageSmem, true>(S, nc, b, sb, eb, last, Wt);
+    }
+    const bool anybad = __syncthreads_or(marked);
+    if (tid < nc) {
+        const uint64_t c = ca + tid;
+        const bool part = (pf && tid == 0) || (pl && tid + 1 == nc);
+        if (!part) {
+            if (anybad && S.badc[tid]) {  // exact serial walk of the chunk
+                const uint32_t wa = S.cw[tid], wz = S.cw[tid + 1];
+                for (uint32_t i = wa; i < wz; i++) S.dpos[i] = kNone;
+                int32_t st;
+                uint32_t used;
+                walk_chunk(S, S.cp[tid], S.cp[tid + 1], wa, wz - wa, st, used);
+                status[c] = st;
+                if (consumed) consumed[c] = used;
+            } else {
+                status[c] = ST_OK;
+                if (consumed)
+                    consumed[c] = S.cw[tid + 1] > S.cw[tid] ? S.cp[tid + 1] - S.cp[tid] : 0u;
+            }
+        }
+    }
+    if (tid == 0) {
+        const uint32_t f = ((pf && S.badc[0]) ? 1u : 0u) | ((pl && S.badc[nc - 1]) ? 2u : 0u);
+        flags[s] = f;
+        if (f) {
+            const unsigned long long k = atomicAdd(&g_wt_stats[1], 1ull);
+            if (k < 256) {
+                unsigned long long m = 0;
+                for (uint32_t i = 0; i < nc && i < 64; i++) m |= (unsigned long long)(S.badc[i] != 0) << i;
+                g_wt_dbg[2 * k] = s;
+                g_wt_dbg[2 * k + 1] = m;
+            }
+        }
+    }
+    if (anybad) __syncthreads();
+    for (uint32_t i = tid; i < Wt; i += kThreads) out[Wa + i] = expand_desc(S.bytes, S.sel, S.dpos[i]);
+}
+
+// Status of every chunk that spans tiles, in the tile where it ends.
+__global__ void __launch_bounds__(256)
+unpack_wt_finish(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                 uint64_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                 int32_t* __restrict__ status, uint64_t* __restrict__ consumed,
+                 const WtPlan* __restrict__ plan, const uint32_t* __restrict__ flags,
+                 uint64_t wlo, uint64_t whi, uint64_t g0, uint64_t ntiles) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= ntiles || !(plan[s].flags & kWtPf)) return;
+    uint64_t Wa, Wb;
+    wt_bounds(s, g0, wlo, whi, Wa, Wb);
+    const uint64_t c = plan[s].ca;
+    if (out_off[c + 1] > Wb) return;  // it goes on: the tile where it ends finishes it
+    const uint64_t s0 = out_off[c] / kWtWords - g0;  // the tile of its first word
+    uint32_t bad = flags[s] & 1u;
+    for (uint64_t u = s - 1; u > s0; u--) bad |= flags[u];  // tiles it covers
+    bad |= flags[s0] >> 1;
+    if (!bad) {
+        status[c] = ST_OK;
+        if (consumed) consumed[c] = in_off[c + 1] - in_off[c];
+    } else {
+        atomicAdd(&g_wt_stats[2], 1ull);
+        serial_chunk_at(in, in_off, out, out_off, status, consumed, c);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Sync kernel (the record sync index is given): every wave is autonomous.  A
 // sub-tile = `tc` consecutive chunks of about kSubWords output words; wave w
 // of workgroup g takes sub-tile 4 g + w, stages its packed bytes in its own
@@ -1162,6 +1588,65 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
         hipLaunchKernelGGL(unpack_kernel<false>, dim3((uint32_t)blocks), dim3(kThreads),
                            UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
                            d_status, d_consumed, d_sync);
+    return hipGetLastError();
+}
+
+// Word tiles (long chunks, record sync index): workspace and launch.  The
+// batch's output words are [wlo, whi) = [out_off[0], out_off[nchunks]), which
+// the caller read (the grid is sized by them).
+extern "C" size_t capnp_unpack_wt_ws_bytes(uint64_t wlo, uint64_t whi) {
+    const uint64_t ntiles = whi > wlo ? (whi + kWtWords - 1) / kWtWords - wlo / kWtWords : 0;
+    return ntiles * (sizeof(WtPlan) + 4) + 64;
+}
+
+extern "C" uint32_t capnp_unpack_wt_words(void) { return kWtWords; }
+
+extern "C" int capnp_unpack_wt_events(uint32_t* out768) {
+#if UNPACK_WT_DEBUG
+    return hipMemcpyFromSymbol(out768, HIP_SYMBOL(g_wt_ev), sizeof(g_wt_ev)) == hipSuccess ? 0 : -1;
+#else
+    (void)out768;
+    return -1;
+#endif
+}
+
+extern "C" int capnp_unpack_wt_dbg(unsigned long long* out512) {
+    return hipMemcpyFromSymbol(out512, HIP_SYMBOL(g_wt_dbg), sizeof(g_wt_dbg)) == hipSuccess ? 0 : -1;
+}
+
+// Word-tile diagnostics since the last reset: fallback tiles, failed pieces,
+// chunks decoded serially by the finish kernel (tests use them to check that
+// a valid index keeps every piece on the fast path).
+extern "C" int capnp_unpack_wt_stats(unsigned long long* out4, int reset) {
+    if (hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_wt_stats), sizeof(g_wt_stats)) != hipSuccess)
+        return -1;
+    if (reset) {
+        static const unsigned long long z[4] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_wt_stats), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+
+extern "C" hipError_t capnp_launch_unpack_wt(const uint8_t* d_in, const uint64_t* d_in_off,
+                                             uint64_t nchunks, uint64_t* d_out,
+                                             const uint64_t* d_out_off, int32_t* d_status,
+                                             uint64_t* d_consumed, const uint32_t* d_sync,
+                                             uint64_t wlo, uint64_t whi, void* d_ws,
+                                             size_t ws_bytes, hipStream_t stream) {
+    if (nchunks == 0 || whi <= wlo || !d_sync) return hipErrorInvalidValue;
+    if (ws_bytes < capnp_unpack_wt_ws_bytes(wlo, whi)) return hipErrorInvalidValue;
+    const uint64_t g0 = wlo / kWtWords;
+    const uint64_t ntiles = (whi + kWtWords - 1) / kWtWords - g0;
+    WtPlan* plan = reinterpret_cast<WtPlan*>((reinterpret_cast<uintptr_t>(d_ws) + 63) & ~uintptr_t(63));
+    uint32_t* flags = reinterpret_cast<uint32_t*>(plan + ntiles);
+    const uint32_t g256 = (uint32_t)((ntiles + 255) / 256);
+    hipLaunchKernelGGL(unpack_wt_plan, dim3(g256), dim3(256), 0, stream, d_in, d_in_off, nchunks,
+                       d_out_off, d_sync, wlo, whi, g0, ntiles, plan);
+    hipLaunchKernelGGL(unpack_wt_kernel, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream, d_in,
+                       d_in_off, d_out, d_out_off, d_status, d_consumed, d_sync, plan, flags, wlo,
+                       whi, g0);
+    hipLaunchKernelGGL(unpack_wt_finish, dim3(g256), dim3(256), 0, stream, d_in, d_in_off, d_out,
+                       d_out_off, d_status, d_consumed, plan, flags, wlo, whi, g0, ntiles);
     return hipGetLastError();
 }
 
