@@ -749,6 +749,247 @@ __device__ Carry carry_into(const uint64_t* __restrict__ in, uint64_t cs, uint64
     return c;
 }
 
+__device__ uint32_t run_ext(const uint64_t* __restrict__ in, uint64_t R, uint64_t ce, Carry c,
+                            uint32_t lane);
+
+// Chunk-start bits of a word-tile batch (pack_wt_bits): bit i & 63 of
+// cb[1 + (i >> 6) - b64] is set when a chunk starts at word i (b64 = the
+// batch's first word >> 6; cb[0] and a tail are zero guards).  The 64 bits
+// for words p .. p + 63 (p >= 64 (b64 - 1)):
+__device__ __forceinline__ uint64_t start_bits(const uint64_t* __restrict__ cb, uint64_t b64,
+                                               uint64_t p) {
+    const uint64_t q = 1 + (p >> 6) - b64;
+    const uint32_t r = (uint32_t)(p & 63);
+    const uint64_t lo = cb[q];
+    return r ? (lo >> r) | (cb[q + 1] << (64 - r)) : lo;
+}
+
+// The run state entering word R from the 64 words before it (w = word
+// R - 64 + lane, wp = word R - 65, bits = their chunk-start bits): the last
+// sure head or chunk start s before R, then heads every 256 words through an
+// all-zero / all-0xFF stretch, or one resolved step.  Deeper stretches load
+// eight windows (words and bits) per round.
+__device__ __forceinline__ Carry carry_in_b(const uint64_t* __restrict__ in,
+                                            const uint64_t* __restrict__ cb, uint64_t b64,
+                                            uint64_t wlo, uint64_t R, uint32_t lane, uint64_t w,
+                                            uint64_t wp, uint64_t bits) {
+    const uint64_t i = R - 64 + lane;
+    const bool v = R + lane >= 64 + wlo;  // i >= wlo
+    const uint32_t tag = v ? tag_of(w) : 0u;
+    const uint32_t up = (uint32_t)__shfl_up((int)tag, 1, 64);
+    const uint32_t ptag = lane ? up : tag_of(wp);
+    const uint64_t G = ballot64(v && (((bits >> lane) & 1) || sure_head(tag, ptag)));
+    if (G) {
+        const uint32_t j = 63u - (uint32_t)__builtin_clzll(G);
+        const uint64_t s = R - 64 + j;
+        const bool mine = lane >= j;
+        const bool allz = ballot64(mine && tag != 0) == 0, allf = ballot64(mine && tag != 0xFF) == 0;
+        if (allz || allf) {
+            const uint64_t h = s + (R - 1 - s) / 256 * 256;
+            return Carry{allz ? 1u : 2u, (uint32_t)(255u - (R - 1 - h))};
+        }
+        const uint32_t pop = __builtin_popcount(tag);
+        const uint64_t Vj = ~low_mask(j);
+        return resolve_step_s(ballot64(tag == 0) & Vj, ballot64(pop >= 7) & Vj,
+                              ballot64(tag == 0xFF) & Vj, 1ull << j, 64, Carry{0, 0}).next;
+    }
+    bool allz = ballot64(tag != 0) == 0, allf = ballot64(tag != 0xFF) == 0;
+    for (uint64_t hi = R - 64; hi > wlo; hi = hi > wlo + 512 ? hi - 512 : wlo) {
+        uint32_t t[8];
+        uint64_t bk[8];
+        {
+            uint64_t x[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint64_t lo = hi - 64 * (k + 1);  // (may wrap below 0: then invalid)
+                const bool inb = hi >= wlo + 64ull * (k + 1) - lane;  // lo + lane >= wlo
+                x[k] = inb ? in[lo + lane] : 0ull;
+                // (words lo .. lo + 63 reach the batch: lo >= 0 and lo + 64 > wlo)
+                bk[k] = (hi >= 64ull * (k + 1) && hi + 64 > wlo + 64ull * (k + 1))
+                            ? start_bits(cb, b64, lo) : 0ull;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) t[k] = tag_of(x[k]);
+        }
+        int kf = -1;
+        uint64_t s = wlo;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const bool vk = hi >= wlo + 64ull * (k + 1) - lane;
+            const uint32_t tk = vk ? t[k] : 0u;
+            const uint32_t pt0 = (uint32_t)__shfl_up((int)tk, 1, 64);
+            const uint32_t below = k < 7 ? (uint32_t)__shfl((int)t[k < 7 ? k + 1 : 7], 63, 64) : 0u;
+            const uint32_t pt = lane ? pt0 : below;
+            const bool sure = vk && (((bk[k] >> lane) & 1) || ((lane || k < 7) && sure_head(tk, pt)));
+            const uint64_t Gk = ballot64(sure);
+            if (kf < 0) {
+                if (Gk) {
+                    const uint32_t j = 63u - (uint32_t)__builtin_clzll(Gk);
+                    kf = k;
+                    s = hi - 64 * (k + 1) + j;
+                    allz = allz && ballot64(lane >= j && tk != 0) == 0;
+                    allf = allf && ballot64(lane >= j && tk != 0xFF) == 0;
+                } else {
+                    allz = allz && ballot64(tk != 0) == 0;
+                    allf = allf && ballot64(tk != 0xFF) == 0;
+                }
+            }
+        }
+        if (kf >= 0) {
+            if (allz || allf) {
+                const uint64_t h = s + (R - 1 - s) / 256 * 256;
+                return Carry{allz ? 1u : 2u, (uint32_t)(255u - (R - 1 - h))};
+            }
+            Carry c{0, 0};  // rare: resolve forward from s
+            for (uint64_t p = s; p < R; p += 64) {
+                const uint32_t nv = (uint32_t)(R - p < 64 ? R - p : 64);
+                const uint32_t tt = lane < nv ? tag_of(in[p + lane]) : 0u;
+                const uint32_t pop = __builtin_popcount(tt);
+                const uint64_t V = low_mask(nv);
+                c = resolve_step_s(ballot64(tt == 0) & V, ballot64(pop >= 7) & V,
+                                   ballot64(tt == 0xFF) & V, start_bits(cb, b64, p) & V, nv, c)
+                        .next;
+            }
+            return c;
+        }
+    }
+    return Carry{0, 0};  // (not reached: the batch's first word is a chunk start)
+}
+
+// Words from R on that the open run c absorbs, up to the next chunk start
+// or the batch end (w = word R + lane, bits = chunk-start bits of R ..).
+__device__ __forceinline__ uint32_t run_ext_b(const uint64_t* __restrict__ in,
+                                              const uint64_t* __restrict__ cb, uint64_t b64,
+                                              uint64_t whi, uint64_t R, Carry c, uint32_t lane,
+                                              uint64_t w, uint64_t bits) {
+    if (c.type == 0 || c.rem == 0) return 0;
+    uint32_t ext = 0;
+    for (uint64_t p = R; p < whi; p += 64) {
+        if (p != R) {
+            w = p + lane < whi ? in[p + lane] : 0ull;
+            bits = start_bits(cb, b64, p);
+        }
+        const uint32_t room = (uint32_t)(whi - p < 64 ? whi - p : 64);
+        const uint32_t cut = ctz64(bits);
+        const uint32_t nv = cut < room ? cut : room;
+        const uint32_t tag = tag_of(w);
+        const bool cls = c.type == 1 ? tag == 0 : __builtin_popcount(tag) >= 7;
+        const uint32_t lead = ctz64(~ballot64(lane < nv && cls));
+        ext += lead;
+        if (lead < 64 || ext >= c.rem) break;
+    }
+    return ext < c.rem ? ext : c.rem;
+}
+
+
+// carry_into_pre below its first window (long zero or 0xFF stretches):
+// eight windows per round go out at once and are reduced to tags right away.
+__device__ __forceinline__ Carry carry_deep(const uint64_t* __restrict__ in, uint64_t cs,
+                                            uint64_t R, uint32_t lane, bool allz, bool allf) {
+    for (uint64_t hi = R - 64; hi > cs; hi = hi > 512 ? hi - 512 : 0) {
+        uint32_t t[8];
+        {
+            uint64_t x[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const uint64_t ik = hi - 64 * (k + 1) + lane;
+                x[k] = (hi + lane >= 64ull * (k + 1) && ik >= cs) ? in[ik] : 0ull;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) t[k] = tag_of(x[k]);
+        }
+        int kf = -1;
+        uint64_t s = cs;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint64_t ik = hi - 64 * (k + 1) + lane;
+            const bool vk = hi + lane >= 64ull * (k + 1) && ik >= cs;
+            const uint32_t tk = vk ? t[k] : 0u;
+            const uint32_t pt0 = (uint32_t)__shfl_up((int)tk, 1, 64);
+            // lane 0's predecessor: lane 63 of the window below (k + 1)
+            const uint32_t below = k < 7 ? (uint32_t)__shfl((int)t[k < 7 ? k + 1 : 7], 63, 64) : 0u;
+            const uint32_t pt = lane ? pt0 : below;
+            const bool sure = vk && (ik == cs || ((lane || k < 7) && sure_head(tk, pt)));
+            const uint64_t Gk = ballot64(sure);
+            if (kf < 0) {
+                if (Gk) {
+                    const uint32_t j = 63u - (uint32_t)__builtin_clzll(Gk);
+                    kf = k;
+                    s = hi - 64 * (k + 1) + j;
+                    allz = allz && ballot64(lane >= j && tk != 0) == 0;
+                    allf = allf && ballot64(lane >= j && tk != 0xFF) == 0;
+                } else {
+                    allz = allz && ballot64(tk != 0) == 0;
+                    allf = allf && ballot64(tk != 0xFF) == 0;
+                }
+            }
+        }
+        if (kf >= 0) {
+            if (allz || allf) {
+                const uint64_t h = s + (R - 1 - s) / 256 * 256;
+                return Carry{allz ? 1u : 2u, (uint32_t)(255u - (R - 1 - h))};
+            }
+            Carry c{0, 0};  // rare: resolve forward from s
+            for (uint64_t p = s; p < R; p += 64) {
+                const uint32_t nv = (uint32_t)(R - p < 64 ? R - p : 64);
+                const uint32_t tt = lane < nv ? tag_of(in[p + lane]) : 0u;
+                const uint32_t pop = __builtin_popcount(tt);
+                const uint64_t V = low_mask(nv);
+                c = resolve_step_s(ballot64(tt == 0) & V, ballot64(pop >= 7) & V,
+                                   ballot64(tt == 0xFF) & V, 0, nv, c).next;
+            }
+            return c;
+        }
+    }
+    return Carry{0, 0};  // (not reached: the windows reach cs, a sure head)
+}
+
+// carry_into with its first window preloaded: w = word R - 64 + lane (0
+// below the batch), wp = word R - 65.  The usual case (a sure head in the 64
+// words before R) costs no further load; deeper, eight windows go out at once.
+__device__ __forceinline__ Carry carry_into_pre(const uint64_t* __restrict__ in, uint64_t cs, uint64_t R,
+                                uint32_t lane, uint64_t w, uint64_t wp) {
+    const uint64_t base = R - 64;
+    const uint64_t i = base + lane;
+    const bool v = R + lane >= 64 && i >= cs;  // (i >= cs implies i >= the batch start)
+    const uint32_t tag = v ? tag_of(w) : 0u;
+    const uint32_t up = (uint32_t)__shfl_up((int)tag, 1, 64);
+    const uint32_t ptag = lane ? up : tag_of(wp);
+    const uint64_t G = ballot64(v && (i == cs || sure_head(tag, ptag)));
+    if (G) {
+        const uint32_t j = 63u - (uint32_t)__builtin_clzll(G);
+        const uint64_t s = base + j;
+        const bool mine = lane >= j;
+        const bool allz = ballot64(mine && tag != 0) == 0, allf = ballot64(mine && tag != 0xFF) == 0;
+        if (allz || allf) {
+            const uint64_t h = s + (R - 1 - s) / 256 * 256;
+            return Carry{allz ? 1u : 2u, (uint32_t)(255u - (R - 1 - h))};
+        }
+        // one step over the window with a forced head at the sure head
+        const uint32_t pop = __builtin_popcount(tag);
+        const uint64_t Sj = 1ull << j;
+        const uint64_t Vj = ~low_mask(j);
+        const StepMasks sm = resolve_step_s(ballot64(tag == 0) & Vj, ballot64(pop >= 7) & Vj,
+                                            ballot64(tag == 0xFF) & Vj, Sj, 64, Carry{0, 0});
+        return sm.next;
+    }
+    // no sure head in the window: all its words are one class
+    return carry_deep(in, cs, R, lane, ballot64(tag != 0) == 0, ballot64(tag != 0xFF) == 0);
+}
+
+
+// run_ext with its first window preloaded: w = word R + lane (valid below ce).
+__device__ __forceinline__ uint32_t run_ext_pre(const uint64_t* __restrict__ in, uint64_t R, uint64_t ce, Carry c,
+                                uint32_t lane, uint64_t w) {
+    if (c.type == 0 || c.rem == 0 || R >= ce) return 0;
+    const uint32_t nv = (uint32_t)(ce - R < 64 ? ce - R : 64);
+    const uint32_t tag = tag_of(w);
+    const bool cls = c.type == 1 ? tag == 0 : __builtin_popcount(tag) >= 7;
+    const uint32_t lead = ctz64(~ballot64(lane < nv && cls));
+    if (lead < 64 || lead >= c.rem) return lead < c.rem ? lead : c.rem;
+    return 64 + run_ext(in, R + 64, ce, Carry{c.type, c.rem - 64}, lane);
+}
+
 // Words from R on (up to the chunk end ce) that the open run c absorbs.
 __device__ uint32_t run_ext(const uint64_t* __restrict__ in, uint64_t R, uint64_t ce, Carry c,
                             uint32_t lane) {
@@ -1241,8 +1482,11 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 // chunk's own start is unknown here, so the entry holds the record's position
 // relative to the tile (24-bit two's complement) and pack_wt_fix_sync adds
 // tile offset - chunk offset once every tile is placed.
+#ifndef PACK_WT_ABL
+#define PACK_WT_ABL 0  // diagnostic timing variants (scripts/wt_ablate.py); 0 = product
+#endif
+
 struct WtSmem {
-    uint64_t smask[kWaves][kStageSteps];   // chunk starts per step
     uint16_t wpos[kWaves][kWtRange];       // region position of chunk-start words
     uint32_t lastcs[kWaves];               // region position of the last chunk start
     uint64_t excl;
@@ -1269,15 +1513,29 @@ __device__ __forceinline__ void size_step_s(StageState& pk, uint64_t w, uint32_t
     pk.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
 }
 
+#ifndef PACK_WT_DEBUG
+#define PACK_WT_DEBUG 0
+#endif
+#if PACK_WT_DEBUG
+__device__ uint32_t g_pwt_dbg[4096 * 8];
+#endif
+#ifndef PACK_WT_PIN
+#define PACK_WT_PIN 1
+#endif
+#ifndef PACK_WT_MIN_WAVES
+#define PACK_WT_MIN_WAVES 5  // the LDS allows 5 workgroups per CU
+#endif
 template <bool SYNC>
-__global__ void __launch_bounds__(kThreads, PACK_MIN_WAVES)
+__global__ void __launch_bounds__(kThreads, PACK_WT_MIN_WAVES)
 pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
                uint64_t nchunks, uint8_t* __restrict__ out, uint64_t out_cap,
                uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts, uint64_t* __restrict__ gs,
                uint32_t* __restrict__ sync, const uint64_t* __restrict__ map,
-               uint64_t* __restrict__ tile_off, uint64_t wlo, uint64_t whi, uint64_t g0) {
+               uint64_t* __restrict__ tile_off, const uint64_t* __restrict__ cbits, uint64_t wlo,
+               uint64_t whi, uint64_t g0) {
     __shared__ Smem sm;
     __shared__ WtSmem wm;
+    const uint64_t b64 = wlo >> 6;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
@@ -1305,46 +1563,48 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     const bool lastr = have && R1 == whi;
     for (uint32_t i = tid; i <= kSelCopy; i += kThreads)
         reinterpret_cast<uint4*>(sm.sel)[i] = reinterpret_cast<const uint4*>(kSelTable.e)[i];
-    if (lane < kStageSteps) wm.smask[wave][lane] = 0;
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
     uint8_t* const outa = out - mis;
-    // the range's words
+    // the range's words, and the windows either side for the run state at
+    // its ends (carry_into_pre, run_ext_pre): every load goes out at once
     uint64_t cache[kStageSteps];
 #pragma unroll
     for (uint32_t s = 0; s < kStageSteps; s++) {
         const uint32_t i = 64u * s + lane;
         cache[s] = i < nw ? in[R0 + i] : 0ull;
     }
+    const uint64_t wbef = (have && R0 >= wlo + 64 - lane) ? in[R0 - 64 + lane] : 0ull;
+    const uint64_t wbp = (have && R0 >= wlo + 65) ? in[R0 - 65] : 0ull;
+    const uint64_t waft = (have && R1 + lane < whi) ? in[R1 + lane] : 0ull;
+    // chunk starts (forced heads) of the steps and of both windows
+    uint64_t smk[kStageSteps];
+#pragma unroll
+    for (uint32_t s = 0; s < kStageSteps; s++) {
+        const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
+        smk[s] = nv ? start_bits(cbits, b64, R0 + 64u * s) & low_mask(nv) : 0ull;
+    }
+    // (R0 < 64 only for the batch's first range, which starts a chunk)
+    const uint64_t bbef = (have && R0 >= 64) ? start_bits(cbits, b64, R0 - 64) : 0ull;
+    const uint64_t baft = have ? start_bits(cbits, b64, R1) : 0ull;
     for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
         *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
     wave_lds_sync();
-    // chunk starts in the range: [cA, cB) (plus, in the batch's last range,
-    // the empty chunks at its end)
-    const uint64_t cA = have ? uniform64(map[tile * kWaves + wave]) : nchunks;
-    uint64_t cB = cA;
-    if (have) {
-        for (uint64_t c0 = cA;; c0 += 64) {
-            const uint64_t c = c0 + lane;
-            const uint64_t st = c < nchunks ? chunk_off[c] : ~0ull;
-            const bool inr = c < nchunks && (st < R1 || (lastr && st == R1));
-            if (inr && st < R1) {
-                const uint32_t r = (uint32_t)(st - R0);
-                atomicOr(reinterpret_cast<unsigned long long*>(&wm.smask[wave][r >> 6]),
-                         1ull << (r & 63u));
-            }
-            const uint64_t m = ballot64(inr);
-            cB = c0 + popc64(m);
-            if (m != ~0ull) break;
-        }
-    }
     Carry cin{0, 0};
-    if (have && uniform64(chunk_off[cA < nchunks ? cA : nchunks]) != R0)
-        cin = carry_into(in, uniform64(chunk_off[cA - 1]), R0, lane);
+    if (PACK_WT_ABL != 1 && have && !(smk[0] & 1)) {  // the range starts inside a chunk
+        cin = carry_in_b(in, cbits, b64, wlo, R0, lane, wbef, wbp, bbef);
+        cin.type = uniform(cin.type);
+        cin.rem = uniform(cin.rem);
+    }
+    // (pin the words here: nothing of pass 1 is computed ahead of the carry,
+    // which would keep eight steps' worth of values live through it)
+#if PACK_WT_PIN
+#pragma unroll
+    for (uint32_t s = 0; s < kStageSteps; s++) asm volatile("" : "+v"(cache[s]));
+#endif
     __syncthreads();
     // pass 1: sizes and positions
     StepInfo si[kStageSteps];
-    uint64_t smk[kStageSteps];
     StageState pk;
     pk.begin(0);
     pk.carry = cin;
@@ -1352,7 +1612,6 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
 #pragma unroll
     for (uint32_t s = 0; s < kStageSteps; s++) {
         const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
-        smk[s] = uniform64(wm.smask[wave][s]);
         size_step_s(pk, cache[s], nv, smk[s], lane, si[s]);
         if ((smk[s] >> lane) & 1) wm.wpos[wave][64u * s + lane] = (uint16_t)si[s].pos;
         if (smk[s])
@@ -1360,13 +1619,19 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
                                                          63 - __builtin_clzll(smk[s]));
     }
     uint32_t rext = 0;
-    if (have && !lastr) {
-        const uint64_t ce = uniform64(chunk_off[cB]);  // end of the chunk holding word R1 - 1
-        rext = run_ext(in, R1, ce, pk.carry, lane);
-    }
+    if (PACK_WT_ABL != 2 && have && !lastr)
+        rext = uniform(run_ext_b(in, cbits, b64, whi, R1, pk.carry, lane, waft, baft));
     if (lane == 0) {
         sm.wave_bytes[wave] = pk.total;
         wm.lastcs[wave] = lastcs;
+#if PACK_WT_DEBUG
+        const uint64_t r = tile * kWaves + wave;
+        if (r < 4096) {
+            uint32_t* d = g_pwt_dbg + 8 * r;
+            d[0] = cin.type; d[1] = cin.rem; d[2] = rext; d[3] = pk.carry.type; d[4] = pk.carry.rem;
+            d[5] = (uint32_t)R0; d[6] = (uint32_t)R1; d[7] = pk.total;
+        }
+#endif
     }
     __syncthreads();
     uint32_t woff = 0, agg = 0;
@@ -1389,7 +1654,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             ext = (si[s].meta >> 16) + (si[s].H == 0 ? e : 0u);
         }
     }
-    if constexpr (SYNC) {
+    if (SYNC && PACK_WT_ABL != 3) {
         // the chunk open at R0 started at tile position oc (0: before the tile)
         uint32_t oc = 0;
         for (int w = (int)wave - 1; w >= 0; w--) {
@@ -1434,7 +1699,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         }
     }
     if (wave == 0) {
-        const uint64_t excl = lookback(LA, tile, agg, lane);
+        const uint64_t excl = PACK_WT_ABL == 5 ? tile * 8192 : lookback(LA, tile, agg, lane);
         if (lane == 0) {
             wm.excl = excl;
             tile_off[tile] = excl;
@@ -1443,13 +1708,30 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     }
     __syncthreads();
     const uint64_t excl = lds_u64(&wm.excl);
-    for (uint64_t c = cA + lane; c < cB; c += CAPNP_WAVE) {
-        const uint64_t st = chunk_off[c];
-        out_off[c] = st < R1 ? excl + woff + wm.wpos[wave][st - R0] : excl + agg;
+    // offsets of the chunks that start in the range (in the batch's last
+    // range also the empty chunks at its end)
+    if (have && PACK_WT_ABL != 4) {
+        for (uint64_t c0 = uniform64(map[tile * kWaves + wave]);; c0 += CAPNP_WAVE) {
+            const uint64_t c = c0 + lane;
+            const uint64_t st = c < nchunks ? chunk_off[c] : ~0ull;
+            const bool inr = c < nchunks && (st < R1 || (lastr && st == R1));
+            if (inr) out_off[c] = st < R1 ? excl + woff + wm.wpos[wave][st - R0] : excl + agg;
+            if (ballot64(inr) != ~0ull) break;
+        }
     }
     if (have)
         copy_out(region, outa, excl + woff + mis, lds_u64(&sm.wave_bytes[wave]), out_cap + mis,
                  lane);
+}
+
+// Chunk-start bits (start_bits); cb zeroed beforehand.
+__global__ void __launch_bounds__(256)
+pack_wt_bits(const uint64_t* __restrict__ chunk_off, uint64_t nchunks, uint64_t whi, uint64_t b64,
+             unsigned long long* __restrict__ cb) {
+    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= nchunks) return;
+    const uint64_t st = chunk_off[c];
+    if (st < whi) atomicOr(&cb[1 + (st >> 6) - b64], 1ull << (st & 63));
 }
 
 // First chunk starting at or after each wave range's first word.
@@ -1559,11 +1841,24 @@ extern "C" uint64_t capnp_pack_wt_tiles(uint64_t wlo, uint64_t whi) {
     return whi > wlo ? (whi + kWtTile - 1) / kWtTile - wlo / kWtTile : 0;
 }
 
+static uint64_t wt_bits_words(uint64_t wlo, uint64_t whi) {
+    return ((whi + 63) >> 6) - (wlo >> 6) + 16;
+}
+
 extern "C" size_t capnp_pack_wt_ws_bytes(uint64_t wlo, uint64_t whi) {
-    return capnp_pack_wt_tiles(wlo, whi) * (kWaves + 1) * 8 + 64;
+    return (capnp_pack_wt_tiles(wlo, whi) * (kWaves + 1) + wt_bits_words(wlo, whi)) * 8 + 64;
 }
 
 extern "C" uint32_t capnp_pack_wt_words(void) { return kWtTile; }
+
+extern "C" int capnp_pack_wt_dbg(uint32_t* out) {
+#if PACK_WT_DEBUG
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pwt_dbg), sizeof(g_pwt_dbg)) == hipSuccess ? 0 : -1;
+#else
+    (void)out;
+    return -1;
+#endif
+}
 
 extern "C" hipError_t capnp_launch_pack_wt(const uint64_t* d_in, const uint64_t* d_chunk_off,
                                            uint64_t nchunks, uint8_t* d_out, uint64_t out_cap,
@@ -1576,21 +1871,27 @@ extern "C" hipError_t capnp_launch_pack_wt(const uint64_t* d_in, const uint64_t*
     const uint64_t g0 = wlo / kWtTile;
     uint64_t* map = reinterpret_cast<uint64_t*>(d_ws);
     uint64_t* toff = map + ntiles * kWaves;
+    uint64_t* cbits = toff + ntiles;
     hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(ntiles, 1), stream);
     if (e != hipSuccess) return e;
+    e = hipMemsetAsync(cbits, 0, wt_bits_words(wlo, whi) * 8, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(pack_wt_bits, dim3((uint32_t)((nchunks + 255) / 256)), dim3(256), 0, stream,
+                       d_chunk_off, nchunks, whi, wlo >> 6,
+                       reinterpret_cast<unsigned long long*>(cbits));
     const uint64_t nr = ntiles * kWaves;
     hipLaunchKernelGGL(pack_wt_map, dim3((uint32_t)((nr + 255) / 256)), dim3(256), 0, stream,
                        d_chunk_off, nchunks, wlo, whi, g0, nr, map);
     if (d_sync) {
         hipLaunchKernelGGL(pack_wt_kernel<true>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
                            d_in, d_chunk_off, nchunks, d_out, out_cap, d_out_off, d_state,
-                           d_state + ntiles, d_sync, map, toff, wlo, whi, g0);
+                           d_state + ntiles, d_sync, map, toff, cbits, wlo, whi, g0);
         hipLaunchKernelGGL(pack_wt_fix_sync, dim3((uint32_t)ntiles), dim3(64), 0, stream,
                            d_chunk_off, d_out_off, map, toff, d_sync, wlo, whi, g0);
     } else {
         hipLaunchKernelGGL(pack_wt_kernel<false>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
                            d_in, d_chunk_off, nchunks, d_out, out_cap, d_out_off, d_state,
-                           d_state + ntiles, d_sync, map, toff, wlo, whi, g0);
+                           d_state + ntiles, d_sync, map, toff, cbits, wlo, whi, g0);
     }
     return hipGetLastError();
 }

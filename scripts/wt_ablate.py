@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Interleaved timing of word-tile pack variants (PACK_WT_ABL builds, wrong
+output by design) on the config-4 workload, in one process:
+    python3 scripts/wt_ablate.py [lib.so ...]"""
+import ctypes as C
+import glob
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "capnproto-rust_amd"))
+
+
+def load(path):
+    L = C.CDLL(path)
+    vp, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
+    L.capnp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int)]
+    L.capnp_ctx_create.restype = vp
+    L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, u32, vp]
+    L.capnp_gpu_unpack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, u32, vp]
+    st = C.c_int(0)
+    ctx = L.capnp_ctx_create(0, C.byref(st))
+    assert ctx
+    return L, C.c_void_p(ctx)
+
+
+def main():
+    import bench
+    import torch
+    from capnp_amd import Context
+    libs = sys.argv[1:] or ([os.path.join(ROOT, "capnproto-rust_amd/capnp_amd/libcapnp_packed.so")]
+                            + sorted(glob.glob(os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_p_*.so"))))
+    args = bench.parse(["--workload", os.environ.get("WL", "config4")])
+    ctx = Context(0)
+    dev = torch.device("cuda", 0)
+    words, offs, n, _ = bench.make_workload(args, ctx, torch, dev, 0)
+    total = words.numel()
+    cap = ctx.batch_bound_bytes(total, n)
+    out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    oo = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    sync = torch.empty(ctx.sync_entries(total), dtype=torch.int32, device=dev)
+    back = torch.empty_like(words)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    ref_out = torch.empty_like(out)
+    ref_oo = torch.empty_like(oo)
+    ref_sync = torch.empty_like(sync)
+    ctx.pack_batch_into(words, offs, ref_out, ref_oo, chunks_per_tile=0, sync=ref_sync)
+    stream = torch.cuda.current_stream()
+    P = C.c_void_p
+    variants = [(os.path.basename(p), *load(p)) for p in libs]
+    res = {v[0]: {"pack": [], "unpack": []} for v in variants}
+    for r in range(5):
+        for name, L, h in variants:
+            for kind in ("pack", "unpack"):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(5):
+                    if kind == "pack":
+                        L.capnp_gpu_pack_batch_sync_tuned(h, P(words.data_ptr()), P(offs.data_ptr()), n,
+                                                          P(out.data_ptr()), cap, P(oo.data_ptr()),
+                                                          P(sync.data_ptr()), 0, P(stream.cuda_stream))
+                    else:
+                        L.capnp_gpu_unpack_batch_sync_tuned(h, P(ref_out.data_ptr()), P(ref_oo.data_ptr()), n,
+                                                            P(back.data_ptr()), P(offs.data_ptr()),
+                                                            P(ref_sync.data_ptr()), P(status.data_ptr()),
+                                                            None, 0, P(stream.cuda_stream))
+                e1.record(stream)
+                e1.synchronize()
+                res[name][kind].append(e0.elapsed_time(e1) / 5)
+    U = total * 8
+    for name, d in res.items():
+        pm, um = statistics.median(d["pack"]), statistics.median(d["unpack"])
+        print(f"{name:36s} pack {pm * 1e3:8.1f} us ({U / pm / 1e6:7.1f} GB/s U)   "
+              f"unpack {um * 1e3:8.1f} us ({U / um / 1e6:7.1f} GB/s U)", flush=True)
+
+
+if __name__ == "__main__":
+    main()

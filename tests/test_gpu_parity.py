@@ -371,6 +371,38 @@ def test_config4_mixed_sizes_round_trip(ctx):
                    lambda c: sizes[c])
 
 
+def test_config5_full_shard_round_trip(ctx):
+    """BASELINE config 5's per-GPU shard: 8 Mi x 1 KiB = 8 GiB of words (the
+    64 GiB batch over 8 GPUs, bench.py --workload config5), packed with the
+    record sync index and unpacked through it on one GPU: exact round trip,
+    statuses, consumed bytes, and 256 sampled chunks byte-equal to the
+    oracle (shard 0: generator ids from 0, as rank 0 of the bench)."""
+    from capnp_amd import tile_chunks_for, unpack_tile_chunks_for
+    n, cw = 8 << 20, 128
+    total = n * cw
+    offs = torch.arange(0, (n + 1) * cw, cw, dtype=torch.int64, device="cuda")
+    words = torch.empty(total, dtype=torch.int64, device="cuda")
+    ctx.gen_batch(words, offs, pz_thresh=O.PZ30, id0=0)
+    cap = ctx.batch_bound_bytes(total, n)
+    packed = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    poffs = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    sync = torch.empty(ctx.sync_entries(total), dtype=torch.int32, device="cuda")
+    ctx.pack_batch_into(words, offs, packed, poffs, chunks_per_tile=tile_chunks_for(total, n),
+                        sync=sync)
+    back = torch.empty_like(words)
+    status = torch.empty(n, dtype=torch.int32, device="cuda")
+    consumed = torch.empty(n, dtype=torch.int64, device="cuda")
+    ctx.unpack_batch_into(packed, poffs, offs, back, status, consumed,
+                          chunks_per_tile=unpack_tile_chunks_for(total, n, sync=True), sync=sync)
+    torch.cuda.synchronize()
+    assert int((status != 0).sum()) == 0
+    assert torch.equal(back, words)
+    assert torch.equal(consumed, poffs[1:] - poffs[:-1])
+    del back
+    idx = np.random.default_rng(55).choice(n, 256, replace=False)
+    _check_sampled(packed, poffs, [(int(c), 0) for c in idx], O.PZ30, lambda c: cw)
+
+
 # ------------------------------------------------------- record sync index
 def _pack_sync(ctx, dw, do, n, total, tc=0):
     cap = ctx.batch_bound_bytes(total, n)
