@@ -211,6 +211,15 @@ uint32_t tile_chunks_for(uint64_t total_words, size_t n) {
     return tc;
 }
 
+// Diagnostics: CAPNP_WORD_TILES=1 takes the word tiles for every tc == 0 call.
+bool force_word_tiles() {
+    static const bool v = [] {
+        const char* e = getenv("CAPNP_WORD_TILES");
+        return e && e[0] == '1';
+    }();
+    return v;
+}
+
 // Batches whose mean chunk is at least this many words pack (and, with the
 // record sync index, unpack) in word tiles.
 constexpr uint64_t kWordTileMean = 512;
@@ -231,7 +240,7 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
         HIP_TRY(hipStreamSynchronize(s));
         if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
         const uint64_t words = wr[1] - wr[0];
-        if (words && words / n >= kWordTileMean) {
+        if (words && (words / n >= kWordTileMean || force_word_tiles())) {
             const uint64_t ntiles = capnp_pack_wt_tiles(wr[0], wr[1]);
             capnp_status st = ensure_state(ctx, capnp_pack_state_bytes(ntiles, 1) + 16);
             if (st != CAPNP_OK) return st;
@@ -471,7 +480,7 @@ static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
         HIP_TRY(hipStreamSynchronize(s));
         if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
         const uint64_t words = wr[1] - wr[0];
-        if (words && words / nchunks >= kWordTileMean) {
+        if (words && (words / nchunks >= kWordTileMean || force_word_tiles())) {
             const size_t ws = capnp_unpack_wt_ws_bytes(wr[0], wr[1]);
             capnp_status st = ensure_buf(ctx, &ctx->d_wt, &ctx->wt_cap, ws);
             if (st != CAPNP_OK) return st;

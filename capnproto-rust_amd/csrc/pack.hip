@@ -41,6 +41,10 @@
 #include "common.h"
 #include "../../include/capnp_packed.h"
 
+#ifndef PACK_EMIT_SKIP0
+#define PACK_EMIT_SKIP0 1  // emit: no LDS OR of zero dwords (0: every lane ORs four dwords)
+#endif
+
 #ifndef PACK_ABLATE
 #define PACK_ABLATE 0  // diagnostic builds only (scripts/ablate.py); 0 = product
 #endif
@@ -510,10 +514,21 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
     // (region_m1 = region - 1, region 16-aligned: align_down(region - 1 + pos)
     // = region + ceil(pos / 4) * 4 - 4)
     uint32_t* b32 = reinterpret_cast<uint32_t*>(__builtin_align_down(region_m1 + pos, 4));
+    // (the region is zeroed, so a zero dword needs no OR: absorbed zero words
+    // and lanes past the step's words would otherwise all OR into the next
+    // record's dword, same-address LDS atomics that serialise; long zero runs
+    // made that the larger part of the emit)
+#if PACK_EMIT_SKIP0
+    if (e0) __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (e1) __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (e2) __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if (e3) __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#else
     __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#endif
 #if PACK_ABLATE != 5
     if constexpr (SYNC) {
         // sync points m = hw + d, d = (t0 - hw) mod kSyncWords, d <= cnt, of
@@ -1487,9 +1502,13 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 #endif
 
 struct WtSmem {
-    uint16_t wpos[kWaves][kWtRange];       // region position of chunk-start words
+    SelEntry sel[kSelCopy + 1];            // record assembly per tag
+    uint64_t wave_bytes[kWaves];
     uint32_t lastcs[kWaves];               // region position of the last chunk start
     uint64_t excl;
+    alignas(16) uint32_t pad[4];           // (emit_step ORs a zero before a region)
+    alignas(16) uint8_t stage[kWaves][kRegion];
+    uint16_t wpos[kWaves][kWtRange];       // region position of chunk-start words
 };
 
 __device__ __forceinline__ void size_step_s(StageState& pk, uint64_t w, uint32_t nvalid,
@@ -1523,7 +1542,7 @@ __device__ uint32_t g_pwt_dbg[4096 * 8];
 #define PACK_WT_PIN 1
 #endif
 #ifndef PACK_WT_MIN_WAVES
-#define PACK_WT_MIN_WAVES 5  // the LDS allows 5 workgroups per CU
+#define PACK_WT_MIN_WAVES 6  // the LDS (26.4 KB) allows 6 workgroups per CU
 #endif
 template <bool SYNC>
 __global__ void __launch_bounds__(kThreads, PACK_WT_MIN_WAVES)
@@ -1531,10 +1550,10 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
                uint64_t nchunks, uint8_t* __restrict__ out, uint64_t out_cap,
                uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts, uint64_t* __restrict__ gs,
                uint32_t* __restrict__ sync, const uint64_t* __restrict__ map,
-               uint64_t* __restrict__ tile_off, const uint64_t* __restrict__ cbits, uint64_t wlo,
-               uint64_t whi, uint64_t g0) {
-    __shared__ Smem sm;
+               uint64_t* __restrict__ tile_off, const uint64_t* __restrict__ cbits,
+               const uint32_t* __restrict__ plan, uint64_t wlo, uint64_t whi, uint64_t g0) {
     __shared__ WtSmem wm;
+    WtSmem& sm = wm;
     const uint64_t b64 = wlo >> 6;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -1568,15 +1587,26 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     uint8_t* const outa = out - mis;
     // the range's words, and the windows either side for the run state at
     // its ends (carry_into_pre, run_ext_pre): every load goes out at once
+    // (a buffer descriptor over the range: a lane past it reads 0, and the
+    // unconditional loads let each step wait for its own load only)
     uint64_t cache[kStageSteps];
+    {
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint64_t*>(in + R0), 0, (int)(nw * 8u), 0x00020000);
 #pragma unroll
-    for (uint32_t s = 0; s < kStageSteps; s++) {
-        const uint32_t i = 64u * s + lane;
-        cache[s] = i < nw ? in[R0 + i] : 0ull;
+        for (uint32_t s = 0; s < kStageSteps; s++) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)((64u * s + lane) * 8u), 0, 0);
+            cache[s] = ((uint64_t)v[1] << 32) | v[0];
+        }
     }
-    const uint64_t wbef = (have && R0 >= wlo + 64 - lane) ? in[R0 - 64 + lane] : 0ull;
-    const uint64_t wbp = (have && R0 >= wlo + 65) ? in[R0 - 65] : 0ull;
-    const uint64_t waft = (have && R1 + lane < whi) ? in[R1 + lane] : 0ull;
+    // the range's first chunks (their offsets are written after the
+    // look-back; loaded now, off that path)
+    const uint64_t cA = have ? uniform64(map[tile * kWaves + wave]) : nchunks;
+    const uint64_t st0 = cA + lane < nchunks ? chunk_off[cA + lane] : ~0ull;
+    // the run states at both ends (pack_wt_plan)
+    const uint64_t r = tile * kWaves + wave;
+    const uint32_t pin = have ? uniform(plan[r]) : 0u;
+    const uint32_t pout = (have && !lastr) ? uniform(plan[r + 1]) : 0u;
     // chunk starts (forced heads) of the steps and of both windows
     uint64_t smk[kStageSteps];
 #pragma unroll
@@ -1584,18 +1614,10 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
         smk[s] = nv ? start_bits(cbits, b64, R0 + 64u * s) & low_mask(nv) : 0ull;
     }
-    // (R0 < 64 only for the batch's first range, which starts a chunk)
-    const uint64_t bbef = (have && R0 >= 64) ? start_bits(cbits, b64, R0 - 64) : 0ull;
-    const uint64_t baft = have ? start_bits(cbits, b64, R1) : 0ull;
     for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
         *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
     wave_lds_sync();
-    Carry cin{0, 0};
-    if (PACK_WT_ABL != 1 && have && !(smk[0] & 1)) {  // the range starts inside a chunk
-        cin = carry_in_b(in, cbits, b64, wlo, R0, lane, wbef, wbp, bbef);
-        cin.type = uniform(cin.type);
-        cin.rem = uniform(cin.rem);
-    }
+    const Carry cin{pin & 3u, (pin >> 2) & 0xFFu};
     // (pin the words here: nothing of pass 1 is computed ahead of the carry,
     // which would keep eight steps' worth of values live through it)
 #if PACK_WT_PIN
@@ -1618,9 +1640,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             lastcs = (uint32_t)__builtin_amdgcn_readlane((int)si[s].pos,
                                                          63 - __builtin_clzll(smk[s]));
     }
-    uint32_t rext = 0;
-    if (PACK_WT_ABL != 2 && have && !lastr)
-        rext = uniform(run_ext_b(in, cbits, b64, whi, R1, pk.carry, lane, waft, baft));
+    const uint32_t rext = pout >> 10;  // (the run open at R1 is the next range's carry)
     if (lane == 0) {
         sm.wave_bytes[wave] = pk.total;
         wm.lastcs[wave] = lastcs;
@@ -1650,7 +1670,8 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
 #pragma unroll
         for (int s = (int)kStageSteps - 1; s >= 0; s--) {
             const uint32_t e = ext;
-            emit_step<false>(cache[s], si[s], e, lane, region_m1, sm.sel, nullptr, 0, 0, 0);
+            if (PACK_WT_ABL != 6)
+                emit_step<false>(cache[s], si[s], e, lane, region_m1, sm.sel, nullptr, 0, 0, 0);
             ext = (si[s].meta >> 16) + (si[s].H == 0 ? e : 0u);
         }
     }
@@ -1711,15 +1732,15 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     // offsets of the chunks that start in the range (in the batch's last
     // range also the empty chunks at its end)
     if (have && PACK_WT_ABL != 4) {
-        for (uint64_t c0 = uniform64(map[tile * kWaves + wave]);; c0 += CAPNP_WAVE) {
+        for (uint64_t c0 = cA;; c0 += CAPNP_WAVE) {
             const uint64_t c = c0 + lane;
-            const uint64_t st = c < nchunks ? chunk_off[c] : ~0ull;
+            const uint64_t st = c0 == cA ? st0 : (c < nchunks ? chunk_off[c] : ~0ull);
             const bool inr = c < nchunks && (st < R1 || (lastr && st == R1));
             if (inr) out_off[c] = st < R1 ? excl + woff + wm.wpos[wave][st - R0] : excl + agg;
             if (ballot64(inr) != ~0ull) break;
         }
     }
-    if (have)
+    if (have && PACK_WT_ABL != 7)
         copy_out(region, outa, excl + woff + mis, lds_u64(&sm.wave_bytes[wave]), out_cap + mis,
                  lane);
 }
@@ -1732,6 +1753,36 @@ pack_wt_bits(const uint64_t* __restrict__ chunk_off, uint64_t nchunks, uint64_t 
     if (c >= nchunks) return;
     const uint64_t st = chunk_off[c];
     if (st < whi) atomicOr(&cb[1 + (st >> 6) - b64], 1ull << (st & 63));
+}
+
+// Run state at every wave range's first word, one wave per range: plan[r] =
+// type | rem << 2 | ext << 10, ext = the words from R0 on that the run open
+// there absorbs (run_ext_b).  The pack kernel reads its own entry and the
+// next range's, so no range waits on the words around its ends.
+__global__ void __launch_bounds__(256)
+pack_wt_plan(const uint64_t* __restrict__ in, const uint64_t* __restrict__ cbits, uint64_t wlo,
+             uint64_t whi, uint64_t g0, uint64_t nranges, uint32_t* __restrict__ plan) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (r >= nranges) return;
+    const uint64_t g = g0 + r / kWaves;
+    const uint64_t Ta = g * kWtTile > wlo ? g * kWtTile : wlo;
+    const uint64_t R = uniform64(Ta + (r % kWaves) * kWtRange);
+    const uint64_t b64 = wlo >> 6;
+    uint32_t rec = 0;
+    if (R < whi && R > wlo) {
+        const uint64_t wb = R >= wlo + 64 - lane ? in[R - 64 + lane] : 0ull;
+        const uint64_t wp = R >= wlo + 65 ? in[R - 65] : 0ull;
+        const uint64_t wa = R + lane < whi ? in[R + lane] : 0ull;
+        const uint64_t bb = R >= 64 ? start_bits(cbits, b64, R - 64) : 0ull;
+        const uint64_t ba = start_bits(cbits, b64, R);
+        if (!(ba & 1)) {  // R inside a chunk
+            const Carry c = carry_in_b(in, cbits, b64, wlo, R, lane, wb, wp, bb);
+            const uint32_t ext = run_ext_b(in, cbits, b64, whi, R, c, lane, wa, ba);
+            rec = c.type | (c.rem << 2) | (ext << 10);
+        }
+    }
+    if (lane == 0) plan[r] = rec;
 }
 
 // First chunk starting at or after each wave range's first word.
@@ -1846,7 +1897,8 @@ static uint64_t wt_bits_words(uint64_t wlo, uint64_t whi) {
 }
 
 extern "C" size_t capnp_pack_wt_ws_bytes(uint64_t wlo, uint64_t whi) {
-    return (capnp_pack_wt_tiles(wlo, whi) * (kWaves + 1) + wt_bits_words(wlo, whi)) * 8 + 64;
+    const uint64_t nt = capnp_pack_wt_tiles(wlo, whi);
+    return (nt * (kWaves + 1) + wt_bits_words(wlo, whi)) * 8 + (nt * kWaves + 1) * 4 + 64;
 }
 
 extern "C" uint32_t capnp_pack_wt_words(void) { return kWtTile; }
@@ -1872,6 +1924,7 @@ extern "C" hipError_t capnp_launch_pack_wt(const uint64_t* d_in, const uint64_t*
     uint64_t* map = reinterpret_cast<uint64_t*>(d_ws);
     uint64_t* toff = map + ntiles * kWaves;
     uint64_t* cbits = toff + ntiles;
+    uint32_t* plan = reinterpret_cast<uint32_t*>(cbits + wt_bits_words(wlo, whi));
     hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(ntiles, 1), stream);
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(cbits, 0, wt_bits_words(wlo, whi) * 8, stream);
@@ -1882,16 +1935,18 @@ extern "C" hipError_t capnp_launch_pack_wt(const uint64_t* d_in, const uint64_t*
     const uint64_t nr = ntiles * kWaves;
     hipLaunchKernelGGL(pack_wt_map, dim3((uint32_t)((nr + 255) / 256)), dim3(256), 0, stream,
                        d_chunk_off, nchunks, wlo, whi, g0, nr, map);
+    hipLaunchKernelGGL(pack_wt_plan, dim3((uint32_t)((nr + 3) / 4)), dim3(256), 0, stream, d_in,
+                       cbits, wlo, whi, g0, nr, plan);
     if (d_sync) {
         hipLaunchKernelGGL(pack_wt_kernel<true>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
                            d_in, d_chunk_off, nchunks, d_out, out_cap, d_out_off, d_state,
-                           d_state + ntiles, d_sync, map, toff, cbits, wlo, whi, g0);
+                           d_state + ntiles, d_sync, map, toff, cbits, plan, wlo, whi, g0);
         hipLaunchKernelGGL(pack_wt_fix_sync, dim3((uint32_t)ntiles), dim3(64), 0, stream,
                            d_chunk_off, d_out_off, map, toff, d_sync, wlo, whi, g0);
     } else {
         hipLaunchKernelGGL(pack_wt_kernel<false>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
                            d_in, d_chunk_off, nchunks, d_out, out_cap, d_out_off, d_state,
-                           d_state + ntiles, d_sync, map, toff, cbits, wlo, whi, g0);
+                           d_state + ntiles, d_sync, map, toff, cbits, plan, wlo, whi, g0);
     }
     return hipGetLastError();
 }
