@@ -394,16 +394,16 @@ def unpack_tile_chunks_for(total_words, nchunks, lib=None, sync=False):
     """Chunks per unpack tile: about capnp_unpack_tile_words() output words
     per 256-thread tile (the staged path's descriptor capacity, unpack.hip),
     or capnp_unpack_sync_tile_words() per wave sub-tile when the record sync
-    index is used.  With the index and a mean chunk of WORD_TILE_MEAN words or
-    more: 0, the library's word tiles (chunks of any length, unpack.hip
-    unpack_wt_kernel)."""
+    index is used.  For a mean chunk of WORD_TILE_MEAN words or more: 0, the
+    library's long-chunk path (word tiles through the index, unpack.hip
+    unpack_wt_kernel; without it the speculative block walk, resync.hip)."""
     L = lib or _lib.lib()
     tw = L.capnp_unpack_sync_tile_words() if sync else L.capnp_unpack_tile_words()
     if nchunks <= 0:
         return max(1, tw // 128)
     mean = max(total_words / nchunks, 1.0)
-    if sync and mean >= WORD_TILE_MEAN:
-        return 0
+    if mean >= WORD_TILE_MEAN:
+        return 0  # the library's long-chunk path: word tiles, or resync with no index
     return int(max(1, min(64, tw // mean)))
 
 

@@ -464,6 +464,11 @@ capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
 // (capnp_launch_unpack_wt: chunks of any length, cut at sync points), others
 // in chunk tiles of about capnp_unpack_tile_words() words.
 
+static capnp_status unpack_resync_dev(capnp_ctx* ctx, const uint8_t* d_packed,
+                                      const uint64_t* d_in_byte_off, size_t nchunks,
+                                      uint64_t* d_words, const uint64_t* d_out_word_off,
+                                      int32_t* d_status, uint64_t* d_consumed, hipStream_t s);
+
 static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
                                      const uint64_t* d_in_byte_off, size_t nchunks,
                                      uint64_t* d_words, const uint64_t* d_out_word_off,
@@ -472,7 +477,7 @@ static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
     if (!ctx || (nchunks && (!d_in_byte_off || !d_out_word_off || !d_status)))
         return CAPNP_E_INVALID_ARGUMENT;
     if (tc > 256) return CAPNP_E_INVALID_ARGUMENT;
-    if (d_sync && tc == 0 && nchunks) {
+    if (tc == 0 && nchunks) {
         hipStream_t s = pick(ctx, stream);
         uint64_t wr[2];
         HIP_TRY(hipMemcpyAsync(&wr[0], d_out_word_off, 8, hipMemcpyDeviceToHost, s));
@@ -480,7 +485,11 @@ static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
         HIP_TRY(hipStreamSynchronize(s));
         if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
         const uint64_t words = wr[1] - wr[0];
-        if (words && (words / nchunks >= kWordTileMean || force_word_tiles())) {
+        const bool longc = words && (words / nchunks >= kWordTileMean || force_word_tiles());
+        if (longc && !d_sync)  // no index: the speculative block walk (resync.hip)
+            return unpack_resync_dev(ctx, d_packed, d_in_byte_off, nchunks, d_words,
+                                     d_out_word_off, d_status, d_consumed, s);
+        if (longc) {
             const size_t ws = capnp_unpack_wt_ws_bytes(wr[0], wr[1]);
             capnp_status st = ensure_buf(ctx, &ctx->d_wt, &ctx->wt_cap, ws);
             if (st != CAPNP_OK) return st;
@@ -566,9 +575,16 @@ capnp_status capnp_gpu_unpack_batch_resync(capnp_ctx* ctx, const uint8_t* d_pack
                                            void* stream) {
     if (!ctx || (nchunks && (!d_in_byte_off || !d_out_word_off || !d_status)))
         return CAPNP_E_INVALID_ARGUMENT;
+    return unpack_resync_dev(ctx, d_packed, d_in_byte_off, nchunks, d_words, d_out_word_off,
+                             d_status, d_consumed, pick(ctx, stream));
+}
+
+static capnp_status unpack_resync_dev(capnp_ctx* ctx, const uint8_t* d_packed,
+                                      const uint64_t* d_in_byte_off, size_t nchunks,
+                                      uint64_t* d_words, const uint64_t* d_out_word_off,
+                                      int32_t* d_status, uint64_t* d_consumed, hipStream_t s) {
     ctx->resync_passes = ctx->resync_serial = 0;
     if (nchunks == 0) return CAPNP_OK;
-    hipStream_t s = pick(ctx, stream);
     uint64_t ends[2];
     HIP_TRY(hipMemcpyAsync(&ends[0], d_in_byte_off, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(&ends[1], d_in_byte_off + nchunks, 8, hipMemcpyDeviceToHost, s));
