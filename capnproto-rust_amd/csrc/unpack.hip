@@ -356,18 +356,42 @@ constexpr uint32_t kSyncWords = CAPNP_SYNC_WORDS;
 constexpr uint32_t kSyncNone = 0xFFFFFFFFu;
 constexpr uint32_t kMaxSeg = kTileWords / kSyncWords + 2;
 
+// Block walk without the index (UNPACK_SPEC): a chunk's packed bytes are cut
+// into kSpecBlk-byte blocks, one thread each.  Tables live over the selector
+// table (reloaded before the expansion) and the sync-walk tables.
+constexpr uint32_t kSpecBlk = 64;
+struct SpecTabs {
+    uint16_t bpos[kThreads];             // block start (LDS position)
+    uint16_t bend[kThreads];             // block end
+    uint8_t bchk[kThreads];              // chunk of the block
+    uint16_t bfirst[kStageChunks + 1];   // first block of each chunk
+};
+struct SpecOut {
+    uint16_t bx[kThreads];  // exit of the block's walk (first record boundary at or past its end)
+    uint16_t bw[kThreads];  // words the walk decoded
+};
+
 struct StageSmem {
     static constexpr uint32_t kDummy = kTileWords;  // dpos[kDummy + 2 lane]: dummy slots
-    uint64_t sel[256];  // expand_selector(tag): 0x00 -> zeros, 0xFF -> identity
-    uint8_t badc[kStageChunks];     // sync walk: 1 = the chunk needs the exact walk
-    uint32_t cw[kStageChunks + 1];  // sync walk: chunk word offsets (tile-relative)
-    uint32_t cp[kStageChunks + 1];  // sync walk: chunk packed offsets (LDS positions)
-    uint32_t ent[kMaxSeg];          // sync walk: entry of segment b (b >= 1)
-    uint8_t segc[kMaxSeg];          // sync walk: chunk that holds segment b's first word
+    union {
+        uint64_t sel[256];  // expand_selector(tag): 0x00 -> zeros, 0xFF -> identity
+        SpecTabs sp;
+    };
+    uint8_t badc[kStageChunks];     // 1 = the chunk needs the exact walk
+    uint32_t cw[kStageChunks + 1];  // chunk word offsets (tile-relative)
+    uint32_t cp[kStageChunks + 1];  // chunk packed offsets (LDS positions)
+    union {
+        struct {
+            uint32_t ent[kMaxSeg];          // sync walk: entry of segment b (b >= 1)
+            uint8_t segc[kMaxSeg];          // sync walk: chunk that holds segment b's first word
+        };
+        SpecOut so;
+    };
     // word tiles (unpack_wt_kernel): walk start of segment 0 (position + 1,
     // word), the state the last walker must reach at the tile end when the
     // last chunk continues, words of the first chunk before the tile, flags
     uint32_t wt_q0, wt_w0, wt_qB, wt_wB, wt_pre, wt_pl;
+    uint32_t spec_nb;  // block walk: blocks in the tile
     alignas(16) uint8_t bytes[kTileBytes + 16];
     alignas(16) uint16_t dpos[kTileWords + 2 * CAPNP_WAVE];  // [kTileWords + 2 lane]: dummy slots
 };
@@ -782,6 +806,194 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     return marked;
 }
 
+#ifndef UNPACK_SPEC
+// index-free tiles: 1 = block walk (spec_tile), 0 = one walker lane per chunk.
+// Measured at config 2: walk phase 23.3 vs 25.0 us per tile, 986 vs 997 us
+// per launch: the block walk shortens the chain 3x but walks every record
+// twice (plus a confirming round) on 10x the lanes, so the tile's total hop
+// work grows 3.4x and the CU saturates; kept as an option, off.
+#define UNPACK_SPEC 0
+#endif
+#ifndef UNPACK_SPEC_ROUNDS
+#define UNPACK_SPEC_ROUNDS 8  // fix-up rounds before a chunk falls to the exact walk
+#endif
+
+// Block walk: from p while p < be inside a chunk whose bytes end at pe ->
+// the exit (first record boundary at or past be), the words decoded, and
+// whether a record ran past the chunk (then the chunk takes the exact walk).
+__device__ __forceinline__ void spec_walk(const uint8_t* B, uint32_t p, uint32_t be, uint32_t pe,
+                                          uint32_t& x, uint32_t& words, bool& err) {
+    uint32_t w = 0;
+    err = false;
+    while (p < be) {
+        uint32_t tag, b1, b9;
+        rec_bytes(B, p + 1, tag, b1, b9);
+        const bool isz = tag == 0, isf = tag == 0xFF;
+        const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+        const uint32_t q = p + 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) +
+                           (isf ? 8u * cnt : 0u);
+        if (q > pe) {
+            err = true;
+            break;
+        }
+        w += 1u + cnt;
+        p = q;
+    }
+    x = p;
+    words = w;
+}
+
+// The descriptors of a block whose walk is final: records from p to x, the
+// first at tile word w; false if a run overruns the chunk's words (wend).
+template <class SM>
+__device__ __forceinline__ bool spec_desc(SM& S, uint32_t p, uint32_t x, uint32_t w,
+                                          uint32_t wend) {
+    while (p < x) {
+        uint32_t tag, b1, b9;
+        rec_bytes(S.bytes, p + 1, tag, b1, b9);
+        const bool isz = tag == 0, isf = tag == 0xFF;
+        const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+        if (w + 1u + cnt > wend) return false;
+        S.dpos[w] = (uint16_t)p;
+        if (isf && cnt) lit_entries(S, w, p, cnt);
+        w += 1u + cnt;
+        p += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) + (isf ? 8u * cnt : 0u);
+    }
+    return true;
+}
+
+// Index-free walk of a staged tile, one thread per kSpecBlk-byte block of a
+// chunk ("resync" inside a tile).  Round 0 walks every block from its first
+// byte (the chunk's first block from the chunk start: exact); then each
+// block's entry becomes the furthest exit of the blocks before it in its
+// chunk, and blocks whose entry moved walk again, until no entry moves.  At
+// that fixed point every block starts where its predecessor ended, so the
+// walks chain exactly from the chunk start; a chunk is fast-path only if its
+// last block ends exactly at its packed end with exactly its words and no
+// record ran past it.  Then the descriptors are written from the final
+// entries (word offsets from the blocks' word counts), and every other chunk
+// takes the exact serial walk.  Speculation changes the speed only.
+template <class SM>
+__device__ __forceinline__ void spec_tile(SM& S, uint64_t ca, uint32_t nc,
+                                          int32_t* __restrict__ status,
+                                          uint64_t* __restrict__ consumed, uint32_t tid,
+                                          uint32_t lane, uint32_t wave) {
+    if (wave == 0) {  // block table, lane = chunk
+        uint32_t nb = 0, len = 0, n = 0;
+        if (lane < nc) {
+            len = S.cp[lane + 1] - S.cp[lane];
+            n = S.cw[lane + 1] - S.cw[lane];
+            nb = (n && len) ? (len + kSpecBlk - 1) / kSpecBlk : 0u;
+            if (n && !len) S.badc[lane] = 1;  // (FailedToFill: the exact walk says so)
+        }
+        uint32_t incl = nb;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, d, 64);
+            if (lane >= d) incl += t;
+        }
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const uint32_t first = incl - nb;
+        if (lane < nc) S.sp.bfirst[lane] = (uint16_t)first;
+        if (total <= kThreads && lane < nc)
+            for (uint32_t j = 0; j < nb; j++) {
+                const uint32_t b = S.cp[lane] + j * kSpecBlk;
+                const uint32_t e = b + kSpecBlk < S.cp[lane + 1] ? b + kSpecBlk : S.cp[lane + 1];
+                S.sp.bpos[first + j] = (uint16_t)b;
+                S.sp.bend[first + j] = (uint16_t)e;
+                S.sp.bchk[first + j] = (uint8_t)lane;
+            }
+        if (lane == 0) S.spec_nb = total;
+    }
+    __syncthreads();
+    const uint32_t NB = S.spec_nb;
+    if (NB > kThreads) {  // (cannot happen: <= kTileBytes / 64 + 64 blocks)
+        if (tid < nc) S.badc[tid] = 1;
+    } else {
+        const bool act = tid < NB;
+        uint32_t c = 0, be = 0, pe = 0, start = 0, first = 0, e = 0;
+        if (act) {
+            c = S.sp.bchk[tid];
+            be = S.sp.bend[tid];
+            first = S.sp.bfirst[c];
+            start = S.cp[c];
+            pe = S.cp[c + 1];
+            e = tid == first ? start : S.sp.bpos[tid];
+        }
+        uint32_t x = 0, wds = 0;
+        bool err = false, walk = act;
+        for (uint32_t r = 0;; r++) {
+            if (walk) {
+                if (e >= be) {
+                    x = e;
+                    wds = 0;
+                    err = false;
+                } else {
+                    spec_walk(S.bytes, e, be, pe, x, wds, err);
+                }
+                S.so.bx[tid] = (uint16_t)(x < 0xFFFFu ? x : 0xFFFFu);
+                S.so.bw[tid] = (uint16_t)(wds < 0xFFFFu ? wds : 0xFFFFu);
+            }
+            __syncthreads();
+            uint32_t ne = start;
+            if (act && tid != first)
+                for (uint32_t j = first; j < tid; j++) {
+                    const uint32_t xj = S.so.bx[j];
+                    ne = xj > ne ? xj : ne;
+                }
+            const bool ch = act && ne != e;
+            e = ne;
+            walk = ch;
+            const bool any = __syncthreads_or(ch);
+            if (!any) break;
+            if (r + 1 >= UNPACK_SPEC_ROUNDS) {  // not settled: the exact walk decides
+                if (ch) S.badc[c] = 1;
+                break;
+            }
+        }
+        if (act && err) S.badc[c] = 1;
+        __syncthreads();
+        // chunk check: its last block ends at its end with exactly its words
+        if (tid < nc && !S.badc[tid]) {
+            const uint32_t n = S.cw[tid + 1] - S.cw[tid];
+            if (n && S.cp[tid + 1] > S.cp[tid]) {
+                const uint32_t f = S.sp.bfirst[tid];
+                const uint32_t l = f + (S.cp[tid + 1] - S.cp[tid] + kSpecBlk - 1) / kSpecBlk - 1;
+                uint32_t sw = 0;
+                for (uint32_t j = f; j <= l; j++) sw += S.so.bw[j];
+                if (S.so.bx[l] != S.cp[tid + 1] || sw != n) S.badc[tid] = 1;
+            }
+        }
+        __syncthreads();
+        if (act && !S.badc[c]) {
+            uint32_t w = S.cw[c];
+            for (uint32_t j = first; j < tid; j++) w += S.so.bw[j];
+            if (!spec_desc(S, e, S.so.bx[tid], w, S.cw[c + 1])) S.badc[c] = 1;
+        }
+    }
+    __syncthreads();
+    if (tid < nc) {
+        const uint64_t cc = ca + tid;
+        if (S.badc[tid]) {  // exact serial walk of the chunk
+#if UNPACK_PROF
+            atomicAdd(&g_uprof[0], 1ull);
+#endif
+            const uint32_t wa = S.cw[tid], wz = S.cw[tid + 1];
+            for (uint32_t i = wa; i < wz; i++) S.dpos[i] = kNone;
+            int32_t st;
+            uint32_t used;
+            walk_chunk(S, S.cp[tid], S.cp[tid + 1], wa, wz - wa, st, used);
+            status[cc] = st;
+            if (consumed) consumed[cc] = used;
+        } else {
+            status[cc] = ST_OK;
+            if (consumed)
+                consumed[cc] = S.cw[tid + 1] > S.cw[tid] ? S.cp[tid + 1] - S.cp[tid] : 0u;
+        }
+    }
+    __syncthreads();
+    S.sel[tid] = kExpandTable.s[tid];  // (the block tables overlaid it)
+}
+
 // One staged sub-tile: chunks [ca, cb) whose packed bytes, output words and
 // count fit the LDS tables (stage, walk, expand).  All threads of the
 // workgroup call it; it ends after its last LDS access of the expansion.
@@ -841,6 +1053,12 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
             for (uint32_t b = tid; b < nseg; b += kThreads)
                 if (b >= 1) S.ent[b] = sync[kf + b - 1];
             if (tid < kStageChunks) S.badc[tid] = 0;
+        } else if (UNPACK_SPEC) {
+            if (tid <= nc) {
+                S.cw[tid] = (uint32_t)(out_off[ca + tid] - W0);
+                S.cp[tid] = (uint32_t)(in_off[ca + tid] - B0) + off0;
+            }
+            if (tid < kStageChunks) S.badc[tid] = 0;
         }
 #pragma unroll
         for (uint32_t k = 0; k < kLoads; k++)
@@ -887,6 +1105,8 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
             }
         }
         if (anybad) __syncthreads();
+    } else if (UNPACK_SPEC) {
+        spec_tile(S, ca, nc, status, consumed, tid, lane, wave);
     } else if (wave == walker && lane < nc) {  // (idle lanes stay off: their LDS traffic counts)
         const uint64_t c = ca + lane;
         const uint64_t gp = in_off[c], ge = in_off[c + 1];

@@ -70,6 +70,7 @@ def main():
         life = (T[st, 3] - T[st, 0]) / 100.0
         span = (T[st, 3].max() - T[st, 0].min()) / 100.0
         print(f"iter {it}: {e0.elapsed_time(e1) * 1e3:.1f} us ok={ok} staged={st.sum()} "
+              f"exact-walk chunks={buf[0]} "
               f"global={(~st).sum()} per tile: stage={d(0, 1):.2f}us walk={d(1, 2):.2f}us "
               f"expand={d(2, 3):.2f}us life={life.mean():.2f}us "
               f"concurrency={life.sum() / max(span, 1e-9):.0f}")
