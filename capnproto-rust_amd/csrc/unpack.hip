@@ -131,8 +131,16 @@ __device__ __forceinline__ uint64_t expand_word(uint32_t tag, uint64_t packed) {
 
 // Global path: lane l < NL of the wave decodes chunk c0 + l (c < c_end);
 // `desc` is this wave's NL x 64 descriptor table (NL * 128 bytes of LDS).
+#ifndef UNPACK_GLOBAL_NOINLINE
+#define UNPACK_GLOBAL_NOINLINE 0
+#endif
+#if UNPACK_GLOBAL_NOINLINE
+#define UNPACK_GLOBAL_ATTR __attribute__((noinline))
+#else
+#define UNPACK_GLOBAL_ATTR
+#endif
 template <uint32_t NL>
-__device__ void unpack_global(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+__device__ UNPACK_GLOBAL_ATTR void unpack_global(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                               uint64_t c0, uint64_t c_end, uint64_t* __restrict__ out,
                               const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
                               uint64_t* __restrict__ consumed, uint16_t (*desc)[CAPNP_WAVE],
@@ -1162,30 +1170,16 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
 // that fit the LDS tables (normally one: the whole tile), each staged,
 // walked and expanded in turn; a single chunk too large for the tables
 // takes the global path.
+// The tile's chunks [ca, cb) when they do not all fit at once: the longest
+// prefixes that fit, staged in turn, and a chunk too large alone on the
+// global path.
 template <bool SYNC>
-__global__ void __launch_bounds__(kThreads, UNPACK_MIN_WAVES)
-unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-              uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
-              const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
-              uint64_t* __restrict__ consumed, const uint32_t* __restrict__ sync) {
-    __shared__ USmem sm;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-    const uint64_t ca = (uint64_t)blockIdx.x * tc;
-    const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
-    sm.st.sel[tid] = kExpandTable.s[tid];  // (read only by the staged expansions)
-    {
-        // the usual case, kept straight-line: the whole tile fits
-        const uint64_t B0 = uniform64(in_off[ca]), W0 = uniform64(out_off[ca]);
-        const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
-        if (cb - ca <= kStageChunks && uniform64(in_off[cb]) - B0 <= kTileBytes - off0 &&
-            uniform64(out_off[cb]) - W0 <= kTileWords) {
-            unpack_staged<SYNC>(sm.st, in, in_off, ca, cb, out, out_off, status, consumed, sync,
-                                tid, lane, wave);
-            return;
-        }
-    }
+__device__ void unpack_tile_rest(USmem& sm, const uint8_t* __restrict__ in,
+                                 const uint64_t* __restrict__ in_off, uint64_t ca, uint64_t cb,
+                                 uint64_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                                 int32_t* __restrict__ status, uint64_t* __restrict__ consumed,
+                                 const uint32_t* __restrict__ sync, uint32_t tid, uint32_t lane,
+                                 uint32_t wave) {
     bool first = true, resel = false;
     for (uint64_t lo = ca; lo < cb;) {
         // the longest prefix of [lo, cb) that fits: <= kStageChunks chunks,
@@ -1225,6 +1219,106 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
         lo += k;
     }
 }
+
+// Whether tile [ca, cb) fits the LDS tables at once (the usual case).
+__device__ __forceinline__ bool tile_fits(const uint8_t* __restrict__ in,
+                                          const uint64_t* __restrict__ in_off,
+                                          const uint64_t* __restrict__ out_off, uint64_t ca,
+                                          uint64_t cb) {
+    const uint64_t B0 = uniform64(in_off[ca]), W0 = uniform64(out_off[ca]);
+    const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
+    return cb - ca <= kStageChunks && uniform64(in_off[cb]) - B0 <= kTileBytes - off0 &&
+           uniform64(out_off[cb]) - W0 <= kTileWords;
+}
+
+// One workgroup per tile of `tc` chunks.  The tile is cut into sub-tiles
+// that fit the LDS tables (normally one: the whole tile), each staged,
+// walked and expanded in turn; a single chunk too large for the tables
+// takes the global path.
+template <bool SYNC>
+__global__ void __launch_bounds__(kThreads, UNPACK_MIN_WAVES)
+unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+              uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
+              const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
+              uint64_t* __restrict__ consumed, const uint32_t* __restrict__ sync) {
+    __shared__ USmem sm;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint64_t ca = (uint64_t)blockIdx.x * tc;
+    const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
+    sm.st.sel[tid] = kExpandTable.s[tid];  // (read only by the staged expansions)
+    if (tile_fits(in, in_off, out_off, ca, cb)) {  // the usual case, kept straight-line
+        unpack_staged<SYNC>(sm.st, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid,
+                            lane, wave);
+        return;
+    }
+    unpack_tile_rest<SYNC>(sm, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid, lane,
+                           wave);
+}
+
+// Split launch (the sync path): unpack_fit_kernel stages the tiles that fit
+// and marks the others in ovf[]; unpack_ovf_kernel takes the marked ones.
+// The fitting path alone needs no registers for the sub-tile loop and the
+// global walk, so it does not spill at 8 waves per SIMD (the combined
+// kernel spilled 44 B per lane).
+template <bool SYNC>
+__global__ void __launch_bounds__(kThreads, UNPACK_MIN_WAVES)
+unpack_fit_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                  uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
+                  const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
+                  uint64_t* __restrict__ consumed, const uint32_t* __restrict__ sync,
+                  uint8_t* __restrict__ ovf) {
+    __shared__ StageSmem S;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint64_t ca = (uint64_t)blockIdx.x * tc;
+    const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
+    const bool fits = tile_fits(in, in_off, out_off, ca, cb);
+    if (tid == 0) ovf[blockIdx.x] = fits ? 0 : 1;
+    if (!fits) return;
+    S.sel[tid] = kExpandTable.s[tid];
+    unpack_staged<SYNC>(S, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid, lane,
+                        wave);
+}
+
+template <bool SYNC>
+__global__ void __launch_bounds__(kThreads)
+unpack_ovf_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                  uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
+                  const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
+                  uint64_t* __restrict__ consumed, const uint32_t* __restrict__ sync,
+                  const uint8_t* __restrict__ ovf, uint64_t ntiles) {
+    __shared__ USmem sm;
+    __shared__ uint32_t lst[kThreads];
+    __shared__ uint32_t nl;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    for (uint64_t base = (uint64_t)blockIdx.x * kThreads; base < ntiles;
+         base += (uint64_t)gridDim.x * kThreads) {
+        if (tid == 0) nl = 0;
+        __syncthreads();
+        if (base + tid < ntiles && ovf[base + tid]) lst[atomicAdd(&nl, 1u)] = tid;
+        __syncthreads();
+        const uint32_t n = nl;
+        for (uint32_t i = 0; i < n; i++) {
+            const uint64_t t = base + lst[i];
+            const uint64_t ca = t * tc;
+            const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
+            __syncthreads();
+            sm.st.sel[tid] = kExpandTable.s[tid];
+            unpack_tile_rest<SYNC>(sm, in, in_off, ca, cb, out, out_off, status, consumed, sync,
+                                   tid, lane, wave);
+        }
+        __syncthreads();
+    }
+}
+
+// Overflow flags of the split launch (tiles per launch up to its size).
+constexpr uint64_t kOvfCap = 1ull << 22;
+__device__ uint8_t g_ovf[kOvfCap];
 
 // ---------------------------------------------------------------------------
 // Word tiles: batches of long chunks with the record sync index.
@@ -1800,7 +1894,21 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
                            d_out, d_out_off, d_status, d_consumed, d_sync);
         return hipGetLastError();
     }
-    if (d_sync)
+#ifndef UNPACK_SPLIT
+#define UNPACK_SPLIT 1  // sync path: fitting tiles and overflow tiles in two kernels
+#endif
+    if (d_sync && UNPACK_SPLIT && blocks <= kOvfCap) {
+        uint8_t* ovf = nullptr;
+        hipError_t e = hipGetSymbolAddress(reinterpret_cast<void**>(&ovf), HIP_SYMBOL(g_ovf));
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(unpack_fit_kernel<true>, dim3((uint32_t)blocks), dim3(kThreads),
+                           UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
+                           d_status, d_consumed, d_sync, ovf);
+        const uint64_t og = (blocks + kThreads - 1) / kThreads;
+        hipLaunchKernelGGL(unpack_ovf_kernel<true>, dim3((uint32_t)(og < 1024 ? og : 1024)),
+                           dim3(kThreads), 0, stream, d_in, d_in_off, nchunks, tc, d_out,
+                           d_out_off, d_status, d_consumed, d_sync, ovf, blocks);
+    } else if (d_sync)
         hipLaunchKernelGGL(unpack_kernel<true>, dim3((uint32_t)blocks), dim3(kThreads),
                            UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
                            d_status, d_consumed, d_sync);
