@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Interleaved timing of word-tile pack variants (PACK_WT_ABL builds, wrong
-output by design) on the config-4 workload, in one process:
+"""Interleaved timing of library variants (pack, sync unpack, index-free
+unpack; PACK_WT_ABL builds give wrong output by design) on a bench workload
+(env WL, default config4), in one process:
     python3 scripts/wt_ablate.py [lib.so ...]"""
 import ctypes as C
 import glob
@@ -20,6 +21,7 @@ def load(path):
     L.capnp_ctx_create.restype = vp
     L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, u32, vp]
     L.capnp_gpu_unpack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, u32, vp]
+    L.capnp_gpu_unpack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, u32, vp]
     st = C.c_int(0)
     ctx = L.capnp_ctx_create(0, C.byref(st))
     assert ctx
@@ -50,10 +52,10 @@ def main():
     stream = torch.cuda.current_stream()
     P = C.c_void_p
     variants = [(os.path.basename(p), *load(p)) for p in libs]
-    res = {v[0]: {"pack": [], "unpack": []} for v in variants}
+    res = {v[0]: {"pack": [], "unpack": [], "nosync": []} for v in variants}
     for r in range(5):
         for name, L, h in variants:
-            for kind in ("pack", "unpack"):
+            for kind in ("pack", "unpack", "nosync"):
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
@@ -62,6 +64,11 @@ def main():
                         L.capnp_gpu_pack_batch_sync_tuned(h, P(words.data_ptr()), P(offs.data_ptr()), n,
                                                           P(out.data_ptr()), cap, P(oo.data_ptr()),
                                                           P(sync.data_ptr()), 0, P(stream.cuda_stream))
+                    elif kind == "nosync":
+                        L.capnp_gpu_unpack_batch_tuned(h, P(ref_out.data_ptr()), P(ref_oo.data_ptr()), n,
+                                                       P(back.data_ptr()), P(offs.data_ptr()),
+                                                       P(status.data_ptr()), None, 0,
+                                                       P(stream.cuda_stream))
                     else:
                         L.capnp_gpu_unpack_batch_sync_tuned(h, P(ref_out.data_ptr()), P(ref_oo.data_ptr()), n,
                                                             P(back.data_ptr()), P(offs.data_ptr()),
@@ -72,9 +79,10 @@ def main():
                 res[name][kind].append(e0.elapsed_time(e1) / 5)
     U = total * 8
     for name, d in res.items():
-        pm, um = statistics.median(d["pack"]), statistics.median(d["unpack"])
+        pm, um, nm = (statistics.median(d[k]) for k in ("pack", "unpack", "nosync"))
         print(f"{name:36s} pack {pm * 1e3:8.1f} us ({U / pm / 1e6:7.1f} GB/s U)   "
-              f"unpack {um * 1e3:8.1f} us ({U / um / 1e6:7.1f} GB/s U)", flush=True)
+              f"unpack {um * 1e3:8.1f} us ({U / um / 1e6:7.1f} GB/s U)   "
+              f"nosync {nm * 1e3:8.1f} us", flush=True)
 
 
 if __name__ == "__main__":
