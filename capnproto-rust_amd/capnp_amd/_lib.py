@@ -7,7 +7,9 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "libcapnp_packed.so")
+# (CAPNP_PACKED_LIB: another build of the same library, e.g. a diagnostic
+# variant from the Makefile's uvariant/pvariant rules, for A/B parity runs)
+LIB_PATH = os.environ.get("CAPNP_PACKED_LIB") or os.path.join(HERE, "libcapnp_packed.so")
 
 OK = 0
 NONE = 1

@@ -764,9 +764,6 @@ __device__ Carry carry_into(const uint64_t* __restrict__ in, uint64_t cs, uint64
     return c;
 }
 
-__device__ uint32_t run_ext(const uint64_t* __restrict__ in, uint64_t R, uint64_t ce, Carry c,
-                            uint32_t lane);
-
 // Chunk-start bits of a word-tile batch (pack_wt_bits): bit i & 63 of
 // cb[1 + (i >> 6) - b64] is set when a chunk starts at word i (b64 = the
 // batch's first word >> 6; cb[0] and a tail are zero guards).  The 64 bits
@@ -788,8 +785,7 @@ __device__ __forceinline__ Carry carry_in_b(const uint64_t* __restrict__ in,
                                             const uint64_t* __restrict__ cb, uint64_t b64,
                                             uint64_t wlo, uint64_t R, uint32_t lane, uint64_t w,
                                             uint64_t wp, uint64_t bits) {
-    const uint64_t i = R - 64 + lane;
-    const bool v = R + lane >= 64 + wlo;  // i >= wlo
+    const bool v = R + lane >= 64 + wlo;  // word R - 64 + lane is at or past wlo
     const uint32_t tag = v ? tag_of(w) : 0u;
     const uint32_t up = (uint32_t)__shfl_up((int)tag, 1, 64);
     const uint32_t ptag = lane ? up : tag_of(wp);
@@ -896,130 +892,6 @@ __device__ __forceinline__ uint32_t run_ext_b(const uint64_t* __restrict__ in,
     return ext < c.rem ? ext : c.rem;
 }
 
-
-// carry_into_pre below its first window (long zero or 0xFF stretches):
-// eight windows per round go out at once and are reduced to tags right away.
-__device__ __forceinline__ Carry carry_deep(const uint64_t* __restrict__ in, uint64_t cs,
-                                            uint64_t R, uint32_t lane, bool allz, bool allf) {
-    for (uint64_t hi = R - 64; hi > cs; hi = hi > 512 ? hi - 512 : 0) {
-        uint32_t t[8];
-        {
-            uint64_t x[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const uint64_t ik = hi - 64 * (k + 1) + lane;
-                x[k] = (hi + lane >= 64ull * (k + 1) && ik >= cs) ? in[ik] : 0ull;
-            }
-#pragma unroll
-            for (int k = 0; k < 8; k++) t[k] = tag_of(x[k]);
-        }
-        int kf = -1;
-        uint64_t s = cs;
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint64_t ik = hi - 64 * (k + 1) + lane;
-            const bool vk = hi + lane >= 64ull * (k + 1) && ik >= cs;
-            const uint32_t tk = vk ? t[k] : 0u;
-            const uint32_t pt0 = (uint32_t)__shfl_up((int)tk, 1, 64);
-            // lane 0's predecessor: lane 63 of the window below (k + 1)
-            const uint32_t below = k < 7 ? (uint32_t)__shfl((int)t[k < 7 ? k + 1 : 7], 63, 64) : 0u;
-            const uint32_t pt = lane ? pt0 : below;
-            const bool sure = vk && (ik == cs || ((lane || k < 7) && sure_head(tk, pt)));
-            const uint64_t Gk = ballot64(sure);
-            if (kf < 0) {
-                if (Gk) {
-                    const uint32_t j = 63u - (uint32_t)__builtin_clzll(Gk);
-                    kf = k;
-                    s = hi - 64 * (k + 1) + j;
-                    allz = allz && ballot64(lane >= j && tk != 0) == 0;
-                    allf = allf && ballot64(lane >= j && tk != 0xFF) == 0;
-                } else {
-                    allz = allz && ballot64(tk != 0) == 0;
-                    allf = allf && ballot64(tk != 0xFF) == 0;
-                }
-            }
-        }
-        if (kf >= 0) {
-            if (allz || allf) {
-                const uint64_t h = s + (R - 1 - s) / 256 * 256;
-                return Carry{allz ? 1u : 2u, (uint32_t)(255u - (R - 1 - h))};
-            }
-            Carry c{0, 0};  // rare: resolve forward from s
-            for (uint64_t p = s; p < R; p += 64) {
-                const uint32_t nv = (uint32_t)(R - p < 64 ? R - p : 64);
-                const uint32_t tt = lane < nv ? tag_of(in[p + lane]) : 0u;
-                const uint32_t pop = __builtin_popcount(tt);
-                const uint64_t V = low_mask(nv);
-                c = resolve_step_s(ballot64(tt == 0) & V, ballot64(pop >= 7) & V,
-                                   ballot64(tt == 0xFF) & V, 0, nv, c).next;
-            }
-            return c;
-        }
-    }
-    return Carry{0, 0};  // (not reached: the windows reach cs, a sure head)
-}
-
-// carry_into with its first window preloaded: w = word R - 64 + lane (0
-// below the batch), wp = word R - 65.  The usual case (a sure head in the 64
-// words before R) costs no further load; deeper, eight windows go out at once.
-__device__ __forceinline__ Carry carry_into_pre(const uint64_t* __restrict__ in, uint64_t cs, uint64_t R,
-                                uint32_t lane, uint64_t w, uint64_t wp) {
-    const uint64_t base = R - 64;
-    const uint64_t i = base + lane;
-    const bool v = R + lane >= 64 && i >= cs;  // (i >= cs implies i >= the batch start)
-    const uint32_t tag = v ? tag_of(w) : 0u;
-    const uint32_t up = (uint32_t)__shfl_up((int)tag, 1, 64);
-    const uint32_t ptag = lane ? up : tag_of(wp);
-    const uint64_t G = ballot64(v && (i == cs || sure_head(tag, ptag)));
-    if (G) {
-        const uint32_t j = 63u - (uint32_t)__builtin_clzll(G);
-        const uint64_t s = base + j;
-        const bool mine = lane >= j;
-        const bool allz = ballot64(mine && tag != 0) == 0, allf = ballot64(mine && tag != 0xFF) == 0;
-        if (allz || allf) {
-            const uint64_t h = s + (R - 1 - s) / 256 * 256;
-            return Carry{allz ? 1u : 2u, (uint32_t)(255u - (R - 1 - h))};
-        }
-        // one step over the window with a forced head at the sure head
-        const uint32_t pop = __builtin_popcount(tag);
-        const uint64_t Sj = 1ull << j;
-        const uint64_t Vj = ~low_mask(j);
-        const StepMasks sm = resolve_step_s(ballot64(tag == 0) & Vj, ballot64(pop >= 7) & Vj,
-                                            ballot64(tag == 0xFF) & Vj, Sj, 64, Carry{0, 0});
-        return sm.next;
-    }
-    // no sure head in the window: all its words are one class
-    return carry_deep(in, cs, R, lane, ballot64(tag != 0) == 0, ballot64(tag != 0xFF) == 0);
-}
-
-
-// run_ext with its first window preloaded: w = word R + lane (valid below ce).
-__device__ __forceinline__ uint32_t run_ext_pre(const uint64_t* __restrict__ in, uint64_t R, uint64_t ce, Carry c,
-                                uint32_t lane, uint64_t w) {
-    if (c.type == 0 || c.rem == 0 || R >= ce) return 0;
-    const uint32_t nv = (uint32_t)(ce - R < 64 ? ce - R : 64);
-    const uint32_t tag = tag_of(w);
-    const bool cls = c.type == 1 ? tag == 0 : __builtin_popcount(tag) >= 7;
-    const uint32_t lead = ctz64(~ballot64(lane < nv && cls));
-    if (lead < 64 || lead >= c.rem) return lead < c.rem ? lead : c.rem;
-    return 64 + run_ext(in, R + 64, ce, Carry{c.type, c.rem - 64}, lane);
-}
-
-// Words from R on (up to the chunk end ce) that the open run c absorbs.
-__device__ uint32_t run_ext(const uint64_t* __restrict__ in, uint64_t R, uint64_t ce, Carry c,
-                            uint32_t lane) {
-    if (c.type == 0 || c.rem == 0) return 0;
-    uint32_t ext = 0;
-    for (uint64_t p = R; p < ce && ext < c.rem; p += 64) {
-        const uint32_t nv = (uint32_t)(ce - p < 64 ? ce - p : 64);
-        const uint32_t tag = lane < nv ? tag_of(in[p + lane]) : 0u;
-        const bool cls = c.type == 1 ? tag == 0 : __builtin_popcount(tag) >= 7;
-        const uint32_t lead = ctz64(~ballot64(lane < nv && cls));
-        ext += lead;
-        if (lead < 64) break;
-    }
-    return ext < c.rem ? ext : c.rem;
-}
 
 __device__ __forceinline__ void wt_tile_bounds(const LookbackArgs& A, uint64_t t, uint64_t& Ta,
                                                uint64_t& Tb) {
@@ -1585,8 +1457,8 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
     uint8_t* const outa = out - mis;
-    // the range's words, and the windows either side for the run state at
-    // its ends (carry_into_pre, run_ext_pre): every load goes out at once
+    // the range's words (the run state at its ends comes from the plan
+    // kernel, pack_wt_plan): every load goes out at once
     // (a buffer descriptor over the range: a lane past it reads 0, and the
     // unconditional loads let each step wait for its own load only)
     uint64_t cache[kStageSteps];

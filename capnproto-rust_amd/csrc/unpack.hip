@@ -851,6 +851,34 @@ __device__ __forceinline__ void spec_walk(const uint8_t* B, uint32_t p, uint32_t
     words = w;
 }
 
+// spec_walk that also marks every record start it visits in `M` (bit
+// p - s; the block [s, be) is at most 64 bytes).
+__device__ __forceinline__ void spec_walk_m(const uint8_t* B, uint32_t s, uint32_t be,
+                                            uint32_t pe, uint64_t& M, uint32_t& x,
+                                            uint32_t& words, bool& err) {
+    uint32_t w = 0, p = s;
+    uint64_t m = 0;
+    err = false;
+    while (p < be) {
+        uint32_t tag, b1, b9;
+        rec_bytes(B, p + 1, tag, b1, b9);
+        m |= 1ull << (p - s);
+        const bool isz = tag == 0, isf = tag == 0xFF;
+        const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+        const uint32_t q = p + 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) +
+                           (isf ? 8u * cnt : 0u);
+        if (q > pe) {
+            err = true;
+            break;
+        }
+        w += 1u + cnt;
+        p = q;
+    }
+    M = m;
+    x = p;
+    words = w;
+}
+
 // The descriptors of a block whose walk is final: records from p to x, the
 // first at tile word w; false if a run overruns the chunk's words (wend).
 template <class SM>
@@ -918,44 +946,67 @@ __device__ __forceinline__ void spec_tile(SM& S, uint64_t ca, uint32_t nc,
         if (tid < nc) S.badc[tid] = 1;
     } else {
         const bool act = tid < NB;
-        uint32_t c = 0, be = 0, pe = 0, start = 0, first = 0, e = 0;
+        uint32_t c = 0, sb = 0, be = 0, pe = 0, first = 0;
         if (act) {
             c = S.sp.bchk[tid];
-            be = S.sp.bend[tid];
             first = S.sp.bfirst[c];
-            start = S.cp[c];
+            sb = tid == first ? S.cp[c] : S.sp.bpos[tid];
+            be = S.sp.bend[tid];
             pe = S.cp[c + 1];
-            e = tid == first ? start : S.sp.bpos[tid];
         }
-        uint32_t x = 0, wds = 0;
-        bool err = false, walk = act;
+        // round 0: every block walks from its first byte (a chunk's first
+        // block from the chunk start: exact), marking the record starts it
+        // visits
+        uint64_t M = 0;
+        uint32_t x0 = sb, w0 = 0;
+        bool err0 = false;
+        if (act) spec_walk_m(S.bytes, sb, be, pe, M, x0, w0, err0);
+        uint32_t e = sb, x = x0, w = w0;
+        bool err = err0;
+        if (act) {
+            S.so.bx[tid] = (uint16_t)x;
+            S.so.bw[tid] = (uint16_t)(w < 0xFFFFu ? w : 0xFFFFu);
+        }
+        // Then each block takes its predecessor's exit as its entry.  The
+        // walks are deterministic, so if the round-0 walk visited that entry
+        // it is the exact walk from there on: same exit, words less those
+        // decoded before the entry (a short walk), and no re-walk.  Otherwise
+        // it walks again from the entry.  Repeat until no entry moves: then
+        // every block starts where its predecessor ended and, by induction
+        // from the chunk start, every walk is exact.
         for (uint32_t r = 0;; r++) {
-            if (walk) {
-                if (e >= be) {
-                    x = e;
-                    wds = 0;
-                    err = false;
-                } else {
-                    spec_walk(S.bytes, e, be, pe, x, wds, err);
-                }
-                S.so.bx[tid] = (uint16_t)(x < 0xFFFFu ? x : 0xFFFFu);
-                S.so.bw[tid] = (uint16_t)(wds < 0xFFFFu ? wds : 0xFFFFu);
-            }
             __syncthreads();
-            uint32_t ne = start;
-            if (act && tid != first)
-                for (uint32_t j = first; j < tid; j++) {
-                    const uint32_t xj = S.so.bx[j];
-                    ne = xj > ne ? xj : ne;
+            bool ch = false;
+            if (act && tid != first) {
+                const uint32_t xp = S.so.bx[tid - 1];
+                if (xp != e) {
+                    ch = true;
+                    e = xp;
+                    if (xp >= be) {  // a record from an earlier block covers this one
+                        x = xp;
+                        w = 0;
+                        err = false;
+                    } else if (xp >= sb && ((M >> (xp - sb)) & 1u)) {
+                        uint32_t xb, wb;
+                        bool eb;
+                        spec_walk(S.bytes, sb, xp, pe, xb, wb, eb);
+                        x = x0;
+                        w = w0 - wb;
+                        err = err0;
+                    } else {
+                        spec_walk(S.bytes, xp, be, pe, x, w, err);
+                    }
                 }
-            const bool ch = act && ne != e;
-            e = ne;
-            walk = ch;
+            }
             const bool any = __syncthreads_or(ch);
             if (!any) break;
             if (r + 1 >= UNPACK_SPEC_ROUNDS) {  // not settled: the exact walk decides
                 if (ch) S.badc[c] = 1;
                 break;
+            }
+            if (ch) {
+                S.so.bx[tid] = (uint16_t)x;
+                S.so.bw[tid] = (uint16_t)(w < 0xFFFFu ? w : 0xFFFFu);
             }
         }
         if (act && err) S.badc[c] = 1;
@@ -973,9 +1024,9 @@ __device__ __forceinline__ void spec_tile(SM& S, uint64_t ca, uint32_t nc,
         }
         __syncthreads();
         if (act && !S.badc[c]) {
-            uint32_t w = S.cw[c];
-            for (uint32_t j = first; j < tid; j++) w += S.so.bw[j];
-            if (!spec_desc(S, e, S.so.bx[tid], w, S.cw[c + 1])) S.badc[c] = 1;
+            uint32_t wa = S.cw[c];
+            for (uint32_t j = first; j < tid; j++) wa += S.so.bw[j];
+            if (!spec_desc(S, e, S.so.bx[tid], wa, S.cw[c + 1])) S.badc[c] = 1;
         }
     }
     __syncthreads();
