@@ -114,11 +114,19 @@ def cpu_baseline(args, threads):
     offs = np.arange(0, (n + 1) * cw, cw, dtype=np.uint64)
     if args.workload == "carsales":
         words, msg_off, _ = O.carsales_stream(n * cw)
+    elif args.workload == "config4":
+        # the first segments of rank 0's config-4 batch (same sizes, kinds and
+        # generator as the GPU workload) up to the sample's words
+        sizes, kinds = config4_layout(0)
+        n = max(1, int(np.searchsorted(np.cumsum(sizes), args.cpu_sample_words, side="right")))
+        offs = np.concatenate([[0], np.cumsum(sizes[:n])]).astype(np.uint64)
+        words = O.gen_fill(offs, kinds=kinds[:n], pz=PZ["config4"], id0=0)
     else:
         words = O.gen_fill(offs, kind0=0, pz=PZ.get(args.workload, PZ["config2"]))
 
     def timed(nn, thr, reps):
-        w, o = words[:nn * cw], offs[:nn + 1]
+        o = offs[:nn + 1]
+        w = words[:int(o[-1])]
         best = None
         for _ in range(reps):
             t0 = time.perf_counter()
@@ -134,14 +142,16 @@ def cpu_baseline(args, threads):
     best = timed(n, threads, args.cpu_reps)
     n1 = max(1, n // 16)
     one = timed(n1, 1, 2)
-    u, u1 = n * cw * 8, n1 * cw * 8
+    u, u1 = int(offs[n]) * 8, int(offs[n1]) * 8
+    shape = (f"{n} segments of 64 B - 64 KiB" if args.workload == "config4"
+             else f"{n} segments x {cw * 8} B")
     res = {
         "value": round(u / best[0] / GiB, 3),
         "unit": "GiB/s",
         "cores": threads,
         "host_cpus": os.cpu_count(),
         "kind": "port",
-        "sample": f"{n} segments x {cw * 8} B ({u / GiB:.3f} GiB) of the same workload, "
+        "sample": f"{shape} ({u / GiB:.3f} GiB) of the same workload, "
                   f"pack+unpack per segment, best of {args.cpu_reps}, {threads} threads "
                   f"(oracle/packed_oracle.c, gcc -O3; cores = threads used: the GPU box's "
                   f"CPU share, OMP_NUM_THREADS; host_cpus = os.cpu_count())",
@@ -170,21 +180,30 @@ def cpu_baseline(args, threads):
     return res
 
 
+def config4_layout(rank):
+    """Config 4's segment sizes (words, log-uniform 8 .. 8192) and generator
+    kinds (0: ~30 %-zero words, 1: long zero runs, 2: long literal runs) for
+    one rank: ~1 GiB of words."""
+    import numpy as np
+    rng = np.random.default_rng(4 + rank)
+    target = (1 << 30) // 8
+    sizes, total = [], 0
+    while total < target:
+        s = int(np.exp(rng.uniform(np.log(8), np.log(8193))))
+        sizes.append(s)
+        total += s
+    kinds = rng.choice(3, size=len(sizes), p=[0.8, 0.1, 0.1]).astype(np.uint8)
+    return np.array(sizes, np.int64), kinds
+
+
 def make_workload(args, ctx, torch, dev, rank):
     """-> (words, chunk_word_off, n, description) resident in HBM."""
     import numpy as np
     cw = args.chunk_words
     wl = args.workload
     if wl == "config4":
-        rng = np.random.default_rng(4 + rank)
-        target = (1 << 30) // 8
-        sizes, total = [], 0
-        while total < target:
-            s = int(np.exp(rng.uniform(np.log(8), np.log(8193))))
-            sizes.append(s)
-            total += s
-        n = len(sizes)
-        kinds = rng.choice(3, size=n, p=[0.8, 0.1, 0.1]).astype(np.uint8)
+        sizes, kinds = config4_layout(rank)
+        n, total = len(sizes), int(sizes.sum())
         offs_h = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
         offs = torch.from_numpy(offs_h).to(dev)
         words = torch.empty(total, dtype=torch.int64, device=dev)
