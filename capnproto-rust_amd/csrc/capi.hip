@@ -402,31 +402,31 @@ capnp_ctx* capnp_ctx_create(int device, capnp_status* status) {
 
 void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (!ctx) return;
-    hipSetDevice(ctx->device);
-    if (ctx->stream) hipStreamSynchronize(ctx->stream);
-    if (ctx->d_state) hipFree(ctx->d_state);
-    if (ctx->d_stage) hipFree(ctx->d_stage);
-    if (ctx->d_body) hipFree(ctx->d_body);
-    if (ctx->d_frame) hipFree(ctx->d_frame);
-    if (ctx->h_frame) hipHostFree(ctx->h_frame);
-    if (ctx->d_msg) hipFree(ctx->d_msg);
-    if (ctx->d_resync) hipFree(ctx->d_resync);
-    if (ctx->d_wt) hipFree(ctx->d_wt);
-    if (ctx->d_pwt) hipFree(ctx->d_pwt);
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->d_state) (void)hipFree(ctx->d_state);
+    if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+    if (ctx->d_body) (void)hipFree(ctx->d_body);
+    if (ctx->d_frame) (void)hipFree(ctx->d_frame);
+    if (ctx->h_frame) (void)hipHostFree(ctx->h_frame);
+    if (ctx->d_msg) (void)hipFree(ctx->d_msg);
+    if (ctx->d_resync) (void)hipFree(ctx->d_resync);
+    if (ctx->d_wt) (void)hipFree(ctx->d_wt);
+    if (ctx->d_pwt) (void)hipFree(ctx->d_pwt);
     for (int k = 0; k < 3; k++)
         if (ctx->sstream[k]) {
-            hipStreamSynchronize(ctx->sstream[k]);
-            hipStreamDestroy(ctx->sstream[k]);
+            (void)hipStreamSynchronize(ctx->sstream[k]);
+            (void)hipStreamDestroy(ctx->sstream[k]);
         }
     for (int k = 0; k < 2; k++) {
-        if (ctx->ev_in[k]) hipEventDestroy(ctx->ev_in[k]);
-        if (ctx->ev_comp[k]) hipEventDestroy(ctx->ev_comp[k]);
-        if (ctx->ev_off[k]) hipEventDestroy(ctx->ev_off[k]);
-        if (ctx->ev_out[k]) hipEventDestroy(ctx->ev_out[k]);
-        if (ctx->d_slot[k]) hipFree(ctx->d_slot[k]);
-        if (ctx->h_slot_off[k]) hipHostFree(ctx->h_slot_off[k]);
+        if (ctx->ev_in[k]) (void)hipEventDestroy(ctx->ev_in[k]);
+        if (ctx->ev_comp[k]) (void)hipEventDestroy(ctx->ev_comp[k]);
+        if (ctx->ev_off[k]) (void)hipEventDestroy(ctx->ev_off[k]);
+        if (ctx->ev_out[k]) (void)hipEventDestroy(ctx->ev_out[k]);
+        if (ctx->d_slot[k]) (void)hipFree(ctx->d_slot[k]);
+        if (ctx->h_slot_off[k]) (void)hipHostFree(ctx->h_slot_off[k]);
     }
-    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
 

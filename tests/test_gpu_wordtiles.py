@@ -284,6 +284,35 @@ def test_word_tile_pack_structures(ctx):
     _check_pack(ctx, np.concatenate(chunks), offs)
 
 
+def test_word_tile_pack_deep_stretches(ctx):
+    """Stretches of tens of thousands of all-zero or all-0xFF words (plan
+    entries deferred and taken from the range 512 words back), entered at
+    every phase after a random prefix, with a lone 7-byte word or a breaker
+    deep inside some of them, and runs of 7-byte words (no closed form)."""
+    rng = random.Random(41)
+    chunks = []
+    for i in range(24):
+        pre = rng.randrange(0, 700)
+        n = rng.choice([3000, 9000, 20000, 41000])
+        c = np.zeros(pre + n, np.uint64)
+        b = c.view(np.uint8).reshape(-1, 8)
+        b[:pre] = np.frombuffer(bytes(rng.randrange(256) if rng.random() < 0.5 else 0
+                                      for _ in range(8 * pre)), np.uint8).reshape(-1, 8)
+        kind = i % 4
+        if kind == 1:
+            c[pre:] = 0x1112131415161718
+        elif kind == 2:
+            c[pre:] = 0x1112131400161718  # 7-byte words: literal runs, no closed form
+        elif kind == 3:
+            c[pre:] = 0x2122232425262728
+            c[pre + rng.randrange(n)] = 0x2122232425002728
+        if i % 3 == 0:
+            c[pre + rng.randrange(n)] = 0x0000000400000001
+        chunks.append(c)
+    offs = np.concatenate([[0], np.cumsum([len(c) for c in chunks])]).astype(np.uint64)
+    _check_pack(ctx, np.concatenate(chunks), offs)
+
+
 def test_word_tile_pack_offset_base(ctx):
     rng = random.Random(12)
     sizes = _sizes_long(rng, 60)
