@@ -77,7 +77,10 @@ namespace {
 #endif
 constexpr int kWaves = PACK_WAVES;
 constexpr int kThreads = kWaves * CAPNP_WAVE;
-constexpr uint32_t kRing = 4096;           // streaming path: per-wave ring (bytes)
+#ifndef PACK_RING
+#define PACK_RING 4096
+#endif
+constexpr uint32_t kRing = PACK_RING;      // streaming path: per-wave ring (bytes)
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr int kMaxTileChunks = 64;
 constexpr uint32_t kZeroAhead = 1024;      // ring bytes zeroed per refill
@@ -92,14 +95,29 @@ constexpr uint32_t kStageWords = 64 * kStageSteps;
 // >= the packed bytes of a wave's range: at most 8.5 bytes per word (a 0xFF
 // head of 10 bytes needs a word of <= 7 bytes before the next one) plus 1.5
 // per chunk, and a range holds at most kStageSteps non-empty chunks
-constexpr uint32_t kStageBytes = 8 * kStageWords + kStageWords / 2 + 2 * kStageSteps;
+constexpr uint32_t kStageBytesMax = 8 * kStageWords + kStageWords / 2 + 2 * kStageSteps;
 // Leading gaps (capnp_launch_pack_gap): a wave's range stays staged while
 // its gaps total at most kGapSlack bytes.
 constexpr uint32_t kGapSlack = 128;
-// plus the 32 bytes copy_out may read past the end
-constexpr uint32_t kRegion = (kStageBytes + kGapSlack + 32 + 15) & ~15u;
-// per-wave LDS region: the staged bytes, or the streaming path's flush ring
-constexpr uint32_t kRegionBytes = kRegion > kRing ? kRegion : kRing;
+// Word tiles (pack_wt_kernel): regions for the worst case, plus the 32
+// bytes copy_out may read past the end.
+constexpr uint32_t kRegion = (kStageBytesMax + kGapSlack + 32 + 15) & ~15u;
+// Chunk tiles (pack_kernel): regions of kStageBytes (gaps included), 8.19
+// bytes per word: incompressible words pack to 8.03, so only adversarial
+// input (0xFF heads alternating with breakers, up to 8.5) overflows, and a
+// tile whose ranges overflow after pass 1 takes the streaming path.  The
+// smaller regions and the 8-byte selector entries fit 8 workgroups per CU
+// (20.3 KB each) where the worst-case layout fit 6 (23.8 KB): 608 -> 570 us
+// at config 2 in a trial build.
+#ifndef PACK_STAGE_BYTES
+#define PACK_STAGE_BYTES 4192
+#endif
+constexpr uint32_t kStageBytes = PACK_STAGE_BYTES;
+static_assert(kStageBytes <= kStageBytesMax && kStageBytes % 16 == 0, "stage capacity");
+constexpr uint32_t kStageRegion = (kStageBytes + 32 + 15) & ~15u;
+// per-wave LDS region of the chunk tiles: the staged bytes, or the
+// streaming path's flush ring
+constexpr uint32_t kRegionBytes = kStageRegion > kRing ? kStageRegion : kRing;
 
 // Record sync index (optional side-band): one entry per global word index
 // m = kSyncWords * k (8k), for the chunk that holds word m: the chunk-relative packed offset of
@@ -122,10 +140,21 @@ constexpr uint64_t kValMask = (1ull << 62) - 1;
 // s0/s1 put a zero byte (the tag's slot) first and then the first seven
 // non-zero bytes of the word; s2 places byte 7 and the count byte of a 0xFF
 // word; m keeps the tag (0xFF), tag and count (0xFFFF, zero word) or nothing.
+// Only s0/s1 live in the (LDS) table: s2 and m follow from the entry index
+// (sel_s2 / sel_m), which halves the table to 2 KiB.
 constexpr uint32_t kSelCopy = 256;
 struct alignas(16) SelEntry {
     uint32_t s0, s1, s2, m;
 };
+struct alignas(8) Sel8 {
+    uint32_t s0, s1;
+};
+__device__ __forceinline__ uint32_t sel_s2(uint32_t idx) {
+    return idx == 0xFFu ? 0x0C0C0403u : 0x0C0C0C0Cu;
+}
+__device__ __forceinline__ uint32_t sel_m(uint32_t idx) {
+    return idx == kSelCopy ? 0u : (idx == 0u ? 0xFFFFu : 0xFFu);
+}
 
 struct SelTable {
     SelEntry e[kSelCopy + 1];
@@ -155,16 +184,30 @@ constexpr SelTable make_sel_table() {
     t.e[kSelCopy].m = 0u;
     return t;
 }
-__device__ constexpr SelTable kSelTable = make_sel_table();
+struct Sel8Table {
+    Sel8 e[kSelCopy + 1];
+};
+constexpr Sel8Table make_sel8_table() {
+    Sel8Table t{};
+    const SelTable f = make_sel_table();
+    for (uint32_t i = 0; i <= kSelCopy; i++) t.e[i] = Sel8{f.e[i].s0, f.e[i].s1};
+    return t;
+}
+__device__ constexpr Sel8Table kSel8Table = make_sel8_table();
 
+// (Reading the 16-byte entries from global memory instead, L1-resident, left
+// 8 workgroups per CU but measured 1-2 % slower: the emit waits on the
+// gather.)
+
+template <bool GAP>
 struct Smem {
-    SelEntry sel[kSelCopy + 1];         // record assembly per tag
+    Sel8 sel[kSelCopy + 1];             // record assembly per tag (s0, s1)
     uint64_t chunk_size[kMaxTileChunks];
     uint64_t chunk_pos[kMaxTileChunks];
     uint64_t wave_bytes[kWaves];
     uint64_t wave_steps[kWaves];
     uint32_t chunk_oc[kMaxTileChunks];  // staged path: chunk start in its wave's region
-    uint32_t chunk_gap[kMaxTileChunks];  // leading gap bytes of each chunk (GAP kernels)
+    uint32_t chunk_gap[GAP ? kMaxTileChunks : 1];  // leading gap bytes of each chunk
     // per-wave staging region; the streaming path uses its first 4 KiB as
     // the flush ring.  emit_step ORs a zero into the dword before a record
     // that starts 4-aligned, hence the pad.
@@ -271,7 +314,7 @@ struct Packer {
     template <int MODE>
     __device__ __forceinline__ void step(uint64_t w, uint32_t nvalid, bool last, uint32_t lane,
                                          uint8_t* buf, uint8_t* __restrict__ out,
-                                         const SelEntry* sel) {
+                                         const Sel8* sel) {
         const bool valid = lane < nvalid;
         const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
         const uint32_t tag = word_tag(lo, hi);
@@ -310,10 +353,10 @@ struct Packer {
             if (head && tag == 0) {
                 r0 = cnt << 8;
             } else if (head) {
-                const SelEntry e = sel[tag];
+                const Sel8 e = sel[tag];
                 r0 = __builtin_amdgcn_perm(hi, lo, e.s0) | tag;
                 r1 = __builtin_amdgcn_perm(hi, lo, e.s1);
-                r2 = __builtin_amdgcn_perm(cnt, hi, e.s2);
+                r2 = __builtin_amdgcn_perm(cnt, hi, sel_s2(tag));
             } else {
                 r0 = lo;
                 r1 = hi;
@@ -453,7 +496,8 @@ struct StageState {
     }
 };
 
-__device__ __forceinline__ void size_step(StageState& pk, uint64_t w, uint32_t nvalid, uint32_t lane,
+[[maybe_unused]] __device__ __forceinline__ void size_step(StageState& pk, uint64_t w,
+                                                           uint32_t nvalid, uint32_t lane,
                                           StepInfo& si) {
     const uint32_t tag = word_tag_dot((uint32_t)w, (uint32_t)(w >> 32));
     const uint32_t pop = __builtin_popcount(tag);
@@ -476,6 +520,61 @@ __device__ __forceinline__ void size_step(StageState& pk, uint64_t w, uint32_t n
     pk.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
 }
 
+// size_step with less scalar work (PACK_LEAN_STEP, the default).  The
+// scalar unit (one per CU, shared by the four SIMDs) was the pack kernel's
+// busiest pipe: ~95 SALU ops per 64-word step in pass 1, and one more SALU op
+// per step cost ~2.1 us per launch against ~1.0 us for one more VALU op
+// (PACK_SALU_PAD / PACK_VALU_PAD builds, config 2).  Here:
+//   * validity is folded into the tag (lanes past nvalid get 0x100, no
+//     class), so the three class ballots and V are bare v_cmp masks;
+//   * the carried run's absorbed words are a v_cmp mask (lane < k);
+//   * the next carry reads the last head's class with one v_readlane from
+//     a per-lane class code instead of testing its bit in two masks;
+//   * no branches.
+__device__ __forceinline__ void size_step_lean(StageState& pk, uint64_t w, uint32_t nvalid,
+                                               uint32_t lane, StepInfo& si) {
+    const uint32_t tag = word_tag_dot((uint32_t)w, (uint32_t)(w >> 32));
+    const uint32_t pop = __builtin_popcount(tag);
+    const bool valid = lane < nvalid;
+    const uint32_t tv = valid ? tag : 0x100u;
+    const uint64_t V = ballot64(valid);
+    const uint64_t Zm = ballot64(tv == 0);
+    const uint64_t Lm = ballot64(valid && pop >= 7);
+    const uint64_t Fm = ballot64(tv == 0xFF);
+    const Carry c = pk.carry;
+    // words of the carried run's class at the step start, at most rem
+    uint32_t k = ctz64(~(c.type == 1 ? Zm : Lm));
+    k = k < c.rem ? k : c.rem;
+    k = c.type ? k : 0u;
+    const uint64_t AC = ballot64(lane < k);
+    const uint64_t Z2 = Zm & ~AC;
+    const uint64_t AZ = Z2 & (Z2 << 1);
+    const uint64_t L2 = Lm & ~AC;
+    const uint64_t F2 = Fm & ~AC;
+    const uint64_t filled = ((L2 ^ (L2 + F2)) & L2) | F2;
+    const uint64_t AF = filled & (filled << 1);
+    const uint64_t H = V & ~(AC | AZ | AF);
+    // the run open at the step end: the last head's, or the carried one
+    // when it covered the whole step
+    const uint32_t code = tv == 0 ? 1u : (tv == 0xFF ? 2u : 0u);
+    const uint32_t h = H ? 63u - (uint32_t)__builtin_clzll(H) : 0u;
+    const uint32_t th = (uint32_t)__builtin_amdgcn_readlane((int)code, h);
+    pk.carry.type = H ? th : c.type;
+    pk.carry.rem = H ? (th ? 192u + h : 0u) : c.rem - 64u;
+    const uint32_t hsize = 1u + pop + ((0x101u >> pop) & 1u);
+    const uint32_t size = mask_sel(H, hsize, tag == 0 ? 0u : 8u);
+    const uint32_t incl = wave_incl_scan(size);
+    si.H = H;
+    si.pos = pk.o_c + pk.total + incl - size;
+    si.tag = tag;
+    si.meta |= k << 16;
+    pk.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+}
+
+#ifndef PACK_LEAN_STEP
+#define PACK_LEAN_STEP 1  // 0: size_step (mask tests in scalar code, per-step LDS bookkeeping)
+#endif
+
 // Pass 2 of one staged step.  With `tab` (record sync index), every head
 // lane also writes the entries of the sync points its record covers: words
 // g + lane .. + the run (t0 = the tile's first sync word, oc = the chunk's
@@ -484,7 +583,7 @@ __device__ __forceinline__ void size_step(StageState& pk, uint64_t w, uint32_t n
 // a few VALU ops and a masked LDS store per step.
 template <bool SYNC>
 __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32_t ext,
-                                          uint32_t lane, uint8_t* region_m1, const SelEntry* sel,
+                                          uint32_t lane, uint8_t* region_m1, const Sel8* sel,
                                           uint8_t* __restrict__ tab, uint32_t t0, uint32_t g,
                                           uint32_t oc) {
     const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
@@ -498,10 +597,11 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
                                   __builtin_elementwise_sub_sat(nvalid + ext, lane + 1u));
     // record dwords r2:r1:r0 = tag, compacted bytes, count byte; absorbed
     // zero words and lanes past nvalid hold w == 0 and emit nothing
-    const SelEntry se = sel[mask_sel(si.H, tag, kSelCopy)];
-    const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, se.s0) | (((cnt << 8) | tag) & se.m);
+    const uint32_t idx = mask_sel(si.H, tag, kSelCopy);
+    const Sel8 se = sel[idx];
+    const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, se.s0) | (((cnt << 8) | tag) & sel_m(idx));
     const uint32_t r1 = __builtin_amdgcn_perm(hi, lo, se.s1);
-    const uint32_t r2 = __builtin_amdgcn_perm(cnt, hi, se.s2);
+    const uint32_t r2 = __builtin_amdgcn_perm(cnt, hi, sel_s2(idx));
     // OR (r << 8k), k = pos & 3, into the dwords from pos & ~3.  Written as
     // alignbyte by (-pos) & 3 from the dword before ceil(pos / 4): for k = 0
     // the first dword gets zero and the rest r0..r2 unshifted.
@@ -609,7 +709,7 @@ __device__ __forceinline__ void copy_out(const uint8_t* region, uint8_t* __restr
 template <int MODE>
 __device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* off,
                               uint64_t* chunk_size, const uint64_t* chunk_pos, uint32_t nc,
-                              uint32_t wave, uint32_t lane, uint8_t* ring, const SelEntry* sel,
+                              uint32_t wave, uint32_t lane, uint8_t* ring, const Sel8* sel,
                               uint8_t* out, uint32_t mis, uint64_t out_cap,
                               const uint32_t* cgap) {
     Packer pk;
@@ -641,6 +741,7 @@ __device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* o
         if (MODE == MODE_SIZE && lane == 0) chunk_size[ci] = pk.total + g;
     }
 }
+
 
 // ---------------------------------------------------------------------------
 // Word tiles (batches of long chunks): the batch is one word stream in which
@@ -1113,14 +1214,16 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
 // (tile-relative); returns the tile aggregate.
 // Staged path: the tile's packed bytes fit 32 bits (<= 4 regions), so the
 // scan is the DPP wave scan.
-__device__ __forceinline__ uint64_t scan_chunks32(Smem& sm, uint32_t nc, uint32_t lane) {
+template <class SM>
+__device__ __forceinline__ uint64_t scan_chunks32(SM& sm, uint32_t nc, uint32_t lane) {
     const uint32_t v = lane < nc ? (uint32_t)sm.chunk_size[lane] : 0u;
     const uint32_t incl = wave_incl_scan(v);
     if (lane < nc) sm.chunk_pos[lane] = incl - v;
     return (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
 }
 
-__device__ __forceinline__ uint64_t scan_chunks(Smem& sm, uint32_t nc, uint32_t lane) {
+template <class SM>
+__device__ __forceinline__ uint64_t scan_chunks(SM& sm, uint32_t nc, uint32_t lane) {
     const uint64_t v = lane < nc ? sm.chunk_size[lane] : 0;
     uint64_t s = v;
     for (uint32_t d = 1; d < 64; d <<= 1) {
@@ -1133,21 +1236,21 @@ __device__ __forceinline__ uint64_t scan_chunks(Smem& sm, uint32_t nc, uint32_t 
 
 // One workgroup per tile (tile = blockIdx.x), 4 waves.
 #ifndef PACK_MIN_WAVES
-#define PACK_MIN_WAVES 6  // per SIMD: 7 (the LDS limit) spills VGPRs to scratch
+#define PACK_MIN_WAVES 8  // per SIMD (LDS 19.7 KB: 8 workgroups per CU; 6 before the selector table left LDS)
 #endif
 
 // GAP: chunk c is preceded by gap[c] bytes of the output that the kernel
 // leaves zero (out_off[c] is the gap's start; capnp_gpu_write_messages puts
 // each message's segment table there).
 template <bool SYNC, bool GAP>
-__global__ void __launch_bounds__(kThreads, PACK_MIN_WAVES)
+__global__ void __launch_bounds__(kThreads, GAP ? 7 : PACK_MIN_WAVES)  // (GAP: 20.6 KB of LDS)
 pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
             uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
             uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts,
             uint64_t* __restrict__ gs, uint32_t* __restrict__ sync,
-            const uint32_t* __restrict__ gap) {
+            const uint32_t* __restrict__ gap, uint8_t* __restrict__ ovf) {
     static_assert(!(SYNC && GAP), "the sync index is not written with gaps");
-    __shared__ Smem sm;
+    __shared__ Smem<GAP> sm;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
@@ -1187,9 +1290,8 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
     if constexpr (GAP)
         for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_gap[i] = gap[c0 + i];
-    // record assembly table: one 16-byte entry per thread (+ the copy entry)
-    for (uint32_t i = tid; i <= kSelCopy; i += kThreads)
-        reinterpret_cast<uint4*>(sm.sel)[i] = reinterpret_cast<const uint4*>(kSelTable.e)[i];
+    // record assembly table: one 8-byte entry per thread (+ the copy entry)
+    for (uint32_t i = tid; i <= kSelCopy; i += kThreads) sm.sel[i] = kSel8Table.e[i];
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
     uint8_t* const outa = out - mis;
@@ -1250,10 +1352,51 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vo, 0, 0);
             cache[s] = ((uint64_t)v[1] << 32) | v[0];
         }
-        for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
+        for (uint32_t o = 16 * lane; o < kStageRegion; o += 16 * CAPNP_WAVE)
             *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
         // pass 1: sizes and positions
         StepInfo si[kStageSteps];
+#if PACK_LEAN_STEP
+        {
+            // (each step's chunk start and running size go to lane s of two
+            // registers; the chunk tables are written once after the loop)
+            StageState pk;
+            pk.begin(0);
+            uint32_t local = 0;
+            uint32_t rec_oc = 0, rec_sz = 0;
+#pragma unroll
+            for (uint32_t s = 0; s < kStageSteps; s++) {
+                const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
+                si[s].meta = meta;
+                if ((meta >> 7) & 1) {
+                    if constexpr (GAP) local += uniform(sm.chunk_gap[wc0 + (meta >> 9)]);
+                    pk.begin(local);
+                }
+#if PACK_ABLATE == 3 || PACK_ABLATE == 4
+                asm volatile("" ::"v"(cache[s]));  // timing-only: skip the arithmetic
+                pk.total += 34 * (meta & 127u) / 8;
+                si[s].H = 0;
+                si[s].pos = 0;
+                si[s].tag = 0;
+#else
+                size_step_lean(pk, cache[s], meta & 127u, lane, si[s]);
+#endif
+                rec_oc = lane == s ? pk.o_c : rec_oc;
+                rec_sz = lane == s ? pk.total : rec_sz;
+                if ((meta >> 8) & 1) local += pk.total;
+            }
+            if (lane < kStageSteps) {
+                const uint32_t ci = wc0 + ((d_meta >> 9) & 63u);
+                if ((d_meta >> 7) & 1) sm.chunk_oc[ci] = rec_oc;
+                if ((d_meta >> 8) & 1) {
+                    uint32_t g = 0;
+                    if constexpr (GAP) g = sm.chunk_gap[ci];
+                    sm.chunk_size[ci] = rec_sz + g;
+                }
+            }
+            if (lane == 0) sm.wave_bytes[wave] = local;
+        }
+#else
         {
             StageState pk;
             pk.begin(0);
@@ -1277,15 +1420,23 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                 size_step(pk, cache[s], meta & 127u, lane, si[s]);
 #endif
                 if ((meta >> 8) & 1) {
-                    if (lane == 0)
-                        sm.chunk_size[wc0 + (meta >> 9)] =
-                            pk.total + (GAP ? uniform(sm.chunk_gap[wc0 + (meta >> 9)]) : 0u);
+                    if (lane == 0) {
+                        uint32_t g = 0;
+                        if constexpr (GAP) g = uniform(sm.chunk_gap[wc0 + (meta >> 9)]);
+                        sm.chunk_size[wc0 + (meta >> 9)] = pk.total + g;
+                    }
                     local += pk.total;
                 }
             }
             if (lane == 0) sm.wave_bytes[wave] = local;
         }
+#endif
         __syncthreads();
+        // every range's bytes (gaps included) must fit its region
+        bool fits = true;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) fits &= sm.wave_bytes[w] <= kStageBytes;
+        fits = __builtin_amdgcn_readfirstlane((int)fits) != 0;
         uint64_t agg = 0;
         if (wave == 0) {
             agg = scan_chunks32(sm, nc, lane);
@@ -1296,7 +1447,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         uint8_t* const region_m1 = region - 1;
 #if PACK_ABLATE != 3 && PACK_ABLATE != 4
         wave_lds_sync();
-        {
+        if (fits) {
             uint32_t ext = 0;  // words the run open at the step end absorbs later
 #pragma unroll
             for (int s = (int)kStageSteps - 1; s >= 0; s--) {
@@ -1323,9 +1474,21 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 #if PACK_ABLATE == 2
         return;  // timing-only: no output stores
 #endif
-        if (wc1 > wc0) {
-            const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
-            copy_out(region, outa, D0, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
+        if (fits) {
+            if (wc1 > wc0) {
+                const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
+                copy_out(region, outa, D0, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
+            }
+        } else {
+            // a range overflowed its region (adversarial input, 8.19 to 8.5
+            // bytes per word): the sizes and offsets stand; pack_ovf_kernel
+            // writes the tile's bytes with the streaming path, and the tile
+            // has no index entries.  (The streaming pass inlined here pushed
+            // this kernel past 64 VGPRs; as a call it cost 3 % of every tile.)
+            if constexpr (SYNC)
+                for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads)
+                    sync[k0 + i] = kSyncNone;
+            if (tid == 0) ovf[tile] = 1;
         }
 #if PACK_PROF
         __syncthreads();
@@ -1356,6 +1519,51 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     }
 }
 
+// Tiles whose staged ranges overflowed (ovf[t] set by pack_kernel, after its
+// look-back wrote the chunks' offsets): the streaming path writes their
+// bytes at those offsets.  One lane per tile finds them; a few workgroups.
+template <bool GAP>
+__global__ void __launch_bounds__(kThreads)
+pack_ovf_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
+                uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
+                const uint64_t* __restrict__ out_off, const uint8_t* __restrict__ ovf,
+                uint64_t ntiles, const uint32_t* __restrict__ gap) {
+    __shared__ Smem<GAP> sm;
+    __shared__ uint32_t lst[kThreads];
+    __shared__ uint32_t nl;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    for (uint32_t i = tid; i <= kSelCopy; i += kThreads) sm.sel[i] = kSel8Table.e[i];
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
+    uint8_t* const outa = out - mis;
+    uint8_t* region = sm.stage[wave];
+    for (uint64_t base = (uint64_t)blockIdx.x * kThreads; base < ntiles;
+         base += (uint64_t)gridDim.x * kThreads) {
+        if (tid == 0) nl = 0;
+        __syncthreads();
+        if (base + tid < ntiles && ovf[base + tid]) lst[atomicAdd(&nl, 1u)] = tid;
+        __syncthreads();
+        const uint32_t n = nl;
+        for (uint32_t k = 0; k < n; k++) {
+            const uint64_t c0 = (base + lst[k]) * tc;
+            const uint64_t c1 = c0 + tc < nchunks ? c0 + tc : nchunks;
+            const uint32_t nc = (uint32_t)(c1 - c0);
+            __syncthreads();  // the previous tile is done with the tables
+            for (uint32_t j = tid; j < nc; j += kThreads) {
+                sm.chunk_pos[j] = out_off[c0 + j];
+                sm.chunk_size[j] = out_off[c0 + j + 1] - out_off[c0 + j];
+                if constexpr (GAP) sm.chunk_gap[j] = gap[c0 + j];
+            }
+            __syncthreads();
+            run_streaming<MODE_RING>(in, chunk_off + c0, sm.chunk_size, sm.chunk_pos, nc, wave,
+                                     lane, region, sm.sel, outa, mis, out_cap,
+                                     GAP ? sm.chunk_gap : nullptr);
+        }
+        __syncthreads();
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Word-tile pack kernel.  Tile t = words [Ta, Tb) of the batch (kWtTile words
 // at global multiples of kWtTile), wave w = range [Ta + w kWtRange, ...): the
@@ -1374,7 +1582,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 #endif
 
 struct WtSmem {
-    SelEntry sel[kSelCopy + 1];            // record assembly per tag
+    Sel8 sel[kSelCopy + 1];                // record assembly per tag (s0, s1)
     uint64_t wave_bytes[kWaves];
     uint32_t lastcs[kWaves];               // region position of the last chunk start
     uint64_t excl;
@@ -1414,7 +1622,7 @@ __device__ uint32_t g_pwt_dbg[4096 * 8];
 #define PACK_WT_PIN 1
 #endif
 #ifndef PACK_WT_MIN_WAVES
-#define PACK_WT_MIN_WAVES 6  // the LDS (26.4 KB) allows 6 workgroups per CU
+#define PACK_WT_MIN_WAVES 6  // the LDS (24.3 KB) allows 6 workgroups per CU
 #endif
 template <bool SYNC>
 __global__ void __launch_bounds__(kThreads, PACK_WT_MIN_WAVES)
@@ -1452,8 +1660,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     const uint64_t R1 = !have ? R0 : (R0 + kWtRange < Tb ? R0 + kWtRange : Tb);
     const uint32_t nw = (uint32_t)(R1 - R0);
     const bool lastr = have && R1 == whi;
-    for (uint32_t i = tid; i <= kSelCopy; i += kThreads)
-        reinterpret_cast<uint4*>(sm.sel)[i] = reinterpret_cast<const uint4*>(kSelTable.e)[i];
+    for (uint32_t i = tid; i <= kSelCopy; i += kThreads) sm.sel[i] = kSel8Table.e[i];
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
     uint8_t* const outa = out - mis;
@@ -1711,7 +1918,16 @@ extern "C" uint32_t capnp_pack_tile_words(void) { return kWaves * 64 * kStageSte
 extern "C" size_t capnp_pack_state_bytes(uint64_t nchunks, uint32_t tc) {
     const uint64_t ntiles = (nchunks + tc - 1) / tc;
     const uint64_t ngroups = (ntiles + kGroup - 1) / kGroup;
-    return ((ntiles + ngroups) * 8 + 15) & ~size_t(15);
+    return ((ntiles + ngroups) * 8 + ntiles + 15) & ~size_t(15);  // + overflow flags
+}
+
+// The tiles' overflow flags follow the tile and group records in the state.
+static uint8_t* pack_ovf_flags(uint64_t* d_state, uint64_t ntiles) {
+    return reinterpret_cast<uint8_t*>(d_state + ntiles + (ntiles + kGroup - 1) / kGroup);
+}
+static dim3 pack_ovf_grid(uint64_t ntiles) {
+    const uint64_t g = (ntiles + kThreads - 1) / kThreads;
+    return dim3((uint32_t)(g < 1024 ? g : 1024));
 }
 
 extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_chunk_off,
@@ -1726,14 +1942,18 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_
     }
     hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(nchunks, tc), stream);
     if (e != hipSuccess) return e;
+    uint8_t* ovf = pack_ovf_flags(d_state, ntiles);
     if (d_sync)
         hipLaunchKernelGGL((pack_kernel<true, false>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
                            stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
-                           d_state, d_state + ntiles, d_sync, nullptr);
+                           d_state, d_state + ntiles, d_sync, nullptr, ovf);
     else
         hipLaunchKernelGGL((pack_kernel<false, false>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
                            stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
-                           d_state, d_state + ntiles, d_sync, nullptr);
+                           d_state, d_state + ntiles, d_sync, nullptr, ovf);
+    hipLaunchKernelGGL((pack_ovf_kernel<false>), pack_ovf_grid(ntiles), dim3(kThreads), 0, stream,
+                       d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, ovf, ntiles,
+                       nullptr);
     return hipGetLastError();
 }
 
@@ -1750,9 +1970,13 @@ extern "C" hipError_t capnp_launch_pack_gap(const uint64_t* d_in, const uint64_t
     if (nchunks == 0) return hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), stream);
     hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(nchunks, tc), stream);
     if (e != hipSuccess) return e;
+    uint8_t* ovf = pack_ovf_flags(d_state, ntiles);
     hipLaunchKernelGGL((pack_kernel<false, true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
                        stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_state,
-                       d_state + ntiles, nullptr, d_gap);
+                       d_state + ntiles, nullptr, d_gap, ovf);
+    hipLaunchKernelGGL((pack_ovf_kernel<true>), pack_ovf_grid(ntiles), dim3(kThreads), 0, stream,
+                       d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, ovf, ntiles,
+                       d_gap);
     return hipGetLastError();
 }
 

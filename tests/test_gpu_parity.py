@@ -489,6 +489,38 @@ def test_sync_long_runs(ctx):
     _check_sync_batch(ctx, np.concatenate(chunks), offs, utcs=(0, 3))
 
 
+def test_pack_region_overflow(ctx):
+    """Adversarial ranges (a 0xFF word then a 6-byte word, 8.5 packed bytes
+    per word) overflow the staged regions: those tiles take the streaming
+    path (bytes and offsets exact, no index entries); mixed with tiles that
+    fit and with empty and short chunks."""
+    rng = random.Random(61)
+    chunks = []
+    for i in range(300):
+        n = rng.choice([0, 1, 64, 128, 128, 128, 200, 256])
+        c = np.zeros(n, np.uint64)
+        if i % 3:
+            c[0::2] = 0x1112131415161718
+            c[1::2] = 0x0000212223242526
+        else:
+            b = c.view(np.uint8)
+            b[:] = np.frombuffer(bytes(rng.randrange(256) if rng.random() < 0.6 else 0
+                                       for _ in range(8 * n)), np.uint8)
+        chunks.append(c)
+    offs = np.concatenate([[0], np.cumsum([len(c) for c in chunks])]).astype(np.uint64)
+    words = np.concatenate(chunks)
+    for tc in (0, 4, 16):
+        _check_sync_batch(ctx, words, offs, tc, utcs=(0, 7))
+    st, ref, ref_offs = O.pack_batch(words, offs)
+    out = torch.zeros(ctx.batch_bound_bytes(int(offs[-1]), len(offs) - 1), dtype=torch.uint8,
+                      device="cuda")
+    oo = torch.empty(len(offs), dtype=torch.int64, device="cuda")
+    ctx.pack_batch_into(dev(words), dev(offs), out, oo)
+    torch.cuda.synchronize()
+    assert np.array_equal(oo.cpu().numpy().view(np.uint64), ref_offs)
+    assert np.array_equal(out[:len(ref)].cpu().numpy(), ref)
+
+
 def test_sync_unpack_error_statuses_vs_oracle(ctx):
     """Malformed chunks through the sync path (index garbage or absent):
     statuses, consumed counts and the words of good chunks equal the oracle."""
