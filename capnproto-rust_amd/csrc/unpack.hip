@@ -362,7 +362,6 @@ __device__ __forceinline__ uint64_t expand_desc(const uint8_t* B, const uint64_t
 // Record sync index (pack.hip): entry k describes global word kSyncWords * k.
 constexpr uint32_t kSyncWords = CAPNP_SYNC_WORDS;
 constexpr uint32_t kSyncNone = 0xFFFFFFFFu;
-constexpr uint32_t kMaxSeg = kTileWords / kSyncWords + 2;
 
 // Block walk without the index (UNPACK_SPEC): a chunk's packed bytes are cut
 // into kSpecBlk-byte blocks, one thread each.  Tables live over the selector
@@ -379,8 +378,12 @@ struct SpecOut {
     uint16_t bw[kThreads];  // words the walk decoded
 };
 
-struct StageSmem {
-    static constexpr uint32_t kDummy = kTileWords;  // dpos[kDummy + 2 lane]: dummy slots
+// The staged tables for tiles of up to TW output words and TB packed bytes
+// (chunk tiles: kTileWords / kTileBytes; word tiles: kWtWords / kWtBytes).
+template <uint32_t TW, uint32_t TB>
+struct StageSmemT {
+    static constexpr uint32_t kDummy = TW;  // dpos[kDummy + 2 lane]: dummy slots
+    static constexpr uint32_t kSeg = TW / kSyncWords + 2;
     union {
         uint64_t sel[256];  // expand_selector(tag): 0x00 -> zeros, 0xFF -> identity
         SpecTabs sp;
@@ -390,8 +393,8 @@ struct StageSmem {
     uint32_t cp[kStageChunks + 1];  // chunk packed offsets (LDS positions)
     union {
         struct {
-            uint32_t ent[kMaxSeg];          // sync walk: entry of segment b (b >= 1)
-            uint8_t segc[kMaxSeg];          // sync walk: chunk that holds segment b's first word
+            uint32_t ent[kSeg];             // sync walk: entry of segment b (b >= 1)
+            uint8_t segc[kSeg];             // sync walk: chunk that holds segment b's first word
         };
         SpecOut so;
     };
@@ -400,9 +403,10 @@ struct StageSmem {
     // last chunk continues, words of the first chunk before the tile, flags
     uint32_t wt_q0, wt_w0, wt_qB, wt_wB, wt_pre, wt_pl;
     uint32_t spec_nb;  // block walk: blocks in the tile
-    alignas(16) uint8_t bytes[kTileBytes + 16];
-    alignas(16) uint16_t dpos[kTileWords + 2 * CAPNP_WAVE];  // [kTileWords + 2 lane]: dummy slots
+    alignas(16) uint8_t bytes[TB + 16];
+    alignas(16) uint16_t dpos[TW + 2 * CAPNP_WAVE];  // [TW + 2 lane]: dummy slots
 };
+using StageSmem = StageSmemT<kTileWords, kTileBytes>;
 
 union USmem {
     StageSmem st;
@@ -1404,10 +1408,27 @@ unpack_ovf_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
 // bytes beyond the LDS table).  unpack_wt_plan (one thread per tile) resolves
 // the tile's chunks and both ends from global memory up front.
 #ifndef UNPACK_WT_WORDS
-#define UNPACK_WT_WORDS 1024
+#define UNPACK_WT_WORDS 1536
 #endif
 constexpr uint32_t kWtWords = UNPACK_WT_WORDS;
-static_assert(kWtWords % kSyncWords == 0 && kWtWords <= kTileWords, "word tile size");
+static_assert(kWtWords % kSyncWords == 0 && kWtWords <= kMaxTileChunks * CAPNP_WAVE,
+              "word tile size");
+// Packed bytes a word tile stages: 8.125 per word, so that runs of literal
+// words (8.03 bytes per word) fit, plus 2064 for a literal run that began up
+// to 255 words before the tile (staged from its head); only adversarial
+// tiles (up to 8.5 bytes per word) exceed it and decode serially.
+// Tile size (config 4, unpack µs): 1024 words in the chunk tiles' tables
+// (half of the 256 walkers had no segment) 730; in their own tables 1280 ->
+// 649, 1536 -> 632 (7 workgroups per CU), 1792 -> 660, 2048 -> 677 (5 per
+// CU).
+#ifndef UNPACK_WT_BYTES
+#define UNPACK_WT_BYTES ((kWtWords * 65 / 8 + 2064 + 15) & ~15u)
+#endif
+constexpr uint32_t kWtBytes = UNPACK_WT_BYTES;
+using WtStageSmem = StageSmemT<kWtWords, kWtBytes>;
+#ifndef UNPACK_WT_MIN_WAVES
+#define UNPACK_WT_MIN_WAVES 7  // the LDS (21.8 KB at 1536 words) allows 7 workgroups per CU
+#endif
 // plan flags
 constexpr uint32_t kWtPf = 1, kWtPl = 2, kWtFallback = 4;
 
@@ -1531,7 +1552,7 @@ unpack_wt_plan(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_o
         }
     }
     const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + bs) & 15u);
-    ok = ok && be >= bs && be - bs <= kTileBytes - off0;
+    ok = ok && be >= bs && be - bs <= kWtBytes - off0;
     P.bs = bs;
     P.span = ok ? (uint32_t)(be - bs) : 0u;
     P.flags = (pf ? kWtPf : 0u) | (pl ? kWtPl : 0u) | (ok ? 0u : kWtFallback);
@@ -1586,14 +1607,13 @@ __device__ __forceinline__ void serial_chunk_at(const uint8_t* __restrict__ in,
     if (consumed) consumed[c] = used;
 }
 
-__global__ void __launch_bounds__(kThreads, UNPACK_MIN_WAVES)
+__global__ void __launch_bounds__(kThreads, UNPACK_WT_MIN_WAVES)
 unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                  uint64_t* __restrict__ out, const uint64_t* __restrict__ out_off,
                  int32_t* __restrict__ status, uint64_t* __restrict__ consumed,
                  const uint32_t* __restrict__ sync, const WtPlan* __restrict__ plan,
                  uint32_t* __restrict__ flags, uint64_t wlo, uint64_t whi, uint64_t g0) {
-    __shared__ USmem sm;
-    StageSmem& S = sm.st;
+    __shared__ WtStageSmem S;
     const uint32_t tid = threadIdx.x;
     const uint64_t s = blockIdx.x;
     uint64_t Wa, Wb;
@@ -1625,7 +1645,7 @@ unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
     const uint32_t r0 = (uint32_t)(Wa % kSyncWords);
     S.sel[tid] = kExpandTable.s[tid];
     {
-        constexpr uint32_t kLoads = (kTileBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
+        constexpr uint32_t kLoads = (kWtBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
         const uint4* src = reinterpret_cast<const uint4*>(in + Bs - off0);
         uint4* dst = reinterpret_cast<uint4*>(S.bytes);
         const uint32_t nblk = (nbytes + 15) / 16;
@@ -1681,7 +1701,7 @@ unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
         const uint32_t sb = b == 0 ? 0u : (uint32_t)((kf + b - 1) * kSyncWords - Wa);
         const bool last = b + 1 == nseg;
         const uint32_t eb = last ? Wt : (uint32_t)((kf + b) * kSyncWords - Wa);
-        marked |= walk_segment<StageSmem, true>(S, nc, b, sb, eb, last, Wt);
+        marked |= walk_segment<WtStageSmem, true>(S, nc, b, sb, eb, last, Wt);
     }
     const bool anybad = __syncthreads_or(marked);
     if (tid < nc) {
