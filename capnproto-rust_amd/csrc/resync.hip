@@ -48,6 +48,9 @@
 #include "common.h"
 #include "../../include/capnp_packed.h"
 
+#ifndef RESYNC_WALK_LDS
+#define RESYNC_WALK_LDS 32768  // 4 workgroups per CU (config 4 index-free: 5.81 -> 4.93 ms; 64 KiB: 5.31)
+#endif
 #ifndef RESYNC_BLOCK
 #define RESYNC_BLOCK 512
 #endif
@@ -61,6 +64,20 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
 namespace {
 
 constexpr uint64_t kBlock = RESYNC_BLOCK;  // packed bytes per lane
+
+// Dynamic LDS the block walks reserve (unused) to cap their workgroups per
+// CU: each lane walks its own block byte by byte from global memory, so the
+// working set is one cache line per lane; at full occupancy (2048 lanes per
+// CU) it is 256 KB per CU, beyond L1 and the CU's share of L2, and every
+// hop refetched its line from HBM (config 4: 11.4 GB read for 0.57 GB of
+// packed bytes).  CAPNP_RESYNC_LDS overrides (bytes; diagnostic).
+static uint32_t walk_lds() {
+    static const uint32_t v = [] {
+        const char* e = getenv("CAPNP_RESYNC_LDS");
+        return e ? (uint32_t)atoi(e) : (uint32_t)RESYNC_WALK_LDS;
+    }();
+    return v;
+}
 constexpr uint32_t kThreads = 256;
 constexpr uint64_t kGroup = 8;  // blocks per fix lane
 constexpr int kMaxPasses = 512;  // fix passes before giving up to the serial path
@@ -282,7 +299,7 @@ size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes) {
 
 size_t scan_tmp_bytes(uint64_t items) {
     size_t bytes = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
                                      (int)items);
     return bytes;
 }
@@ -338,7 +355,7 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
         return e;
-    k_spec<<<grid(nbb), kThreads, 0, s>>>(d_in, d_in_off, n, w.bstart, w.spec_exit, w.spec_words,
+    k_spec<<<grid(nbb), kThreads, walk_lds(), s>>>(d_in, d_in_off, n, w.bstart, w.spec_exit, w.spec_words,
                                           w.exit, w.entry, w.words);
     // fix passes, kPassBatch at a time; a pass after one that changed nothing
     // returns at once, so the flag of a batch's last pass says whether the
@@ -351,7 +368,7 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
             break;
         }
         for (int i = 0; i < kPassBatch; i++, pass++)
-            k_fix<<<grid(ngroups), kThreads, 0, s>>>(d_in, d_in_off, n, w.bstart, w.spec_exit,
+            k_fix<<<grid(ngroups), kThreads, walk_lds(), s>>>(d_in, d_in_off, n, w.bstart, w.spec_exit,
                                                      w.spec_words, w.exit, w.entry, w.words,
                                                      w.flags, pass);
         int32_t last = 0;
@@ -567,7 +584,7 @@ extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t n
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
         return e;
-    k_spec<<<grid(nbb), kThreads, 0, s>>>(d_in, in_off, n, w.bstart, w.spec_exit, w.spec_words,
+    k_spec<<<grid(nbb), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart, w.spec_exit, w.spec_words,
                                           w.exit, w.entry, w.words);
     int pass = 0;
     const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
@@ -575,7 +592,7 @@ extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t n
         if (pass >= kMaxPasses) break;  // (not converged: k_consistent bounds the walk
                                         // to the exact prefix; the caller continues)
         for (int i = 0; i < kPassBatch; i++, pass++)
-            k_fix<<<grid(ngroups), kThreads, 0, s>>>(d_in, in_off, n, w.bstart, w.spec_exit,
+            k_fix<<<grid(ngroups), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart, w.spec_exit,
                                                      w.spec_words, w.exit, w.entry, w.words,
                                                      w.flags, pass);
         int32_t last = 0;
