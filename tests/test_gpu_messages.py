@@ -104,6 +104,24 @@ def test_write_messages_carsales_like_batch(ctx):
     _check_messages(ctx, msgs)
 
 
+def test_write_messages_region_overflow(ctx):
+    """Segments that pack to 8.5 bytes per word (a 0xFF word, then a 6-byte
+    word) overflow the pack kernel's staged regions, on the gap path that
+    leaves each message's segment table in front of its bytes: those tiles'
+    bytes come from the overflow pass and must still equal the oracle's."""
+    rng = random.Random(21)
+    adv = np.zeros(128, np.uint64)
+    adv[0::2] = 0x1112131415161718
+    adv[1::2] = 0x0000212223242526
+    msgs = []
+    for i in range(400):
+        if i % 3:
+            msgs.append([adv.copy() for _ in range(rng.choice([1, 2, 3]))])
+        else:
+            msgs.append([_segment(rng, rng.choice([0, 64, 128, 200]))])
+    _check_messages(ctx, msgs)
+
+
 def test_write_messages_staging_path(ctx):
     """Message offsets that do not span the batch (a segment before the first
     message and one after the last) take the staging path; the messages must
