@@ -90,7 +90,8 @@ def main():
               f"global={(~st).sum()} per tile: stage={d(0, 1):.2f}us walk={d(1, 2):.2f}us "
               f"expand={d(2, 3):.2f}us life={life.mean():.2f}us "
               f"concurrency={life.sum() / max(span, 1e-9):.0f} "
-              f"phaseB-iters={T[st, 5].mean():.2f} walk_segment={T[st, 6].mean() / 100.0:.2f}us")
+              f"phaseB-iters={T[st, 5].mean():.2f} walk_segment={T[st, 6].mean():.0f}cyc "
+              f"phaseA={T[st, 7].mean():.0f}cyc")
 
 if __name__ == "__main__":
     main()
