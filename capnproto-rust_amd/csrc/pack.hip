@@ -1199,13 +1199,18 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
         spins = 0;
     }
     if (group_last && lane == 0) publish_agent(&A.gs[g], kFlagInc | (gexcl + within + agg));
-#if PACK_PROF
+#if PACK_PROF == 1
     if (lane == 0) {
         TRACE(t, 5, n_ws);
         TRACE(t, 6, n_gs);
         TRACE(t, 7, n_win);
     }
+#endif
+#if PACK_PROF
     (void)tp0;
+    (void)n_ws;
+    (void)n_gs;
+    (void)n_win;
 #endif
     return gexcl + within;
 }
@@ -1284,8 +1289,9 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     const uint64_t* __restrict__ toff = chunk_off + c0;  // the tile's chunk offsets
     // sync entries of the tile: k in [k0, k1), words kSyncWords * k in [W0, W1)
     const uint64_t TW0 = uniform64(chunk_off[c0]);
+    const uint64_t TW1 = uniform64(chunk_off[c1]);
     const uint64_t k0 = (TW0 + kSyncWords - 1) / kSyncWords;
-    const uint64_t k1 = (uniform64(chunk_off[c1]) + kSyncWords - 1) / kSyncWords;
+    const uint64_t k1 = (TW1 + kSyncWords - 1) / kSyncWords;
     const uint32_t t0 = (uint32_t)(k0 * kSyncWords - TW0);  // first sync word, tile-relative
     for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
     if constexpr (GAP)
@@ -1295,7 +1301,15 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
     uint8_t* const outa = out - mis;
-    __syncthreads();
+#ifndef PACK_ONE_BARRIER
+#define PACK_ONE_BARRIER 1
+#endif
+    // (the ranges below read only chunk_off, so without gaps the barrier
+    // after them also covers the table writes above)
+    if (GAP || !PACK_ONE_BARRIER) __syncthreads();
+#if PACK_PROF == 2
+    if (tid == 0) TRACE(tile, 5, RT());  // (2: prelude timeline instead of look-back counters)
+#endif
 
     // contiguous chunk ranges per wave for the staged path.  Lane s of the
     // wave describes step s of the range: source word offset and
@@ -1332,6 +1346,9 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 #pragma unroll
     for (int w = 0; w < kWaves; w++) staged &= sm.wave_steps[w] <= kStageSteps;
     staged = __builtin_amdgcn_readfirstlane((int)staged) != 0;
+#if PACK_PROF == 2
+    if (tid == 0) TRACE(tile, 6, RT());
+#endif
 
     if (staged) {
         // Load every step of the range into registers and zero the region.
@@ -1340,7 +1357,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         // compiler sees a straight line and counts the loads' waits exactly.
         // The loads go through a buffer descriptor over the tile's words (<=
         // 16 KiB here): a lane past nvalid reads out of range and gets 0.
-        const uint32_t tile_bytes = (uint32_t)((uniform64(toff[nc]) - TW0) * 8);
+        const uint32_t tile_bytes = (uint32_t)((TW1 - TW0) * 8);
         const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
         uint64_t cache[kStageSteps];
@@ -1354,6 +1371,10 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         }
         for (uint32_t o = 16 * lane; o < kStageRegion; o += 16 * CAPNP_WAVE)
             *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
+#if PACK_PROF == 2
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0) TRACE(tile, 7, RT());
+#endif
         // pass 1: sizes and positions
         StepInfo si[kStageSteps];
 #if PACK_LEAN_STEP

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--tc", type=int, default=0)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--lib", default="")
+    ap.add_argument("--phases", action="store_true",
+                    help="PACK_PROF=2 build (make prof PROF=2): prelude / ranges / loads / pass 1")
     ap.add_argument("--trace", default="", help="save the per-tile timeline (.npy)")
     a = ap.parse_args()
     import torch
@@ -77,6 +79,9 @@ def main():
               f"windows/tile={T[:, 7].mean():.2f} pass1={us(0, 1):.1f}us "
               f"pub->offset={us(1, 2):.1f}us offset->end={us(2, 3):.1f}us "
               f"life={us(0, 3):.1f}us conc={(T[:, 3] - T[:, 0]).sum() / max(T[:, 3].max() - T[:, 0].min(), 1):.0f}")
+        if a.phases:  # PACK_PROF=2 build: slots 5-7 hold the prelude timeline
+            print(f"  prelude={us(0, 5):.1f}us ranges={us(5, 6):.1f}us loads={us(6, 7):.1f}us "
+                  f"pass1={us(7, 1):.1f}us")
     if a.trace:
         import numpy as np
         np.save(a.trace, trace.view(ntiles, 8).cpu().numpy())
