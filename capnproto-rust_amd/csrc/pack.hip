@@ -1317,6 +1317,33 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     const uint32_t q = (nc + kWaves - 1) / kWaves;
     const uint32_t wc0 = wave * q < nc ? wave * q : nc;
     const uint32_t wc1 = wc0 + q < nc ? wc0 + q : nc;
+#ifndef PACK_SPEC_LOAD
+#define PACK_SPEC_LOAD 1
+#endif
+    // The range's words go out to registers before its steps are known
+    // (PACK_SPEC_LOAD): step s loads the 64 words from the range start
+    // + 64 s.  That is the staged layout exactly when every chunk of the
+    // range is a whole number of steps (checked below; otherwise the steps
+    // are loaded again), and the load latency then overlaps the range walk.
+    const uint32_t tile_bytes = (uint32_t)((TW1 - TW0) * 8);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
+    uint64_t cache[kStageSteps];
+    // (messages with segment tables, GAP, have ragged segments: no speculation)
+    constexpr bool kSpec = PACK_SPEC_LOAD && !GAP;
+    if constexpr (kSpec) {
+        const uint32_t r0 = (uint32_t)(uniform64(toff[wc0]) - TW0);
+        const uint32_t r1 = (uint32_t)(uniform64(toff[wc1]) - TW0);
+#pragma unroll
+        for (uint32_t s = 0; s < kStageSteps; s++) {
+            const uint32_t w = r0 + 64 * s + lane;
+            const uint32_t vo = w < r1 ? w * 8u : 0x80000000u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vo, 0, 0);
+            cache[s] = ((uint64_t)v[1] << 32) | v[0];
+        }
+    }
+    uint64_t ragged = kSpec ? 0 : 63;  // OR of the range's chunk lengths: low bits set = load again
+
     uint64_t d_src = 0;
     uint32_t d_g = 0;  // tile-relative word of the step's lane 0
     uint32_t d_meta = 0;
@@ -1326,6 +1353,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         const uint64_t woff = uniform64(toff[ci]);
         const uint64_t len = uniform64(toff[ci + 1]) - woff;
         const uint32_t nst = (uint32_t)((len + 63) / 64);
+        ragged |= len;
         if constexpr (GAP) {
             const uint32_t g = uniform(sm.chunk_gap[ci]);
             gsum += (len == 0 && g) ? kGapSlack + 1 : g;
@@ -1357,17 +1385,15 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         // compiler sees a straight line and counts the loads' waits exactly.
         // The loads go through a buffer descriptor over the tile's words (<=
         // 16 KiB here): a lane past nvalid reads out of range and gets 0.
-        const uint32_t tile_bytes = (uint32_t)((TW1 - TW0) * 8);
-        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
-        uint64_t cache[kStageSteps];
+        if (__builtin_amdgcn_readfirstlane((int)(uint32_t)(ragged & 63u)) != 0) {
 #pragma unroll
-        for (uint32_t s = 0; s < kStageSteps; s++) {
-            const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)d_g, s);
-            const uint32_t nv = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s) & 127u;
-            const uint32_t vo = lane < nv ? (g + lane) * 8u : 0x80000000u;
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vo, 0, 0);
-            cache[s] = ((uint64_t)v[1] << 32) | v[0];
+            for (uint32_t s = 0; s < kStageSteps; s++) {
+                const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)d_g, s);
+                const uint32_t nv = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s) & 127u;
+                const uint32_t vo = lane < nv ? (g + lane) * 8u : 0x80000000u;
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vo, 0, 0);
+                cache[s] = ((uint64_t)v[1] << 32) | v[0];
+            }
         }
         for (uint32_t o = 16 * lane; o < kStageRegion; o += 16 * CAPNP_WAVE)
             *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
