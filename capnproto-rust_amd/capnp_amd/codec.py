@@ -135,7 +135,8 @@ class Context:
                                  consumed=None, stream=None):
         """Index-free UNPACK of chunks of any length (capnp_gpu_unpack_batch_resync):
         results identical to unpack_batch_into; blocks until done.  Returns
-        (fix passes, 1 if the batch went to the serial batch unpack)."""
+        (fix passes; serial: 1 the batch went to the serial batch unpack, 2 short chunks went
+        there directly, 3 only the chunks that failed their check were decoded serially)."""
         import ctypes as C
         n = in_byte_off.numel() - 1
         L = _lib.lib()

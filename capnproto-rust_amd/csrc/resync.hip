@@ -39,10 +39,10 @@
 //          kernel as a batch of ~120-word units (staged LDS tiles, coalesced
 //          stores).
 //
-// Any chunk that fails the check (a malformed stream, or a valid unit
-// followed by spare bytes in its range) makes the call re-decode the batch
-// with the serial batch unpack, so statuses, consumed counts and partial
-// output are exactly capnp_gpu_unpack_batch's.
+// A chunk that fails the check (a malformed stream, or a valid unit followed
+// by spare bytes in its range) is decoded serially as one unit of that same
+// launch, so its status, consumed count and partial output are exactly
+// capnp_gpu_unpack_batch's; the other chunks keep the block decode.
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
@@ -106,8 +106,8 @@ __device__ __forceinline__ void hop(const uint8_t* __restrict__ in, uint64_t& p,
     p = q > b ? b + 1 : q;
 }
 
-// Chunk of block `blk`: the last c with bstart[c] <= blk (empty chunks own
-// no blocks, so equal starts are skipped by taking the last one).
+// Chunk of block `blk`: the last c with bstart[c] <= blk (chunks without
+// blocks have equal starts, skipped by taking the last one).
 __device__ __forceinline__ uint64_t chunk_of(const uint64_t* __restrict__ bstart, uint64_t n,
                                              uint64_t blk) {
     uint64_t lo = 0, hi = n;  // bstart[lo] <= blk < bstart[hi]
@@ -134,11 +134,19 @@ struct Ws {
     size_t tmp_bytes;
 };
 
+// (a chunk with no packed bytes but a nonzero word count owns one empty
+// block: it fails its check and is decoded as a unit of its own, below)
 __global__ void __launch_bounds__(kThreads) k_count(const uint64_t* __restrict__ in_off, uint64_t n,
+                                                    const uint64_t* __restrict__ out_off,
                                                     uint64_t* __restrict__ nblk) {
     const uint64_t c = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (c > n) return;
-    nblk[c] = c == n ? 0 : (in_off[c + 1] - in_off[c] + kBlock - 1) / kBlock;
+    if (c == n) {
+        nblk[c] = 0;
+        return;
+    }
+    const uint64_t len = in_off[c + 1] - in_off[c];
+    nblk[c] = len == 0 ? (out_off[c + 1] != out_off[c] ? 1 : 0) : (len + kBlock - 1) / kBlock;
 }
 
 __global__ void __launch_bounds__(kThreads)
@@ -255,12 +263,17 @@ k_check(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __restr
 // Lane k writes block k's packed start and first output word, so the blocks
 // tile the batch's packed bytes and words contiguously (a block inside a
 // literal run is an empty unit; a chunk of 0 words keeps its blocks empty,
-// since read() of an empty buffer consumes nothing).
+// since read() of an empty buffer consumes nothing).  A chunk that failed its
+// check (ok[c] = 0: malformed, or spare bytes in its range) becomes one unit:
+// its blocks but the last are empty and the last spans the whole chunk, so
+// the batch unpack decodes it exactly as capnp_gpu_unpack_batch would (status,
+// consumed bytes and partial output; k_fail copies them to the chunk).
+// ok = nullptr: every chunk passed.
 __global__ void __launch_bounds__(kThreads)
 k_blocks(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __restrict__ out_off,
          const uint64_t* __restrict__ bstart, const uint64_t* __restrict__ exit,
-         const uint64_t* __restrict__ wbase, uint64_t* __restrict__ blk_in,
-         uint64_t* __restrict__ blk_out) {
+         const uint64_t* __restrict__ wbase, const int32_t* __restrict__ ok,
+         uint64_t* __restrict__ blk_in, uint64_t* __restrict__ blk_out) {
     const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     const uint64_t nb = bstart[n];
     if (k > nb) return;
@@ -271,8 +284,26 @@ k_blocks(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __rest
     }
     const uint64_t c = chunk_of(bstart, n, k);
     const uint64_t f = bstart[c];
+    if (ok && !ok[c]) {
+        blk_in[k] = in_off[c];
+        blk_out[k] = out_off[c];
+        return;
+    }
     blk_in[k] = k == f ? in_off[c] : exit[k - 1];
     blk_out[k] = out_off[c] + (out_off[c + 1] == out_off[c] ? 0 : wbase[k] - wbase[f]);
+}
+
+// Status and consumed bytes of the chunks that failed their check: those of
+// the unit that spans the chunk (its last block).
+__global__ void __launch_bounds__(kThreads)
+k_fail(uint64_t n, const uint64_t* __restrict__ bstart, const int32_t* __restrict__ ok,
+       const int32_t* __restrict__ blk_status, const uint64_t* __restrict__ blk_consumed,
+       int32_t* __restrict__ status, uint64_t* __restrict__ consumed) {
+    const uint64_t c = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (c >= n || ok[c]) return;
+    const uint64_t l = bstart[c + 1] - 1;  // (a failing chunk owns at least one block)
+    status[c] = blk_status[l];
+    if (consumed) consumed[c] = blk_consumed[l];
 }
 
 size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes) {
@@ -322,8 +353,9 @@ extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes) {
 
 // Blocking (the fix passes read a flag back).  On return, *passes = fix passes
 // run and *serial = 1 if the batch was re-decoded by the serial batch unpack
-// (a chunk failed its check), 2 if its chunks were short enough to go there
-// directly.
+// (the fix passes did not converge), 2 if its chunks were short enough to go
+// there directly, 3 if some chunks failed their check (those alone were
+// decoded serially, each as one unit of the block decode).
 extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d_in_off, uint64_t n,
                                           uint64_t total_bytes, uint64_t* d_out,
                                           const uint64_t* d_out_off, int32_t* d_status,
@@ -350,7 +382,7 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
         return hipErrorInvalidValue;
     int32_t hflags[2] = {0, 0};
     if ((e = hipMemsetAsync(w.flags, 0, 4 * (2 + kMaxPasses), s)) != hipSuccess) return e;
-    k_count<<<grid(n + 1), kThreads, 0, s>>>(d_in_off, n, w.nblk);
+    k_count<<<grid(n + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.nblk);
     size_t tb = w.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
@@ -392,20 +424,24 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
         if ((e = hipMemcpyAsync(&nb, w.bstart + n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess)
             return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        if (!hflags[1]) {
-            // every chunk resolved: decode the blocks as independent read
-            // units with the batch unpack (staged LDS tiles, coalesced stores)
-            uint64_t* blk_in = w.spec_exit;  // (spec state is dead by now)
-            uint64_t* blk_out = w.entry;
-            int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
-            k_blocks<<<grid(nbb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit,
-                                                        w.wbase, blk_in, blk_out);
-            if ((e = capnp_launch_unpack(d_in, blk_in, nb, 0, d_out, blk_out, blk_status, nullptr,
-                                         nullptr, s)) != hipSuccess)
-                return e;
+        // decode the blocks as independent read units with the batch unpack
+        // (staged LDS tiles, coalesced stores); a chunk that failed its check
+        // is one unit of its own, decoded serially in the same launch
+        uint64_t* blk_in = w.spec_exit;  // (spec state is dead by now)
+        uint64_t* blk_out = w.entry;
+        int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
+        uint64_t* blk_consumed = w.words;  // (dead after the wbase scan and the check)
+        k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit,
+                                                   w.wbase, w.ok, blk_in, blk_out);
+        if ((e = capnp_launch_unpack(d_in, blk_in, nb, 0, d_out, blk_out, blk_status,
+                                     hflags[1] ? blk_consumed : nullptr, nullptr, s)) != hipSuccess)
+            return e;
+        if (hflags[1]) {
+            if (serial) *serial = 3;
+            k_fail<<<grid(n), kThreads, 0, s>>>(n, w.bstart, w.ok, blk_status, blk_consumed,
+                                                d_status, d_consumed);
         }
-    }
-    if (hflags[1]) {
+    } else {
         if (serial) *serial = 1;
         if ((e = capnp_launch_unpack(d_in, d_in_off, n, 0, d_out, d_out_off, d_status, d_consumed,
                                      nullptr, s)) != hipSuccess)
@@ -579,7 +615,8 @@ extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t n
     const uint64_t h_in_off[2] = {0, nbytes};
     if ((e = hipMemcpyAsync(in_off, h_in_off, 16, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.flags, 0, 4 * (2 + kMaxPasses), s)) != hipSuccess) return e;
-    k_count<<<grid(n + 1), kThreads, 0, s>>>(in_off, n, w.nblk);
+    // (one chunk of nbytes > 0 bytes: k_count never reads its word offsets)
+    k_count<<<grid(n + 1), kThreads, 0, s>>>(in_off, n, in_off, w.nblk);
     size_t tb = w.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
@@ -630,7 +667,7 @@ extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t n
     uint64_t* blk_out = w.entry;
     int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
     k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(in_off, n, out_off, w.bstart, w.exit, w.wbase,
-                                               blk_in, blk_out);
+                                               nullptr, blk_in, blk_out);
     k_set_tail<<<1, 64, 0, s>>>(blk_in, nb, tail);
     if ((e = capnp_launch_unpack(d_in, blk_in, nb, 0, d_words, blk_out, blk_status, nullptr,
                                  nullptr, s)) != hipSuccess)

@@ -63,6 +63,9 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--serial-max-mib", type=int, default=64,
                     help="skip the serial unpack of single chunks above this size")
+    ap.add_argument("--corrupt", action="store_true",
+                    help="also time the batch with one chunk that fails its check "
+                         "(its word count one too many)")
     ap.add_argument("--workloads", default="config2_1GiB,config4_1GiB,one_chunk_16MiB,"
                                             "one_chunk_256MiB")
     a = ap.parse_args()
@@ -94,6 +97,19 @@ def main():
             rec.update({"serial_ms": round(t_se * 1e3, 3),
                         "serial_GiBps": round(ub / t_se / 2**30, 1),
                         "serial_ok": bool(torch.equal(back, words))})
+        if a.corrupt and n > 1:
+            bad = torch.arange(n + 1, device="cuda") > n // 2
+            offs2 = offs + bad.to(offs.dtype)  # chunk n/2 claims one word more
+            back2 = torch.zeros(words.numel() + 1, dtype=torch.int64, device="cuda")
+
+            def rs2():
+                info["r2"] = ctx.unpack_batch_resync_into(packed, poffs, offs2, back2, st)
+
+            t_rs2 = timed(rs2, a.reps)
+            nbad = int((st != 0).sum().item())
+            rec.update({"corrupt_resync_ms": round(t_rs2 * 1e3, 3), "corrupt_failed": nbad,
+                        "corrupt_serial": info["r2"][1]})
+            del back2, offs2
         print(json.dumps(rec), flush=True)
         del words, packed, back
         torch.cuda.empty_cache()

@@ -6,8 +6,8 @@ The resync decode walks each chunk's tag chain block by block from
 speculative starts, so the cases that matter are the ones where a
 speculative start lands badly: literal runs that span several blocks, zero
 runs, chunks shorter than one block, one chunk many blocks long, and
-malformed chunks (which must hand the batch to the serial unpack and come out
-with the oracle's statuses)."""
+malformed chunks (decoded serially, each on its own, and coming out with the
+oracle's statuses while the rest of the batch keeps the block decode)."""
 import random
 
 import numpy as np
@@ -133,9 +133,12 @@ def _rand_chunk(rng, n):
     return w
 
 
-def test_resync_malformed_goes_serial(ctx):
-    """Truncated, corrupted, mis-sized and over-long chunks: statuses,
-    consumed counts and the good chunks' words equal the oracle's."""
+def test_resync_malformed_chunks_alone_serial(ctx):
+    """Truncated, corrupted, mis-sized, over-long and byte-less chunks:
+    statuses, consumed counts and the good chunks' words equal the oracle's;
+    only the failing chunks leave the block decode (serial == 3), and the
+    whole output, partial words of failing chunks included, equals the serial
+    batch unpack's (capnp_gpu_unpack_batch)."""
     rng = random.Random(23)
     chunks, lens = [], []
     for _ in range(300):
@@ -143,7 +146,9 @@ def test_resync_malformed_goes_serial(ctx):
         st, k = O.pack(_rand_chunk(rng, n).tobytes())
         k = bytearray(k)
         r = rng.random()
-        if r < 0.15 and len(k) > 1:
+        if r < 0.02:
+            k = bytearray()  # no packed bytes for n > 0 words
+        elif r < 0.15 and len(k) > 1:
             k = k[:rng.randrange(len(k))]
         elif r < 0.3 and len(k):
             k[rng.randrange(len(k))] = rng.choice([0, 0xFF, rng.randrange(256)])
@@ -158,8 +163,13 @@ def test_resync_malformed_goes_serial(ctx):
     packed = np.frombuffer(b"".join(chunks), np.uint8)
     ref, rst, rused = O.unpack_batch(packed, in_offs, out_offs)
     g, st, used, passes, serial = resync(ctx, packed, in_offs, out_offs)
-    assert serial == 1
+    assert serial == 3
     assert np.array_equal(st, rst)
+    sw = torch.zeros(max(int(out_offs[-1]), 1), dtype=torch.int64, device="cuda")
+    sst = torch.empty(len(chunks), dtype=torch.int32, device="cuda")
+    ctx.unpack_batch_into(dev(packed), dev(in_offs), dev(out_offs), sw, sst)
+    assert np.array_equal(sst.cpu().numpy(), rst)
+    assert np.array_equal(g, sw.cpu().numpy().view(np.uint64)[:len(g)])
     ok = rst == 0
     assert ok.sum() > 50 and (~ok).sum() > 50
     assert np.array_equal(used, rused)  # error chunks too
