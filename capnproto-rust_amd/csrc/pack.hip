@@ -1323,26 +1323,39 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     // The range's words go out to registers before its steps are known
     // (PACK_SPEC_LOAD): step s loads the 64 words from the range start
     // + 64 s.  That is the staged layout exactly when every chunk of the
-    // range is a whole number of steps (checked below; otherwise the steps
-    // are loaded again), and the load latency then overlaps the range walk.
+    // range is a whole number of steps (checked in the walk; otherwise the
+    // steps are loaded again), and the load latency then overlaps the walk.
+    // Interleaved A/B on three boxes (us): config 2 583 / 584 vs 597 / 587 /
+    // 593, carsales 591 / 596 vs 610 / 609; equal chunks of 100 words pay
+    // 1.8-3 % (every step loaded twice).  PACK_SPEC_LOAD=2 speculates only
+    // when the range's first chunk is whole steps and the range is that many
+    // of it: ragged batches then pay ~1.5 % (code), config 2 gains the same.
     const uint32_t tile_bytes = (uint32_t)((TW1 - TW0) * 8);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
     uint64_t cache[kStageSteps];
     // (messages with segment tables, GAP, have ragged segments: no speculation)
     constexpr bool kSpec = PACK_SPEC_LOAD && !GAP;
-    if constexpr (kSpec) {
-        const uint32_t r0 = (uint32_t)(uniform64(toff[wc0]) - TW0);
+    uint64_t ragged = 63;  // OR of the range's chunk lengths (| 63: not speculated): low bits = load
+    if (kSpec && wc1 > wc0) {
+        // speculate when the range's chunks look whole steps: its first chunk
+        // is, and the range is as long as that many of it (a batch of equal
+        // chunks of 100 words loads once, after the walk, as before)
+        const uint64_t a = uniform64(toff[wc0]);
+        const uint64_t l0 = uniform64(toff[wc0 + 1]) - a;
+        const uint32_t r0 = (uint32_t)(a - TW0);
         const uint32_t r1 = (uint32_t)(uniform64(toff[wc1]) - TW0);
+        if (PACK_SPEC_LOAD == 1 || ((l0 & 63u) == 0 && (uint64_t)(r1 - r0) == l0 * (wc1 - wc0))) {
+            ragged = 0;
 #pragma unroll
-        for (uint32_t s = 0; s < kStageSteps; s++) {
-            const uint32_t w = r0 + 64 * s + lane;
-            const uint32_t vo = w < r1 ? w * 8u : 0x80000000u;
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vo, 0, 0);
-            cache[s] = ((uint64_t)v[1] << 32) | v[0];
+            for (uint32_t s = 0; s < kStageSteps; s++) {
+                const uint32_t w = r0 + 64 * s + lane;
+                const uint32_t vo = w < r1 ? w * 8u : 0x80000000u;
+                const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vo, 0, 0);
+                cache[s] = ((uint64_t)v[1] << 32) | v[0];
+            }
         }
     }
-    uint64_t ragged = kSpec ? 0 : 63;  // OR of the range's chunk lengths: low bits set = load again
 
     uint64_t d_src = 0;
     uint32_t d_g = 0;  // tile-relative word of the step's lane 0

@@ -1,5 +1,6 @@
 #!/bin/bash
-# Parity tests (optional) then interleaved A/B of build/abl variants vs the product library.
+# Parity tests (optional) then interleaved A/B of build/abl variants vs the product library
+# (workload[:chunk_words], e.g. config2:100).
 #   scripts/gpu_ab.sh <tag> <pytest targets or "-"> [workloads...]
 set -o pipefail
 TAG=${1:-ab}; T=${2:--}; shift 2 || true
@@ -12,6 +13,6 @@ if [ "$T" != "-" ]; then
 fi
 for w in "${WL[@]}"; do
   echo "== $w"
-  WL=$w timeout -k 10 300 python -u scripts/wt_ablate.py > gpurun_out/${TAG}_ab_$w.log 2>&1 || { tail -20 gpurun_out/${TAG}_ab_$w.log; exit 1; }
+  WL=${w%%:*} CW=$( [[ $w == *:* ]] && echo ${w##*:} || echo 128 ) timeout -k 10 300 python -u scripts/wt_ablate.py > gpurun_out/${TAG}_ab_$w.log 2>&1 || { tail -20 gpurun_out/${TAG}_ab_$w.log; exit 1; }
   cat gpurun_out/${TAG}_ab_$w.log
 done

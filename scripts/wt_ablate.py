@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved timing of library variants (pack, sync unpack, index-free
 unpack; PACK_WT_ABL builds give wrong output by design) on a bench workload
-(env WL, default config4), in one process:
+(env WL, default config4; env CW = words per chunk for the fixed-size
+workloads, default 128), in one process:
     python3 scripts/wt_ablate.py [lib.so ...]"""
 import ctypes as C
 import glob
@@ -34,7 +35,8 @@ def main():
     from capnp_amd import Context
     libs = sys.argv[1:] or ([os.path.join(ROOT, "capnproto-rust_amd/capnp_amd/libcapnp_packed.so")]
                             + sorted(glob.glob(os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_p_*.so"))))
-    args = bench.parse(["--workload", os.environ.get("WL", "config4")])
+    args = bench.parse(["--workload", os.environ.get("WL", "config4"),
+                        "--chunk-words", os.environ.get("CW", "128")])
     ctx = Context(0)
     dev = torch.device("cuda", 0)
     words, offs, n, _ = bench.make_workload(args, ctx, torch, dev, 0)
