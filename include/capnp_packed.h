@@ -185,9 +185,11 @@ capnp_status capnp_gpu_unpack_batch_sync(capnp_ctx* ctx, const uint8_t* d_packed
    bytes are split into fixed blocks decoded in parallel: a block's tag chain
    is walked speculatively from its first byte and resynchronised against
    its predecessor's exit (csrc/resync.hip).  A chunk whose chain does not
-   end exactly at its packed end with exactly its word count makes the call
-   re-decode the whole batch with capnp_gpu_unpack_batch, so every result is
-   that function's.  Blocking: synchronises `stream` (typically twice). */
+   end exactly at its packed end with exactly its word count is decoded
+   serially on its own (in the same launch as the resolved blocks), so its
+   status, consumed count and partial output are exactly what
+   capnp_gpu_unpack_batch gives it.  Blocking: synchronises `stream`
+   (typically twice). */
 capnp_status capnp_gpu_unpack_batch_resync(capnp_ctx* ctx, const uint8_t* d_packed,
                                            const uint64_t* d_in_byte_off, size_t nchunks,
                                            uint64_t* d_words, const uint64_t* d_out_word_off,

@@ -80,7 +80,9 @@ uint32_t capnp_unpack_tile_words(void);
 uint32_t capnp_pack_tile_words(void);
 
 /* Diagnostics of the last capnp_gpu_unpack_batch_resync on ctx: fix passes
- * run, and 1 if the batch went to the serial batch unpack. */
+ * run; serial = 1 if the batch went to the serial batch unpack (fix passes
+ * did not converge), 2 if its chunks were short enough to go there directly,
+ * 3 if only the chunks that failed their check were decoded serially. */
 capnp_status capnp_resync_stats(capnp_ctx* ctx, int* passes, int* serial);
 
 /* Packed bytes per lane of the index-free decode. */
