@@ -395,7 +395,7 @@ def main():
         }
         if e2e:
             line["e2e"] = e2e
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:  # (the CPU baseline is an N=1 figure)
             line["cpu_baseline"] = cpu_baseline(args, cpu_threads(args))
         print(json.dumps(line), flush=True)
     if world > 1:
