@@ -1416,6 +1416,14 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 #endif
         // pass 1: sizes and positions
         StepInfo si[kStageSteps];
+#ifndef PACK_HBITS
+#define PACK_HBITS 1  // 1: pass 2 rebuilds each step's head mask from bit s of one VGPR
+                      // (not the SGPR pair kept, i.e. spilled, from pass 1); 2: and its meta
+#endif
+        uint32_t hbits = 0;  // PACK_HBITS: bit s = this lane heads a record in step s
+        uint32_t kin_l = 0;  // PACK_HBITS 2: lane s = step s's carried-run words (meta >> 16)
+        (void)hbits;
+        (void)kin_l;
 #if PACK_LEAN_STEP
         {
             // (each step's chunk start and running size go to lane s of two
@@ -1428,6 +1436,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             for (uint32_t s = 0; s < kStageSteps; s++) {
                 const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
                 si[s].meta = meta;
+                (void)meta;
                 if ((meta >> 7) & 1) {
                     if constexpr (GAP) local += uniform(sm.chunk_gap[wc0 + (meta >> 9)]);
                     pk.begin(local);
@@ -1440,6 +1449,12 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                 si[s].tag = 0;
 #else
                 size_step_lean(pk, cache[s], meta & 127u, lane, si[s]);
+#endif
+#if PACK_HBITS
+                hbits |= mask_sel(si[s].H, 1u << s, 0u);
+#endif
+#if PACK_HBITS >= 2
+                kin_l = lane == s ? (si[s].meta >> 16) : kin_l;
 #endif
                 rec_oc = lane == s ? pk.o_c : rec_oc;
                 rec_sz = lane == s ? pk.total : rec_sz;
@@ -1511,15 +1526,23 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             uint32_t ext = 0;  // words the run open at the step end absorbs later
 #pragma unroll
             for (int s = (int)kStageSteps - 1; s >= 0; s--) {
-                const uint32_t meta = si[s].meta;
+                StepInfo sj = si[s];
+#if PACK_HBITS
+                sj.H = ballot64(((hbits >> s) & 1u) != 0);
+#endif
+#if PACK_HBITS >= 2
+                sj.meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s) |
+                          ((uint32_t)__builtin_amdgcn_readlane((int)kin_l, s) << 16);
+#endif
+                const uint32_t meta = sj.meta;
                 const uint32_t e = ((meta >> 8) & 1) ? 0u : ext;
-                emit_step<SYNC>(cache[s], si[s], e, lane, region_m1, sm.sel,
+                emit_step<SYNC>(cache[s], sj, e, lane, region_m1, sm.sel,
                           SYNC ? reinterpret_cast<uint8_t*>(sync + k0) : nullptr, t0,
                           (uint32_t)__builtin_amdgcn_readlane((int)d_g, s),
                           uniform(sm.chunk_oc[(wc0 + ((meta >> 9) & 63u)) & (kMaxTileChunks - 1)]));
                 // ext for step s-1: absorbed here, plus later if the run
                 // covered this whole step
-                ext = ((meta >> 7) & 1) ? 0u : (meta >> 16) + (si[s].H == 0 ? e : 0u);
+                ext = ((meta >> 7) & 1) ? 0u : (meta >> 16) + (sj.H == 0 ? e : 0u);
             }
         }
 #endif
