@@ -176,6 +176,14 @@ def test_resync_malformed_chunks_alone_serial(ctx):
     for c in np.nonzero(ok)[0]:
         a, b = int(out_offs[c]), int(out_offs[c + 1])
         assert np.array_equal(g[a:b], ref[a:b]), c
+    # the same batch without a consumed array (d_consumed = NULL)
+    w2 = torch.zeros(max(int(out_offs[-1]), 1), dtype=torch.int64, device="cuda")
+    st2 = torch.full((len(chunks),), -1, dtype=torch.int32, device="cuda")
+    passes2, serial2 = ctx.unpack_batch_resync_into(dev(packed), dev(in_offs), dev(out_offs),
+                                                    w2, st2)
+    assert serial2 == 3
+    assert np.array_equal(st2.cpu().numpy(), rst)
+    assert np.array_equal(w2.cpu().numpy().view(np.uint64)[:len(g)], g)
 
 
 def test_resync_config4_round_trip(ctx):
