@@ -128,7 +128,7 @@ def lib():
     L.capnp_gpu_write_messages.argtypes = [vp, vp, vp, vp, sz, sz, sz, vp, sz, vp, vp]
     L.capnp_gpu_read_messages.argtypes = [vp, vp, vp, sz, C.POINTER(ReaderOptionsC), i32, vp, sz,
                                           vp, vp, sz, vp, vp, vp, vp]
-    L.capnp_gpu_read_flat_messages.argtypes = [vp, vp, vp, sz, C.POINTER(ReaderOptionsC), i32,
+    L.capnp_gpu_read_flat_messages.argtypes = [vp, vp, sz, vp, sz, C.POINTER(ReaderOptionsC), i32,
                                                vp, sz, vp, vp, vp, vp, vp]
     L.capnp_packed_write_message.argtypes = [vp, vp, vp, u32, vp, sz, C.POINTER(C.c_size_t)]
     L.capnp_packed_read_message.argtypes = [vp, vp, sz, C.POINTER(ReaderOptionsC), i32, vp, sz,

@@ -197,27 +197,41 @@ class Context:
         total = int(mo[-1].item())
         return out[:total], mo
 
-    def read_messages(self, packed, msg_byte_off, words_cap, segs_cap, try_mode=False,
+    def read_messages(self, packed, msg_byte_off, words_cap=None, segs_cap=None, try_mode=False,
                       limit=8 * 1024 * 1024, stream=None):
         """serialize_packed::read_message for a batch of messages on the
         device (capnp_gpu_read_messages).  Returns (words, msg_word_off,
         seg_words, msg_seg_off, status, consumed) as device tensors; limit
-        None = no traversal limit."""
+        None = no traversal limit.  words_cap / segs_cap None size the
+        outputs in two phases: a first guess, then exactly the totals the
+        library reports with CAPNP_E_BUFFER_NOT_LARGE_ENOUGH (a packed zero
+        run expands 2 bytes into up to 256 words, so no fixed ratio to the
+        packed size is safe)."""
         import torch
         nmsg = msg_byte_off.numel() - 1
         dev = msg_byte_off.device
-        words = torch.empty(max(words_cap, 1), dtype=torch.int64, device=dev)
+        wc = int(words_cap) if words_cap is not None else \
+            int(msg_byte_off[-1].item() - msg_byte_off[0].item()) + 64 if nmsg else 1
+        sc = int(segs_cap) if segs_cap is not None else 4 * max(nmsg, 1)
         mwo = torch.empty(nmsg + 1, dtype=torch.int64, device=dev)
-        segs = torch.empty(max(segs_cap, 1), dtype=torch.int64, device=dev)
         mso = torch.empty(nmsg + 1, dtype=torch.int64, device=dev)
         status = torch.empty(max(nmsg, 1), dtype=torch.int32, device=dev)
         consumed = torch.empty(max(nmsg, 1), dtype=torch.int64, device=dev)
         o = _lib.ReaderOptionsC(int(limit or 0), 1 if limit is not None else 0, 64)
-        st = _lib.lib().capnp_gpu_read_messages(self._h, _ptr(packed), _ptr(msg_byte_off), nmsg,
-                                                C.byref(o), int(bool(try_mode)), _ptr(words),
-                                                int(words_cap), _ptr(mwo), _ptr(segs),
-                                                int(segs_cap), _ptr(mso), _ptr(status),
-                                                _ptr(consumed), self._stream(stream))
+        for phase in range(2):
+            words = torch.empty(max(wc, 1), dtype=torch.int64, device=dev)
+            segs = torch.empty(max(sc, 1), dtype=torch.int64, device=dev)
+            st = _lib.lib().capnp_gpu_read_messages(
+                self._h, _ptr(packed), _ptr(msg_byte_off), nmsg, C.byref(o),
+                int(bool(try_mode)), _ptr(words), wc, _ptr(mwo), _ptr(segs), sc, _ptr(mso),
+                _ptr(status), _ptr(consumed), self._stream(stream))
+            if st == 9 and phase == 0 and (words_cap is None or segs_cap is None):
+                need_w, need_s = int(mwo[nmsg].item()), int(mso[nmsg].item())
+                if (need_w > wc and words_cap is not None) or (need_s > sc and segs_cap is not None):
+                    break  # a caller-given capacity is too small: report it
+                wc, sc = max(wc, need_w), max(sc, need_s)
+                continue
+            break
         _check(st, self._h)
         return words, mwo, segs, mso, status[:nmsg], consumed[:nmsg]
 
@@ -226,7 +240,10 @@ class Context:
         (capnp_gpu_find_messages).  -> (offs int64 device tensor of nmsg + 1
         entries, nmsg): messages [offs[k], offs[k+1]) read completely;
         offs[nmsg] is where the next try_read_message starts (== nbytes: a
-        clean end)."""
+        clean end).  At most max_msgs are returned (default nbytes // 8 + 1);
+        nmsg == max_msgs with offs[nmsg] < nbytes means the walk stopped at
+        the cap and goes on from offs[nmsg] (a packed message can be as short
+        as 2 bytes, so the default does not cover every stream)."""
         import torch
         nb = int(packed.numel() if nbytes is None else nbytes)
         cap = int(max_msgs if max_msgs is not None else nb // 8 + 1)
@@ -237,40 +254,67 @@ class Context:
         _check(st, self._h)
         return offs[:n.value + 1], n.value
 
-    def read_message_stream(self, packed, limit=8 * 1024 * 1024, stream=None):
-        """serialize_packed::try_read_message in a loop over one device
-        stream until it returns None or fails (serialize.rs:310-325).
-        -> (messages, end): messages = list of (segment word arrays as device
-        tensors, consumed bytes) in stream order; end = CAPNP_NONE (1) after
-        a clean end, else the status of the try_read_message that failed."""
-        import torch
-        nb = int(packed.numel())
-        offs, n = self.find_messages(packed, nb, stream=stream)
-        stop = int(offs[n].item())
-        ranges = offs if stop == nb else torch.cat(
-            [offs, torch.tensor([nb], dtype=torch.int64, device=offs.device)])
+    def _read_ranges(self, packed, ranges, limit, stream):
+        """read_messages in try mode over byte ranges of `packed` -> (list of
+        (segments, consumed) up to the first failing message, its status or
+        0 when every one read)."""
         m = ranges.numel() - 1
-        if m == 0:
-            return [], 1
-        words_cap, segs_cap = nb * 64 // 8 + 64, m * 512
         words, mwo, segs, mso, status, consumed = self.read_messages(
-            packed, ranges, words_cap, segs_cap, try_mode=True, limit=limit, stream=stream)
+            packed, ranges, try_mode=True, limit=limit, stream=stream)
         st = status.cpu().tolist()
         mwo_h, mso_h = mwo.cpu().tolist(), mso.cpu().tolist()
         seg_h = segs.cpu().numpy().view(np.uint64) if segs.numel() else np.zeros(0, np.uint64)
         cons = consumed.cpu().tolist()
-        out, end = [], 1
+        out = []
         for k in range(m):
             if st[k] != 0:
-                end = st[k]
-                break
+                return out, st[k]
             a, p = mwo_h[k], []
             for j in range(mso_h[k], mso_h[k + 1]):
                 ln = int(seg_h[j]) & 0xFFFFFFFF
                 p.append(words[a:a + ln])
                 a += ln
             out.append((p, cons[k]))
-        return out, end
+        return out, 0
+
+    def read_message_stream(self, packed, limit=8 * 1024 * 1024, stream=None, max_msgs=None):
+        """serialize_packed::try_read_message in a loop over one device
+        stream until it returns None or fails (serialize.rs:310-325).
+        -> (messages, end): messages = list of (segment word arrays as device
+        tensors, consumed bytes) in stream order; end = CAPNP_NONE (1) after
+        a clean end, else the status of the try_read_message that failed.
+        Discovery runs in rounds of at most `max_msgs` messages (default
+        bytes // 8 + 1); a round stopped by its cap continues where it
+        stopped, and where the walk stops early the next message is read as
+        the loop's next try_read_message, which fails as the reference does or
+        succeeds and the loop goes on after it."""
+        import torch
+        nb = int(packed.numel())
+        out, start = [], 0
+        while start < nb:
+            view = packed[start:]
+            rest = nb - start
+            cap = int(max_msgs) if max_msgs is not None else rest // 8 + 1
+            offs, n = self.find_messages(view, rest, max_msgs=cap, stream=stream)
+            stop = int(offs[n].item())
+            if n:
+                msgs, bad = self._read_ranges(view, offs, limit, stream)
+                out += msgs
+                if bad:
+                    return out, bad
+            if stop >= rest:
+                break
+            if n == cap:  # the round's cap, not the stream, stopped the walk
+                start += stop
+                continue
+            # the walk stopped at `stop`: one try_read_message from there
+            tail = torch.tensor([stop, rest], dtype=torch.int64, device=offs.device)
+            msgs, bad = self._read_ranges(view, tail, limit, stream)
+            if bad:
+                return out, bad
+            out += msgs
+            start += stop + int(msgs[0][1])
+        return out, 1
 
     def read_flat_messages(self, buf, slice_off, segs_cap=None, no_alloc=False,
                            limit=8 * 1024 * 1024, stream=None):
@@ -283,19 +327,14 @@ class Context:
         `seg_words_u32`).  limit None = no traversal limit.  segs_cap None
         sizes the segment array in two phases: one entry per message first,
         then exactly msg_seg_off[nmsg] on CAPNP_E_BUFFER_NOT_LARGE_ENOUGH.
-        slice_off must be non-decreasing and end within buf (checked here,
-        CapnpError 64 otherwise)."""
+        slice_off must be non-decreasing and end within buf (checked by the
+        library on the device, CapnpError 64 otherwise)."""
         import torch
         if buf.dtype != torch.uint8 or buf.dim() != 1 or not buf.is_contiguous():
             raise CapnpError(64, "buf must be a contiguous 1-D uint8 tensor")
         nmsg = slice_off.numel() - 1
         dev = slice_off.device
         slice_off = slice_off.to(torch.int64).contiguous()
-        if nmsg > 0:
-            bad = (slice_off[1:] < slice_off[:-1]).any() | (slice_off[0] < 0) \
-                | (slice_off[-1] > buf.numel())
-            if bool(bad):
-                raise CapnpError(64, "slice_off must be non-decreasing and within buf")
         mso = torch.empty(nmsg + 1, dtype=torch.int64, device=dev)
         status = torch.empty(max(nmsg, 1), dtype=torch.int32, device=dev)
         body_off = torch.empty(max(nmsg, 1), dtype=torch.int64, device=dev)
@@ -305,7 +344,8 @@ class Context:
         for phase in range(2):
             segs = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
             st = _lib.lib().capnp_gpu_read_flat_messages(
-                self._h, _ptr(buf), _ptr(slice_off), nmsg, C.byref(o), int(bool(no_alloc)),
+                self._h, _ptr(buf), buf.numel(), _ptr(slice_off), nmsg, C.byref(o),
+                int(bool(no_alloc)),
                 _ptr(segs), cap, _ptr(mso), _ptr(status), _ptr(body_off), _ptr(consumed),
                 self._stream(stream))
             if st == 9 and segs_cap is None and phase == 0:

@@ -72,22 +72,33 @@ class SliceRead:
 class BufReader:
     """std::io::BufReader over a raw reader (`.read(n) -> bytes`, b"" at the
     end): fill_buf() returns the current buffer of up to `capacity` bytes,
-    reading the next one only once it is consumed."""
+    reading the next one only once it is consumed.  `unread(bufs)` puts
+    whole buffers back in front (in order), so _refilling can look ahead and
+    still leave the reader exactly where the reference's PackedRead would."""
 
     def __init__(self, raw, capacity=8192):
         self.raw = raw
         self.capacity = capacity
         self.buf = b""
         self.pos = 0
+        self.back = []  # buffers put back by unread, next first
 
     def fill_buf(self):
         if self.pos >= len(self.buf):
-            self.buf = bytes(self.raw.read(self.capacity))
+            self.buf = self.back.pop() if self.back else bytes(self.raw.read(self.capacity))
             self.pos = 0
         return memoryview(self.buf)[self.pos:]
 
     def consume(self, n):
         self.pos = min(self.pos + n, len(self.buf))
+
+    def unread(self, bufs):
+        """Puts `bufs` back; the current buffer's unconsumed rest follows them."""
+        rest = self.buf[self.pos:]
+        if rest:
+            self.back.append(rest)
+        self.back.extend(reversed([b for b in bufs if b]))
+        self.buf, self.pos = b"", 0
 
 
 # statuses that mean "the unit ran past the bytes in hand"
@@ -97,23 +108,66 @@ _NEEDS_MORE = (2, 4, 5)  # PrematureEndOfPackedInput, FailedToFill, PrematureEnd
 def _refilling(r, attempt):
     """Runs attempt(data) on the reader's current buffer; while it fails for
     lack of input and the reader has more, consumes that buffer (the
-    reference's refresh_buffer!) and retries over everything seen so far.
-    On success consumes exactly the bytes used: `attempt` returns (status,
-    used, result)."""
-    seen = b""
+    reference's refresh_buffer!, serialize_packed.rs:59-74) and retries over
+    everything seen so far.  On success consumes exactly the bytes used:
+    `attempt` returns (status, used, result).
+
+    The reference streams, so the result is the outcome at the first buffer
+    boundary where the unit stops needing input.  Retrying at every boundary
+    re-decodes everything seen each time (O(k^2) for a unit spanning k
+    buffers); with a reader that can put buffers back (`unread`) the retries
+    happen only once the bytes in hand have doubled, and the first boundary
+    whose outcome is final is then found by bisection over the buffers taken
+    since the last retry (a decode is left to right, so once the outcome over
+    a prefix is final it is the same over every longer prefix); the buffers
+    past that boundary are put back."""
+    bufs = []           # buffers taken so far; all consumed but maybe the last
+    plen = [0]          # plen[j] = bytes in bufs[:j]
+    lookahead = hasattr(r, "unread")
+    tried = 0           # the outcome over bufs[:tried] is known to need more
+    last = None
     while True:
         cur = bytes(r.fill_buf())
-        data = seen + cur
-        st, used, res = attempt(data)
-        if st in _NEEDS_MORE and len(cur) > 0:
+        if not cur:  # the reader has nothing more (or was empty at entry)
+            if not bufs:
+                st, used, res = attempt(b"")
+                return st, res
+            if len(bufs) == tried:
+                return last  # the failure stands over all the bytes seen, all consumed
+            j, cur_taken = len(bufs), True
+            st, used, res = attempt(b"".join(bufs))
+            if st in _NEEDS_MORE:
+                return st, res
+            break
+        bufs.append(cur)
+        plen.append(plen[-1] + len(cur))
+        j = len(bufs)
+        if lookahead and tried and plen[j] < 2 * plen[tried]:
+            r.consume(len(cur))  # not worth a retry yet: take the next buffer too
+            continue
+        st, used, res = attempt(b"".join(bufs))
+        if st in _NEEDS_MORE:
             r.consume(len(cur))
-            if len(r.fill_buf()) > 0:
-                seen = data
-                continue
-            return st, res  # nothing more: the failure stands over all the bytes seen
-        if st == _lib.OK:
-            r.consume(used - len(seen))
-        return st, res
+            tried, last = j, (st, res)
+            continue
+        cur_taken = False
+        break
+    # the outcome over bufs[:j] is final; the reference stopped at the first
+    # such boundary in (tried, j], with that boundary's buffer current
+    lo, hi = tried, j
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        s2, u2, r2 = attempt(b"".join(bufs[:mid]))
+        if s2 in _NEEDS_MORE:
+            lo = mid
+        else:
+            hi, st, used, res = mid, s2, u2, r2
+    if cur_taken or hi < j:
+        r.unread(bufs[hi - 1:j] if cur_taken else bufs[hi - 1:j - 1])
+        r.fill_buf()
+    if st == _lib.OK:
+        r.consume(used - plen[hi - 1])
+    return st, res
 
 
 class OwnedSegments:

@@ -101,18 +101,24 @@ class PackedRead:
         self.inner = inner
         self.ctx = ctx or default_context()
         self._err = None
+        self._extra = b""  # bytes an inner reader returned beyond what was asked
 
         def read_cb(_user, buf, n):
-            try:
-                r = self.inner.read(n)
-            except Exception as e:
-                self._err = e
-                return -2
-            if r is None:
-                return _lib.IO_PENDING
-            r = bytes(r)
-            C.memmove(buf, r, len(r))
-            return len(r)
+            if self._extra:
+                r = self._extra
+            else:
+                try:
+                    r = self.inner.read(n)
+                except Exception as e:
+                    self._err = e
+                    return -2
+                if r is None:
+                    return _lib.IO_PENDING
+                r = bytes(r)
+            # never more than n into the adaptor's n-byte staging slot
+            self._extra = r[n:]
+            C.memmove(buf, r, min(len(r), n))
+            return min(len(r), n)
 
         self._cb = _lib.READ_FN(read_cb)
         self._h = _lib.lib().capnp_packed_reader_new(self.ctx.handle, self._cb, None)

@@ -84,6 +84,9 @@ extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t n
                                                  uint64_t* nmsg, int* clean, void* d_ws,
                                                  size_t ws_bytes, hipStream_t s,
                                                  uint64_t* words_needed);
+extern "C" hipError_t capnp_resync_prefix(const uint8_t* d_in, uint64_t nbytes, void* d_ws,
+                                          size_t ws_bytes, hipStream_t s, uint64_t* bytes,
+                                          uint64_t* words);
 extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d_in_off, uint64_t n,
                                           uint64_t total_bytes, uint64_t* d_out,
                                           const uint64_t* d_out_off, int32_t* d_status,
@@ -133,8 +136,30 @@ struct capnp_ctx {
     uint8_t* d_stream_words = nullptr;  // message discovery: the stream decoded to words
     size_t stream_words_cap = 0;
     int resync_passes = 0, resync_serial = 0;  // last capnp_gpu_unpack_batch_resync
+    uint32_t* d_bad = nullptr;  // offset validation flag (check_offsets)
+    uint32_t* h_bad = nullptr;  // pinned copy
     std::string err;
 };
+
+namespace {
+
+// Offset-array validation for the synchronising entry points: off[0..n] must
+// be non-decreasing and off[n] <= limit.  A kernel handed backwards offsets
+// would read or write outside the caller's buffers (a chunk of "negative"
+// length), so these calls return CAPNP_E_INVALID_ARGUMENT before any kernel
+// touches the data.  (The reference takes slices, which cannot be backwards:
+// serialize.rs:53-97, serialize_packed.rs:300-304.)
+__global__ void __launch_bounds__(256) k_check_offsets(const uint64_t* __restrict__ off,
+                                                       uint64_t n, uint64_t limit,
+                                                       uint32_t* __restrict__ bad) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t a = off[i], b = off[i + 1];
+        if (b < a || b > limit) atomicOr(bad, 1u);  // (vector atomic, rare)
+    }
+}
+
+}  // namespace
 
 namespace {
 
@@ -195,6 +220,40 @@ capnp_status ensure_stage(capnp_ctx* ctx, size_t bytes) {
     return ensure_buf(ctx, &ctx->d_stage, &ctx->stage_cap, bytes);
 }
 
+// Enqueues the checks of `arrays` (device offset arrays of n + 1 entries with
+// their limits) on `s`, copies the verdict to the pinned flag and waits for
+// it.  CAPNP_OK, CAPNP_E_INVALID_ARGUMENT or a HIP error.
+struct OffCheck {
+    const uint64_t* off;
+    size_t n;
+    uint64_t limit;
+};
+// With wait == false the verdict is only enqueued: the caller synchronises
+// `s` itself (it has its own reason to) and then calls offsets_verdict().
+capnp_status offsets_verdict(capnp_ctx* ctx) {
+    if (*ctx->h_bad) {
+        ctx->err = "offset array not non-decreasing or past its buffer";
+        return CAPNP_E_INVALID_ARGUMENT;
+    }
+    return CAPNP_OK;
+}
+capnp_status check_offsets(capnp_ctx* ctx, hipStream_t s, std::initializer_list<OffCheck> arrays,
+                           bool wait = true) {
+    HIP_TRY(hipMemsetAsync(ctx->d_bad, 0, 4, s));
+    for (const OffCheck& a : arrays) {
+        if (a.n == 0 || !a.off) continue;
+        const uint64_t blocks = std::min<uint64_t>((a.n + 255) / 256, 2048);
+        hipLaunchKernelGGL(k_check_offsets, dim3((uint32_t)blocks), dim3(256), 0, s, a.off,
+                           (uint64_t)a.n, a.limit, ctx->d_bad);
+        HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->h_bad, ctx->d_bad, 4, hipMemcpyDeviceToHost, s));
+    if (!wait) return CAPNP_OK;
+    HIP_TRY(hipStreamSynchronize(s));
+    return offsets_verdict(ctx);
+}
+
+
 size_t state_bytes_for(size_t nchunks, uint32_t tc) {
     return capnp_pack_state_bytes(nchunks, tc) + 16;
 }
@@ -235,9 +294,13 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
     if (!d_out_off) return CAPNP_E_INVALID_ARGUMENT;
     if (tc == 0 && n > 0) {
         uint64_t wr[2];
+        capnp_status vst = check_offsets(ctx, s, {{d_off, n, ~0ull}}, false);
+        if (vst != CAPNP_OK) return vst;
         HIP_TRY(hipMemcpyAsync(&wr[0], d_off, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(&wr[1], d_off + n, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        vst = offsets_verdict(ctx);
+        if (vst != CAPNP_OK) return vst;
         if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
         const uint64_t words = wr[1] - wr[0];
         if (words && (words / n >= kWordTileMean || force_word_tiles())) {
@@ -391,6 +454,8 @@ capnp_ctx* capnp_ctx_create(int device, capnp_status* status) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&ctx->d_frame, sizeof(FrameResult));
     if (e == hipSuccess) e = hipHostMalloc(&ctx->h_frame, sizeof(FrameResult), 0);
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_bad, 4);
+    if (e == hipSuccess) e = hipHostMalloc(&ctx->h_bad, 4, 0);
     if (e != hipSuccess) {
         if (status) *status = CAPNP_E_HIP;
         capnp_ctx_destroy(ctx);
@@ -409,6 +474,8 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (ctx->d_body) (void)hipFree(ctx->d_body);
     if (ctx->d_frame) (void)hipFree(ctx->d_frame);
     if (ctx->h_frame) (void)hipHostFree(ctx->h_frame);
+    if (ctx->d_bad) (void)hipFree(ctx->d_bad);
+    if (ctx->h_bad) (void)hipHostFree(ctx->h_bad);
     if (ctx->d_msg) (void)hipFree(ctx->d_msg);
     if (ctx->d_resync) (void)hipFree(ctx->d_resync);
     if (ctx->d_wt) (void)hipFree(ctx->d_wt);
@@ -480,9 +547,14 @@ static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
     if (tc == 0 && nchunks) {
         hipStream_t s = pick(ctx, stream);
         uint64_t wr[2];
+        capnp_status vst = check_offsets(
+            ctx, s, {{d_in_byte_off, nchunks, ~0ull}, {d_out_word_off, nchunks, ~0ull}}, false);
+        if (vst != CAPNP_OK) return vst;
         HIP_TRY(hipMemcpyAsync(&wr[0], d_out_word_off, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipMemcpyAsync(&wr[1], d_out_word_off + nchunks, 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
+        vst = offsets_verdict(ctx);
+        if (vst != CAPNP_OK) return vst;
         if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
         const uint64_t words = wr[1] - wr[0];
         const bool longc = words && (words / nchunks >= kWordTileMean || force_word_tiles());
@@ -586,9 +658,14 @@ static capnp_status unpack_resync_dev(capnp_ctx* ctx, const uint8_t* d_packed,
     ctx->resync_passes = ctx->resync_serial = 0;
     if (nchunks == 0) return CAPNP_OK;
     uint64_t ends[2];
+    capnp_status vst = check_offsets(
+        ctx, s, {{d_in_byte_off, nchunks, ~0ull}, {d_out_word_off, nchunks, ~0ull}}, false);
+    if (vst != CAPNP_OK) return vst;
     HIP_TRY(hipMemcpyAsync(&ends[0], d_in_byte_off, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipMemcpyAsync(&ends[1], d_in_byte_off + nchunks, 8, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    vst = offsets_verdict(ctx);
+    if (vst != CAPNP_OK) return vst;
     if (ends[1] < ends[0]) return CAPNP_E_INVALID_ARGUMENT;
     const size_t ws = capnp_resync_ws_bytes(nchunks, ends[1] - ends[0]);
     capnp_status st = ensure_buf(ctx, &ctx->d_resync, &ctx->resync_cap, ws);
@@ -899,6 +976,13 @@ capnp_status capnp_gpu_write_messages(capnp_ctx* ctx, const uint64_t* d_words,
         return CAPNP_OK;
     }
     if (total_segs < nmsg || (total_words && !d_words)) return CAPNP_E_INVALID_ARGUMENT;
+    {
+        // message m's segments [msg_seg_off[m], msg_seg_off[m+1]) within
+        // [0, total_segs]; segment offsets non-decreasing
+        capnp_status vst = check_offsets(
+            ctx, s, {{d_msg_seg_off, nmsg, (uint64_t)total_segs}, {d_seg_word_off, total_segs, ~0ull}});
+        if (vst != CAPNP_OK) return vst;
+    }
     // Gap path: the segments are packed in place as the chunks, each
     // message's first chunk preceded by a gap of its packed table's size, and
     // the tables are written into the gaps afterwards.  Messages without
@@ -981,6 +1065,10 @@ capnp_status capnp_gpu_read_messages(capnp_ctx* ctx, const uint8_t* d_packed,
         HIP_TRY(hipMemsetAsync(d_msg_word_off, 0, 8, s));
         HIP_TRY(hipMemsetAsync(d_msg_seg_off, 0, 8, s));
         return CAPNP_OK;
+    }
+    {
+        capnp_status vst = check_offsets(ctx, s, {{d_msg_byte_off, nmsg, ~0ull}});
+        if (vst != CAPNP_OK) return vst;
     }
     const capnp_reader_options o = opts ? *opts : capnp_default_reader_options();
     size_t scan_bytes = 0;
@@ -1082,7 +1170,26 @@ capnp_status capnp_gpu_find_messages(capnp_ctx* ctx, const uint8_t* d_packed, si
     return CAPNP_OK;
 }
 
-capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf,
+// Streaming reader support (stream_io.hip; not part of the public header):
+// the longest prefix of complete records of n host bytes, resolved on the
+// device (capnp_resync_prefix).
+capnp_status capnp_stream_complete_prefix(capnp_ctx* ctx, const uint8_t* host, size_t n,
+                                          uint64_t* bytes, uint64_t* words) {
+    if (!ctx || !bytes || !words || (n && !host)) return CAPNP_E_INVALID_ARGUMENT;
+    *bytes = *words = 0;
+    if (n == 0) return CAPNP_OK;
+    capnp_status st = ensure_stage(ctx, round16(n) + 64);
+    if (st != CAPNP_OK) return st;
+    const size_t ws = capnp_resync_ws_bytes(1, n) + 4096;
+    st = ensure_buf(ctx, &ctx->d_resync, &ctx->resync_cap, ws);
+    if (st != CAPNP_OK) return st;
+    hipStream_t s = ctx->stream;
+    HIP_TRY(hipMemcpyAsync(ctx->d_stage, host, n, hipMemcpyHostToDevice, s));
+    HIP_TRY(capnp_resync_prefix(ctx->d_stage, n, ctx->d_resync, ctx->resync_cap, s, bytes, words));
+    return CAPNP_OK;
+}
+
+capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf, size_t buf_len,
                                           const uint64_t* d_slice_off, size_t nmsg,
                                           const capnp_reader_options* opts, int no_alloc,
                                           uint32_t* d_seg_words, size_t segs_cap,
@@ -1096,6 +1203,11 @@ capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf,
     if (nmsg == 0) {
         HIP_TRY(hipMemsetAsync(d_msg_seg_off, 0, 8, s));
         return CAPNP_OK;
+    }
+    {
+        // slices [slice_off[m], slice_off[m+1]) inside d_buf[0, buf_len)
+        capnp_status vst = check_offsets(ctx, s, {{d_slice_off, nmsg, (uint64_t)buf_len}});
+        if (vst != CAPNP_OK) return vst;
     }
     const capnp_reader_options o = opts ? *opts : capnp_default_reader_options();
     size_t scan_bytes = 0;

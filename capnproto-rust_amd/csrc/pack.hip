@@ -39,6 +39,7 @@
 //   only known once the run ends, possibly several steps later; it is
 //   patched in LDS (the ring holds back the block that contains it).
 #include "common.h"
+#include <stdlib.h>
 #include "../../include/capnp_packed.h"
 
 #ifndef PACK_EMIT_SKIP0
@@ -1602,6 +1603,643 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     }
 }
 
+// ---------------------------------------------------------------------------
+// Lean chunk-tile pack kernel (the default for batches without gaps).
+//
+// The same tiles, wave ranges, look-back and copy-out as pack_kernel's staged
+// path, with the two passes rebuilt for fewer instructions per 64-word step.
+// pack_kernel's step issued ~158 VALU and ~109 SALU instructions per step
+// (profiles/r02i_config2_pmc_summary.txt: 332 M VALU, 229 M SALU per
+// 1 GiB launch): the scalar unit, one per CU and shared by its four SIMDs,
+// was ~75 % busy and the per-tile chain of dependent phases could not be
+// hidden.  Here:
+//   * pass 1 does everything that needs the step's head mask H while H is
+//     in scalar registers: byte positions (DPP scan), each head's run count
+//     within the step and whether its run reaches the step end, and the
+//     record sync index entries (written straight to memory, masked lanes
+//     through an out-of-range buffer offset, no exec-mask branches);
+//   * one 32-bit VGPR per step carries pass 1's result to pass 2:
+//     pos (13 bits, in the wave's region) | idx (9: the record assembly
+//     entry, the tag for a head, kSelCopy for a literal word inside a run)
+//     << 13 | run count (6) << 22 | reaches step end << 28 | no bytes << 29;
+//     the step's carried-run words and "no head" flag go to lane s of one
+//     more VGPR, so no mask stays live across the passes (no SGPR spills);
+//   * pass 2 is the record assembly and four LDS ORs under a single exec
+//     mask (lanes with no bytes skip them), with the run count of the head
+//     whose run crosses into later steps completed from those steps (ext).
+// Tiles whose ranges do not fit the staged steps (chunks longer than the
+// steps, or more chunks than steps) compute their chunk sizes with the
+// streaming size pass, take part in the look-back, and leave their bytes to
+// pack_ovf_kernel (as tiles whose staged bytes overflow their regions do).
+
+#ifndef LEAN_EXP
+#define LEAN_EXP 0  // diagnostic variants (1: no streaming fallback)
+#endif
+#ifndef LEAN_SCHED
+#define LEAN_SCHED 1  // scheduling barrier between steps
+#endif
+
+struct LeanCarry {
+    uint32_t type;   // run open at the step start: 0 none, 1 zero run, 2 literal run
+    uint32_t rem;    // words it may still absorb
+    uint32_t total;  // packed bytes of the chunk so far
+};
+
+constexpr uint32_t kInfoPosBits = 13;
+static_assert(kStageRegion + 16 <= (1u << kInfoPosBits), "region positions fit 13 bits");
+
+// Pass 1 of one step: the step's records sized and placed (chunk-relative
+// `c.total`, wave-region start of the chunk `oc`), returned packed into one
+// VGPR (see above); kin = words the carried run absorbs | no head << 8.
+__device__ __forceinline__ uint32_t lean_size_step(uint64_t w, uint32_t nvalid, uint32_t lane,
+                                                   LeanCarry& c, uint32_t oc, uint32_t& kin) {
+    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+    const uint32_t tag = word_tag_dot(lo, hi);
+    const uint32_t pop = __builtin_popcount(tag);
+    // lanes past nvalid hold zero words (out-of-range loads): no class
+    const bool valid = lane < nvalid;
+    const uint32_t pv = valid ? pop : 64u;
+    const uint64_t V = ballot64(valid);
+    const uint64_t Zm = ballot64(pv == 0);
+    const uint64_t Lm = ballot64(pop >= 7);
+    const uint64_t Fm = ballot64(pop == 8);
+    // words of the carried run's class at the step start, at most rem
+    uint32_t k = ctz64(~(c.type == 1 ? Zm : Lm));
+    k = k < c.rem ? k : c.rem;
+    k = c.type ? k : 0u;
+    const uint64_t AC = ballot64(lane < k);
+    const uint64_t Z2 = Zm & ~AC;
+    const uint64_t AZ = Z2 & (Z2 << 1);
+    const uint64_t L2 = Lm & ~AC;
+    const uint64_t F2 = Fm & ~AC;
+    const uint64_t filled = ((L2 ^ (L2 + F2)) & L2) | F2;
+    const uint64_t AF = filled & (filled << 1);
+    const uint64_t H = V & ~(AC | AZ | AF);
+    // record sizes and positions
+    const uint32_t hsize = 1u + pop + ((0x101u >> pop) & 1u);
+    const uint32_t size = mask_sel(H, hsize, tag == 0 ? 0u : 8u);
+    const uint32_t incl = wave_incl_scan(size);
+    const uint32_t prel = c.total + incl - size;  // chunk-relative
+    // a head's run: the words up to the next head (none: to the step end)
+    const uint64_t nxt = (H >> 1) >> lane;
+    const uint32_t dn = min(ffbl((uint32_t)nxt), ffbl((uint32_t)(nxt >> 32)) | 32u);
+    const uint32_t reach = dn > 63u ? 1u : 0u;
+    const uint32_t cnt = min(dn, __builtin_elementwise_sub_sat(nvalid, lane + 1u));
+    const uint32_t idx = mask_sel(H, tag, kSelCopy);
+    const uint32_t skip = size == 0 ? 1u : 0u;
+    uint32_t info = (oc + prel) | (idx << kInfoPosBits) | ((cnt & 63u) << 22) | (reach << 28) |
+                    (skip << 29);
+    // (materialised here: otherwise the compiler sinks the packing into pass
+    // 2 and keeps its parts live across the steps, spilling)
+    asm volatile("" : "+v"(info));
+    // the run open at the step end: the last head's, or the carried one when
+    // it covered the whole step
+    const uint32_t code = pv == 0 ? 1u : (pv == 8 ? 2u : 0u);
+    const uint32_t h = H ? 63u - (uint32_t)__builtin_clzll(H) : 0u;
+    const uint32_t th = (uint32_t)__builtin_amdgcn_readlane((int)code, h);
+    kin = k | (H ? 0u : 0x100u);
+    c.type = H ? th : c.type;
+    c.rem = H ? (th ? 192u + h : 0u) : c.rem - 64u;
+    c.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    return info;
+}
+
+// Pass 2 of one step: the records of the step ORed into the wave's zeroed
+// region (region_m1 = region - 1; see emit_step for the alignbyte placement).
+// ext = words the run open at the step end absorbs in later steps.
+// SYNC: every head writes the entries of the sync points its record covers
+// (as emit_step; oc = the chunk's region start, g = tile-relative word of
+// lane 0, t0 = the tile's first sync word, srs = the tile's entries).
+template <bool SYNC>
+__device__ __forceinline__ void lean_emit_step(uint64_t w, uint32_t info, uint32_t ext,
+                                               uint32_t lane, uint8_t* region_m1, const Sel8* sel,
+                                               __amdgpu_buffer_rsrc_t srs, uint32_t oc,
+                                               uint32_t g, uint32_t t0) {
+    if (info & (1u << 29)) return;  // no bytes (absorbed zero word, past the words)
+    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+    const uint32_t pos = info & ((1u << kInfoPosBits) - 1u);
+    const uint32_t idx = __builtin_amdgcn_ubfe(info, kInfoPosBits, 9);
+    const uint32_t cnt = __builtin_amdgcn_ubfe(info, 22, 6) +
+                         __builtin_amdgcn_ubfe(info, 28, 1) * ext;
+    const Sel8 se = sel[idx];
+    const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, se.s0) | (((cnt << 8) | idx) & sel_m(idx));
+    const uint32_t r1 = __builtin_amdgcn_perm(hi, lo, se.s1);
+    const uint32_t r2 = __builtin_amdgcn_perm(cnt, hi, sel_s2(idx));
+    const uint32_t s = 0u - pos;
+    const uint32_t e0 = __builtin_amdgcn_alignbyte(r0, 0u, s);
+    const uint32_t e1 = __builtin_amdgcn_alignbyte(r1, r0, s);
+    const uint32_t e2 = __builtin_amdgcn_alignbyte(r2, r1, s);
+    const uint32_t e3 = __builtin_amdgcn_alignbyte(0u, r2, s);
+    uint32_t* b32 = reinterpret_cast<uint32_t*>(__builtin_align_down(region_m1 + pos, 4));
+    __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if constexpr (SYNC) {
+        // sync points m = hw + d (d = (t0 - hw) mod kSyncWords, d <= cnt) of
+        // the record headed at tile word hw = g + lane; entry (m - t0) / 8
+        const uint32_t c = t0 - g;
+        const uint32_t d = (c - lane) & (kSyncWords - 1);
+        const uint32_t dh = idx < kSelCopy ? d : ~0u;
+        const uint32_t rel = pos - oc;
+        const uint32_t b = (lane + d - c) / (kSyncWords / 4u);
+        __builtin_amdgcn_raw_buffer_store_b32(rel | (d << 24), srs,
+                                              (int)(dh <= cnt ? b : 0x80000000u), 0, 0);
+        // (runs longer than kSyncWords words: rare)
+        if (dh < kSyncWords && dh + kSyncWords <= cnt) {  // (dh = ~0: not a head)
+#pragma clang loop unroll(disable) vectorize(disable)
+            for (uint32_t dd = d + kSyncWords, bb = b + 4; dd <= cnt; dd += kSyncWords, bb += 4)
+                __builtin_amdgcn_raw_buffer_store_b32(rel | (dd << 24), srs, (int)bb, 0, 0);
+        }
+    }
+}
+
+template <bool SYNC>
+__global__ void __launch_bounds__(kThreads, 8)
+pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
+                 uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
+                 uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts,
+                 uint64_t* __restrict__ gs, uint32_t* __restrict__ sync,
+                 uint8_t* __restrict__ ovf) {
+    __shared__ Smem<false> sm;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint64_t ntiles = gridDim.x;
+    const uint64_t tile = blockIdx.x;
+    LookbackArgs LA;
+    LA.ts = ts;
+    LA.gs = gs;
+    LA.ntiles = ntiles;
+    LA.in = in;
+    LA.chunk_off = chunk_off;
+    LA.nchunks = nchunks;
+    LA.tc = tc;
+    LA.gap = nullptr;
+    LA.wt = 0;
+    LA.wlo = LA.whi = LA.g0 = 0;
+    LA.map = nullptr;
+
+    const uint64_t c0 = tile * tc;
+    const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
+    const uint32_t nc = (uint32_t)(c1 - c0);
+    const uint64_t* __restrict__ toff = chunk_off + c0;
+    const uint64_t TW0 = uniform64(chunk_off[c0]);
+    const uint64_t TW1 = uniform64(chunk_off[c1]);
+    const uint64_t k0 = (TW0 + kSyncWords - 1) / kSyncWords;
+    const uint64_t k1 = (TW1 + kSyncWords - 1) / kSyncWords;
+    const uint32_t t0 = (uint32_t)(k0 * kSyncWords - TW0);
+    for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
+    for (uint32_t i = tid; i <= kSelCopy; i += kThreads) sm.sel[i] = kSel8Table.e[i];
+    uint8_t* region = sm.stage[wave];
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
+    uint8_t* const outa = out - mis;
+
+    // contiguous chunk ranges per wave; lane s describes step s of the range
+    const uint32_t q = (nc + kWaves - 1) / kWaves;
+    const uint32_t wc0 = wave * q < nc ? wave * q : nc;
+    const uint32_t wc1 = wc0 + q < nc ? wc0 + q : nc;
+    const uint32_t tile_bytes = (uint32_t)((TW1 - TW0) * 8);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
+    // speculative loads (see pack_kernel): step s = the 64 words from the
+    // range start + 64 s, the staged layout when every chunk is whole steps
+    uint64_t cache[kStageSteps];
+    uint64_t ragged = 63;
+    if (wc1 > wc0) {
+        const uint32_t r0 = (uint32_t)(uniform64(toff[wc0]) - TW0);
+        const uint32_t r1 = (uint32_t)(uniform64(toff[wc1]) - TW0);
+        ragged = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < kStageSteps; s++) {
+            const uint32_t w = r0 + 64 * s + lane;
+            const uint32_t vo = w < r1 ? w * 8u : 0x80000000u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vo, 0, 0);
+            cache[s] = ((uint64_t)v[1] << 32) | v[0];
+        }
+    }
+    uint32_t d_g = 0, d_meta = 0, nsteps = 0;
+    for (uint32_t ci = wc0; ci < wc1; ci++) {
+        const uint64_t woff = uniform64(toff[ci]);
+        const uint64_t len = uniform64(toff[ci + 1]) - woff;
+        const uint32_t nst = (uint32_t)((len + 63) / 64);
+        ragged |= len;
+        const uint32_t kk = lane - nsteps;
+        if (lane >= nsteps && kk < nst) {
+            const uint64_t rest = len - 64ull * kk;
+            d_g = (uint32_t)(woff + 64ull * kk - TW0);
+            d_meta = (uint32_t)(rest < 64 ? rest : 64) | ((kk == 0) << 7) |
+                     ((kk + 1 == nst) << 8) | ((ci - wc0) << 9);
+        }
+        nsteps += nst;
+    }
+    if (lane == 0) sm.wave_steps[wave] = nsteps;
+    __syncthreads();
+    bool staged = true;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) staged &= sm.wave_steps[w] <= kStageSteps;
+    staged = __builtin_amdgcn_readfirstlane((int)staged) != 0;
+
+    if (LEAN_EXP != 1 && !staged) {
+        // sizes by the streaming size pass, offsets by the look-back; the
+        // bytes come from pack_ovf_kernel
+        if constexpr (SYNC)
+            for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
+        run_streaming<MODE_SIZE>(in, toff, sm.chunk_size, sm.chunk_pos, nc, wave, lane, region,
+                                 sm.sel, outa, mis, out_cap, nullptr);
+        __syncthreads();
+        if (wave == 0) {
+            const uint64_t agg = scan_chunks(sm, nc, lane);
+            publish(LA, tile, agg, lane);
+            const uint64_t excl = lookback(LA, tile, agg, lane);
+            if (lane < nc) sm.chunk_pos[lane] += excl;
+            if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
+            if (lane == 0) ovf[tile] = 1;
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
+        return;
+    }
+
+    if (__builtin_amdgcn_readfirstlane((int)(uint32_t)(ragged & 63u)) != 0) {
+#pragma unroll
+        for (uint32_t s = 0; s < kStageSteps; s++) {
+            const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)d_g, s);
+            const uint32_t nv = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s) & 127u;
+            const uint32_t vo = lane < nv ? (g + lane) * 8u : 0x80000000u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vo, 0, 0);
+            cache[s] = ((uint64_t)v[1] << 32) | v[0];
+        }
+    }
+    for (uint32_t o = 16 * lane; o < kStageRegion; o += 16 * CAPNP_WAVE)
+        *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
+
+    // the tile's sync entries [k0, k1) as a buffer (out-of-range stores drop)
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+        SYNC ? sync + k0 : nullptr, 0, SYNC ? (int)((k1 - k0) * 4) : 0, 0x00020000);
+
+    // ---- pass 1: sizes, positions, run counts
+    uint32_t info[kStageSteps];
+    uint32_t kin_l = 0;  // lane s: step s's carried-run words | no head << 8
+    uint32_t rec_oc = 0;  // lane s: region start of step s's chunk
+    {
+        LeanCarry c{0, 0, 0};
+        uint32_t local = 0, oc = 0;
+        uint32_t rec_sz = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < kStageSteps; s++) {
+            const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
+            if ((meta >> 7) & 1) {
+                c.type = 0;
+                c.rem = 0;
+                c.total = 0;
+                oc = local;
+            }
+            uint32_t kin = 0;
+            info[s] = lean_size_step(cache[s], meta & 127u, lane, c, oc, kin);
+            kin_l = lane == s ? kin : kin_l;
+            rec_oc = lane == s ? oc : rec_oc;
+            rec_sz = lane == s ? c.total : rec_sz;
+            if ((meta >> 8) & 1) local += c.total;
+#if LEAN_SCHED
+            __builtin_amdgcn_sched_barrier(0);  // one step at a time: registers
+#endif
+        }
+        if (lane < kStageSteps && ((d_meta >> 8) & 1))
+            sm.chunk_size[wc0 + ((d_meta >> 9) & 63u)] = rec_sz;
+        if (lane == 0) sm.wave_bytes[wave] = local;
+    }
+    __syncthreads();
+    bool fits = true;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) fits &= sm.wave_bytes[w] <= kStageBytes;
+    fits = __builtin_amdgcn_readfirstlane((int)fits) != 0;
+    uint64_t agg = 0;
+    if (wave == 0) {
+        agg = scan_chunks32(sm, nc, lane);
+        publish(LA, tile, agg, lane);
+    }
+    // ---- pass 2: the bytes (the look-back loads are in flight)
+    if (fits) {
+        uint8_t* const region_m1 = region - 1;
+        uint32_t ext = 0;
+#pragma unroll
+        for (int s = (int)kStageSteps - 1; s >= 0; s--) {
+            const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
+            const uint32_t kin = (uint32_t)__builtin_amdgcn_readlane((int)kin_l, s);
+            const uint32_t e = ((meta >> 8) & 1) ? 0u : ext;
+            lean_emit_step<SYNC>(cache[s], info[s], e, lane, region_m1, sm.sel, srs,
+                                 (uint32_t)__builtin_amdgcn_readlane((int)rec_oc, s),
+                                 (uint32_t)__builtin_amdgcn_readlane((int)d_g, s), t0);
+            ext = ((meta >> 7) & 1) ? 0u : (kin & 0xFFu) + ((kin & 0x100u) ? e : 0u);
+#if LEAN_SCHED
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+    }
+    if (wave == 0) {
+        const uint64_t excl = lookback(LA, tile, agg, lane);
+        if (lane < nc) sm.chunk_pos[lane] += excl;
+        if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
+    if (fits) {
+        if (wc1 > wc0) {
+            const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
+            copy_out(region, outa, D0, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
+        }
+    } else {
+        // a range overflowed its region (adversarial input): the sizes and
+        // offsets stand; pack_ovf_kernel writes the bytes; no index entries
+        if constexpr (SYNC)
+            for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
+        if (tid == 0) ovf[tile] = 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Chunk-step pack kernel (pack_cs_kernel): batches whose chunks hold at most
+// 128 words (1 KiB segments: configs 2, 3, 5 and the carsales workload).
+//
+// A step is one whole chunk: lane l holds its words l and 64 + l, so the
+// step's masks are 128-bit (lo = words 0-63, hi = words 64-127) and, since a
+// run never crosses a write_all chunk (serialize_packed.rs:375-427 scan only
+// the chunk) and a 128-word chunk cannot reach the 255-word cap, there is no
+// run state carried between steps at all: no carry logic, no per-step chunk
+// bookkeeping, one scalar segmentation per 128 words.  Each wave owns up to
+// kCsSteps chunks of its tile.  Tiles with a longer chunk (or more chunks per
+// wave) take the streaming size pass and leave their bytes to
+// pack_ovf_kernel.
+constexpr uint32_t kCsSteps = 4;   // chunks (steps) per wave
+constexpr uint32_t kCsWords = 128; // words per step
+
+// 128-bit masks on the scalar unit: {lo, hi}.
+struct M128 {
+    uint64_t lo, hi;
+};
+__device__ __forceinline__ M128 shl1(M128 a) { return {a.lo << 1, (a.hi << 1) | (a.lo >> 63)}; }
+__device__ __forceinline__ M128 operator&(M128 a, M128 b) { return {a.lo & b.lo, a.hi & b.hi}; }
+__device__ __forceinline__ M128 operator|(M128 a, M128 b) { return {a.lo | b.lo, a.hi | b.hi}; }
+__device__ __forceinline__ M128 operator^(M128 a, M128 b) { return {a.lo ^ b.lo, a.hi ^ b.hi}; }
+__device__ __forceinline__ M128 andnot(M128 a, M128 b) { return {a.lo & ~b.lo, a.hi & ~b.hi}; }
+__device__ __forceinline__ M128 add128(M128 a, M128 b) {
+    const uint64_t lo = a.lo + b.lo;
+    return {lo, a.hi + b.hi + (lo < a.lo ? 1ull : 0ull)};
+}
+
+// Index of the lowest set bit of a 64-bit lane value, >= 64 if none.
+__device__ __forceinline__ uint32_t ffbl64(uint64_t x) {
+    return min(ffbl((uint32_t)x), ffbl((uint32_t)(x >> 32)) | 32u);
+}
+
+// info of one word: pos (13) | idx (9) << 13 | run count (7) << 22 | no bytes << 29
+constexpr uint32_t kCsSkip = 1u << 29;
+
+__device__ __forceinline__ uint32_t cs_info(uint32_t pos, uint32_t idx, uint32_t cnt,
+                                            uint32_t size) {
+    uint32_t info = pos | (idx << kInfoPosBits) | (cnt << 22) | (size == 0 ? kCsSkip : 0u);
+    asm volatile("" : "+v"(info));  // (materialised in pass 1: see lean_size_step)
+    return info;
+}
+
+// Pass 1 of one chunk of n <= 128 words (lo = word lane, hi = word 64 +
+// lane) placed at region position oc: both words' info; returns the chunk's
+// packed size.
+__device__ __forceinline__ uint32_t cs_size_step(uint64_t wlo, uint64_t whi, uint32_t n,
+                                                 uint32_t lane, uint32_t oc, uint32_t& ilo,
+                                                 uint32_t& ihi) {
+    const uint32_t tlo = word_tag_dot((uint32_t)wlo, (uint32_t)(wlo >> 32));
+    const uint32_t thi = word_tag_dot((uint32_t)whi, (uint32_t)(whi >> 32));
+    const uint32_t plo = __builtin_popcount(tlo), phi = __builtin_popcount(thi);
+    const bool vlo = lane < n, vhi = lane + 64u < n;
+    // (words past n are zero: out-of-range loads; only Z needs the bound)
+    const M128 V{ballot64(vlo), ballot64(vhi)};
+    const M128 Z{ballot64((vlo ? plo : 64u) == 0), ballot64((vhi ? phi : 64u) == 0)};
+    const M128 L{ballot64(plo >= 7), ballot64(phi >= 7)};
+    const M128 F{ballot64(plo == 8), ballot64(phi == 8)};
+    const M128 AZ = Z & shl1(Z);
+    const M128 filled = ((L ^ add128(L, F)) & L) | F;
+    const M128 AF = filled & shl1(filled);
+    const M128 H = andnot(V, AZ | AF);
+    const uint32_t hs_lo = 1u + plo + ((0x101u >> plo) & 1u);
+    const uint32_t hs_hi = 1u + phi + ((0x101u >> phi) & 1u);
+    const uint32_t slo = mask_sel(H.lo, hs_lo, tlo == 0 ? 0u : 8u);
+    const uint32_t shi = mask_sel(H.hi, hs_hi, thi == 0 ? 0u : 8u);
+    const uint32_t clo = wave_incl_scan(slo);
+    const uint32_t tot_lo = (uint32_t)__builtin_amdgcn_readlane((int)clo, 63);
+    const uint32_t chi = wave_incl_scan(shi);
+    // run counts: the words up to the next head within the chunk
+    const uint64_t nlo = (H.lo >> 1) >> lane;         // heads after word lane, in lo
+    const uint32_t dlo0 = ffbl64(nlo);
+    const uint32_t dlo1 = (63u - lane) + ffbl64(H.hi);  // the first head in hi
+    const uint32_t dlo = dlo0 < 64u ? dlo0 : dlo1;
+    const uint32_t dhi = ffbl64((H.hi >> 1) >> lane);
+    const uint32_t cnt_lo = min(dlo, __builtin_elementwise_sub_sat(n, lane + 1u));
+    const uint32_t cnt_hi = min(dhi, __builtin_elementwise_sub_sat(n, lane + 65u));
+    ilo = cs_info(oc + clo - slo, mask_sel(H.lo, tlo, kSelCopy), cnt_lo & 127u, slo);
+    ihi = cs_info(oc + tot_lo + chi - shi, mask_sel(H.hi, thi, kSelCopy), cnt_hi & 127u, shi);
+    return tot_lo + (uint32_t)__builtin_amdgcn_readlane((int)chi, 63);
+}
+
+// Pass 2 of one word (cs info layout): as lean_emit_step with no run
+// extension; SYNC entries from head lanes (hw = g + word of the chunk).
+template <bool SYNC>
+__device__ __forceinline__ void cs_emit_word(uint64_t w, uint32_t info, uint32_t lane,
+                                             uint8_t* region_m1, const Sel8* sel,
+                                             __amdgpu_buffer_rsrc_t srs, uint32_t oc, uint32_t g,
+                                             uint32_t t0) {
+    if (info & kCsSkip) return;
+    const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+    const uint32_t pos = info & ((1u << kInfoPosBits) - 1u);
+    const uint32_t idx = __builtin_amdgcn_ubfe(info, kInfoPosBits, 9);
+    const uint32_t cnt = __builtin_amdgcn_ubfe(info, 22, 7);
+    const Sel8 se = sel[idx];
+    const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, se.s0) | (((cnt << 8) | idx) & sel_m(idx));
+    const uint32_t r1 = __builtin_amdgcn_perm(hi, lo, se.s1);
+    const uint32_t r2 = __builtin_amdgcn_perm(cnt, hi, sel_s2(idx));
+    const uint32_t s = 0u - pos;
+    const uint32_t e0 = __builtin_amdgcn_alignbyte(r0, 0u, s);
+    const uint32_t e1 = __builtin_amdgcn_alignbyte(r1, r0, s);
+    const uint32_t e2 = __builtin_amdgcn_alignbyte(r2, r1, s);
+    const uint32_t e3 = __builtin_amdgcn_alignbyte(0u, r2, s);
+    uint32_t* b32 = reinterpret_cast<uint32_t*>(__builtin_align_down(region_m1 + pos, 4));
+    __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    if constexpr (SYNC) {
+        const uint32_t c = t0 - g;
+        const uint32_t d = (c - lane) & (kSyncWords - 1);
+        const uint32_t dh = idx < kSelCopy ? d : ~0u;
+        const uint32_t rel = pos - oc;
+        const uint32_t b = (lane + d - c) / (kSyncWords / 4u);
+        __builtin_amdgcn_raw_buffer_store_b32(rel | (d << 24), srs,
+                                              (int)(dh <= cnt ? b : 0x80000000u), 0, 0);
+        if (dh < kSyncWords && dh + kSyncWords <= cnt) {  // (dh = ~0: not a head)
+#pragma clang loop unroll(disable) vectorize(disable)
+            for (uint32_t dd = d + kSyncWords, bb = b + 4; dd <= cnt; dd += kSyncWords, bb += 4)
+                __builtin_amdgcn_raw_buffer_store_b32(rel | (dd << 24), srs, (int)bb, 0, 0);
+        }
+    }
+}
+
+template <bool SYNC>
+__global__ void __launch_bounds__(kThreads, 8)
+pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
+               uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
+               uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts,
+               uint64_t* __restrict__ gs, uint32_t* __restrict__ sync,
+               uint8_t* __restrict__ ovf) {
+    __shared__ Smem<false> sm;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint64_t tile = blockIdx.x;
+    const uint64_t c0 = tile * tc;
+    const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
+    const uint32_t nc = (uint32_t)(c1 - c0);
+    const uint64_t* __restrict__ toff = chunk_off + c0;
+    const uint64_t TW0 = uniform64(chunk_off[c0]);
+    const uint64_t TW1 = uniform64(chunk_off[c1]);
+    for (uint32_t i = tid; i <= kSelCopy; i += kThreads) sm.sel[i] = kSel8Table.e[i];
+    uint8_t* region = sm.stage[wave];
+
+    // wave w: chunks [wc0, wc1), one per step; lane s < kCsSteps + 1 holds
+    // the tile-relative word offset of chunk wc0 + s
+    const uint32_t q = (nc + kWaves - 1) / kWaves;
+    const uint32_t wc0 = wave * q < nc ? wave * q : nc;
+    const uint32_t wc1 = wc0 + q < nc ? wc0 + q : nc;
+    const uint32_t nw = wc1 - wc0;
+    const uint32_t d_off = lane < nw ? (uint32_t)(toff[wc0 + lane] - TW0) : 0u;
+    const uint32_t d_len = lane < nw ? (uint32_t)(toff[wc0 + lane + 1] - TW0) - d_off : 0u;
+    const bool ok = nw <= kCsSteps && ballot64(lane < nw && d_len > kCsWords) == 0;
+    if (lane == 0) sm.wave_steps[wave] = ok ? 0u : 1u;
+    const uint32_t tile_bytes = (uint32_t)((TW1 - TW0) * 8);
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
+    uint64_t clo[kCsSteps], chi[kCsSteps];
+#pragma unroll
+    for (uint32_t s = 0; s < kCsSteps; s++) {
+        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)d_off, s);
+        const uint32_t n = s < nw ? (uint32_t)__builtin_amdgcn_readlane((int)d_len, s) : 0u;
+        const uint32_t vlo = lane < n ? (a + lane) * 8u : 0x80000000u;
+        const uint32_t vhi = lane + 64u < n ? (a + lane + 64u) * 8u : 0x80000000u;
+        const auto x = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vlo, 0, 0);
+        const auto y = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vhi, 0, 0);
+        clo[s] = ((uint64_t)x[1] << 32) | x[0];
+        chi[s] = ((uint64_t)y[1] << 32) | y[0];
+    }
+    for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
+    __syncthreads();
+    bool staged = true;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) staged &= sm.wave_steps[w] == 0;
+    staged = __builtin_amdgcn_readfirstlane((int)staged) != 0;
+
+    LookbackArgs LA;
+    LA.ts = ts;
+    LA.gs = gs;
+    LA.ntiles = gridDim.x;
+    LA.in = in;
+    LA.chunk_off = chunk_off;
+    LA.nchunks = nchunks;
+    LA.tc = tc;
+    LA.gap = nullptr;
+    LA.wt = 0;
+    LA.wlo = LA.whi = LA.g0 = 0;
+    LA.map = nullptr;
+    const uint64_t k0 = (TW0 + kSyncWords - 1) / kSyncWords;
+    const uint64_t k1 = (TW1 + kSyncWords - 1) / kSyncWords;
+
+    if (!staged) {
+        // a chunk longer than a step: sizes by the streaming size pass,
+        // offsets by the look-back; the bytes come from pack_ovf_kernel
+        if constexpr (SYNC)
+            for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
+        run_streaming<MODE_SIZE>(in, toff, sm.chunk_size, sm.chunk_pos, nc, wave, lane, region,
+                                 sm.sel, out - mis, mis, out_cap, nullptr);
+        __syncthreads();
+        if (wave == 0) {
+            const uint64_t agg = scan_chunks(sm, nc, lane);
+            publish(LA, tile, agg, lane);
+            const uint64_t excl = lookback(LA, tile, agg, lane);
+            if (lane < nc) sm.chunk_pos[lane] += excl;
+            if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
+            if (lane == 0) ovf[tile] = 1;
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
+        return;
+    }
+
+    for (uint32_t o = 16 * lane; o < kStageRegion; o += 16 * CAPNP_WAVE)
+        *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
+
+    // ---- pass 1: sizes and positions
+    uint32_t ilo[kCsSteps], ihi[kCsSteps];
+    uint32_t rec_oc = 0;  // lane s: region start of chunk s
+    uint32_t local = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < kCsSteps; s++) {
+        const uint32_t n = s < nw ? (uint32_t)__builtin_amdgcn_readlane((int)d_len, s) : 0u;
+        const uint32_t sz = cs_size_step(clo[s], chi[s], n, lane, local, ilo[s], ihi[s]);
+        rec_oc = lane == s ? local : rec_oc;
+        if (lane == s && s < nw) sm.chunk_size[wc0 + s] = sz;
+        local += sz;
+#if LEAN_SCHED
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
+    if (lane == 0) sm.wave_bytes[wave] = local;
+    __syncthreads();
+    bool fits = true;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) fits &= sm.wave_bytes[w] <= kStageBytes;
+    fits = __builtin_amdgcn_readfirstlane((int)fits) != 0;
+    uint64_t agg = 0;
+    if (wave == 0) {
+        agg = scan_chunks32(sm, nc, lane);
+        publish(LA, tile, agg, lane);
+    }
+    // ---- pass 2: the bytes (the look-back loads are in flight)
+    if (fits) {
+        uint8_t* const region_m1 = region - 1;
+        const uint32_t t0 = (uint32_t)(k0 * kSyncWords - TW0);
+        const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+            SYNC ? sync + k0 : nullptr, 0, SYNC ? (int)((k1 - k0) * 4) : 0, 0x00020000);
+#pragma unroll
+        for (uint32_t s = 0; s < kCsSteps; s++) {
+            const uint32_t oc = (uint32_t)__builtin_amdgcn_readlane((int)rec_oc, s);
+            const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)d_off, s);
+            cs_emit_word<SYNC>(clo[s], ilo[s], lane, region_m1, sm.sel, srs, oc, g, t0);
+            cs_emit_word<SYNC>(chi[s], ihi[s], lane, region_m1, sm.sel, srs, oc, g + 64u, t0);
+#if LEAN_SCHED
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+    }
+    if (wave == 0) {
+        const uint64_t excl = lookback(LA, tile, agg, lane);
+        if (lane < nc) sm.chunk_pos[lane] += excl;
+        if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
+    if (fits) {
+        if (nw) {
+            const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
+            const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
+            copy_out(region, out - mis, D0, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
+        }
+    } else {
+        if constexpr (SYNC)
+            for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
+        if (tid == 0) ovf[tile] = 1;
+    }
+}
+
 // Tiles whose staged ranges overflowed (ovf[t] set by pack_kernel, after its
 // look-back wrote the chunks' offsets): the streaming path writes their
 // bytes at those offsets.  One lane per tile finds them; a few workgroups.
@@ -2013,6 +2651,24 @@ static dim3 pack_ovf_grid(uint64_t ntiles) {
     return dim3((uint32_t)(g < 1024 ? g : 1024));
 }
 
+// CAPNP_PACK_LEAN=0 selects pack_kernel for the chunk tiles (A/B builds).
+static bool pack_lean_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("CAPNP_PACK_LEAN");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
+// CAPNP_PACK_CS=0 leaves 128-word-chunk batches to pack_lean_kernel (A/B).
+static bool pack_cs_enabled() {
+    static const bool v = [] {
+        const char* e = getenv("CAPNP_PACK_CS");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_chunk_off,
                                         uint64_t nchunks, uint32_t tc, uint8_t* d_out,
                                         uint64_t out_cap, uint64_t* d_out_off,
@@ -2026,7 +2682,26 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_
     hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(nchunks, tc), stream);
     if (e != hipSuccess) return e;
     uint8_t* ovf = pack_ovf_flags(d_state, ntiles);
-    if (d_sync)
+    if (pack_cs_enabled() && tc <= kWaves * kCsSteps && tc * 2 > kWaves * kCsSteps) {
+        // chunks of at most 128 words (tc chosen for a mean of 65-128 words)
+        if (d_sync)
+            hipLaunchKernelGGL((pack_cs_kernel<true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
+                               stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
+                               d_state, d_state + ntiles, d_sync, ovf);
+        else
+            hipLaunchKernelGGL((pack_cs_kernel<false>), dim3((uint32_t)ntiles), dim3(kThreads),
+                               0, stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap,
+                               d_out_off, d_state, d_state + ntiles, d_sync, ovf);
+    } else if (pack_lean_enabled()) {
+        if (d_sync)
+            hipLaunchKernelGGL((pack_lean_kernel<true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
+                               stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
+                               d_state, d_state + ntiles, d_sync, ovf);
+        else
+            hipLaunchKernelGGL((pack_lean_kernel<false>), dim3((uint32_t)ntiles), dim3(kThreads),
+                               0, stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap,
+                               d_out_off, d_state, d_state + ntiles, d_sync, ovf);
+    } else if (d_sync)
         hipLaunchKernelGGL((pack_kernel<true, false>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
                            stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
                            d_state, d_state + ntiles, d_sync, nullptr, ovf);

@@ -580,6 +580,68 @@ k_msg_pos(const uint8_t* __restrict__ in, uint64_t nbytes, const uint64_t* __res
 
 }  // namespace
 
+// The longest prefix of complete records of nbytes packed bytes that may
+// end inside a record: *bytes = its packed length, *words = the words it
+// decodes to (the spec / fix / scan resolution above, then k_tail on the
+// last block).  Blocking.  The async stream reader uses it where its inner
+// reader pends or ends: capnp-futures' PackedRead hands out every complete
+// record before it waits or fails (capnp-futures/src/serialize_packed.rs:
+// 87-225).
+extern "C" hipError_t capnp_resync_prefix(const uint8_t* d_in, uint64_t nbytes, void* d_ws,
+                                          size_t ws_bytes, hipStream_t s, uint64_t* bytes,
+                                          uint64_t* words) {
+    *bytes = *words = 0;
+    if (nbytes == 0) return hipSuccess;
+    hipError_t e;
+    const uint64_t n = 1;
+    const uint64_t nbb = blocks_bound(n, nbytes);
+    Ws w;
+    uint8_t* base = (uint8_t*)(((uintptr_t)d_ws + 255) & ~uintptr_t(255));
+    size_t need = carve(&w, base, n, nbb, scan_tmp_bytes(nbb > 2 ? nbb : 2)) + (base - (uint8_t*)d_ws);
+    uint64_t* aux = (uint64_t*)(base + ((need - (base - (uint8_t*)d_ws) + 255) & ~size_t(255)));
+    need = (uint8_t*)(aux + 16) - (uint8_t*)d_ws;
+    if (need > ws_bytes) return hipErrorInvalidValue;
+    uint64_t* in_off = aux;      // [2]
+    uint64_t* tail = aux + 8;    // [2]
+    const uint64_t h_in_off[2] = {0, nbytes};
+    if ((e = hipMemcpyAsync(in_off, h_in_off, 16, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.flags, 0, 4 * (2 + kMaxPasses), s)) != hipSuccess) return e;
+    k_count<<<grid(n + 1), kThreads, 0, s>>>(in_off, n, in_off, w.nblk);
+    size_t tb = w.tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
+        hipSuccess)
+        return e;
+    k_spec<<<grid(nbb), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart, w.spec_exit,
+                                                   w.spec_words, w.exit, w.entry, w.words);
+    const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
+    for (int pass = 0; pass < kMaxPasses;) {
+        for (int i = 0; i < kPassBatch; i++, pass++)
+            k_fix<<<grid(ngroups), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart,
+                                                              w.spec_exit, w.spec_words, w.exit,
+                                                              w.entry, w.words, w.flags, pass);
+        int32_t last = 0;
+        if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
+            hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (!last) break;
+        if (pass >= kMaxPasses) return hipErrorNotReady;  // (not converged)
+    }
+    uint64_t nb = 0;
+    if ((e = hipMemcpyAsync(&nb, w.bstart + n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    tb = w.tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.words, w.wbase, (int)nb, s)) != hipSuccess)
+        return e;
+    k_tail<<<1, 64, 0, s>>>(d_in, nbytes, w.exit, w.wbase, nb, tail);
+    uint64_t htail[2] = {0, 0};
+    if ((e = hipMemcpyAsync(htail, tail, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    *bytes = htail[0];
+    *words = htail[1];
+    return hipSuccess;
+}
+
 // -> *nmsg complete messages with byte starts d_pos[0..nmsg) and
 // d_pos[nmsg] = where the walk stopped (the next message's start, or the
 // stream end); *clean = 1 if that is the end of the stream after the last

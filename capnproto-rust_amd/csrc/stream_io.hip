@@ -31,10 +31,12 @@
 // pulls more.  At the end of the stream with a partial record left the read
 // fails with PrematureEndOfFile (the async reader's UnexpectedEof, :109-114,
 // :164-168, :207-212, which capnp maps to PrematureEndOfFile, lib.rs:481-499).
-// Divergence (documented): the async reader hands out the head word of a
-// literal run whose raw words the stream then lacks before failing; here
-// the read that would return that word fails at once.  Any read covering the
-// truncated run fails in both.
+// A literal run whose raw words have not all arrived (the inner reader pends
+// or ends inside them) is handed out as the async reader's stages do: the
+// run's head word once its 10 bytes (tag, 8 bytes, count) are in
+// (BufferingWord -> DrainingBuffer, :139-185), then its raw bytes as they
+// come in (WritingPassthrough, :186-220: copied from the inner reader, no
+// transform), and UnexpectedEof if the stream ends first.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -43,6 +45,11 @@
 #include <vector>
 
 #include "../../include/capnp_packed.h"
+
+// capi.hip (internal): the longest prefix of complete records of n host
+// bytes, resolved on the device.
+extern "C" capnp_status capnp_stream_complete_prefix(capnp_ctx* ctx, const uint8_t* host,
+                                                     size_t n, uint64_t* bytes, uint64_t* words);
 
 namespace {
 
@@ -82,6 +89,7 @@ struct capnp_packed_reader {
     bool eof = false;
     std::vector<uint8_t> dec;  // decoded bytes not yet handed out
     size_t dp = 0;
+    size_t pass_rem = 0;       // raw bytes of a literal run still to pass through
 };
 
 namespace {
@@ -151,8 +159,8 @@ capnp_status reader_pull(capnp_packed_reader* r) {
 // A stream decodes at most 10 input bytes per output word (tag, 8 bytes,
 // count), so only that much of the staged input is handed to the kernel.
 capnp_status reader_unit(capnp_packed_reader* r, size_t nw, std::vector<uint8_t>& out,
-                         size_t* used, int32_t* status) {
-    const size_t avail = r->in.size() - r->ip;
+                         size_t* used, int32_t* status, size_t max_bytes = ~size_t(0)) {
+    const size_t avail = std::min(r->in.size() - r->ip, max_bytes);
     const size_t take = std::min(avail, nw * 10 + 16);
     out.resize(nw * 8);
     uint64_t io[2] = {0, take}, oo[2] = {0, nw};
@@ -162,6 +170,52 @@ capnp_status reader_unit(capnp_packed_reader* r, size_t nw, std::vector<uint8_t>
                                               &cons);
     *used = (size_t)cons;
     return st;
+}
+
+// WritingPassthrough (capnp-futures serialize_packed.rs:186-220): the raw
+// bytes of a literal run go straight from the inner reader to the caller;
+// the stream ending inside them is UnexpectedEof.
+capnp_status reader_pass(capnp_packed_reader* r) {
+    if (r->ip == r->in.size()) {
+        capnp_status p = reader_pull(r);
+        if (p == CAPNP_NONE) return CAPNP_E_PREMATURE_END_OF_FILE;
+        if (p != CAPNP_OK) return p;
+    }
+    const size_t k = std::min(r->in.size() - r->ip, r->pass_rem);
+    r->dec.assign(r->in.begin() + (ptrdiff_t)r->ip, r->in.begin() + (ptrdiff_t)(r->ip + k));
+    r->dp = 0;
+    r->ip += k;
+    r->pass_rem -= k;
+    return CAPNP_OK;
+}
+
+// The staged input starts with a record no unit decodes (the inner reader
+// pends or has ended): if it is a literal run's head (tag 0xFF, 8 bytes,
+// count) whose raw words are not all in, hand out the head word as the
+// async reader's DrainingBuffer stage does, plus the raw bytes already
+// staged, and pass the rest through (reader_pass).  The head word is decoded
+// by the GPU unpack (a 1-word unit of the record with a zero count).
+// CAPNP_NONE when the record is anything else.
+capnp_status reader_lit_head(capnp_packed_reader* r) {
+    const size_t avail = r->in.size() - r->ip;
+    if (avail < 10 || r->in[r->ip] != 0xFF) return CAPNP_NONE;
+    const size_t c8 = 8 * (size_t)r->in[r->ip + 9];
+    uint8_t head[10];
+    memcpy(head, r->in.data() + r->ip, 9);
+    head[9] = 0;
+    uint64_t io[2] = {0, 10}, oo[2] = {0, 1}, word = 0, cons = 0;
+    int32_t st = 0;
+    capnp_status e = capnp_unpack_batch_host(r->ctx, head, io, 1, &word, oo, &st, &cons);
+    if (e != CAPNP_OK) return e;
+    if (st != CAPNP_OK) return (capnp_status)st;
+    const size_t k = std::min(avail - 10, c8);
+    r->dec.resize(8 + k);
+    memcpy(r->dec.data(), &word, 8);
+    memcpy(r->dec.data() + 8, r->in.data() + r->ip + 10, k);
+    r->dp = 0;
+    r->ip += 10 + k;
+    r->pass_rem = c8 - k;
+    return CAPNP_OK;
 }
 
 // Decodes at least one word into r->dec (empty only at a clean end of the
@@ -175,6 +229,7 @@ capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
     want = std::max<size_t>(want, 1);
     size_t nw = std::max(want, kMinUnit);
     std::vector<uint8_t> out;
+    if (r->pass_rem) return reader_pass(r);
     for (;;) {
         if (r->ip == r->in.size()) {
             capnp_status p = reader_pull(r);
@@ -200,24 +255,25 @@ capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
         capnp_status p = reader_pull(r);
         if (p == CAPNP_OK) continue;
         if (p != CAPNP_NONE && p != CAPNP_PENDING) return p;
-        // nothing more now (pending) or ever (end of stream): the largest unit
-        // the staged bytes decode (DidNotEndCleanly = too small, PrematureEnd
-        // / FailedToFill = too large), else pending / a partial record
-        size_t lo = 1, hi = nw;
-        while (lo <= hi) {
-            const size_t mid = lo + (hi - lo) / 2;
-            e = reader_unit(r, mid, out, &used, &st);
+        // nothing more now (pending) or ever (end of stream): every complete
+        // record staged (the device resolves where the last one ends), then
+        // a literal run's head, else pending / a partial record
+        uint64_t pb = 0, pw = 0;
+        e = capnp_stream_complete_prefix(r->ctx, r->in.data() + r->ip, r->in.size() - r->ip, &pb,
+                                         &pw);
+        if (e != CAPNP_OK) return e;
+        if (pw > 0) {
+            // the unit is exactly the complete records
+            e = reader_unit(r, pw, out, &used, &st, (size_t)pb);
             if (e != CAPNP_OK) return e;
-            if (st == CAPNP_OK) {
-                r->ip += used;
-                out.resize(mid * 8);
-                r->dec.swap(out);
-                r->dp = 0;
-                return CAPNP_OK;
-            }
-            if (st == CAPNP_E_DID_NOT_END_CLEANLY) lo = mid + 1;
-            else hi = mid - 1;
+            if (st != CAPNP_OK) return (capnp_status)st;
+            r->ip += used;
+            r->dec.swap(out);
+            r->dp = 0;
+            return CAPNP_OK;
         }
+        e = reader_lit_head(r);
+        if (e != CAPNP_NONE) return e;
         return p == CAPNP_PENDING ? CAPNP_PENDING : CAPNP_E_PREMATURE_END_OF_FILE;  // UnexpectedEof
     }
 }

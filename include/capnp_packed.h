@@ -18,9 +18,16 @@
  *     hipStream_t passed as void* (NULL = the HIP null stream; the context's
  *     own stream is returned by capnp_ctx_stream).
  *   - All buffers are caller-owned.  The library never frees caller memory.
- *   - Functions prefixed capnp_gpu_* take DEVICE pointers and are stream
- *     ordered (asynchronous).  All other functions take HOST pointers and are
- *     blocking; they stage through pinned memory and run the same HIP kernels.
+ *   - Functions prefixed capnp_gpu_* take DEVICE pointers and enqueue their
+ *     kernels on `stream`.  Those that size their launch from device data
+ *     say so ("Synchronises"): they copy a few bytes back and wait for
+ *     `stream` before returning, so they must not be captured into a
+ *     hipGraph.  capnp_gpu_pack_batch, capnp_gpu_unpack_batch and their _sync
+ *     forms do that (they read the batch's word range to pick the tiling);
+ *     their _tuned forms with chunks_per_tile != 0 are fully asynchronous
+ *     (stream ordered, capture-safe, no host wait).  All other functions take
+ *     HOST pointers and are blocking; they stage through pinned memory and
+ *     run the same HIP kernels.
  *   - There is no CPU implementation of the transform in this library: if no
  *     gfx950 device is present, capnp_ctx_create fails with CAPNP_E_NO_DEVICE.
  *   - Status codes map 1:1 onto capnp::ErrorKind (capnp/src/lib.rs:211-426).
@@ -128,7 +135,11 @@ size_t capnp_packed_batch_bound_bytes(size_t total_words, size_t nchunks);
    out_cap nothing at or past out_cap is written (the chunk that straddles
    out_cap may be partially written) and the total still reports the size
    that was needed (caller checks after the stream syncs).
-   d_chunk_word_off: nchunks+1 non-decreasing word offsets. */
+   d_chunk_word_off: nchunks+1 non-decreasing word offsets, checked on the
+   device first (CAPNP_E_INVALID_ARGUMENT, nothing launched, if one
+   decreases).  Synchronises `stream` once (the check, and d_chunk_word_off[0]
+   and [nchunks] to choose chunk tiles or word tiles);
+   capnp_gpu_pack_batch_tuned below does neither. */
 capnp_status capnp_gpu_pack_batch(capnp_ctx* ctx, const uint64_t* d_words,
                                   const uint64_t* d_chunk_word_off, size_t nchunks,
                                   uint8_t* d_out, size_t out_cap,
@@ -140,7 +151,14 @@ capnp_status capnp_gpu_pack_batch(capnp_ctx* ctx, const uint64_t* d_words,
    many bytes would (serialize_packed.rs:80-228, io.rs:16-31).
    d_status[c] receives the capnp_status of the chunk; d_consumed[c] (may be
    NULL) the packed bytes the decode used.  Bytes of d_words that belong to a
-   chunk with a non-OK status are unspecified. */
+   chunk with a non-OK status are unspecified.
+   d_in_byte_off and d_out_word_off (nchunks+1 entries each) must be
+   non-decreasing: checked on the device first (CAPNP_E_INVALID_ARGUMENT,
+   nothing launched, otherwise).  Synchronises `stream` once (the check, and
+   d_out_word_off[0] and [nchunks] to size the launch); a batch whose mean
+   chunk is >= 512 words then takes the index-free block decode of
+   capnp_gpu_unpack_batch_resync, which synchronises again.
+   capnp_gpu_unpack_batch_tuned below does neither. */
 capnp_status capnp_gpu_unpack_batch(capnp_ctx* ctx, const uint8_t* d_packed,
                                     const uint64_t* d_in_byte_off, size_t nchunks,
                                     uint64_t* d_words, const uint64_t* d_out_word_off,
@@ -176,6 +194,43 @@ capnp_status capnp_gpu_unpack_batch_sync(capnp_ctx* ctx, const uint8_t* d_packed
                                          const uint32_t* d_sync, int32_t* d_status,
                                          uint64_t* d_consumed, void* stream);
 
+/* Stream-ordered forms: the same calls with an explicit tile size and no
+   host synchronisation (capture-safe).  Pack: chunks per 256-thread
+   workgroup, 1..64, about capnp_pack_tile_words() / mean chunk words, for
+   batches whose chunks fit a tile's staged steps (longer chunks are packed by
+   the slower in-kernel streaming path; chunks_per_tile 0 = choose, which
+   synchronises).  Unpack: 1..256 chunks per workgroup; a tile takes the
+   LDS-staged path when it has <= 64 chunks, <= capnp_unpack_tile_words()
+   output words and <= 4.5x that many packed bytes.  The offset arrays are
+   not validated by these forms: the caller guarantees them non-decreasing
+   (a decreasing offset is a chunk of negative length, read or written out
+   of bounds). */
+capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
+                                        const uint64_t* d_chunk_word_off, size_t nchunks,
+                                        uint8_t* d_out, size_t out_cap,
+                                        uint64_t* d_out_byte_off, uint32_t chunks_per_tile,
+                                        void* stream);
+
+capnp_status capnp_gpu_unpack_batch_tuned(capnp_ctx* ctx, const uint8_t* d_packed,
+                                          const uint64_t* d_in_byte_off, size_t nchunks,
+                                          uint64_t* d_words, const uint64_t* d_out_word_off,
+                                          int32_t* d_status, uint64_t* d_consumed,
+                                          uint32_t chunks_per_tile, void* stream);
+
+/* The record-sync-index batch calls with an explicit tile size. */
+capnp_status capnp_gpu_pack_batch_sync_tuned(capnp_ctx* ctx, const uint64_t* d_words,
+                                             const uint64_t* d_chunk_word_off, size_t nchunks,
+                                             uint8_t* d_out, size_t out_cap,
+                                             uint64_t* d_out_byte_off, uint32_t* d_sync,
+                                             uint32_t chunks_per_tile, void* stream);
+capnp_status capnp_gpu_unpack_batch_sync_tuned(capnp_ctx* ctx, const uint8_t* d_packed,
+                                               const uint64_t* d_in_byte_off, size_t nchunks,
+                                               uint64_t* d_words, const uint64_t* d_out_word_off,
+                                               const uint32_t* d_sync, int32_t* d_status,
+                                               uint64_t* d_consumed, uint32_t chunks_per_tile,
+                                               void* stream);
+
+
 /* ---- index-free decode of long read units ---------- */
 /* The same transform, statuses and consumed counts as capnp_gpu_unpack_batch
    (PackedRead::read under read_exact, serialize_packed.rs:76-229, io.rs:16-31)
@@ -188,8 +243,9 @@ capnp_status capnp_gpu_unpack_batch_sync(capnp_ctx* ctx, const uint8_t* d_packed
    end exactly at its packed end with exactly its word count is decoded
    serially on its own (in the same launch as the resolved blocks), so its
    status, consumed count and partial output are exactly what
-   capnp_gpu_unpack_batch gives it.  Blocking: synchronises `stream`
-   (typically twice). */
+   capnp_gpu_unpack_batch gives it.  The offset arrays are checked first as
+   for capnp_gpu_unpack_batch.  Blocking: synchronises `stream` (typically
+   twice). */
 capnp_status capnp_gpu_unpack_batch_resync(capnp_ctx* ctx, const uint8_t* d_packed,
                                            const uint64_t* d_in_byte_off, size_t nchunks,
                                            uint64_t* d_words, const uint64_t* d_out_word_off,
@@ -253,8 +309,11 @@ capnp_status capnp_stream_unpack_batch(capnp_ctx* ctx, const uint8_t* packed,
    segments are packed in place with a gap before each message's first
    segment that then receives the packed table; a batch whose message offsets
    do not span [0, total_segs) goes through a staging copy instead.
-   Synchronises the stream once (to choose the path, or to size the staging
-   pack); out_cap as in capnp_gpu_pack_batch. */
+   d_msg_seg_off must be non-decreasing and end at or before total_segs, and
+   d_seg_word_off non-decreasing: checked on the device first
+   (CAPNP_E_INVALID_ARGUMENT otherwise).  Synchronises the stream twice (the
+   check; then to choose the path, or to size the staging pack); out_cap as
+   in capnp_gpu_pack_batch. */
 capnp_status capnp_gpu_write_messages(capnp_ctx* ctx, const uint64_t* d_words,
                                       const uint64_t* d_seg_word_off,
                                       const uint64_t* d_msg_seg_off, size_t nmsg,
@@ -274,9 +333,11 @@ capnp_status capnp_gpu_write_messages(capnp_ctx* ctx, const uint64_t* d_words,
    nmsg+1 entries), the segment lengths in d_seg_words (message m's at
    [d_msg_seg_off[m], d_msg_seg_off[m+1])), d_status[m] and d_consumed[m]
    (may be NULL; packed bytes the message used).  A message whose table
-   fails gets no words and no segments.  Synchronises the stream once (the
-   totals are checked against words_cap and segs_cap:
-   CAPNP_E_BUFFER_NOT_LARGE_ENOUGH, with only the offset arrays written). */
+   fails gets no words and no segments.  d_msg_byte_off must be
+   non-decreasing: checked on the device first (CAPNP_E_INVALID_ARGUMENT).
+   Synchronises the stream twice (the check; the totals are checked against
+   words_cap and segs_cap: CAPNP_E_BUFFER_NOT_LARGE_ENOUGH, with only the
+   offset arrays written). */
 capnp_status capnp_gpu_read_messages(capnp_ctx* ctx, const uint8_t* d_packed,
                                      const uint64_t* d_msg_byte_off, size_t nmsg,
                                      const capnp_reader_options* opts, int try_mode,
@@ -300,12 +361,14 @@ capnp_status capnp_gpu_read_messages(capnp_ctx* ctx, const uint8_t* d_packed,
    failed message has none).  On CAPNP_E_MESSAGE_ENDS_PREMATURELY,
    d_body_off[m] / d_consumed[m] carry the reference's
    MessageEndsPrematurely(header, body) payload instead (serialize.rs:67-71,
-   no_alloc_buffer_segments.rs:77-80, :254-257).  d_slice_off must be
-   non-decreasing and end within d_buf (not checked here; the Python mirror
-   checks it).  d_body_off / d_consumed may be NULL.
-   Synchronises the stream once (segment total against segs_cap:
-   CAPNP_E_BUFFER_NOT_LARGE_ENOUGH, with only d_msg_seg_off written). */
-capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf,
+   no_alloc_buffer_segments.rs:77-80, :254-257).  d_buf holds buf_len
+   bytes; d_slice_off must be non-decreasing with d_slice_off[nmsg] <=
+   buf_len, checked on the device before anything is read
+   (CAPNP_E_INVALID_ARGUMENT otherwise).  d_body_off / d_consumed may be NULL.
+   Synchronises the stream twice (the offset check, then the segment total
+   against segs_cap: CAPNP_E_BUFFER_NOT_LARGE_ENOUGH, with only d_msg_seg_off
+   written). */
+capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf, size_t buf_len,
                                           const uint64_t* d_slice_off, size_t nmsg,
                                           const capnp_reader_options* opts, int no_alloc,
                                           uint32_t* d_seg_words, size_t segs_cap,

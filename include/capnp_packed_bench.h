@@ -36,37 +36,8 @@ capnp_status capnp_gpu_gen_carsales(capnp_ctx* ctx, uint64_t* d_words, uint64_t 
                                     uint64_t skip_requests, uint64_t* h_req_off,
                                     size_t max_req, size_t* nreq, void* stream);
 
-/* capnp_gpu_pack_batch with an explicit tile size (chunks per 256-thread
- * workgroup, 1..64; 0 = default).  Pick ~1024 / mean_chunk_words. */
-capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
-                                        const uint64_t* d_chunk_word_off, size_t nchunks,
-                                        uint8_t* d_out, size_t out_cap,
-                                        uint64_t* d_out_byte_off, uint32_t chunks_per_tile,
-                                        void* stream);
-
-/* capnp_gpu_unpack_batch with an explicit tile size (chunks per 256-thread
- * workgroup, 1..256; 0 = default).  A tile takes the LDS-staged path when it
- * has <= 64 chunks, <= capnp_unpack_tile_words() output words and <= 4.5x
- * that many packed bytes; pick about capnp_unpack_tile_words() / mean chunk
- * words. */
-capnp_status capnp_gpu_unpack_batch_tuned(capnp_ctx* ctx, const uint8_t* d_packed,
-                                          const uint64_t* d_in_byte_off, size_t nchunks,
-                                          uint64_t* d_words, const uint64_t* d_out_word_off,
-                                          int32_t* d_status, uint64_t* d_consumed,
-                                          uint32_t chunks_per_tile, void* stream);
-
-/* The record-sync-index batch calls with an explicit tile size. */
-capnp_status capnp_gpu_pack_batch_sync_tuned(capnp_ctx* ctx, const uint64_t* d_words,
-                                             const uint64_t* d_chunk_word_off, size_t nchunks,
-                                             uint8_t* d_out, size_t out_cap,
-                                             uint64_t* d_out_byte_off, uint32_t* d_sync,
-                                             uint32_t chunks_per_tile, void* stream);
-capnp_status capnp_gpu_unpack_batch_sync_tuned(capnp_ctx* ctx, const uint8_t* d_packed,
-                                               const uint64_t* d_in_byte_off, size_t nchunks,
-                                               uint64_t* d_words, const uint64_t* d_out_word_off,
-                                               const uint32_t* d_sync, int32_t* d_status,
-                                               uint64_t* d_consumed, uint32_t chunks_per_tile,
-                                               void* stream);
+/* (The explicit-tile-size batch calls, capnp_gpu_*_tuned, are declared in
+ * capnp_packed.h: they are the stream-ordered variants of the boundary.) */
 
 /* Output words per wave sub-tile of the record-sync-index unpack (the
  * chunks_per_tile of the _sync_ calls ~ this / mean chunk words). */

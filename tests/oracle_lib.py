@@ -132,15 +132,21 @@ def write_message(segments):
 def read_message(packed, try_mode=False, limit=DEFAULT_TRAVERSAL_LIMIT, body_cap=None):
     """-> (status, [segments as np.uint64 arrays], consumed)."""
     a = _buf(packed)
+    grow = body_cap is None  # (a packed byte can stand for up to 128 words)
     if body_cap is None:
         body_cap = max(8 * len(a) + 8, 1)
-    body = np.zeros(body_cap, np.uint64)
-    seg = np.zeros(512, np.uint32)
-    nseg, used = C.c_uint32(0), C.c_size_t(0)
-    st = lib().oracle_read_message(a.ctypes.data if len(a) else None, len(a),
-                                   limit if limit is not None else 0, limit is not None,
-                                   int(try_mode), body.ctypes.data, body_cap, seg.ctypes.data,
-                                   C.byref(nseg), C.byref(used))
+    while True:
+        body = np.zeros(body_cap, np.uint64)
+        seg = np.zeros(512, np.uint32)
+        nseg, used = C.c_uint32(0), C.c_size_t(0)
+        st = lib().oracle_read_message(a.ctypes.data if len(a) else None, len(a),
+                                       limit if limit is not None else 0, limit is not None,
+                                       int(try_mode), body.ctypes.data, body_cap,
+                                       seg.ctypes.data, C.byref(nseg), C.byref(used))
+        if st == 9 and grow and body_cap < 128 * len(a) + 8:
+            body_cap = min(4 * body_cap, 128 * len(a) + 8)
+            continue
+        break
     segs = []
     if st == 0:
         o = 0

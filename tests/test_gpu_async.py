@@ -303,3 +303,269 @@ def test_bufread_refill_read_exact():
                 rest += b
                 r.consume(len(b))
             assert rest == b"\x07\x07", (cap, v)
+
+
+class _PlainBufRead:
+    """A BufRead with no look-ahead support (fill_buf / consume only): the
+    per-buffer retry path of _refilling, the reference's stopping points."""
+
+    def __init__(self, raw, capacity):
+        self.raw, self.capacity, self.buf, self.pos = raw, capacity, b"", 0
+
+    def fill_buf(self):
+        if self.pos >= len(self.buf):
+            self.buf, self.pos = bytes(self.raw.read(self.capacity)), 0
+        return memoryview(self.buf)[self.pos:]
+
+    def consume(self, n):
+        self.pos = min(self.pos + n, len(self.buf))
+
+
+def _drain(r):
+    rest = b""
+    while True:
+        b = bytes(r.fill_buf())
+        if not b:
+            return rest
+        rest += b
+        r.consume(len(b))
+
+
+def test_bufread_lookahead_stops_where_reference_does():
+    """With look-ahead (BufReader.unread) the reader ends each message, and
+    each failure, exactly where the per-buffer retries end it: same
+    messages, same error, same bytes left."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from capnp_amd import serialize_packed as S
+    from capnp_amd import CapnpError
+    rng = random.Random(23)
+    stream = b""
+    for _ in range(12):
+        st, b = O.write_message(_rand_segments(rng))
+        stream += b
+    cases = [stream, stream[:len(stream) * 2 // 3], stream + b"\x00\x05",
+             stream[:200] + b"\xff\x01\x02", stream + bytes([0xff] + [7] * 8 + [3])]
+    for data in cases:
+        for cap in (5, 33, 256, 4096):
+            res = []
+            for mk in (lambda: S.BufReader(_Raw(data), capacity=cap),
+                       lambda: _PlainBufRead(_Raw(data), cap)):
+                r = mk()
+                got, err = [], None
+                try:
+                    while True:
+                        m = S.try_read_message(r)
+                        if m is None:
+                            break
+                        got.append([np.asarray(s).view(np.uint64).tobytes()
+                                    for s in m.segments()])
+                except CapnpError as e:
+                    err = e.status
+                res.append((got, err, _drain(r)))
+            assert res[0] == res[1], (cap, len(data))
+
+
+def test_bufread_large_message_small_buffer():
+    """An 8 MiB message through 8 KiB buffers (1024 refills): look-ahead
+    retries keep it to a handful of decodes."""
+    import time
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from capnp_amd import serialize_packed as S
+    words = O.gen_fill(np.array([0, 1 << 20], np.uint64))
+    st, b = O.write_message([words])
+    assert st == 0
+    r = S.BufReader(_Raw(b + b"\x01\x02\x03"), capacity=8192)
+    t0 = time.perf_counter()
+    m = S.read_message(r, S.ReaderOptions(traversal_limit_in_words=None))
+    dt = time.perf_counter() - t0
+    assert np.array_equal(np.asarray(m.get_segment(0)).view(np.uint64), words)
+    assert _drain(r) == b"\x01\x02\x03"
+    assert dt < 30, dt
+
+
+def test_async_reader_inner_overread():
+    """An inner reader that returns more bytes than asked: the adaptor takes
+    only what fits and keeps the rest for the next pull."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from capnp_amd import serialize_packed_async as A
+    u = bytes(range(1, 65)) * 64
+    st, p = O.pack(u)
+    assert st == 0
+
+    class Greedy:
+        def __init__(self, data):
+            self.data, self.pos = data, 0
+
+        def read(self, n):
+            b = self.data[self.pos:self.pos + 2 * n + 7]  # more than asked
+            self.pos += len(b)
+            return b
+
+    r = A.PackedRead(Greedy(p))
+    got = b""
+    while len(got) < len(u):
+        b = r.read(len(u) - len(got))
+        assert b
+        got += b
+    assert got == u
+
+
+def _ref_poll_reads(packed, size, inner_max=1 << 30):
+    """Test-side restatement of capnp-futures PackedRead::poll_read
+    (capnp-futures/src/serialize_packed.rs:87-225) over a slice reader that
+    returns up to `inner_max` bytes per read: the bytes each read of `size`
+    returns, until b"" (clean end) or "EOF" (UnexpectedEof)."""
+    data, pos = bytes(packed), 0
+    st = {"stage": "start", "buf": [0] * 10, "bp": 0, "bs": 10, "bit": 0, "rem": 0}
+
+    def inner(n):
+        nonlocal pos
+        b = data[pos:pos + min(n, inner_max)]
+        pos += len(b)
+        return b
+
+    def poll():
+        while True:
+            s = st["stage"]
+            if s == "start":
+                b = inner(2 - st["bp"])
+                if not b:
+                    return "EOF" if st["bp"] > 0 else b""
+                st["buf"][st["bp"]:st["bp"] + len(b)] = list(b)
+                st["bp"] += len(b)
+                if st["bp"] >= 2:
+                    tag, cnt = st["buf"][0], st["buf"][1]
+                    if tag == 0:
+                        st["stage"], st["rem"] = "zero", (cnt + 1) * 8
+                    else:
+                        st["stage"] = "buffering"
+                        st["bs"] = bin(tag).count("1") + 1
+                        if st["bs"] == 9:
+                            st["bs"] = 10
+                        if st["bp"] >= st["bs"]:
+                            st["stage"], st["bp"], st["bit"] = "drain", 1, 0
+            elif s == "zero":
+                k = min(size, st["rem"])
+                if k >= st["rem"]:
+                    st["bp"], st["stage"] = 0, "start"
+                else:
+                    st["rem"] -= k
+                return bytes(k)
+            elif s == "buffering":
+                b = inner(st["bs"] - st["bp"])
+                if not b:
+                    return "EOF"
+                st["buf"][st["bp"]:st["bp"] + len(b)] = list(b)
+                st["bp"] += len(b)
+                if st["bp"] >= st["bs"]:
+                    st["stage"], st["bp"], st["bit"] = "drain", 1, 0
+            elif s == "drain":
+                out = []
+                while len(out) < size and st["bit"] < 8:
+                    nz = (st["buf"][0] >> st["bit"]) & 1
+                    out.append(st["buf"][st["bp"]] if nz else 0)
+                    st["bp"] += nz
+                    st["bit"] += 1
+                if st["bit"] == 8:
+                    if st["bp"] == st["bs"]:
+                        st["stage"] = "start"
+                    else:
+                        st["rem"], st["stage"] = st["buf"][st["bp"]] * 8, "pass"
+                    st["bp"] = 0
+                return bytes(out)
+            else:  # pass
+                ub = min(st["rem"], size)
+                if ub == 0:
+                    st["stage"] = "start"
+                    continue
+                b = inner(ub)
+                if not b:
+                    return "EOF"
+                if len(b) >= st["rem"]:
+                    st["stage"] = "start"
+                st["rem"] -= len(b)
+                return b
+
+    got = b""
+    while True:
+        r = poll()
+        if r == "EOF" or r == b"":
+            return got, r
+        got += r
+
+
+def test_partial_delivery_before_eof(A):
+    """Truncated streams read in 1-, 3- and 8-byte reads: the bytes handed
+    out before the error (or the clean end) are those of the reference's
+    stage machine: a literal run's head word and whatever raw bytes arrived
+    come out before UnexpectedEof (eof_mid_passthrough_run, :779-793)."""
+    from capnp_amd import CapnpError
+    lit = bytes([0xff, 1, 2, 3, 4, 5, 6, 7, 8, 2, 10, 11, 12, 13])
+    st_, full = O.pack(bytes([9, 0, 3, 0, 0, 0, 0, 1]) + bytes(range(1, 33)) * 4 + bytes(24)
+                       + bytes(range(2, 26)))
+    cases = [lit, lit[:9], lit[:10], lit[:11], bytes([0x81]), bytes([0xfe, 3, 3]), bytes([0]),
+             bytes([0, 3]), bytes([0x81, 42, 99]), lit + bytes(12)]
+    cases += [full[:k] for k in range(len(full) + 1)]
+    for data in cases:
+        for size in (1, 3, 8):
+            ref, end = _ref_poll_reads(data, size)
+            pr = A.PackedRead(_Plain(data))
+            got, err = b"", None
+            while True:
+                try:
+                    b = pr.read(size)
+                except CapnpError as e:
+                    err = e.kind
+                    break
+                if not b:
+                    break
+                assert len(b) <= size
+                got += b
+            assert got == ref, (data, size, got, ref)
+            assert (err == "PrematureEndOfFile") == (end == "EOF"), (data, size, err, end)
+
+
+def test_literal_head_while_pending(A):
+    """An inner reader that pends inside a literal run's raw words: the head
+    word is handed out at once (the reference's DrainingBuffer stage), the
+    raw bytes pass through as they arrive."""
+    from capnp_amd import CapnpError
+    lit = bytes([0xff, 1, 2, 3, 4, 5, 6, 7, 8, 2]) + bytes(range(10, 26))
+
+    class Trickle:
+        """The first 12 bytes, then pending once, then the rest."""
+        def __init__(self, data):
+            self.data, self.pos, self.pended = data, 0, False
+
+        def read(self, n):
+            if self.pos == 12 and not self.pended:
+                self.pended = True
+                return None
+            end = 12 if self.pos < 12 else len(self.data)
+            b = self.data[self.pos:min(end, self.pos + n)]
+            self.pos += len(b)
+            return b
+
+    pr = A.PackedRead(Trickle(lit))
+    got = b""
+    pends = 0
+    while len(got) < 24:
+        try:
+            b = pr.read(24 - len(got))
+        except CapnpError as e:
+            assert e.status == 15  # pending
+            pends += 1
+            continue
+        assert b
+        got += b
+        if len(got) == 10:
+            assert pends == 0  # head word + 2 raw bytes before the inner reader pended
+    assert got == bytes(range(1, 9)) + bytes(range(10, 26))
+    assert pends <= 1  # (the pend may be absorbed while the head word is decoded)
+    assert pr.read(8) == b""

@@ -111,3 +111,47 @@ def test_invalid_tables_and_limit(ctx):
     # a message over the traversal limit ends the loop there
     big = _stream(rng, 3, big=True)
     _check(ctx, good + big + good, limit=2000)
+
+
+def test_many_tiny_messages(ctx):
+    """Hundreds of 1-word (null root) and empty-segment messages: 2-4 packed
+    bytes each, more than bytes // 8 + 1 of them, so discovery runs in
+    several capped rounds and every message must still come back."""
+    rng = random.Random(11)
+    out = b""
+    for k in range(700):
+        segs = [np.zeros(rng.choice([0, 1]), np.uint64)]
+        if k % 97 == 5:
+            segs = [np.array([rng.getrandbits(64)], np.uint64)]
+        st, b = O.write_message(segs)
+        assert st == 0
+        out += b
+    assert len(out) // 8 + 1 < 700
+    _check(ctx, out)
+    _check(ctx, out + b"\x10\x02\x00")  # a truncated tail after them
+
+
+def test_small_discovery_rounds(ctx):
+    """The same loop with a cap of 3 messages per discovery round."""
+    import torch
+    rng = random.Random(12)
+    stream = _stream(rng, 40)
+    ref, ref_end = _oracle_loop(stream)
+    dev = torch.from_numpy(np.frombuffer(stream, np.uint8).copy()).cuda()
+    got, end = ctx.read_message_stream(dev, max_msgs=3)
+    assert end == ref_end and len(got) == len(ref)
+    assert [u for _, u in got] == [u for _, u in ref]
+
+
+def test_zero_heavy_stream(ctx):
+    """All-zero segments expand 2 packed bytes into 256 words: the decoded
+    words far exceed any fixed multiple of the packed size."""
+    segs1 = [np.zeros(1 << 17, np.uint64)]                       # 1 MiB of zeros
+    segs2 = [np.zeros(5000, np.uint64), np.arange(1, 9, dtype=np.uint64)]
+    out = b""
+    for segs in (segs1, segs2, segs1):
+        st, b = O.write_message(segs)
+        assert st == 0
+        out += b
+    assert len(out) < 10000
+    _check(ctx, out)
