@@ -2032,7 +2032,7 @@ __device__ __forceinline__ uint32_t cs_size_step(uint64_t wlo, uint64_t whi, uin
     // run counts: the words up to the next head within the chunk
     const uint64_t nlo = (H.lo >> 1) >> lane;         // heads after word lane, in lo
     const uint32_t dlo0 = ffbl64(nlo);
-    const uint32_t dlo1 = (63u - lane) + ffbl64(H.hi);  // the first head in hi
+    const uint32_t dlo1 = H.hi ? (63u - lane) + ffbl64(H.hi) : ~0u;  // the first head in hi
     const uint32_t dlo = dlo0 < 64u ? dlo0 : dlo1;
     const uint32_t dhi = ffbl64((H.hi >> 1) >> lane);
     const uint32_t cnt_lo = min(dlo, __builtin_elementwise_sub_sat(n, lane + 1u));
@@ -2096,6 +2096,15 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     const uint32_t lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     const uint64_t tile = blockIdx.x;
+#if PACK_PROF == 3
+    if (tid == 0) {
+        uint32_t xcc, hwid;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+        TRACE(tile, 0, RT());
+        TRACE(tile, 6, ((uint64_t)xcc << 32) | hwid);
+    }
+#endif
     const uint64_t c0 = tile * tc;
     const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
     const uint32_t nc = (uint32_t)(c1 - c0);
@@ -2176,6 +2185,10 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
 
     for (uint32_t o = 16 * lane; o < kStageRegion; o += 16 * CAPNP_WAVE)
         *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
+#if PACK_PROF == 3
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) TRACE(tile, 1, RT());
+#endif
 
     // ---- pass 1: sizes and positions
     uint32_t ilo[kCsSteps], ihi[kCsSteps];
@@ -2202,6 +2215,9 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     if (wave == 0) {
         agg = scan_chunks32(sm, nc, lane);
         publish(LA, tile, agg, lane);
+#if PACK_PROF == 3
+        if (lane == 0) TRACE(tile, 2, RT());
+#endif
     }
     // ---- pass 2: the bytes (the look-back loads are in flight)
     if (fits) {
@@ -2221,7 +2237,14 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         }
     }
     if (wave == 0) {
+#if PACK_PROF == 3
+        wave_lds_sync();
+        if (lane == 0) TRACE(tile, 3, RT());
+#endif
         const uint64_t excl = lookback(LA, tile, agg, lane);
+#if PACK_PROF == 3
+        if (lane == 0) TRACE(tile, 4, RT());
+#endif
         if (lane < nc) sm.chunk_pos[lane] += excl;
         if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
     }
@@ -2233,6 +2256,10 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
             copy_out(region, out - mis, D0, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
         }
+#if PACK_PROF == 3
+        __syncthreads();
+        if (tid == 0) TRACE(tile, 5, RT());
+#endif
     } else {
         if constexpr (SYNC)
             for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
@@ -2682,8 +2709,9 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_
     hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(nchunks, tc), stream);
     if (e != hipSuccess) return e;
     uint8_t* ovf = pack_ovf_flags(d_state, ntiles);
-    if (pack_cs_enabled() && tc <= kWaves * kCsSteps && tc * 2 > kWaves * kCsSteps) {
-        // chunks of at most 128 words (tc chosen for a mean of 65-128 words)
+    if (pack_cs_enabled() && tc == kWaves * kCsSteps) {
+        // chunks of at most 128 words (tc chosen for a mean of 65-128 words;
+        // a tile with a longer chunk takes the streaming size pass)
         if (d_sync)
             hipLaunchKernelGGL((pack_cs_kernel<true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
                                stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,

@@ -849,7 +849,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
 // per launch: the block walk shortens the chain 3x but walks every record
 // twice (plus a confirming round) on 10x the lanes, so the tile's total hop
 // work grows 3.4x and the CU saturates; kept as an option, off.
-#define UNPACK_SPEC 0
+#define UNPACK_SPEC 2  // 2 = segment walk (spec_seg_tile, below)
 #endif
 #ifndef UNPACK_SPEC_ROUNDS
 #define UNPACK_SPEC_ROUNDS 8  // fix-up rounds before a chunk falls to the exact walk
@@ -1082,6 +1082,147 @@ __device__ __forceinline__ void spec_tile(SM& S, uint64_t ca, uint32_t nc,
     S.sel[tid] = kExpandTable.s[tid];  // (the block tables overlaid it)
 }
 
+// Index-free walk of a staged tile on every thread (UNPACK_SPEC 2): each
+// chunk's packed bytes are cut into S equal byte segments (S = 16 for up to
+// 16 chunks, 4 for up to 64), one thread each, so a chunk's ~117-record
+// chain becomes S chains of ~117 / S records and all four waves walk
+// (the serial walker used 16 lanes of one wave for the whole chain).
+//   1. spec: thread (c, j) walks from its segment's first byte (j = 0: the
+//      chunk start, exact) until it passes the segment end; it keeps the
+//      first kSegK record starts it visits with the words before each, its
+//      exit (first record start at or past the segment end) and its words;
+//   2. meet: the true entry of segment j is the exit of segment j - 1.  Tag
+//      chains couple within a few records (a record is 1-10 bytes), so the
+//      entry is normally among the first kSegK starts segment j visited:
+//      from there its walk is the exact one, its exit stands and its words
+//      drop those before the entry.  The chunk is exact if every entry meets
+//      and the last exit is the chunk's packed end with exactly its words;
+//      otherwise (a long literal run across segments, a malformed chunk)
+//      the chunk takes the exact serial walk, as with a bad sync index;
+//   3. desc: word bases by a scan of the segment words; each thread writes
+//      the descriptors of its records, from its entry to its exit.
+// Speculation changes the speed only, never the result.
+constexpr uint32_t kSegK = 4;
+
+__device__ __forceinline__ void seg_hop(const uint8_t* B, uint32_t& p, uint32_t& w, uint32_t pe,
+                                        bool& err) {
+    uint32_t tag, b1, b9;
+    rec_bytes(B, p + 1u, tag, b1, b9);
+    const bool isz = tag == 0, isf = tag == 0xFF;
+    const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+    const uint32_t q = p + 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) +
+                       (isf ? 8u * cnt : 0u);
+    err = err || q > pe;
+    w += 1u + cnt;
+    p = q;
+}
+
+template <class SM>
+__device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
+                                              int32_t* __restrict__ status,
+                                              uint64_t* __restrict__ consumed, uint32_t tid,
+                                              uint32_t lane) {
+    const uint32_t lg = nc <= 16 ? 4u : 2u;  // S = 16 or 4 segments per chunk
+    const uint32_t nseg = 1u << lg;
+    const uint32_t c = tid >> lg, j = tid & (nseg - 1u);
+    const bool act = c < nc;
+    uint32_t cs = 0, pe = 0, n = 0, sb = 0, se = 0;
+    if (act) {
+        cs = S.cp[c];
+        pe = S.cp[c + 1];
+        n = S.cw[c + 1] - S.cw[c];
+        const uint32_t len = pe - cs;
+        sb = cs + (uint32_t)(((uint64_t)len * j) >> lg);
+        se = cs + (uint32_t)(((uint64_t)len * (j + 1u)) >> lg);
+    }
+    // 1. spec walk from sb while p < se, the first kSegK starts kept
+    uint32_t p = sb, w = 0;
+    bool err = false;
+    uint32_t kl[kSegK];  // start | words before it << 16 (0xFFFFFFFF: none)
+#pragma unroll
+    for (uint32_t i = 0; i < kSegK; i++) {
+        const bool go = act && p < se && !err;
+        kl[i] = go ? (p | (w << 16)) : 0xFFFFFFFFu;
+        if (go) seg_hop(S.bytes, p, w, pe, err);
+    }
+    while (act && p < se && !err) seg_hop(S.bytes, p, w, pe, err);
+    const uint32_t x = p;
+    if (act) S.so.bx[tid] = (uint16_t)x;
+    __syncthreads();
+    // 2. meet: entry = the previous segment's exit
+    const uint32_t e = (!act || j == 0) ? sb : (uint32_t)S.so.bx[tid - 1];
+    uint32_t wd = w;   // words from the entry to the exit
+    bool ok = !err;
+    if (act && j > 0) {
+        bool hit = false;
+        uint32_t before = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kSegK; i++) {
+            const bool h = (kl[i] & 0xFFFFu) == e && kl[i] != 0xFFFFFFFFu;
+            before = h ? (kl[i] >> 16) : before;
+            hit = hit || h;
+        }
+        // (an entry at or past the exit: the previous segment's last record
+        // covers this whole segment; only a spec walk that stopped exactly
+        // there can continue it)
+        if (!hit && e == x) {
+            hit = true;
+            before = w;
+        }
+        ok = ok && hit;
+        wd = w - before;
+    }
+    // chunk: segments (c, 0..S-1) are nseg consecutive threads of one wave
+    // (S <= 16 divides 64): inclusive scan of wd within the group, all ok,
+    // and the last exit at the packed end
+    uint32_t incl = wd;
+    for (uint32_t d = 1; d < nseg; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, d, 64);
+        if (j >= d) incl += t;
+    }
+    const uint64_t bad_m = ballot64(act && !ok);
+    const uint32_t gl = lane & ~(nseg - 1u);  // first lane of the group
+    const uint64_t gm = ((nseg == 64u) ? ~0ull : ((1ull << nseg) - 1ull)) << gl;
+    const uint32_t tot = (uint32_t)__shfl((int)incl, (int)(gl + nseg - 1u), 64);
+    const uint32_t xl = (uint32_t)__shfl((int)x, (int)(gl + nseg - 1u), 64);
+    const bool chunk_ok = act && (bad_m & gm) == 0 && tot == n && xl == pe && n > 0 && pe > cs;
+    if (act && j == 0) S.badc[c] = chunk_ok ? 0 : 1;
+    // 3. descriptors of the good chunks: records from the entry to the exit
+    if (chunk_ok) {
+        uint32_t q = e, ww = S.cw[c] + incl - wd;
+        while (q < x) {
+            uint32_t tag, b1, b9;
+            rec_bytes(S.bytes, q + 1u, tag, b1, b9);
+            const bool isz = tag == 0, isf = tag == 0xFF;
+            const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+            S.dpos[ww] = (uint16_t)q;
+            if (isf && cnt) lit_entries(S, ww, q, cnt);
+            ww += 1u + cnt;
+            q += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) + (isf ? 8u * cnt : 0u);
+        }
+    }
+    __syncthreads();
+    if (tid < nc) {
+        const uint64_t cc = ca + tid;
+        const uint32_t nn = S.cw[tid + 1] - S.cw[tid];
+        if (S.badc[tid] && nn) {  // exact serial walk of the chunk
+#if UNPACK_PROF
+            atomicAdd(&g_uprof[0], 1ull);
+#endif
+            const uint32_t wa = S.cw[tid], wz = S.cw[tid + 1];
+            for (uint32_t i = wa; i < wz; i++) S.dpos[i] = kNone;
+            int32_t st;
+            uint32_t used;
+            walk_chunk(S, S.cp[tid], S.cp[tid + 1], wa, wz - wa, st, used);
+            status[cc] = st;
+            if (consumed) consumed[cc] = used;
+        } else {
+            status[cc] = ST_OK;
+            if (consumed) consumed[cc] = nn ? S.cp[tid + 1] - S.cp[tid] : 0u;
+        }
+    }
+}
+
 // One staged sub-tile: chunks [ca, cb) whose packed bytes, output words and
 // count fit the LDS tables (stage, walk, expand).  All threads of the
 // workgroup call it; it ends after its last LDS access of the expansion.
@@ -1193,6 +1334,8 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
             }
         }
         if (anybad) __syncthreads();
+    } else if (UNPACK_SPEC == 2) {
+        spec_seg_tile(S, ca, nc, status, consumed, tid, lane);
     } else if (UNPACK_SPEC) {
         spec_tile(S, ca, nc, status, consumed, tid, lane, wave);
     } else if (wave == walker && lane < nc) {  // (idle lanes stay off: their LDS traffic counts)
@@ -2016,7 +2159,16 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
         hipLaunchKernelGGL(unpack_kernel<true>, dim3((uint32_t)blocks), dim3(kThreads),
                            UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
                            d_status, d_consumed, d_sync);
-    else
+    else if (UNPACK_SPEC == 2) {
+        // index-free with the segment walk: split as the sync path (the walk's
+        // registers and the global path's no longer meet in one kernel)
+        hipLaunchKernelGGL(unpack_fit_kernel<false>, dim3((uint32_t)blocks), dim3(kThreads),
+                           UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
+                           d_status, d_consumed, d_sync);
+        hipLaunchKernelGGL(unpack_ovf_kernel<false>, ogrid, dim3(kThreads), 0, stream, d_in,
+                           d_in_off, nchunks, tc, d_out, d_out_off, d_status, d_consumed, d_sync,
+                           blocks);
+    } else
         hipLaunchKernelGGL(unpack_kernel<false>, dim3((uint32_t)blocks), dim3(kThreads),
                            UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
                            d_status, d_consumed, d_sync);

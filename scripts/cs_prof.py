@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Per-tile phase timeline of pack_cs_kernel from the PACK_PROF=3 build
+(`make -C capnproto-rust_amd prof PROF=3`): start, loads landed, pass 1 +
+publish, pass 2, look-back, end (s_memrealtime, 100 MHz).  Prints the mean of
+each phase and how many tiles are in each phase on average over the launch
+(the memory-level parallelism of the load phase).  Diagnostic only.
+
+    python3 scripts/cs_prof.py [--chunks N] [--pz P] [--iters K]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "capnproto-rust_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--chunks", type=int, default=1 << 20)
+    ap.add_argument("--pz", type=int, default=1288490189)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--sync", action="store_true")
+    ap.add_argument("--lib", default="")
+    a = ap.parse_args()
+    import torch
+    from capnp_amd import Context
+    path = a.lib or os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_prof3.so")
+    L = C.CDLL(path)
+    vp, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
+    L.capnp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int)]
+    L.capnp_ctx_create.restype = vp
+    L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, u32, vp]
+    L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, u32, vp]
+    L.capnp_ctx_reserve.argtypes = [vp, sz]
+    L.capnp_pack_trace.argtypes = [vp]
+    st = C.c_int(0)
+    h = vp(L.capnp_ctx_create(0, C.byref(st)))
+    n, cw, tc = a.chunks, 128, 16
+    ctx = Context(0)
+    offs = torch.arange(0, (n + 1) * cw, cw, dtype=torch.int64, device="cuda")
+    words = torch.empty(n * cw, dtype=torch.int64, device="cuda")
+    ctx.gen_batch(words, offs, pz_thresh=a.pz)
+    ref_out, ref_oo = ctx.pack_batch(words, offs)
+    cap = ctx.batch_bound_bytes(n * cw, n)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    oo = torch.empty(n + 1, dtype=torch.int64, device="cuda")
+    sync = torch.empty(ctx.sync_entries(n * cw), dtype=torch.int32, device="cuda")
+    L.capnp_ctx_reserve(h, n)
+    ntiles = (n + tc - 1) // tc
+    trace = torch.zeros(ntiles * 8, dtype=torch.int64, device="cuda")
+    L.capnp_pack_trace(C.c_void_p(trace.data_ptr()))
+    stream = torch.cuda.current_stream()
+    P = C.c_void_p
+    for it in range(a.iters + 1):
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        if a.sync:
+            L.capnp_gpu_pack_batch_sync_tuned(h, P(words.data_ptr()), P(offs.data_ptr()), n,
+                                              P(out.data_ptr()), cap, P(oo.data_ptr()),
+                                              P(sync.data_ptr()), tc, P(stream.cuda_stream))
+        else:
+            L.capnp_gpu_pack_batch_tuned(h, P(words.data_ptr()), P(offs.data_ptr()), n,
+                                         P(out.data_ptr()), cap, P(oo.data_ptr()), tc,
+                                         P(stream.cuda_stream))
+        e1.record(stream)
+        e1.synchronize()
+        if it == 0:
+            continue
+        ok = torch.equal(oo, ref_oo) and torch.equal(out[:ref_out.numel()], ref_out)
+        T = trace.view(ntiles, 8).cpu().numpy().astype(np.int64)
+        t0 = T[:, 0].min()
+        span = (T[:, 5].max() - t0) / 100.0
+        ph = ["load", "pass1+pub", "pass2", "lookback", "copyout"]
+        means = [(T[:, k + 1] - T[:, k]).mean() / 100.0 for k in range(5)]
+        life = (T[:, 5] - T[:, 0]).mean() / 100.0
+        # average tiles in each phase over the launch = sum of durations / span
+        inflight = [(T[:, k + 1] - T[:, k]).sum() / 100.0 / span for k in range(5)]
+        starts = np.sort(T[:, 0] - t0) / 100.0
+        print(f"iter {it}: {e0.elapsed_time(e1) * 1e3:.1f} us (traced span {span:.1f}) ok={ok} "
+              f"tiles={ntiles} lifetime {life:.2f} us")
+        print("   phase us : " + "  ".join(f"{p} {m:.2f}" for p, m in zip(ph, means)))
+        print("   in flight: " + "  ".join(f"{p} {x:.0f}" for p, x in zip(ph, inflight))
+              + f"  (total {sum(inflight):.0f})")
+        q = np.percentile(T[:, 5] - T[:, 0], [10, 50, 90]) / 100.0
+        print(f"   lifetime p10/p50/p90 {q[0]:.2f}/{q[1]:.2f}/{q[2]:.2f} us; "
+              f"first start->last start {starts[-1] - starts[0]:.1f} us")
+
+
+if __name__ == "__main__":
+    main()
