@@ -385,6 +385,14 @@ def main():
                                         P + U + 2 * offs_bytes + 12 * n)
         kernels["unpack_nosync"]["roundtrip_ok"] = ok_ns
         ok = ok and ok_ns
+        # and the index-free pack (the same bytes, no sync index written)
+        e[0].record(stream)
+        for _ in range(reps):
+            ctx.pack_batch_into(words, offs, packed, poffs, chunks_per_tile=tc)
+        e[1].record(stream)
+        torch.cuda.synchronize()
+        ok = ok and int(poffs[-1].item()) == P
+        kernels["pack_nosync"] = kern(e[0].elapsed_time(e[1]) / reps, U + P + 2 * offs_bytes)
     dom = "pack" if pack_ms >= unpack_ms else "unpack"
     achieved = kernels[dom]["GBps"]
     traffic = traffic_rw = None
@@ -439,6 +447,12 @@ def main():
                                            (elapsed / args.steps) / 1e9 /
                                            (world * HBM_PEAK_GBS), 4),
             "kernels": kernels,
+            # reference-compatible round trip: no side-band index either way,
+            # U / (pack without index + index-free unpack), kernel times
+            "roundtrip_noindex_GiBps": (
+                round(U / GiB / ((kernels["pack_nosync"]["ms"] +
+                                  kernels["unpack_nosync"]["ms"]) * 1e-3), 2)
+                if "unpack_nosync" in kernels else None),
             "packed_ratio": round(P / U, 4),
             "sync_index": sync is not None,
             "roundtrip_ok": ok,

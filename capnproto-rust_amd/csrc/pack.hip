@@ -1983,9 +1983,20 @@ __device__ __forceinline__ M128 operator&(M128 a, M128 b) { return {a.lo & b.lo,
 __device__ __forceinline__ M128 operator|(M128 a, M128 b) { return {a.lo | b.lo, a.hi | b.hi}; }
 __device__ __forceinline__ M128 operator^(M128 a, M128 b) { return {a.lo ^ b.lo, a.hi ^ b.hi}; }
 __device__ __forceinline__ M128 andnot(M128 a, M128 b) { return {a.lo & ~b.lo, a.hi & ~b.hi}; }
+// (an add-with-carry chain on the scalar unit; the C form compares in a VALU
+// op and reads the carry back)
 __device__ __forceinline__ M128 add128(M128 a, M128 b) {
-    const uint64_t lo = a.lo + b.lo;
-    return {lo, a.hi + b.hi + (lo < a.lo ? 1ull : 0ull)};
+    uint32_t r0, r1, r2, r3;
+    asm("s_add_u32 %0, %4, %8\n\t"
+        "s_addc_u32 %1, %5, %9\n\t"
+        "s_addc_u32 %2, %6, %10\n\t"
+        "s_addc_u32 %3, %7, %11"
+        : "=&s"(r0), "=&s"(r1), "=&s"(r2), "=s"(r3)
+        : "s"((uint32_t)a.lo), "s"((uint32_t)(a.lo >> 32)), "s"((uint32_t)a.hi),
+          "s"((uint32_t)(a.hi >> 32)), "s"((uint32_t)b.lo), "s"((uint32_t)(b.lo >> 32)),
+          "s"((uint32_t)b.hi), "s"((uint32_t)(b.hi >> 32))
+        : "scc");
+    return {((uint64_t)r1 << 32) | r0, ((uint64_t)r3 << 32) | r2};
 }
 
 // Index of the lowest set bit of a 64-bit lane value, >= 64 if none.
@@ -2005,17 +2016,17 @@ __device__ __forceinline__ uint32_t cs_info(uint32_t pos, uint32_t idx, uint32_t
 
 // Pass 1 of one chunk of n <= 128 words (lo = word lane, hi = word 64 +
 // lane) placed at region position oc: both words' info; returns the chunk's
-// packed size.
+// packed size.  The two halves' record sizes (<= 10 bytes, <= 640 per half)
+// share one 16:16 scan.
 __device__ __forceinline__ uint32_t cs_size_step(uint64_t wlo, uint64_t whi, uint32_t n,
                                                  uint32_t lane, uint32_t oc, uint32_t& ilo,
                                                  uint32_t& ihi) {
     const uint32_t tlo = word_tag_dot((uint32_t)wlo, (uint32_t)(wlo >> 32));
     const uint32_t thi = word_tag_dot((uint32_t)whi, (uint32_t)(whi >> 32));
     const uint32_t plo = __builtin_popcount(tlo), phi = __builtin_popcount(thi);
-    const bool vlo = lane < n, vhi = lane + 64u < n;
     // (words past n are zero: out-of-range loads; only Z needs the bound)
-    const M128 V{ballot64(vlo), ballot64(vhi)};
-    const M128 Z{ballot64((vlo ? plo : 64u) == 0), ballot64((vhi ? phi : 64u) == 0)};
+    const M128 V{ballot64(lane < n), ballot64(lane + 64u < n)};
+    const M128 Z = V & M128{ballot64(tlo == 0), ballot64(thi == 0)};
     const M128 L{ballot64(plo >= 7), ballot64(phi >= 7)};
     const M128 F{ballot64(plo == 8), ballot64(phi == 8)};
     const M128 AZ = Z & shl1(Z);
@@ -2026,9 +2037,11 @@ __device__ __forceinline__ uint32_t cs_size_step(uint64_t wlo, uint64_t whi, uin
     const uint32_t hs_hi = 1u + phi + ((0x101u >> phi) & 1u);
     const uint32_t slo = mask_sel(H.lo, hs_lo, tlo == 0 ? 0u : 8u);
     const uint32_t shi = mask_sel(H.hi, hs_hi, thi == 0 ? 0u : 8u);
-    const uint32_t clo = wave_incl_scan(slo);
-    const uint32_t tot_lo = (uint32_t)__builtin_amdgcn_readlane((int)clo, 63);
-    const uint32_t chi = wave_incl_scan(shi);
+    const uint32_t x = slo | (shi << 16);
+    const uint32_t incl = wave_incl_scan(x);
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    const uint32_t tot_lo = tot & 0xFFFFu;
+    const uint32_t excl = incl - x;  // (per half: no borrow crosses bit 16)
     // run counts: the words up to the next head within the chunk
     const uint64_t nlo = (H.lo >> 1) >> lane;         // heads after word lane, in lo
     const uint32_t dlo0 = ffbl64(nlo);
@@ -2037,46 +2050,47 @@ __device__ __forceinline__ uint32_t cs_size_step(uint64_t wlo, uint64_t whi, uin
     const uint32_t dhi = ffbl64((H.hi >> 1) >> lane);
     const uint32_t cnt_lo = min(dlo, __builtin_elementwise_sub_sat(n, lane + 1u));
     const uint32_t cnt_hi = min(dhi, __builtin_elementwise_sub_sat(n, lane + 65u));
-    ilo = cs_info(oc + clo - slo, mask_sel(H.lo, tlo, kSelCopy), cnt_lo & 127u, slo);
-    ihi = cs_info(oc + tot_lo + chi - shi, mask_sel(H.hi, thi, kSelCopy), cnt_hi & 127u, shi);
-    return tot_lo + (uint32_t)__builtin_amdgcn_readlane((int)chi, 63);
+    ilo = cs_info(oc + (excl & 0xFFFFu), mask_sel(H.lo, tlo, kSelCopy), cnt_lo & 127u, slo);
+    ihi = cs_info(oc + tot_lo + (excl >> 16), mask_sel(H.hi, thi, kSelCopy), cnt_hi & 127u, shi);
+    return tot_lo + (tot >> 16);
 }
 
-// Pass 2 of one word (cs info layout): as lean_emit_step with no run
-// extension; SYNC entries from head lanes (hw = g + word of the chunk).
+// Pass 2 of one word (cs info layout): the record from the selector table
+// (s0, s1), with the header and the 0xFF head's tail computed here:
+//   r0 = perm(hi, lo, s0) | (zero head ? cnt << 8 : tag), r2 = 0xFF head ?
+//   byte 7 | cnt << 8 : 0,
+// shifted to its byte position and ORed into the region.  SYNC: a head
+// writes the entries of the sync points it covers, d, d + 8, ... <= cnt words
+// after it (d = the distance to the next sync point, shared by both words of
+// a lane; b = the entry's byte offset in the tile's index window).
 template <bool SYNC>
-__device__ __forceinline__ void cs_emit_word(uint64_t w, uint32_t info, uint32_t lane,
-                                             uint8_t* region_m1, const Sel8* sel,
-                                             __amdgpu_buffer_rsrc_t srs, uint32_t oc, uint32_t g,
-                                             uint32_t t0) {
-    if (info & kCsSkip) return;
+__device__ __forceinline__ void cs_emit_word(uint64_t w, uint32_t info, uint8_t* region_m1,
+                                             const Sel8* sel, __amdgpu_buffer_rsrc_t srs,
+                                             uint32_t oc, uint32_t d, uint32_t b) {
+    if (info >= kCsSkip) return;  // (the skip flag is the top field)
     const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
-    const uint32_t pos = info & ((1u << kInfoPosBits) - 1u);
     const uint32_t idx = __builtin_amdgcn_ubfe(info, kInfoPosBits, 9);
-    const uint32_t cnt = __builtin_amdgcn_ubfe(info, 22, 7);
+    const uint32_t cnt = info >> 22;
     const Sel8 se = sel[idx];
-    const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, se.s0) | (((cnt << 8) | idx) & sel_m(idx));
+    const uint32_t hdr = idx == 0 ? (cnt << 8) : (idx & 0xFFu);  // (copy words: 256 & 0xFF)
+    const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, se.s0) | hdr;
     const uint32_t r1 = __builtin_amdgcn_perm(hi, lo, se.s1);
-    const uint32_t r2 = __builtin_amdgcn_perm(cnt, hi, sel_s2(idx));
-    const uint32_t s = 0u - pos;
+    const uint32_t r2 = idx == 0xFFu ? ((hi >> 24) | (cnt << 8)) : 0u;
+    const uint32_t s = 0u - info;  // (alignbyte reads bits 1:0: -pos mod 4)
     const uint32_t e0 = __builtin_amdgcn_alignbyte(r0, 0u, s);
     const uint32_t e1 = __builtin_amdgcn_alignbyte(r1, r0, s);
     const uint32_t e2 = __builtin_amdgcn_alignbyte(r2, r1, s);
     const uint32_t e3 = __builtin_amdgcn_alignbyte(0u, r2, s);
+    const uint32_t pos = info & ((1u << kInfoPosBits) - 1u);
     uint32_t* b32 = reinterpret_cast<uint32_t*>(__builtin_align_down(region_m1 + pos, 4));
     __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     if constexpr (SYNC) {
-        const uint32_t c = t0 - g;
-        const uint32_t d = (c - lane) & (kSyncWords - 1);
-        const uint32_t dh = idx < kSelCopy ? d : ~0u;
-        const uint32_t rel = pos - oc;
-        const uint32_t b = (lane + d - c) / (kSyncWords / 4u);
-        __builtin_amdgcn_raw_buffer_store_b32(rel | (d << 24), srs,
-                                              (int)(dh <= cnt ? b : 0x80000000u), 0, 0);
-        if (dh < kSyncWords && dh + kSyncWords <= cnt) {  // (dh = ~0: not a head)
+        if (idx < kSelCopy && d <= cnt) {
+            const uint32_t rel = pos - oc;
+            __builtin_amdgcn_raw_buffer_store_b32(rel | (d << 24), srs, (int)b, 0, 0);
 #pragma clang loop unroll(disable) vectorize(disable)
             for (uint32_t dd = d + kSyncWords, bb = b + 4; dd <= cnt; dd += kSyncWords, bb += 4)
                 __builtin_amdgcn_raw_buffer_store_b32(rel | (dd << 24), srs, (int)bb, 0, 0);
@@ -2229,8 +2243,12 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         for (uint32_t s = 0; s < kCsSteps; s++) {
             const uint32_t oc = (uint32_t)__builtin_amdgcn_readlane((int)rec_oc, s);
             const uint32_t g = (uint32_t)__builtin_amdgcn_readlane((int)d_off, s);
-            cs_emit_word<SYNC>(clo[s], ilo[s], lane, region_m1, sm.sel, srs, oc, g, t0);
-            cs_emit_word<SYNC>(chi[s], ihi[s], lane, region_m1, sm.sel, srs, oc, g + 64u, t0);
+            const uint32_t c = t0 - g;
+            const uint32_t d = (c - lane) & (kSyncWords - 1);
+            const uint32_t b = (lane + d - c) / (kSyncWords / 4u);
+            cs_emit_word<SYNC>(clo[s], ilo[s], region_m1, sm.sel, srs, oc, d, b);
+            cs_emit_word<SYNC>(chi[s], ihi[s], region_m1, sm.sel, srs, oc, d,
+                               b + 64u / (kSyncWords / 4u));
 #if LEAN_SCHED
             __builtin_amdgcn_sched_barrier(0);
 #endif

@@ -1087,22 +1087,33 @@ __device__ __forceinline__ void spec_tile(SM& S, uint64_t ca, uint32_t nc,
 // 16 chunks, 4 for up to 64), one thread each, so a chunk's ~117-record
 // chain becomes S chains of ~117 / S records and all four waves walk
 // (the serial walker used 16 lanes of one wave for the whole chain).
-//   1. spec: thread (c, j) walks from its segment's first byte (j = 0: the
-//      chunk start, exact) until it passes the segment end; it keeps the
-//      first kSegK record starts it visits with the words before each, its
-//      exit (first record start at or past the segment end) and its words;
-//   2. meet: the true entry of segment j is the exit of segment j - 1.  Tag
-//      chains couple within a few records (a record is 1-10 bytes), so the
-//      entry is normally among the first kSegK starts segment j visited:
-//      from there its walk is the exact one, its exit stands and its words
-//      drop those before the entry.  The chunk is exact if every entry meets
-//      and the last exit is the chunk's packed end with exactly its words;
-//      otherwise (a long literal run across segments, a malformed chunk)
-//      the chunk takes the exact serial walk, as with a bad sync index;
+//   1. spec: thread (c, j) walks from its segment's first byte sb until it
+//      passes the segment end se, keeping the first kSegM record starts it
+//      visits (with the words before each) and its exit.  j = 0 starts at
+//      the chunk start: its walk is the true one.
+//   2. couple: the true entry of segment j is the exit of segment j - 1.
+//      The thread walks the true chain from its entry until that chain
+//      lands on one of its kept starts (the two chains coincide from there:
+//      exit and words follow from the spec walk) or passes se (the true exit
+//      is where it stopped).  The result is exact for an exact entry; a
+//      segment whose exit changed makes its successor walk again from the
+//      new entry, round after round, until no exit changes (segment 0 is
+//      exact, so round r leaves segments <= r exact).  Random record chains
+//      couple within a few records: on config-2 data 1-3 walks of ~3 hops.
+//      A chunk is exact if its last exit is its packed end with exactly its
+//      words and no record ran past the end; otherwise (malformed input) it
+//      takes the exact serial walk for the status.
 //   3. desc: word bases by a scan of the segment words; each thread writes
 //      the descriptors of its records, from its entry to its exit.
 // Speculation changes the speed only, never the result.
-constexpr uint32_t kSegK = 4;
+#ifndef UNPACK_SEG_COUPLE
+#define UNPACK_SEG_COUPLE 0  // 1: exact walks stop where they meet the spec walk (kept starts)
+#endif
+#ifndef UNPACK_SEG_KEEP
+#define UNPACK_SEG_KEEP 16
+#endif
+constexpr uint32_t kSegM = UNPACK_SEG_KEEP;  // spec starts kept per segment (UNPACK_SEG_COUPLE)
+constexpr uint32_t kSegNone = 0xFFFFu;       // exit of a spec walk that ran past the chunk
 
 __device__ __forceinline__ void seg_hop(const uint8_t* B, uint32_t& p, uint32_t& w, uint32_t pe,
                                         bool& err) {
@@ -1135,52 +1146,87 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
         sb = cs + (uint32_t)(((uint64_t)len * j) >> lg);
         se = cs + (uint32_t)(((uint64_t)len * (j + 1u)) >> lg);
     }
-    // 1. spec walk from sb while p < se, the first kSegK starts kept
+    // 1. spec walk
     uint32_t p = sb, w = 0;
-    bool err = false;
-    uint32_t kl[kSegK];  // start | words before it << 16 (0xFFFFFFFF: none)
+    bool serr = false;
+#if UNPACK_SEG_COUPLE
+    uint32_t hl[kSegM];  // start | words before it << 16
+    uint32_t nh = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < kSegK; i++) {
-        const bool go = act && p < se && !err;
-        kl[i] = go ? (p | (w << 16)) : 0xFFFFFFFFu;
-        if (go) seg_hop(S.bytes, p, w, pe, err);
+    for (uint32_t i = 0; i < kSegM; i++) {
+        const bool go = act && p < se && !serr;
+        hl[i] = p | (w << 16);
+        if (go) {
+            seg_hop(S.bytes, p, w, pe, serr);
+            nh++;
+        }
     }
-    while (act && p < se && !err) seg_hop(S.bytes, p, w, pe, err);
-    const uint32_t x = p;
-    if (act) S.so.bx[tid] = (uint16_t)x;
-    __syncthreads();
-    // 2. meet: entry = the previous segment's exit
-    const uint32_t e = (!act || j == 0) ? sb : (uint32_t)S.so.bx[tid - 1];
-    uint32_t wd = w;   // words from the entry to the exit
-    bool ok = !err;
-    if (act && j > 0) {
-        bool hit = false;
-        uint32_t before = 0;
+#endif
+    while (act && p < se && !serr) seg_hop(S.bytes, p, w, pe, serr);
+    const uint32_t xs = serr ? kSegNone : p, ws = w;
+    // 2. exact walks from the entries, in rounds within the wave (a chunk's
+    // segments are nseg consecutive lanes); segment 0's spec walk is the
+    // true one.  Each round the entries come from a prefix max of the
+    // segments' own exits (an exit is never below its entry): a segment
+    // whose entry lies past its end owns no exit (0) and passes its entry
+    // on, so a record covering several segments settles them all in one
+    // round, however often its start moves.  At the fixed point every exit
+    // is its segment's walk from its predecessor's exit, and every round
+    // settles at least one more segment: at most S + 1 rounds.
+    uint32_t own = xs, x = xs, wd = ws;  // own: this segment's exit from e_used
+    bool err = j == 0 && serr;
+    uint32_t e_used = j == 0 ? sb : ~0u;
+    for (;;) {
+        const uint32_t xu = (uint32_t)__shfl_up((int)x, 1, 64);
+        const uint32_t e = j == 0 ? sb : xu;
+        const bool need = act && e != e_used;
+        if (ballot64(need) == 0) break;
+        if (need) {
+            e_used = e;
+            uint32_t q = e, wt = 0;
+            bool terr = false;
+#if UNPACK_SEG_COUPLE
+            // (the spec chain from one of its kept starts on is the true one)
+            bool coupled = false;
+            uint32_t wc = 0;
+            while (q < se && !terr) {
 #pragma unroll
-        for (uint32_t i = 0; i < kSegK; i++) {
-            const bool h = (kl[i] & 0xFFFFu) == e && kl[i] != 0xFFFFFFFFu;
-            before = h ? (kl[i] >> 16) : before;
-            hit = hit || h;
+                for (uint32_t i = 0; i < kSegM; i++) {
+                    const bool h = i < nh && (hl[i] & 0xFFFFu) == q;
+                    wc = h ? (hl[i] >> 16) : wc;
+                    coupled = coupled || h;
+                }
+                if (coupled) break;
+                seg_hop(S.bytes, q, wt, pe, terr);
+            }
+            if (coupled) {
+                q = xs;
+                wt += ws - wc;
+                terr = serr;
+            }
+#else
+            while (q < se && !terr) seg_hop(S.bytes, q, wt, pe, terr);
+#endif
+            own = terr ? kSegNone : (e >= se ? 0u : q);
+            wd = wt;
+            err = terr || e == kSegNone;
         }
-        // (an entry at or past the exit: the previous segment's last record
-        // covers this whole segment; only a spec walk that stopped exactly
-        // there can continue it)
-        if (!hit && e == x) {
-            hit = true;
-            before = w;
+        x = own;
+        for (uint32_t d = 1; d < nseg; d <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)x, d, 64);
+            if (j >= d) x = max(x, t);
         }
-        ok = ok && hit;
-        wd = w - before;
     }
+    const uint32_t e = e_used;
     // chunk: segments (c, 0..S-1) are nseg consecutive threads of one wave
-    // (S <= 16 divides 64): inclusive scan of wd within the group, all ok,
+    // (S <= 16 divides 64): inclusive scan of wd within the group, no error,
     // and the last exit at the packed end
     uint32_t incl = wd;
     for (uint32_t d = 1; d < nseg; d <<= 1) {
         const uint32_t t = (uint32_t)__shfl_up((int)incl, d, 64);
         if (j >= d) incl += t;
     }
-    const uint64_t bad_m = ballot64(act && !ok);
+    const uint64_t bad_m = ballot64(act && err);
     const uint32_t gl = lane & ~(nseg - 1u);  // first lane of the group
     const uint64_t gm = ((nseg == 64u) ? ~0ull : ((1ull << nseg) - 1ull)) << gl;
     const uint32_t tot = (uint32_t)__shfl((int)incl, (int)(gl + nseg - 1u), 64);

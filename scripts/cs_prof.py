@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--sync", action="store_true")
     ap.add_argument("--lib", default="")
+    ap.add_argument("--pipe", action="store_true",
+                    help="pack_pipe_kernel's trace layout (CAPNP_PACK_PIPE on)")
     a = ap.parse_args()
     import torch
     from capnp_amd import Context
@@ -76,18 +78,29 @@ def main():
         T = trace.view(ntiles, 8).cpu().numpy().astype(np.int64)
         t0 = T[:, 0].min()
         span = (T[:, 5].max() - t0) / 100.0
-        ph = ["load", "pass1+pub", "pass2", "lookback", "copyout"]
-        means = [(T[:, k + 1] - T[:, k]).mean() / 100.0 for k in range(5)]
-        life = (T[:, 5] - T[:, 0]).mean() / 100.0
+        if a.pipe:
+            # [6] iteration start, [0] wave 0's pass 1 done, [1] published, [2] pass 2 done,
+            # [3] look-back start (next iteration), [4] offset known, [5] copied out
+            order = [6, 0, 1, 2, 3, 4, 5]
+            ph = ["words+pass1(w0)", "barrier+pub", "retire-prev+pass2", "next-pass1", "lookback",
+                  "copyout"]
+            t0 = T[:, 6].min()
+            span = (T[:, 5].max() - t0) / 100.0
+        else:
+            order = [0, 1, 2, 3, 4, 5]
+            ph = ["load", "pass1+pub", "pass2", "lookback", "copyout"]
+        means = [(T[:, order[k + 1]] - T[:, order[k]]).mean() / 100.0 for k in range(len(ph))]
+        life = (T[:, 5] - T[:, order[0]]).mean() / 100.0
         # average tiles in each phase over the launch = sum of durations / span
-        inflight = [(T[:, k + 1] - T[:, k]).sum() / 100.0 / span for k in range(5)]
-        starts = np.sort(T[:, 0] - t0) / 100.0
+        inflight = [(T[:, order[k + 1]] - T[:, order[k]]).sum() / 100.0 / span
+                    for k in range(len(ph))]
+        starts = np.sort(T[:, order[0]] - t0) / 100.0
         print(f"iter {it}: {e0.elapsed_time(e1) * 1e3:.1f} us (traced span {span:.1f}) ok={ok} "
               f"tiles={ntiles} lifetime {life:.2f} us")
         print("   phase us : " + "  ".join(f"{p} {m:.2f}" for p, m in zip(ph, means)))
         print("   in flight: " + "  ".join(f"{p} {x:.0f}" for p, x in zip(ph, inflight))
               + f"  (total {sum(inflight):.0f})")
-        q = np.percentile(T[:, 5] - T[:, 0], [10, 50, 90]) / 100.0
+        q = np.percentile(T[:, 5] - T[:, order[0]], [10, 50, 90]) / 100.0
         print(f"   lifetime p10/p50/p90 {q[0]:.2f}/{q[1]:.2f}/{q[2]:.2f} us; "
               f"first start->last start {starts[-1] - starts[0]:.1f} us")
 
