@@ -1087,45 +1087,37 @@ __device__ __forceinline__ void spec_tile(SM& S, uint64_t ca, uint32_t nc,
 // 16 chunks, 4 for up to 64), one thread each, so a chunk's ~117-record
 // chain becomes S chains of ~117 / S records and all four waves walk
 // (the serial walker used 16 lanes of one wave for the whole chain).
-//   1. spec: thread (c, j) walks from its segment's first byte sb until it
-//      passes the segment end se, keeping the first kSegM record starts it
-//      visits (with the words before each) and its exit.  j = 0 starts at
-//      the chunk start: its walk is the true one.
-//   2. couple: the true entry of segment j is the exit of segment j - 1.
-//      The thread walks the true chain from its entry until that chain
-//      lands on one of its kept starts (the two chains coincide from there:
-//      exit and words follow from the spec walk) or passes se (the true exit
-//      is where it stopped).  The result is exact for an exact entry; a
-//      segment whose exit changed makes its successor walk again from the
-//      new entry, round after round, until no exit changes (segment 0 is
-//      exact, so round r leaves segments <= r exact).  Random record chains
-//      couple within a few records: on config-2 data 1-3 walks of ~3 hops.
-//      A chunk is exact if its last exit is its packed end with exactly its
-//      words and no record ran past the end; otherwise (malformed input) it
-//      takes the exact serial walk for the status.
+//   1. spec: thread (c, j) walks from kSegOverlap bytes before its segment
+//      start sb until it passes the segment end se, and keeps its first
+//      record start at or past sb (f) and its exit.  Tag chains from
+//      different starts couple within tens of bytes, so by sb the chain is
+//      mostly the true one already.  j = 0 starts at the chunk start.
+//   2. meet / repair: the true entry of segment j is the exit of segment
+//      j - 1.  If the spec chain passes through it (f = entry), its exit and
+//      words stand; otherwise the thread walks exactly from the entry.  A
+//      segment whose exit changed makes its successor check again, round
+//      after round within the wave, until no exit changes.  On config-2 data
+//      4 % of the segments miss (16 % with no lead-in), so most waves need
+//      one repair round.  A chunk is exact if its last exit is its packed
+//      end with exactly its words and no record ran past the end; otherwise
+//      (malformed input) it takes the exact serial walk for the status.
 //   3. desc: word bases by a scan of the segment words; each thread writes
 //      the descriptors of its records, from its entry to its exit.
 // Speculation changes the speed only, never the result.
-#ifndef UNPACK_SEG_COUPLE
-#define UNPACK_SEG_COUPLE 0  // 1: exact walks stop where they meet the spec walk (kept starts)
+#ifndef UNPACK_SEG_OVERLAP
+#define UNPACK_SEG_OVERLAP 48  // config 2 nosync: 0 -> 724 us, 16 -> 699, 32 -> 646, 48 -> 614, 64 -> 640
 #endif
-#ifndef UNPACK_SEG_KEEP
-#define UNPACK_SEG_KEEP 16
-#endif
-constexpr uint32_t kSegM = UNPACK_SEG_KEEP;  // spec starts kept per segment (UNPACK_SEG_COUPLE)
-constexpr uint32_t kSegNone = 0xFFFFu;       // exit of a spec walk that ran past the chunk
+constexpr uint32_t kSegOverlap = UNPACK_SEG_OVERLAP;  // spec walk lead-in (bytes)
 
-__device__ __forceinline__ void seg_hop(const uint8_t* B, uint32_t& p, uint32_t& w, uint32_t pe,
-                                        bool& err) {
+// One record hop (the walk's loops stop once p >= the segment end, so a
+// record running past the chunk end shows as p > pe at the stop).
+__device__ __forceinline__ void seg_hop(const uint8_t* B, uint32_t& p, uint32_t& w) {
     uint32_t tag, b1, b9;
     rec_bytes(B, p + 1u, tag, b1, b9);
     const bool isz = tag == 0, isf = tag == 0xFF;
     const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
-    const uint32_t q = p + 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) +
-                       (isf ? 8u * cnt : 0u);
-    err = err || q > pe;
+    p += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) + (isf ? 8u * cnt : 0u);
     w += 1u + cnt;
-    p = q;
 }
 
 template <class SM>
@@ -1146,36 +1138,39 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
         sb = cs + (uint32_t)(((uint64_t)len * j) >> lg);
         se = cs + (uint32_t)(((uint64_t)len * (j + 1u)) >> lg);
     }
-    // 1. spec walk
-    uint32_t p = sb, w = 0;
-    bool serr = false;
-#if UNPACK_SEG_COUPLE
-    uint32_t hl[kSegM];  // start | words before it << 16
-    uint32_t nh = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kSegM; i++) {
-        const bool go = act && p < se && !serr;
-        hl[i] = p | (w << 16);
-        if (go) {
-            seg_hop(S.bytes, p, w, pe, serr);
-            nh++;
-        }
-    }
+    // 1. spec walk from kSegOverlap bytes before the segment (the chain
+    // couples with the true one on the way in, mostly): f = its first start
+    // at or past sb and the words before it, x = its exit
+    const uint32_t s0 = j == 0 ? sb : max(cs, sb >= kSegOverlap ? sb - kSegOverlap : 0u);
+    uint32_t p = s0, w = 0;
+    while (act && p < sb) seg_hop(S.bytes, p, w);
+    const uint32_t f = p, wf = w;
+    while (act && p < se) seg_hop(S.bytes, p, w);
+    const bool serr = p > pe;  // (a record past the chunk end: garbage, or j = 0's error)
+    const uint32_t xs = serr ? 0u : p, ws = w - wf;
+#if UNPACK_PROF
+    if (tid == 0 && g_utrace) g_utrace[blockIdx.x * 8 + 5] = __builtin_amdgcn_s_memrealtime();
 #endif
-    while (act && p < se && !serr) seg_hop(S.bytes, p, w, pe, serr);
-    const uint32_t xs = serr ? kSegNone : p, ws = w;
-    // 2. exact walks from the entries, in rounds within the wave (a chunk's
-    // segments are nseg consecutive lanes); segment 0's spec walk is the
-    // true one.  Each round the entries come from a prefix max of the
-    // segments' own exits (an exit is never below its entry): a segment
-    // whose entry lies past its end owns no exit (0) and passes its entry
-    // on, so a record covering several segments settles them all in one
-    // round, however often its start moves.  At the fixed point every exit
-    // is its segment's walk from its predecessor's exit, and every round
-    // settles at least one more segment: at most S + 1 rounds.
+    // 2. meet and repair, in rounds within the wave (a chunk's segments are
+    // nseg consecutive lanes).  A segment whose spec chain passes through
+    // its entry (f = the previous exit) continues the true chain: its exit
+    // and words stand.  Otherwise it walks exactly from the entry.  The
+    // entries come from a prefix max of the segments' own exits (an exit is
+    // never below its entry): a segment whose entry lies past its end owns
+    // no exit (0) and passes its entry on, so a record covering several
+    // segments settles them all in one round.  A walk that ran past the
+    // chunk end owns no exit either (its error flag fails the chunk), so a
+    // garbage spec chain cannot hold back the segments after it.  At the
+    // fixed point every exit is its segment's walk from its predecessor's
+    // exit, and every round settles at least one more segment: at most S + 1
+    // rounds.
     uint32_t own = xs, x = xs, wd = ws;  // own: this segment's exit from e_used
     bool err = j == 0 && serr;
     uint32_t e_used = j == 0 ? sb : ~0u;
+    for (uint32_t d = 1; d < nseg; d <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)x, d, 64);
+        if (j >= d) x = max(x, t);
+    }
     for (;;) {
         const uint32_t xu = (uint32_t)__shfl_up((int)x, 1, 64);
         const uint32_t e = j == 0 ? sb : xu;
@@ -1183,33 +1178,17 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
         if (ballot64(need) == 0) break;
         if (need) {
             e_used = e;
-            uint32_t q = e, wt = 0;
-            bool terr = false;
-#if UNPACK_SEG_COUPLE
-            // (the spec chain from one of its kept starts on is the true one)
-            bool coupled = false;
-            uint32_t wc = 0;
-            while (q < se && !terr) {
-#pragma unroll
-                for (uint32_t i = 0; i < kSegM; i++) {
-                    const bool h = i < nh && (hl[i] & 0xFFFFu) == q;
-                    wc = h ? (hl[i] >> 16) : wc;
-                    coupled = coupled || h;
-                }
-                if (coupled) break;
-                seg_hop(S.bytes, q, wt, pe, terr);
+            if (e == f) {
+                own = xs;
+                wd = ws;
+                err = serr;
+            } else {
+                uint32_t q = e, wt = 0;
+                while (q < se) seg_hop(S.bytes, q, wt);
+                err = q > pe;
+                own = (err || e >= se) ? 0u : q;
+                wd = wt;
             }
-            if (coupled) {
-                q = xs;
-                wt += ws - wc;
-                terr = serr;
-            }
-#else
-            while (q < se && !terr) seg_hop(S.bytes, q, wt, pe, terr);
-#endif
-            own = terr ? kSegNone : (e >= se ? 0u : q);
-            wd = wt;
-            err = terr || e == kSegNone;
         }
         x = own;
         for (uint32_t d = 1; d < nseg; d <<= 1) {
@@ -1218,6 +1197,9 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
         }
     }
     const uint32_t e = e_used;
+#if UNPACK_PROF
+    if (tid == 0 && g_utrace) g_utrace[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+#endif
     // chunk: segments (c, 0..S-1) are nseg consecutive threads of one wave
     // (S <= 16 divides 64): inclusive scan of wd within the group, no error,
     // and the last exit at the packed end
@@ -1247,6 +1229,9 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
             q += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) + (isf ? 8u * cnt : 0u);
         }
     }
+#if UNPACK_PROF
+    if (tid == 0 && g_utrace) g_utrace[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+#endif
     __syncthreads();
     if (tid < nc) {
         const uint64_t cc = ca + tid;

@@ -90,8 +90,10 @@ def main():
               f"global={(~st).sum()} per tile: stage={d(0, 1):.2f}us walk={d(1, 2):.2f}us "
               f"expand={d(2, 3):.2f}us life={life.mean():.2f}us "
               f"concurrency={life.sum() / max(span, 1e-9):.0f} "
-              f"phaseB-iters={T[st, 5].mean():.2f} walk_segment={T[st, 6].mean():.0f}cyc "
-              f"phaseA={T[st, 7].mean():.0f}cyc")
+              + (f"phaseB-iters={T[st, 5].mean():.2f} walk_segment={T[st, 6].mean():.0f}cyc "
+                 f"phaseA={T[st, 7].mean():.0f}cyc" if a.sync else
+                 f"| wave 0: spec={d(1, 5):.2f}us rounds={d(5, 6):.2f}us desc={d(6, 7):.2f}us "
+                 f"status+barrier={d(7, 2):.2f}us"))
 
 if __name__ == "__main__":
     main()

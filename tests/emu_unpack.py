@@ -1,6 +1,7 @@
 """Emulation of the index-free segment walk (csrc/unpack.hip spec_seg_tile)
-on the CPU: test infrastructure that checks the walk's round logic (spec
-walk, coupling walks, prefix max of owned exits, pass-through segments)
+on the CPU: test infrastructure that checks the walk's round logic (led-in
+spec walk, meet check, repair walks, prefix max of owned exits,
+pass-through segments)
 against the true record chain, before any GPU run.  Not a decoder: it
 returns each segment's exit and words, which the kernel turns into
 descriptors."""
@@ -15,31 +16,31 @@ def record_hop(B, p, pe):
     return q, 1 + cnt, q > pe
 
 
-def seg_walk(B, L, S=16, M=16, couple=True):
-    """Chunk bytes B[0:L] (zero padded past L), S byte segments: returns
-    (exits, words, err, rounds) as the kernel computes them (couple: the
-    UNPACK_SEG_COUPLE build, whose exact walks stop on a kept spec start)."""
-    NONE = 0xFFFF
+def seg_walk(B, L, S=16, OV=32):
+    """Chunk bytes B[0:L] (zero padded past L), S byte segments, spec walks
+    led in by OV bytes: returns (exits, words, err, rounds) as the kernel
+    computes them."""
     sb = [(L * j) // S for j in range(S)]
     se = [(L * (j + 1)) // S for j in range(S)]
-    kept, xs, ws, serr = [], [], [], []
+    f, xs, ws, serr = [], [], [], []
     for j in range(S):  # 1. spec walks
-        p, w, e, kl = sb[j], 0, False, []
-        while p < se[j] and not e:
-            if len(kl) < M:
-                kl.append((p, w))
-            p, dw, er = record_hop(B, p, L)
+        p, w = (sb[j] if j == 0 else max(0, sb[j] - OV)), 0
+        while p < sb[j]:
+            p, dw, _ = record_hop(B, p, L)
             w += dw
-            e = e or er
-        kept.append(kl)
-        xs.append(NONE if e else p)
-        ws.append(w)
-        serr.append(e)
-    own, x, wd = list(xs), list(xs), list(ws)
+        fj, wf = p, w
+        while p < se[j]:
+            p, dw, _ = record_hop(B, p, L)
+            w += dw
+        f.append(fj)
+        serr.append(p > L)
+        xs.append(0 if p > L else p)
+        ws.append(w - wf)
+    own, x, wd = list(xs), [max(xs[:j + 1]) for j in range(S)], list(ws)
     err = [serr[0]] + [False] * (S - 1)
     used = [sb[0]] + [None] * (S - 1)
     rounds = 0
-    while True:  # 2. coupling rounds
+    while True:  # 2. meet / repair rounds
         ent = [sb[0]] + x[:-1]
         need = [j > 0 and ent[j] != used[j] for j in range(S)]
         if not any(need):
@@ -49,18 +50,16 @@ def seg_walk(B, L, S=16, M=16, couple=True):
             if not need[j]:
                 continue
             e = used[j] = ent[j]
-            q, wt, terr, coupled, wc = e, 0, False, False, 0
-            while q < se[j] and not terr:
-                hit = [w for (pp, w) in kept[j] if pp == q] if couple else []
-                if hit:
-                    coupled, wc = True, hit[0]
-                    break
-                q, dw, er = record_hop(B, q, L)
-                wt += dw
-                terr = terr or er
-            own[j] = xs[j] if coupled else (NONE if terr else (0 if e >= se[j] else q))
-            wd[j] = wt + (ws[j] - wc) if coupled else wt
-            err[j] = terr or (coupled and serr[j]) or e == NONE
+            if e == f[j]:
+                own[j], wd[j], err[j] = xs[j], ws[j], serr[j]
+            else:
+                q, wt = e, 0
+                while q < se[j]:
+                    q, dw, _ = record_hop(B, q, L)
+                    wt += dw
+                err[j] = q > L
+                own[j] = 0 if (err[j] or e >= se[j]) else q
+                wd[j] = wt
         x, m = [], 0
         for v in own:
             m = max(m, v)

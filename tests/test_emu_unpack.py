@@ -18,12 +18,12 @@ def _chunks(words, offs):
         yield B0[a:b + 2100], b - a, int(offs[c + 1] - offs[c])
 
 
-def _check(words, offs, max_rounds, couple=True):
+def _check(words, offs, max_rounds, ov=32):
     worst = 0
     for B, L, n in _chunks(words, offs):
         if L == 0:
             continue
-        x, wd, err, rounds = E.seg_walk(B, L, couple=couple)
+        x, wd, err, rounds = E.seg_walk(B, L, OV=ov)
         assert not any(err) and sum(wd) == n and x[-1] == L
         assert x == E.true_exits(B, L)
         worst = max(worst, rounds)
@@ -34,8 +34,8 @@ def test_segment_walk_config2_kinds():
     n, cw = 150, 128
     offs = np.arange(0, (n + 1) * cw, cw, dtype=np.uint64)
     for kind in (0, 1, 2):
-        for couple in (False, True):
-            _check(O.gen_fill(offs, kind0=kind, pz=O.PZ30), offs, 16, couple)
+        for ov in (0, 32):
+            _check(O.gen_fill(offs, kind0=kind, pz=O.PZ30), offs, 16, ov)
 
 
 def test_segment_walk_literal_and_zero_runs():
@@ -44,11 +44,11 @@ def test_segment_walk_literal_and_zero_runs():
     rng = np.random.default_rng(1)
     lit = rng.integers(1 << 56, 1 << 63, n * cw, dtype=np.uint64) * 2 + 1
     _check(lit, offs, 16)
-    _check(lit, offs, 16, False)
+    _check(lit, offs, 16, 0)
     z = np.zeros(n * cw, np.uint64)
     z[::37] = 5
     _check(z, offs, 16)
-    _check(z, offs, 16, False)
+    _check(z, offs, 16, 0)
     # literal runs of every length placed across segment boundaries
     w = np.zeros(n * cw, np.uint64)
     for c in range(n):
@@ -56,4 +56,4 @@ def test_segment_walk_literal_and_zero_runs():
         w[c * cw + 3:c * cw + 3 + k] = 0x1112131415161718
         w[c * cw + 3 + k::7][:4] = 0x0000000100000001
     _check(w, offs, 16)
-    _check(w, offs, 16, False)
+    _check(w, offs, 16, 0)
