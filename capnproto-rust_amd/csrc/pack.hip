@@ -1085,7 +1085,11 @@ __device__ uint64_t tile_aggregate(const LookbackArgs& A, uint64_t j, uint32_t l
 // microseconds after another XCD's store.  Measured alternatives (round 1,
 // config 2): hipMalloc'd records 1154 us/launch, uncached 748 us; adding
 // per-group atomic totals (memory-side atomics) 2295 us; issuing the first
-// polls before pass 2 822 us.
+// polls before pass 2 822 us.  Round 3 (pack_cs_kernel, config 2): polling
+// the group's tiles and the group window together, one round trip when all
+// is published, 524 vs 506 us (the tile's wait is the group chain, not the
+// polls); a persistent grid pipelining each tile's look-back behind the next
+// tile's pass 1 (4 workgroups per CU) 1262 vs 472 us.
 //
 // Every wait is bounded: on timeout the waiter computes the missing aggregate
 // itself from the input (records are idempotent), so the kernel finishes with
