@@ -48,6 +48,7 @@ EXPORTS = [
     "capnp_packed_reader_free", "capnp_packed_reader_read", "capnp_packed_reader_read_exact",
     "capnp_packed_reader_read_message", "capnp_packed_reader_buffered",
     "capnp_gpu_find_messages",
+    "capnp_gpu_read_message_stream",
 ]
 
 
@@ -152,6 +153,10 @@ def lib():
                                                    vp, C.POINTER(C.c_uint32),
                                                    C.POINTER(C.c_uint64)]
     L.capnp_gpu_find_messages.argtypes = [vp, vp, sz, sz, vp, C.POINTER(C.c_size_t), vp]
+    L.capnp_gpu_read_message_stream.argtypes = [
+        vp, vp, sz, C.POINTER(ReaderOptionsC), vp, sz, vp, vp, sz, vp, sz, vp,
+        C.POINTER(C.c_size_t), C.POINTER(C.c_int32), C.POINTER(C.c_size_t),
+        C.POINTER(C.c_size_t), C.POINTER(C.c_size_t), vp]
     L.capnp_unpack_wt_stats.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     L.capnp_unpack_wt_stats.restype = C.c_int
     L.capnp_packed_reader_buffered.argtypes = [vp]

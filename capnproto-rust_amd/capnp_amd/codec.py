@@ -277,38 +277,79 @@ class Context:
             out.append((p, cons[k]))
         return out, 0
 
+    def decode_stream(self, packed, limit=8 * 1024 * 1024, words_cap=None, msgs_cap=None,
+                      segs_cap=None, stream=None):
+        """try_read_message's loop over one device stream in one pass
+        (capnp_gpu_read_message_stream): the stream is decoded once and its
+        messages described in place.  -> (words, msg_byte_off, body_word_off,
+        seg_words, msg_seg_off, nmsg, clean) as device tensors (nmsg + 1
+        entries for the offset lists): message m's segments start at word
+        body_word_off[m] of words, with lengths seg_words[msg_seg_off[m]:
+        msg_seg_off[m + 1]]; clean = the loop ended at the end of the stream.
+        Capacities None are guessed (decoded words: twice the packed words)
+        and grown to what the library reports on
+        CAPNP_E_BUFFER_NOT_LARGE_ENOUGH (each retry decodes again)."""
+        import torch
+        dev = packed.device
+        nb = int(packed.numel())
+        wc = int(words_cap if words_cap is not None else nb // 4 + 64)
+        mc = int(msgs_cap if msgs_cap is not None else nb // 1024 + 64)
+        sc = int(segs_cap if segs_cap is not None else mc)
+        o = _lib.ReaderOptionsC(int(limit or 0), 1 if limit is not None else 0, 64)
+        for _ in range(4):
+            words = torch.empty(max(wc, 1), dtype=torch.int64, device=dev)
+            mbo = torch.empty(mc + 1, dtype=torch.int64, device=dev)
+            bwo = torch.empty(max(mc, 1), dtype=torch.int64, device=dev)
+            segw = torch.empty(max(sc, 1), dtype=torch.int64, device=dev)
+            mso = torch.empty(mc + 1, dtype=torch.int64, device=dev)
+            n, cl = C.c_size_t(0), C.c_int32(0)
+            wn, mn, sn = C.c_size_t(0), C.c_size_t(0), C.c_size_t(0)
+            st = _lib.lib().capnp_gpu_read_message_stream(
+                self._h, _ptr(packed) if nb else None, nb, C.byref(o), _ptr(words), wc,
+                _ptr(mbo), _ptr(bwo), mc, _ptr(segw), sc, _ptr(mso), C.byref(n), C.byref(cl),
+                C.byref(wn), C.byref(mn), C.byref(sn), self._stream(stream))
+            if st == 9:  # CAPNP_E_BUFFER_NOT_LARGE_ENOUGH: grow and decode again
+                wc, mc, sc = max(wc, wn.value), max(mc, mn.value), max(sc, sn.value)
+                continue
+            _check(st, self._h)
+            k = n.value
+            return (words, mbo[:k + 1], bwo[:k], segw[:int(mso[k].item()) if k else 0],
+                    mso[:k + 1], k, bool(cl.value))
+        raise _lib.CapnpError(9, "read_message_stream: capacities did not settle")
+
     def read_message_stream(self, packed, limit=8 * 1024 * 1024, stream=None, max_msgs=None):
         """serialize_packed::try_read_message in a loop over one device
         stream until it returns None or fails (serialize.rs:310-325).
         -> (messages, end): messages = list of (segment word arrays as device
         tensors, consumed bytes) in stream order; end = CAPNP_NONE (1) after
         a clean end, else the status of the try_read_message that failed.
-        Discovery runs in rounds of at most `max_msgs` messages (default
-        bytes // 8 + 1); a round stopped by its cap continues where it
-        stopped, and where the walk stops early the next message is read as
-        the loop's next try_read_message, which fails as the reference does or
-        succeeds and the loop goes on after it."""
+        One pass (decode_stream) finds and describes the messages; where it
+        stops short of a clean end, the next message is read as the loop's
+        next try_read_message (capnp_gpu_read_messages), which fails as the
+        reference does, or succeeds and the loop goes on after it.
+        max_msgs caps the messages one pass lists (None: no cap)."""
         import torch
         nb = int(packed.numel())
         out, start = [], 0
         while start < nb:
             view = packed[start:]
             rest = nb - start
-            cap = int(max_msgs) if max_msgs is not None else rest // 8 + 1
-            offs, n = self.find_messages(view, rest, max_msgs=cap, stream=stream)
-            stop = int(offs[n].item())
-            if n:
-                msgs, bad = self._read_ranges(view, offs, limit, stream)
-                out += msgs
-                if bad:
-                    return out, bad
-            if stop >= rest:
+            words, mbo, bwo, segw, mso, n, clean = self.decode_stream(
+                view, limit=limit, msgs_cap=max_msgs, stream=stream)
+            mbo_h, bwo_h, mso_h = mbo.cpu().tolist(), bwo.cpu().tolist(), mso.cpu().tolist()
+            seg_h = segw.cpu().tolist()
+            for k in range(n):
+                a, p = bwo_h[k], []
+                for j in range(mso_h[k], mso_h[k + 1]):
+                    ln = seg_h[j]
+                    p.append(words[a:a + ln])
+                    a += ln
+                out.append((p, mbo_h[k + 1] - mbo_h[k]))
+            stop = mbo_h[n]
+            if clean or stop >= rest:
                 break
-            if n == cap:  # the round's cap, not the stream, stopped the walk
-                start += stop
-                continue
-            # the walk stopped at `stop`: one try_read_message from there
-            tail = torch.tensor([stop, rest], dtype=torch.int64, device=offs.device)
+            # the loop's next try_read_message, from `stop`
+            tail = torch.tensor([stop, rest], dtype=torch.int64, device=packed.device)
             msgs, bad = self._read_ranges(view, tail, limit, stream)
             if bad:
                 return out, bad
@@ -386,8 +427,10 @@ class Context:
     def gen_carsales(self, words, skip_requests=0, stream=None):
         """Fill `words` (int64, HBM) with the reference benchmark's carsales
         request stream (capnp_gpu_gen_carsales) -> host list of request word
-        offsets (nreq + 1 entries; the last request may be cut at
-        words.numel())."""
+        offsets (nreq + 1 entries).  The last request is cut at
+        words.numel(), but its end offset is the uncut request's (it may
+        exceed words.numel(): use the first nreq - 1 requests as whole
+        messages)."""
         import numpy as np
         total = words.numel()
         cap = total // 3 + 2

@@ -68,6 +68,18 @@ extern "C" uint64_t capnp_carsales_plan(const uint32_t*, uint64_t, uint64_t, uin
 extern "C" hipError_t capnp_launch_gen_carsales(uint64_t*, uint64_t, const uint32_t*,
                                                 const uint64_t*, uint64_t, hipStream_t);
 extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes);
+extern "C" size_t capnp_msg_chain_ws_bytes(uint64_t words_cap);
+extern "C" hipError_t capnp_resync_read_stream(const uint8_t*, uint64_t, uint64_t, uint64_t*,
+                                               uint64_t*, uint64_t, uint64_t*, uint64_t*,
+                                               uint64_t*, int*, void*, size_t, hipStream_t,
+                                               uint64_t*);
+extern "C" hipError_t capnp_launch_msg_meta(const uint64_t*, const uint64_t*, uint64_t, uint64_t,
+                                            int, uint64_t*, uint64_t*, uint64_t*, hipStream_t);
+extern "C" hipError_t capnp_launch_msg_seglist(const uint64_t*, const uint64_t*, uint64_t,
+                                               const uint64_t*, uint64_t*, hipStream_t);
+extern "C" hipError_t capnp_scan_counts(const uint64_t*, uint64_t, uint64_t*, void*, size_t,
+                                        hipStream_t);
+extern "C" size_t capnp_scan_counts_tmp_bytes(uint64_t n);
 extern "C" size_t capnp_unpack_wt_ws_bytes(uint64_t wlo, uint64_t whi);
 extern "C" uint64_t capnp_pack_wt_tiles(uint64_t wlo, uint64_t whi);
 extern "C" size_t capnp_pack_wt_ws_bytes(uint64_t wlo, uint64_t whi);
@@ -1131,10 +1143,11 @@ capnp_status capnp_gpu_find_messages(capnp_ctx* ctx, const uint8_t* d_packed, si
     for (;;) {
         const uint64_t rest = nbytes - start;
         if (rest == 0 || found == max_msgs) break;
-        const size_t ws = capnp_resync_ws_bytes(1, rest) + 8 * (max_msgs - found + 16) + 4096;
+        uint64_t words_cap = ctx->stream_words_cap / 8, need = 0, m = 0;
+        const size_t ws = capnp_resync_ws_bytes(1, rest) + 8 * (max_msgs - found + 16) + 4096 +
+                          capnp_msg_chain_ws_bytes(words_cap);
         capnp_status st = ensure_buf(ctx, &ctx->d_resync, &ctx->resync_cap, ws);
         if (st != CAPNP_OK) return st;
-        uint64_t words_cap = ctx->stream_words_cap / 8, need = 0, m = 0;
         int clean = 0;
         hipError_t e = capnp_resync_find_messages(d_packed + start, rest, max_msgs - found,
                                                   d_msg_byte_off + found,
@@ -1167,6 +1180,90 @@ capnp_status capnp_gpu_find_messages(capnp_ctx* ctx, const uint8_t* d_packed, si
     if (found == 0) HIP_TRY(hipMemcpyAsync(d_msg_byte_off, &start, 8, hipMemcpyHostToDevice, s));
     HIP_TRY(hipStreamSynchronize(s));
     *nmsg = found;
+    return CAPNP_OK;
+}
+
+// try_read_message in a loop over one packed stream, in one pass: the
+// stream is resolved and decoded once into the caller's d_words
+// (capnp_resync_read_stream: block walk, decode, message chain), and the
+// messages are described in place from their tables.  See the header.
+capnp_status capnp_gpu_read_message_stream(capnp_ctx* ctx, const uint8_t* d_packed,
+                                           size_t nbytes, const capnp_reader_options* opts,
+                                           uint64_t* d_words, size_t words_cap,
+                                           uint64_t* d_msg_byte_off, uint64_t* d_body_word_off,
+                                           size_t msgs_cap, uint64_t* d_seg_words,
+                                           size_t segs_cap, uint64_t* d_msg_seg_off,
+                                           size_t* nmsg, int32_t* clean, size_t* words_need,
+                                           size_t* msgs_need, size_t* segs_need, void* stream) {
+    if (!ctx || !nmsg || !clean || !d_msg_byte_off || !d_msg_seg_off || (nbytes && !d_packed) ||
+        (msgs_cap && !d_body_word_off) || (words_cap && !d_words))
+        return CAPNP_E_INVALID_ARGUMENT;
+    hipStream_t s = pick(ctx, stream);
+    *nmsg = 0;
+    *clean = 0;
+    if (words_need) *words_need = 0;
+    if (msgs_need) *msgs_need = 0;
+    if (segs_need) *segs_need = 0;
+    const capnp_reader_options o = opts ? *opts : capnp_default_reader_options();
+    // scratch: word starts [msgs_cap + 1], segment counts [msgs_cap], the
+    // first message over the traversal limit, the scan's temporary
+    const size_t scan_tmp = capnp_scan_counts_tmp_bytes(msgs_cap + 1);
+    const size_t o_ustart = 0, o_nseg = round16(8 * (msgs_cap + 1));
+    const size_t o_bad = o_nseg + round16(8 * (msgs_cap + 1));
+    const size_t o_tmp = o_bad + 16, o_end = o_tmp + round16(scan_tmp);
+    capnp_status st = ensure_buf(ctx, &ctx->d_stream_words, &ctx->stream_words_cap, o_end + 64);
+    if (st != CAPNP_OK) return st;
+    uint8_t* d = ctx->d_stream_words;
+    uint64_t* ustart = reinterpret_cast<uint64_t*>(d + o_ustart);
+    uint64_t* nseg = reinterpret_cast<uint64_t*>(d + o_nseg);
+    uint64_t* bad = reinterpret_cast<uint64_t*>(d + o_bad);
+    const size_t ws = capnp_resync_ws_bytes(1, nbytes) + 8 * (msgs_cap + 16) + 4096 +
+                      capnp_msg_chain_ws_bytes(words_cap);
+    st = ensure_buf(ctx, &ctx->d_resync, &ctx->resync_cap, ws);
+    if (st != CAPNP_OK) return st;
+    uint64_t m = 0, total = 0, wneed = 0;
+    int cl = 0;
+    hipError_t e = capnp_resync_read_stream(d_packed, nbytes, msgs_cap, d_msg_byte_off, d_words,
+                                            words_cap, ustart, &m, &total, &cl, ctx->d_resync,
+                                            ctx->resync_cap, s, &wneed);
+    if (e == hipErrorInvalidValue && wneed > words_cap) {
+        if (words_need) *words_need = wneed;
+        return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;
+    }
+    HIP_TRY(e);
+    if (total > msgs_cap) {  // (the lists hold msgs_cap; the chain has more)
+        if (words_need) *words_need = wneed;
+        if (msgs_need) *msgs_need = total;
+        return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;
+    }
+    // tables; a message over the traversal limit ends the loop there
+    const uint64_t none = ~0ull;
+    HIP_TRY(hipMemcpyAsync(bad, &none, 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(capnp_launch_msg_meta(d_words, ustart, m, o.traversal_limit_in_words,
+                                  o.has_traversal_limit != 0, d_body_word_off, nseg, bad, s));
+    uint64_t hbad = ~0ull;
+    HIP_TRY(hipMemcpyAsync(&hbad, bad, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (hbad < m) {
+        m = hbad;
+        cl = 0;
+    }
+    HIP_TRY(capnp_scan_counts(nseg, m, d_msg_seg_off, d + o_tmp, scan_tmp, s));
+    uint64_t nsegs = 0;
+    HIP_TRY(hipMemcpyAsync(&nsegs, d_msg_seg_off + m, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (nsegs > segs_cap || (nsegs && !d_seg_words)) {
+        if (words_need) *words_need = wneed;
+        if (segs_need) *segs_need = nsegs;
+        return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;
+    }
+    HIP_TRY(capnp_launch_msg_seglist(d_words, ustart, m, d_msg_seg_off, d_seg_words, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (words_need) *words_need = wneed;
+    if (msgs_need) *msgs_need = m;
+    if (segs_need) *segs_need = nsegs;
+    *nmsg = m;
+    *clean = cl;
     return CAPNP_OK;
 }
 

@@ -549,6 +549,268 @@ __global__ void k_msg_walk(const uint64_t* __restrict__ words, const uint64_t* _
     out[1] = u;
 }
 
+// ---------------------------------------------------------------------------
+// Message chain on the decoded words, in parallel (k_msg_walk's result).
+// try_read_message's loop is a chain over the words: message k's table gives
+// its length and so message k+1's start.  A 1 GiB stream of 12 KiB messages
+// is ~87 k dependent loads for one thread (tens of ms); here the words are cut
+// into kMsgRange-word ranges, one thread each:
+//   spec   thread t > 0 scans its range for the first word that starts a
+//          chain of kMsgVerify messages the loop would read (a body word
+//          passes one header check easily, pointers have small low halves,
+//          but not kMsgVerify in a row), then follows the chain to its first
+//          start at or past the range end (its exit), counting messages.
+//          Range 0 starts at word 0: its chain is the true one.  A chain that
+//          stops inside the range (a table the loop rejects, or the end of
+//          the words) exits kMsgStop | where it stopped.
+//   fix    rounds, as the unpack's segment walk: the entry of range t is the
+//          max of the ranges' own exits before it; a range whose spec start
+//          is its entry keeps its exit and count, another walks from the
+//          entry; an entry past the range end (a message longer than a
+//          range) or a stop passes through (owns no exit).  Rounds repeat
+//          until no entry changes; at that fixed point every exit is its
+//          range's walk from its predecessor's exit, by induction the serial
+//          chain's.
+//   list   exclusive scan of the counts; each range writes its messages'
+//          starts (ustart) as k_msg_walk does.
+constexpr uint64_t kMsgRange = 4096;
+constexpr uint32_t kMsgVerify = 16;
+constexpr uint64_t kMsgStop = 1ull << 63;
+constexpr uint64_t kMsgBad = ~0ull;
+constexpr int kMsgMaxRounds = 64;  // then the serial walk (k_msg_walk)
+
+// The start of the message after the one at word u, or kMsgBad if the loop
+// does not read a message at u (k_msg_walk's checks).
+__device__ __forceinline__ uint64_t msg_next(const uint64_t* __restrict__ words, uint64_t W,
+                                             uint64_t u) {
+    if (u >= W) return kMsgBad;
+    const uint64_t w0 = words[u];
+    const uint32_t nseg = (uint32_t)w0 + 1u;
+    if (nseg == 0 || nseg >= 512) return kMsgBad;
+    const uint64_t rest = nseg / 2;
+    if (u + 1 + rest > W) return kMsgBad;
+    uint64_t total = w0 >> 32;
+    for (uint64_t i = 1; i < nseg; i++) {
+        const uint64_t tw = words[u + 1 + (i - 1) / 2];
+        total += ((i - 1) & 1) ? (tw >> 32) : (tw & 0xFFFFFFFFull);
+    }
+    const uint64_t next = u + 1 + rest + total;
+    return (next > W || next < u) ? kMsgBad : next;
+}
+
+// Follows the chain from x while x < b: -> exit (kMsgStop | x if it stopped
+// first), *m = messages passed.
+__device__ __forceinline__ uint64_t msg_follow(const uint64_t* __restrict__ words, uint64_t W,
+                                               uint64_t x, uint64_t b, uint64_t* m) {
+    uint64_t k = 0;
+    while (x < b) {
+        const uint64_t n = msg_next(words, W, x);
+        if (n == kMsgBad) {
+            *m = k;
+            return kMsgStop | x;
+        }
+        x = n;
+        k++;
+    }
+    *m = k;
+    return x;
+}
+
+struct MsgRanges {
+    uint64_t* s;     // spec start (kMsgBad: none found)
+    uint64_t* xs;    // spec exit
+    uint64_t* ms;    // spec messages
+    uint64_t* own;   // exit from the entry used
+    uint64_t* eu;    // entry used
+    uint64_t* cnt;   // messages from the entry used
+    uint64_t* xmax;  // inclusive max of own
+    uint64_t* base;  // exclusive scan of cnt
+    int32_t* flag;   // [0]: a round changed an entry
+    void* tmp;
+    size_t tmp_bytes;
+};
+
+__global__ void __launch_bounds__(kThreads)
+k_msg_spec(const uint64_t* __restrict__ words, const uint64_t* __restrict__ res, uint64_t T,
+           MsgRanges R) {
+    const uint64_t t = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (t >= T) return;
+    const uint64_t W = res[0];
+    const uint64_t a = t * kMsgRange, b = min(a + kMsgRange, W);
+    uint64_t st = t == 0 ? 0 : kMsgBad;
+    for (uint64_t u = a; t > 0 && u < b; u++) {
+        uint64_t v = u;
+        uint32_t k = 0;
+        for (; k < kMsgVerify && v < W; k++) {
+            v = msg_next(words, W, v);
+            if (v == kMsgBad) break;
+        }
+        if (v != kMsgBad && (k == kMsgVerify || (v == W && k > 0))) {
+            st = u;
+            break;
+        }
+    }
+    uint64_t m = 0, x = 0;  // (no start found: owns no exit)
+    if (st != kMsgBad && a < W) x = msg_follow(words, W, st, b, &m);
+    R.s[t] = st;
+    R.xs[t] = x;
+    R.ms[t] = m;
+    R.own[t] = x;
+    R.eu[t] = kMsgBad;
+    R.cnt[t] = m;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_msg_round(const uint64_t* __restrict__ words, const uint64_t* __restrict__ res, uint64_t T,
+            MsgRanges R) {
+    const uint64_t t = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (t >= T) return;
+    const uint64_t W = res[0];
+    const uint64_t e = t == 0 ? 0 : R.xmax[t - 1];
+    if (e == R.eu[t]) return;
+    R.eu[t] = e;
+    R.flag[0] = 1;
+    const uint64_t a = t * kMsgRange, b = min(a + kMsgRange, W);
+    uint64_t own = 0, m = 0;
+    if ((e & kMsgStop) || e >= b || a >= W) {
+        own = 0;  // passes its entry on
+    } else if (e == R.s[t]) {
+        own = R.xs[t];
+        m = R.ms[t];
+    } else {
+        own = msg_follow(words, W, e, b, &m);
+    }
+    R.own[t] = own;
+    R.cnt[t] = m;
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_msg_list(const uint64_t* __restrict__ words, const uint64_t* __restrict__ res, uint64_t T,
+           MsgRanges R, uint64_t max_msgs, uint64_t* __restrict__ ustart) {
+    const uint64_t t = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (t >= T) return;
+    const uint64_t W = res[0];
+    const uint64_t a = t * kMsgRange, b = min(a + kMsgRange, W);
+    const uint64_t e = R.eu[t];
+    uint64_t k = R.base[t];
+    if (!(e & kMsgStop) && e < b && a < W) {
+        // (k == max_msgs included: the start where a capped list stops)
+        for (uint64_t x = e; x < b && k <= max_msgs; k++) {
+            const uint64_t n = msg_next(words, W, x);
+            if (n == kMsgBad) break;
+            ustart[k] = x;
+            x = n;
+        }
+    }
+}
+
+// The chain's end: its stop, or the last exit (>= W); capped at max_msgs
+// messages as k_msg_walk.
+__global__ void k_msg_end(const uint64_t* __restrict__ res, uint64_t T, MsgRanges R,
+                          uint64_t max_msgs, uint64_t* __restrict__ ustart,
+                          uint64_t* __restrict__ out, uint64_t* __restrict__ total_out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint64_t W = res[0];
+    const uint64_t total = R.base[T - 1] + R.cnt[T - 1];
+    const uint64_t xm = R.xmax[T - 1];
+    uint64_t stop = (xm & kMsgStop) ? (xm & ~kMsgStop) : (xm < W ? xm : W);
+    uint64_t n = total;
+    if (n > max_msgs) {
+        n = max_msgs;
+        stop = ustart[max_msgs];
+    }
+    ustart[n] = stop;
+    out[0] = n;
+    out[1] = stop;
+    total_out[0] = total;
+}
+
+struct MaxOp {
+    __device__ __forceinline__ uint64_t operator()(uint64_t a, uint64_t b) const {
+        return a > b ? a : b;
+    }
+};
+
+size_t msg_chain_tmp_bytes(uint64_t T) {
+    size_t a = 0, b = 0;
+    (void)hipcub::DeviceScan::InclusiveScan(nullptr, a, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                            MaxOp(), (int)T);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                           (int)T);
+    return (a > b ? a : b) + 256;
+}
+
+size_t msg_chain_carve(MsgRanges* R, uint8_t* base, uint64_t T) {
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        uint8_t* p = base ? base + off : nullptr;
+        off += (bytes + 255) & ~size_t(255);
+        return p;
+    };
+    R->s = (uint64_t*)take(8 * T);
+    R->xs = (uint64_t*)take(8 * T);
+    R->ms = (uint64_t*)take(8 * T);
+    R->own = (uint64_t*)take(8 * T);
+    R->eu = (uint64_t*)take(8 * T);
+    R->cnt = (uint64_t*)take(8 * T);
+    R->xmax = (uint64_t*)take(8 * T);
+    R->base = (uint64_t*)take(8 * T);
+    R->flag = (int32_t*)take(16);
+    R->tmp_bytes = msg_chain_tmp_bytes(T);
+    R->tmp = take(R->tmp_bytes);
+    return off;
+}
+
+// (the ranges for a decoded stream of at most W words)
+uint64_t msg_ranges(uint64_t W) { return W / kMsgRange + 1; }
+
+size_t msg_chain_ws_bytes(uint64_t W) {
+    MsgRanges R;
+    return msg_chain_carve(&R, nullptr, msg_ranges(W)) + 256;
+}
+
+// The chain over W words (W = res[0], on the device; *W_host the same) into
+// ustart / out as k_msg_walk.  d_chain: msg_chain_ws_bytes(W) bytes.
+hipError_t msg_chain(const uint64_t* d_words, const uint64_t* res, uint64_t W_host,
+                     uint64_t max_msgs, uint64_t* ustart, uint64_t* out, uint64_t* d_total,
+                     void* d_chain, size_t chain_bytes, hipStream_t s) {
+    const uint64_t T = msg_ranges(W_host);
+    MsgRanges R;
+    uint8_t* base = (uint8_t*)(((uintptr_t)d_chain + 255) & ~uintptr_t(255));
+    if (msg_chain_carve(&R, base, T) + (base - (uint8_t*)d_chain) > chain_bytes)
+        return hipErrorInvalidValue;
+    hipError_t e;
+    const dim3 g((uint32_t)((T + kThreads - 1) / kThreads));
+    k_msg_spec<<<g, kThreads, 0, s>>>(d_words, res, T, R);
+    bool done = false;
+    for (int round = 0; round < kMsgMaxRounds; round++) {
+        size_t tb = R.tmp_bytes;
+        if ((e = hipcub::DeviceScan::InclusiveScan(R.tmp, tb, R.own, R.xmax, MaxOp(), (int)T, s)) !=
+            hipSuccess)
+            return e;
+        if ((e = hipMemsetAsync(R.flag, 0, 4, s)) != hipSuccess) return e;
+        k_msg_round<<<g, kThreads, 0, s>>>(d_words, res, T, R);
+        int32_t changed = 0;
+        if ((e = hipMemcpyAsync(&changed, R.flag, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (!changed) {
+            done = true;
+            break;
+        }
+    }
+    if (!done) {  // (not settled: the serial walk, exact; its count is capped)
+        k_msg_walk<<<1, 64, 0, s>>>(d_words, res, max_msgs, ustart, out);
+        return hipMemcpyAsync(d_total, out, 8, hipMemcpyDeviceToDevice, s);
+    }
+    size_t tb = R.tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(R.tmp, tb, R.cnt, R.base, (int)T, s)) != hipSuccess)
+        return e;
+    k_msg_list<<<g, kThreads, 0, s>>>(d_words, res, T, R, max_msgs, ustart);
+    k_msg_end<<<1, 64, 0, s>>>(res, T, R, max_msgs, ustart, out, d_total);
+    return hipGetLastError();
+}
+
 // Packed byte of the record that starts at word u (or ~0 if u is inside a
 // record), from block j's entry.
 __device__ uint64_t word_to_byte(const uint8_t* __restrict__ in, uint64_t nbytes,
@@ -579,6 +841,91 @@ k_msg_pos(const uint8_t* __restrict__ in, uint64_t nbytes, const uint64_t* __res
 }
 
 }  // namespace
+
+namespace {
+
+// capnp_gpu_read_message_stream: message m (word start ustart[m] in the
+// decoded stream) -> its first segment's word, its segment count, and the
+// first message whose words exceed the traversal limit (read_message's
+// check, serialize.rs:494-501 via read_segment_table).
+__global__ void __launch_bounds__(kThreads)
+k_msg_meta(const uint64_t* __restrict__ words, const uint64_t* __restrict__ ustart, uint64_t n,
+           uint64_t limit, int has_limit, uint64_t* __restrict__ body_off,
+           uint64_t* __restrict__ nseg_out, unsigned long long* __restrict__ first_bad) {
+    const uint64_t m = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (m >= n) return;
+    const uint64_t u = ustart[m];
+    const uint64_t w0 = words[u];
+    const uint32_t nseg = (uint32_t)w0 + 1u;  // (the chain checked 1 <= nseg < 512)
+    uint64_t total = w0 >> 32;
+    for (uint32_t i = 1; i < nseg; i++) {
+        const uint64_t tw = words[u + 1 + (i - 1) / 2];
+        total += ((i - 1) & 1) ? (tw >> 32) : (tw & 0xFFFFFFFFull);
+    }
+    body_off[m] = u + 1 + nseg / 2;
+    nseg_out[m] = nseg;
+    if (has_limit && total > limit) atomicMin(first_bad, (unsigned long long)m);
+}
+
+__global__ void __launch_bounds__(kThreads)
+k_msg_seglist(const uint64_t* __restrict__ words, const uint64_t* __restrict__ ustart, uint64_t n,
+              const uint64_t* __restrict__ seg_off, uint64_t* __restrict__ seg_words) {
+    const uint64_t m = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (m >= n) return;
+    const uint64_t u = ustart[m];
+    const uint64_t w0 = words[u];
+    const uint32_t nseg = (uint32_t)w0 + 1u;
+    uint64_t* out = seg_words + seg_off[m];
+    out[0] = w0 >> 32;
+    for (uint32_t i = 1; i < nseg; i++) {
+        const uint64_t tw = words[u + 1 + (i - 1) / 2];
+        out[i] = ((i - 1) & 1) ? (tw >> 32) : (tw & 0xFFFFFFFFull);
+    }
+}
+
+}  // namespace
+
+extern "C" hipError_t capnp_launch_msg_meta(const uint64_t* d_words, const uint64_t* d_ustart,
+                                            uint64_t n, uint64_t limit, int has_limit,
+                                            uint64_t* d_body_off, uint64_t* d_nseg,
+                                            uint64_t* d_first_bad, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_msg_meta<<<dim3((uint32_t)((n + kThreads - 1) / kThreads)), kThreads, 0, s>>>(
+        d_words, d_ustart, n, limit, has_limit, d_body_off, d_nseg,
+        reinterpret_cast<unsigned long long*>(d_first_bad));
+    return hipGetLastError();
+}
+
+extern "C" hipError_t capnp_launch_msg_seglist(const uint64_t* d_words, const uint64_t* d_ustart,
+                                               uint64_t n, const uint64_t* d_seg_off,
+                                               uint64_t* d_seg_words, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_msg_seglist<<<dim3((uint32_t)((n + kThreads - 1) / kThreads)), kThreads, 0, s>>>(
+        d_words, d_ustart, n, d_seg_off, d_seg_words);
+    return hipGetLastError();
+}
+
+// Exclusive scan of n counts into out[0..n] (out[n] = the total).
+extern "C" hipError_t capnp_scan_counts(const uint64_t* d_in, uint64_t n, uint64_t* d_out,
+                                        void* d_tmp, size_t tmp_bytes, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(d_out, 0, 8, s);
+    if (e != hipSuccess || n == 0) return e;
+    size_t tb = tmp_bytes;
+    return hipcub::DeviceScan::InclusiveSum(d_tmp, tb, d_in, d_out + 1, (int)n, s);
+}
+
+extern "C" size_t capnp_scan_counts_tmp_bytes(uint64_t n) {
+    size_t b = 0;
+    (void)hipcub::DeviceScan::InclusiveSum(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr,
+                                           (int)(n ? n : 1));
+    return b + 256;
+}
+
+// Workspace of the message chain for a decoded stream of up to words_cap
+// words (capnp_resync_find_messages: on top of capnp_resync_ws_bytes).
+extern "C" size_t capnp_msg_chain_ws_bytes(uint64_t words_cap) {
+    return msg_chain_ws_bytes(words_cap) + 256;
+}
 
 // The longest prefix of complete records of nbytes packed bytes that may
 // end inside a record: *bytes = its packed length, *words = the words it
@@ -642,22 +989,26 @@ extern "C" hipError_t capnp_resync_prefix(const uint8_t* d_in, uint64_t nbytes, 
     return hipSuccess;
 }
 
-// -> *nmsg complete messages with byte starts d_pos[0..nmsg) and
-// d_pos[nmsg] = where the walk stopped (the next message's start, or the
-// stream end); *clean = 1 if that is the end of the stream after the last
-// message, i.e. the next try_read_message returns None.  A message whose
-// start could not be placed truncates the list before the message that
-// ended inside a record.  Blocking.
-extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t nbytes,
-                                                 uint64_t max_msgs, uint64_t* d_pos,
-                                                 uint64_t* d_words, uint64_t words_cap,
-                                                 uint64_t* nmsg, int* clean, void* d_ws,
-                                                 size_t ws_bytes, hipStream_t s,
-                                                 uint64_t* words_needed) {
+// The message discovery of capnp_resync_find_messages (below); for
+// capnp_resync_read_stream also: the messages' word starts in d_words,
+// d_ustart[0..nmsg], and *total_msgs = the messages the chain holds before
+// any cap)
+static hipError_t find_messages_impl(const uint8_t* d_in, uint64_t nbytes, uint64_t max_msgs,
+                                     uint64_t* d_pos, uint64_t* d_words, uint64_t words_cap,
+                                     uint64_t* nmsg, int* clean, void* d_ws, size_t ws_bytes,
+                                     hipStream_t s, uint64_t* words_needed, uint64_t* d_ustart,
+                                     uint64_t* total_msgs) {
     *nmsg = 0;
     *clean = nbytes == 0;
     if (words_needed) *words_needed = 0;
-    if (nbytes == 0) return hipMemsetAsync(d_pos, 0, 8, s);
+    if (total_msgs) *total_msgs = 0;
+    if (nbytes == 0) {
+        if (d_ustart) {
+            hipError_t e = hipMemsetAsync(d_ustart, 0, 8, s);
+            if (e != hipSuccess) return e;
+        }
+        return hipMemsetAsync(d_pos, 0, 8, s);
+    }
     hipError_t e;
     const uint64_t n = 1;
     const uint64_t nbb = blocks_bound(n, nbytes);
@@ -666,14 +1017,19 @@ extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t n
     size_t need = carve(&w, base, n, nbb, scan_tmp_bytes(nbb > 2 ? nbb : 2)) + (base - (uint8_t*)d_ws);
     // + in_off[2], out_off[2], res[2], walk out[2], bad, ustart[max_msgs + 1]
     uint64_t* aux = (uint64_t*)(base + ((need - (base - (uint8_t*)d_ws) + 255) & ~size_t(255)));
-    need = (uint8_t*)(aux + 10 + max_msgs + 1) - (uint8_t*)d_ws;
+    need = (uint8_t*)(aux + 12 + max_msgs + 1) - (uint8_t*)d_ws;
     if (need > ws_bytes) return hipErrorInvalidValue;
     uint64_t* in_off = aux;       // [2]
     uint64_t* out_off = aux + 2;  // [2]
     uint64_t* res = aux + 4;      // [1]
     uint64_t* wout = aux + 5;     // [2]
     uint64_t* bad = aux + 7;      // [1]
-    uint64_t* ustart = aux + 10;  // [max_msgs + 1]
+    uint64_t* dtotal = aux + 10;  // [1]
+    uint64_t* ustart = aux + 12;  // [max_msgs + 1]
+    // then the message chain's ranges (msg_chain_ws_bytes(words_cap))
+    uint8_t* chain = (uint8_t*)(ustart + max_msgs + 1);
+    const size_t chain_bytes = msg_chain_ws_bytes(words_cap);
+    if ((size_t)(chain + chain_bytes - (uint8_t*)d_ws) > ws_bytes) return hipErrorInvalidValue;
     const uint64_t h_in_off[2] = {0, nbytes};
     if ((e = hipMemcpyAsync(in_off, h_in_off, 16, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.flags, 0, 4 * (2 + kMaxPasses), s)) != hipSuccess) return e;
@@ -735,11 +1091,16 @@ extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t n
                                  nullptr, s)) != hipSuccess)
         return e;
     k_valid_words<<<grid(nb), kThreads, 0, s>>>(blk_status, nb, w.wbase, res);
-    k_msg_walk<<<1, 64, 0, s>>>(d_words, res, max_msgs, ustart, wout);
+    if ((e = msg_chain(d_words, res, W, max_msgs, ustart, wout, dtotal, chain, chain_bytes, s)) !=
+        hipSuccess)
+        return e;
     k_msg_pos<<<grid(max_msgs + 1), kThreads, 0, s>>>(d_in, nbytes, w.exit, w.wbase, nb, ustart,
                                                       wout, d_pos, bad);
     uint64_t hout[2] = {0, 0}, hbad = 0, hres = 0;
     if ((e = hipMemcpyAsync(hout, wout, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if (total_msgs &&
+        (e = hipMemcpyAsync(total_msgs, dtotal, 8, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return e;
     if ((e = hipMemcpyAsync(&hbad, bad, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipMemcpyAsync(&hres, res, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
@@ -761,5 +1122,39 @@ extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t n
         }
     }
     *nmsg = m;
+    if (d_ustart &&
+        (e = hipMemcpyAsync(d_ustart, ustart, 8 * (m + 1), hipMemcpyDeviceToDevice, s)) != hipSuccess)
+        return e;
     return hipStreamSynchronize(s);
+}
+
+// -> *nmsg complete messages with byte starts d_pos[0..nmsg) and
+// d_pos[nmsg] = where the walk stopped (the next message's start, or the
+// stream end); *clean = 1 if that is the end of the stream after the last
+// message, i.e. the next try_read_message returns None.  A message whose
+// start could not be placed truncates the list before the message that
+// ended inside a record.  Blocking.
+extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t nbytes,
+                                                 uint64_t max_msgs, uint64_t* d_pos,
+                                                 uint64_t* d_words, uint64_t words_cap,
+                                                 uint64_t* nmsg, int* clean, void* d_ws,
+                                                 size_t ws_bytes, hipStream_t s,
+                                                 uint64_t* words_needed) {
+    return find_messages_impl(d_in, nbytes, max_msgs, d_pos, d_words, words_cap, nmsg, clean,
+                              d_ws, ws_bytes, s, words_needed, nullptr, nullptr);
+}
+
+// As capnp_resync_find_messages, keeping the decode: d_words holds the
+// stream's words, d_ustart[0..nmsg] the messages' word starts in it (and
+// where the chain stopped), *total_msgs the messages the chain holds (more
+// than max_msgs: the caller's lists are too short).
+extern "C" hipError_t capnp_resync_read_stream(const uint8_t* d_in, uint64_t nbytes,
+                                               uint64_t max_msgs, uint64_t* d_pos,
+                                               uint64_t* d_words, uint64_t words_cap,
+                                               uint64_t* d_ustart, uint64_t* nmsg,
+                                               uint64_t* total_msgs, int* clean, void* d_ws,
+                                               size_t ws_bytes, hipStream_t s,
+                                               uint64_t* words_needed) {
+    return find_messages_impl(d_in, nbytes, max_msgs, d_pos, d_words, words_cap, nmsg, clean,
+                              d_ws, ws_bytes, s, words_needed, d_ustart, total_msgs);
 }

@@ -1082,9 +1082,9 @@ __device__ __forceinline__ void spec_tile(SM& S, uint64_t ca, uint32_t nc,
     S.sel[tid] = kExpandTable.s[tid];  // (the block tables overlaid it)
 }
 
-// Index-free walk of a staged tile on every thread (UNPACK_SPEC 2): each
-// chunk's packed bytes are cut into S equal byte segments (S = 16 for up to
-// 16 chunks, 4 for up to 64), one thread each, so a chunk's ~117-record
+// Index-free walk of a staged tile on every thread (UNPACK_SPEC 2, tiles of
+// at most 16 chunks): each chunk's packed bytes are cut into S = 16 equal
+// byte segments, one thread each, so a chunk's ~117-record
 // chain becomes S chains of ~117 / S records and all four waves walk
 // (the serial walker used 16 lanes of one wave for the whole chain).
 //   1. spec: thread (c, j) walks from kSegOverlap bytes before its segment
@@ -1108,6 +1108,7 @@ __device__ __forceinline__ void spec_tile(SM& S, uint64_t ca, uint32_t nc,
 #define UNPACK_SEG_OVERLAP 48  // config 2 nosync: 0 -> 724 us, 16 -> 699, 32 -> 646, 48 -> 614, 64 -> 640
 #endif
 constexpr uint32_t kSegOverlap = UNPACK_SEG_OVERLAP;  // spec walk lead-in (bytes)
+constexpr uint32_t kSegChunks = 16;  // tiles of at most this many chunks take the segment walk
 
 // One record hop (the walk's loops stop once p >= the segment end, so a
 // record running past the chunk end shows as p > pe at the stop).
@@ -1125,7 +1126,7 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
                                               int32_t* __restrict__ status,
                                               uint64_t* __restrict__ consumed, uint32_t tid,
                                               uint32_t lane) {
-    const uint32_t lg = nc <= 16 ? 4u : 2u;  // S = 16 or 4 segments per chunk
+    const uint32_t lg = 4u;  // S = 16 segments per chunk (nc <= kSegChunks)
     const uint32_t nseg = 1u << lg;
     const uint32_t c = tid >> lg, j = tid & (nseg - 1u);
     const bool act = c < nc;
@@ -1365,11 +1366,15 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
             }
         }
         if (anybad) __syncthreads();
-    } else if (UNPACK_SPEC == 2) {
+    } else if (UNPACK_SPEC == 2 && nc <= kSegChunks) {
         spec_seg_tile(S, ca, nc, status, consumed, tid, lane);
-    } else if (UNPACK_SPEC) {
+    } else if (UNPACK_SPEC == 1) {
         spec_tile(S, ca, nc, status, consumed, tid, lane, wave);
-    } else if (wave == walker && lane < nc) {  // (idle lanes stay off: their LDS traffic counts)
+    } else if (wave == walker && lane < nc) {
+        // (many short chunks -- the resync blocks, ~120 words -- keep 64
+        // serial walkers busy; the segment walk is for few long chunks:
+        // config 4 index-free 4.9 ms with this walk, 8.1 with 4 segments
+        // per chunk)  // (idle lanes stay off: their LDS traffic counts)
         const uint64_t c = ca + lane;
         const uint64_t gp = in_off[c], ge = in_off[c + 1];
         const uint64_t ow = out_off[c], oe = out_off[c + 1];
@@ -1580,6 +1585,62 @@ unpack_ovf_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
                                    tid, lane, wave);
         }
         __syncthreads();
+    }
+}
+
+// The overflow tiles of the index-free split launch.  Index-free batches
+// can overflow in bulk -- the resync block decode of config 4 hands over
+// ~10 % of its tiles expanding past the tables (zero-run blocks) -- so the
+// tiles are checked in windows of 64 (one lane each) spread over up to 4096
+// workgroups, where unpack_ovf_kernel's windows of 256 on at most 1024
+// workgroups left a few hundred of them serialising the overflow tiles
+// (config 4 index-free: 4.3 ms in the overflow kernel; one workgroup per
+// tile instead cost config 2 0.13 ms of empty workgroups).
+constexpr uint32_t kOvfWindow = CAPNP_WAVE;
+
+template <bool SYNC>
+__global__ void __launch_bounds__(kThreads)
+unpack_ovf_win_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                      uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
+                      const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
+                      uint64_t* __restrict__ consumed, const uint32_t* __restrict__ sync,
+                      uint64_t ntiles) {
+    __shared__ USmem sm;
+    __shared__ uint64_t ovf_mask;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    bool sel_ok = false;
+    for (uint64_t base = (uint64_t)blockIdx.x * kOvfWindow; base < ntiles;
+         base += (uint64_t)gridDim.x * kOvfWindow) {
+        if (wave == 0) {
+            const uint64_t t = base + lane;
+            bool o = false;
+            if (t < ntiles) {
+                const uint64_t ca = t * tc;
+                const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
+                o = !tile_fits_lane(in, in_off, out_off, ca, cb);
+            }
+            const uint64_t m = ballot64(o);
+            if (lane == 0) ovf_mask = m;
+        }
+        __syncthreads();
+        uint64_t m = ovf_mask;
+        while (m) {
+            const uint64_t t = base + ctz64(m);
+            m &= m - 1;
+            const uint64_t ca = t * tc;
+            const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
+            __syncthreads();  // the previous tile is done with the tables
+            if (!sel_ok) {
+                sm.st.sel[tid] = kExpandTable.s[tid];
+                sel_ok = true;
+            }
+            unpack_tile_rest<SYNC>(sm, in, in_off, ca, cb, out, out_off, status, consumed, sync,
+                                   tid, lane, wave);
+            sel_ok = false;  // (the global path may overlay the selectors)
+        }
+        __syncthreads();  // ovf_mask is rewritten next window
     }
 }
 
@@ -2196,9 +2257,10 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
         hipLaunchKernelGGL(unpack_fit_kernel<false>, dim3((uint32_t)blocks), dim3(kThreads),
                            UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
                            d_status, d_consumed, d_sync);
-        hipLaunchKernelGGL(unpack_ovf_kernel<false>, ogrid, dim3(kThreads), 0, stream, d_in,
-                           d_in_off, nchunks, tc, d_out, d_out_off, d_status, d_consumed, d_sync,
-                           blocks);
+        const uint64_t wg = (blocks + kOvfWindow - 1) / kOvfWindow;
+        hipLaunchKernelGGL(unpack_ovf_win_kernel<false>, dim3((uint32_t)(wg < 4096 ? wg : 4096)),
+                           dim3(kThreads), 0, stream, d_in, d_in_off, nchunks, tc, d_out,
+                           d_out_off, d_status, d_consumed, d_sync, blocks);
     } else
         hipLaunchKernelGGL(unpack_kernel<false>, dim3((uint32_t)blocks), dim3(kThreads),
                            UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,

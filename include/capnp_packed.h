@@ -428,6 +428,42 @@ capnp_status capnp_gpu_find_messages(capnp_ctx* ctx, const uint8_t* d_packed, si
                                      size_t max_msgs, uint64_t* d_msg_byte_off, size_t* nmsg,
                                      void* stream);
 
+/* try_read_message in a loop over one packed stream in device memory with
+   no byte index, in ONE pass (serialize.rs:310-325, :448-524;
+   serialize_packed.rs:246-255): the stream is resolved and decoded once (the
+   block walk of capnp_gpu_find_messages) into d_words, the message chain is
+   followed through the decoded segment tables in parallel, and the messages
+   are described in place, with no second decode:
+     d_words            the decoded stream (segment tables and bodies), words_cap words;
+     d_msg_byte_off[m]  message m's first packed byte (nmsg + 1 entries: the
+                        last is where the loop's next try_read_message starts);
+     d_body_word_off[m] the word of d_words where message m's first segment
+                        starts (its segments follow back to back);
+     d_seg_words        segment lengths in words, message m's at
+                        [d_msg_seg_off[m], d_msg_seg_off[m+1]) (nmsg + 1 entries).
+   Messages are read while the loop reads them: a segment table the reader
+   rejects (segment count, total words over opts' traversal limit; opts
+   NULL = defaults), a message cut by the stream end, or one the resolution
+   could not place, ends the list.  *clean = 1 if the loop ended at the end of
+   the stream (the next try_read_message returns None); otherwise the
+   message at d_msg_byte_off[*nmsg] is the one the loop tries next: its status
+   (or, where the resolution stopped early, its contents, and the loop goes
+   on after it) is what capnp_gpu_read_messages gives over
+   [d_msg_byte_off[*nmsg], nbytes) in try mode.
+   Capacities: msgs_cap messages (d_msg_byte_off and d_msg_seg_off hold
+   msgs_cap + 1 entries, d_body_word_off msgs_cap), segs_cap segments,
+   words_cap words.  CAPNP_E_BUFFER_NOT_LARGE_ENOUGH when one is short, with
+   *words_need / *msgs_need / *segs_need (may be NULL) set to what is known
+   to be needed so far (call again with at least those).  Blocking. */
+capnp_status capnp_gpu_read_message_stream(capnp_ctx* ctx, const uint8_t* d_packed,
+                                           size_t nbytes, const capnp_reader_options* opts,
+                                           uint64_t* d_words, size_t words_cap,
+                                           uint64_t* d_msg_byte_off, uint64_t* d_body_word_off,
+                                           size_t msgs_cap, uint64_t* d_seg_words,
+                                           size_t segs_cap, uint64_t* d_msg_seg_off,
+                                           size_t* nmsg, int32_t* clean, size_t* words_need,
+                                           size_t* msgs_need, size_t* segs_need, void* stream);
+
 /* ---- Streaming adaptors over caller-supplied byte streams ----------------
  * The async PackedWrite / PackedRead of capnp-futures
  * (capnp-futures/src/serialize_packed.rs:34-225, :330-521) and its message

@@ -20,8 +20,9 @@ import os
 import re
 import sys
 
-PACK = {"pack_kernel", "pack_wt_bits", "pack_wt_map", "pack_wt_plan", "pack_wt_kernel",
-        "pack_wt_fix_sync"}
+PACK = {"pack_kernel", "pack_cs_kernel", "pack_lean_kernel", "pack_ovf_kernel", "pack_wt_bits",
+        "pack_wt_map", "pack_wt_plan", "pack_wt_kernel", "pack_wt_fix_sync"}
+PACK_SYNC_TEMPLATED = {"pack_kernel", "pack_cs_kernel", "pack_lean_kernel", "pack_wt_kernel"}
 UNPACK_SYNC = {"unpack_fit_kernel", "unpack_ovf_kernel", "unpack_wt_plan", "unpack_wt_kernel",
                "unpack_wt_finish", "unpack_kernel<true>"}
 
@@ -38,8 +39,14 @@ def templ(name):
 
 def role(t):
     bare = t.split("<")[0]
+    if bare == "k_check_offsets":  # (the C ABI's offset validation, every call)
+        return None
+    if bare in PACK_SYNC_TEMPLATED and t.startswith(bare + "<false"):
+        return "pack_nosync"  # (bench.py times the index-free pack too)
     if bare in PACK:
         return "pack"
+    if bare in ("unpack_fit_kernel", "unpack_ovf_kernel") and t.endswith("<false>"):
+        return "unpack_nosync"
     if bare in UNPACK_SYNC or t in UNPACK_SYNC:
         return "unpack"
     if t == "unpack_kernel<false>" or bare.startswith("k_"):
@@ -76,8 +83,11 @@ def main():
             e["write"] += int(wr)
             e["total"] += int(rd + wr)
             e["kernels"][k] = {"read": int(rd), "write": int(wr)}
-        if not key.endswith(":sync") and "unpack_nosync" in ent:
-            ent["unpack"] = ent.pop("unpack_nosync")  # the index-free run's only decode
+        if not key.endswith(":sync"):  # the index-free run's only encode / decode
+            if "unpack_nosync" in ent:
+                ent["unpack"] = ent.pop("unpack_nosync")
+            if "pack_nosync" in ent:
+                ent["pack"] = ent.pop("pack_nosync")
         tj[key] = ent
         print(key, {r: (round(e["read"] / 1e6, 1), round(e["write"] / 1e6, 1))
                     for r, e in ent.items()})

@@ -155,3 +155,45 @@ def test_zero_heavy_stream(ctx):
         out += b
     assert len(out) < 10000
     _check(ctx, out)
+
+
+def test_one_pass_matches_discovery(ctx):
+    """decode_stream (one pass: capnp_gpu_read_message_stream) against
+    find_messages + read_messages and the oracle's loop, on a stream of
+    thousands of messages (hundreds of 4096-word chain ranges, messages
+    longer than a range, a truncated tail): the same starts, segment tables
+    and words."""
+    import torch
+    rng = random.Random(21)
+    parts = []
+    for k in range(2500):
+        segs = _segments(rng, big=(k % 50 == 7))
+        st, b = O.write_message(segs)
+        assert st == 0
+        parts.append((b, segs))
+    stream = b"".join(b for b, _ in parts)
+    stream_cut = stream[:-5]
+    for s in (stream, stream_cut):
+        dev = torch.from_numpy(np.frombuffer(s, np.uint8).copy()).cuda()
+        words, mbo, bwo, segw, mso, n, clean = ctx.decode_stream(dev)
+        ref, ref_end = _oracle_loop(s)
+        offs, nf = ctx.find_messages(dev)
+        assert clean == (ref_end == 1)
+        assert n == nf and mbo.cpu().tolist() == offs.cpu().tolist()
+        if s is stream:
+            assert n == len(ref)
+        else:
+            assert n <= len(ref)
+        mbo_h, bwo_h, mso_h = mbo.cpu().tolist(), bwo.cpu().tolist(), mso.cpu().tolist()
+        segw_h = segw.cpu().tolist()
+        w = words.cpu().numpy().view(np.uint64)
+        for m in range(n):
+            rsegs, rused = ref[m]
+            assert mbo_h[m + 1] - mbo_h[m] == rused
+            assert mso_h[m + 1] - mso_h[m] == len(rsegs)
+            a = bwo_h[m]
+            for j, rs in enumerate(rsegs):
+                ln = segw_h[mso_h[m] + j]
+                assert ln == len(rs)
+                assert np.array_equal(w[a:a + ln], np.asarray(rs, np.uint64))
+                a += ln
