@@ -21,6 +21,6 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_W
   -- python3 bench.py "${ARGS[@]}" > "$OUT/sq2.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_LDS_ADDR_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH -d "$OUT/sq3" -o run --output-format csv \
   -- python3 bench.py "${ARGS[@]}" > "$OUT/sq3.log" 2>&1
-python3 scripts/summarize_prof.py "$OUT" pack_kernel unpack_fit_kernel unpack_ovf_kernel unpack_kernel > "$OUT/summary.txt"
+python3 scripts/summarize_prof.py "$OUT" pack_cs_kernel pack_ovf_kernel unpack_fit_kernel unpack_ovf_kernel unpack_ovf_win_kernel > "$OUT/summary.txt"
 cat "$OUT/summary.txt"
 echo "profile done: $OUT"
