@@ -780,11 +780,16 @@ capnp_status capnp_unpack_batch_host(capnp_ctx* ctx, const uint8_t* packed,
     if (ie > ib) HIP_TRY(hipMemcpyAsync(d + o_in, packed + ib, ie - ib, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d + o_ri, ri.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d + o_ro, ro.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
-    HIP_TRY(capnp_launch_unpack(d + o_in, reinterpret_cast<uint64_t*>(d + o_ri), n, 0,
-                                reinterpret_cast<uint64_t*>(d + o_out),
-                                reinterpret_cast<uint64_t*>(d + o_ro),
-                                reinterpret_cast<int32_t*>(d + o_st),
-                                reinterpret_cast<uint64_t*>(d + o_cs), nullptr, s));
+    // the device batch's own plan: long chunks (a stream reader's 1 MiB unit)
+    // take the speculative block walk rather than one wave's serial walk
+    if (n) {
+        st = unpack_batch_dev(ctx, d + o_in, reinterpret_cast<uint64_t*>(d + o_ri), n,
+                              reinterpret_cast<uint64_t*>(d + o_out),
+                              reinterpret_cast<uint64_t*>(d + o_ro),
+                              reinterpret_cast<int32_t*>(d + o_st),
+                              reinterpret_cast<uint64_t*>(d + o_cs), 0, s);
+        if (st != CAPNP_OK) return st;
+    }
     if (oe > ob) HIP_TRY(hipMemcpyAsync(words + ob, d + o_out, (oe - ob) * 8, hipMemcpyDeviceToHost, s));
     if (n) HIP_TRY(hipMemcpyAsync(status, d + o_st, n * 4, hipMemcpyDeviceToHost, s));
     if (n && consumed) HIP_TRY(hipMemcpyAsync(consumed, d + o_cs, n * 8, hipMemcpyDeviceToHost, s));

@@ -55,6 +55,7 @@ namespace {
 
 constexpr size_t kBatchWords = size_t(1) << 17;  // writer: pack every 1 MiB of input
 constexpr size_t kPull = size_t(1) << 16;        // reader: bytes asked of the inner reader
+constexpr size_t kPullMax = size_t(1) << 24;     // ... at most, when a unit needs more
 
 struct Drain {
     std::vector<uint8_t> q;
@@ -130,15 +131,16 @@ capnp_status writer_drain(capnp_packed_writer* w) {
 
 // Pulls more packed input; CAPNP_OK with bytes added, CAPNP_NONE at the end
 // of the stream, CAPNP_PENDING, or an I/O error.
-capnp_status reader_pull(capnp_packed_reader* r) {
+capnp_status reader_pull(capnp_packed_reader* r, size_t ask = kPull) {
     if (r->eof) return CAPNP_NONE;
+    ask = std::min(std::max(ask, kPull), kPullMax);
     if (r->ip > 0 && r->ip * 2 >= r->in.size()) {  // drop the decoded prefix
         r->in.erase(r->in.begin(), r->in.begin() + (ptrdiff_t)r->ip);
         r->ip = 0;
     }
     const size_t base = r->in.size();
-    r->in.resize(base + kPull);
-    const ptrdiff_t got = r->fn(r->user, r->in.data() + base, kPull);
+    r->in.resize(base + ask);
+    const ptrdiff_t got = r->fn(r->user, r->in.data() + base, ask);
     if (got == CAPNP_IO_PENDING) {
         r->in.resize(base);
         return CAPNP_PENDING;
@@ -237,6 +239,11 @@ capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
             if (p != CAPNP_OK) return p;
             continue;
         }
+        // stage what the unit can consume (<= 10 bytes a word) before the
+        // decode, so one read costs one launch rather than one per pull; a
+        // pull that stops short (pending, end, error) is met again below
+        for (size_t need = nw * 10 + 16; r->in.size() - r->ip < need;)
+            if (reader_pull(r, need - (r->in.size() - r->ip)) != CAPNP_OK) break;
         size_t used = 0;
         int32_t st = 0;
         capnp_status e = reader_unit(r, nw, out, &used, &st);
