@@ -96,6 +96,10 @@ extern "C" hipError_t capnp_resync_find_messages(const uint8_t* d_in, uint64_t n
                                                  uint64_t* nmsg, int* clean, void* d_ws,
                                                  size_t ws_bytes, hipStream_t s,
                                                  uint64_t* words_needed);
+extern "C" hipError_t capnp_resync_decode_prefix(const uint8_t* d_in, uint64_t nbytes,
+                                                 uint64_t max_words, uint64_t* d_out, void* d_ws,
+                                                 size_t ws_bytes, hipStream_t s, uint64_t* bytes,
+                                                 uint64_t* words);
 extern "C" hipError_t capnp_resync_prefix(const uint8_t* d_in, uint64_t nbytes, void* d_ws,
                                           size_t ws_bytes, hipStream_t s, uint64_t* bytes,
                                           uint64_t* words);
@@ -1288,6 +1292,33 @@ capnp_status capnp_stream_complete_prefix(capnp_ctx* ctx, const uint8_t* host, s
     hipStream_t s = ctx->stream;
     HIP_TRY(hipMemcpyAsync(ctx->d_stage, host, n, hipMemcpyHostToDevice, s));
     HIP_TRY(capnp_resync_prefix(ctx->d_stage, n, ctx->d_resync, ctx->resync_cap, s, bytes, words));
+    return CAPNP_OK;
+}
+
+// ... and decoded: the longest prefix of complete records of n host bytes
+// with at most max_words words, its words into out[0, *words) (host).
+capnp_status capnp_stream_decode_prefix(capnp_ctx* ctx, const uint8_t* host, size_t n,
+                                        uint64_t max_words, uint64_t* out, uint64_t* bytes,
+                                        uint64_t* words) {
+    if (!ctx || !bytes || !words || (n && !host) || (max_words && !out))
+        return CAPNP_E_INVALID_ARGUMENT;
+    *bytes = *words = 0;
+    if (n == 0 || max_words == 0) return CAPNP_OK;
+    const size_t o_out = round16(n) + 64;
+    capnp_status st = ensure_stage(ctx, o_out + max_words * 8 + 16);
+    if (st != CAPNP_OK) return st;
+    const size_t ws = capnp_resync_ws_bytes(1, n) + 4096;
+    st = ensure_buf(ctx, &ctx->d_resync, &ctx->resync_cap, ws);
+    if (st != CAPNP_OK) return st;
+    hipStream_t s = ctx->stream;
+    uint64_t* d_out = reinterpret_cast<uint64_t*>(ctx->d_stage + o_out);
+    HIP_TRY(hipMemcpyAsync(ctx->d_stage, host, n, hipMemcpyHostToDevice, s));
+    HIP_TRY(capnp_resync_decode_prefix(ctx->d_stage, n, max_words, d_out, ctx->d_resync,
+                                       ctx->resync_cap, s, bytes, words));
+    if (*words) {
+        HIP_TRY(hipMemcpyAsync(out, d_out, *words * 8, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
     return CAPNP_OK;
 }
 

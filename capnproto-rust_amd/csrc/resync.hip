@@ -230,6 +230,232 @@ k_fix(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint6
     if (changed) flags[2 + pass] = 1;
 }
 
+// ---- tile resolution (round 3; RESYNC_TILE, the default) ----
+// k_spec + k_fix walk each block from global memory, one lane per block, and
+// a chain that no speculative walk couples with (a literal-run region) moved
+// kGroup blocks per fix pass: config 4 spent 0.9 ms in k_spec and 1.95 ms in
+// 24 fix passes.  Here one wave takes a tile of kTileBlocks consecutive
+// blocks (contiguous packed bytes, <= 32 KiB), stages them in LDS and
+// resolves them among its lanes:
+//   spec   lane j walks from kLead bytes before its block (or from its
+//          chunk's start) to its first record start f >= s, then on to its
+//          exit; the lead-in lets chains from different starts couple before
+//          the block begins, so f is usually the true start;
+//   rounds entries are a prefix max over the lanes' own exits (a block whose
+//          entry lies past its end -- inside a literal run -- owns none and
+//          passes the entry on; a walk that runs past its chunk owns none
+//          either), with lane 0's entry the tile's and a chunk's first block
+//          entered at the chunk start.  A lane whose entry is not the one its
+//          state derives from walks again from it, in lockstep with its spec
+//          chain until they meet (then its exit stands).  At the fixed point
+//          every block's entry is its predecessor's exit.
+// Lane 0's entry is the previous tile's last exit: the spec launch assumes
+// its own f; fix passes (k_tile with fix = 1) re-resolve a tile whose stored
+// entry differs from the predecessor's exit, and flag a pass whose last exits
+// moved.  A region no walk couples with now costs one tile per pass (32 KiB)
+// instead of kGroup blocks (4 KiB).  The results (exit, entry, words per
+// block) are k_spec + k_fix's, so the scan, check and block decode follow
+// unchanged.
+#ifndef RESYNC_TILE
+#define RESYNC_TILE 1
+#endif
+constexpr uint32_t kTileBlocks = CAPNP_WAVE;
+constexpr uint64_t kLead = 48;
+constexpr uint32_t kTileLds = (uint32_t)(kTileBlocks * kBlock + kLead + 64);
+
+// hop() on the staged bytes (buf holds in[base ...]).
+__device__ __forceinline__ void hop_lds(const uint8_t* buf, uint64_t base, uint64_t& p,
+                                        uint64_t& w, uint64_t b) {
+    const uint32_t tag = buf[p - base];
+    uint64_t q = p + 1 + __builtin_popcount(tag);
+    w += 1;
+    if (tag == 0u || tag == 0xFFu) {
+        if (q >= b) {
+            p = b + 1;
+            return;
+        }
+        const uint32_t r = buf[q - base];
+        q += 1;
+        w += r;
+        if (tag == 0xFFu) q += 8ull * r;
+    }
+    p = q > b ? b + 1 : q;
+}
+
+__device__ __forceinline__ uint64_t wave_excl_max(uint64_t v, uint32_t lane) {
+    uint64_t x = v;
+#pragma unroll
+    for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d);
+        if (lane >= d && y > x) x = y;
+    }
+    const uint64_t e = __shfl_up(x, 1);
+    return lane == 0 ? 0 : e;
+}
+
+__global__ void __launch_bounds__(CAPNP_WAVE)
+k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
+       const uint64_t* __restrict__ bstart, uint64_t* exit, uint64_t* __restrict__ entry,
+       uint64_t* __restrict__ words, int32_t* flags, int pass, int fix) {
+    extern __shared__ __align__(16) uint8_t tbuf[];
+    const uint64_t nb = uniform64(bstart[n]);
+    const uint64_t k0 = (uint64_t)blockIdx.x * kTileBlocks;
+    if (k0 >= nb) return;
+    if (fix && pass > 0 && __atomic_load_n(&flags[2 + pass - 1], __ATOMIC_RELAXED) == 0) return;
+    const uint32_t lane = threadIdx.x;
+    const uint64_t kn = nb - k0 < kTileBlocks ? nb - k0 : kTileBlocks;
+    uint64_t e0 = 0;  // lane 0's entry
+    if (fix) {
+        e0 = __atomic_load_n(&exit[k0 - 1], __ATOMIC_RELAXED);
+        if (e0 == uniform64(entry[k0])) return;  // consistent
+    }
+    // c0 = the last chunk with bstart[c0] <= k0: a 64-way search (3 probes
+    // deep for 10^5 chunks, where one lane's binary search was 17 dependent
+    // loads)
+    uint64_t clo = 0, chi = n;  // bstart[clo] <= k0 < bstart[chi]
+    while (chi - clo > 1) {
+        const uint64_t idx = clo + 1 + ((chi - clo - 1) * lane) / CAPNP_WAVE;
+        const uint64_t m = ballot64(bstart[idx] <= k0);  // (monotone in the lane)
+        const uint32_t nle = popc64(m);
+        const uint64_t nlo = nle ? readlane64(idx, nle - 1) : clo;
+        const uint64_t nhi = nle < CAPNP_WAVE ? readlane64(idx, nle) : chi;
+        clo = nlo;
+        chi = nhi;
+    }
+    const uint64_t c0 = clo;
+    const uint64_t bs0 = uniform64(bstart[c0]), a0 = uniform64(in_off[c0]);
+    // (a tile that starts a chunk is exact since the spec launch)
+    if (fix && bs0 == k0) return;
+    // stage [s0 - kLead, s0 + 32 KiB + 16) (clamped to the batch: the tile's
+    // blocks are contiguous bytes, at most kBlock each) by LDS DMA, 16 bytes a
+    // lane, every load in flight at once
+    const uint64_t A = uniform64(in_off[0]), Z = uniform64(in_off[n]);
+    const uint64_t s0 = a0 + (k0 - bs0) * kBlock;
+    const uint64_t lo = s0 > A + kLead ? s0 - kLead : A;
+    const uint64_t hi = s0 + kTileBlocks * kBlock + 16 < Z ? s0 + kTileBlocks * kBlock + 16 : Z;
+    // (base: 16-byte aligned in memory; may lie below in_off[0] inside that vector)
+    const uint64_t base = lo - (uint64_t)(reinterpret_cast<uintptr_t>(in + lo) & 15u);
+    {
+        const uint32_t nv = (uint32_t)((hi - base + 15) >> 4);
+        const uint8_t* src = in + base;
+        for (uint32_t i0 = 0; i0 < nv; i0 += CAPNP_WAVE) {
+            if (i0 + lane < nv)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(src + 16ull * (i0 + lane)),
+                    (__attribute__((address_space(3))) void*)(tbuf + 16u * i0), 16, 0, 0);
+        }
+    }
+    // lane j's chunk: c0 + the chunk starts in (k0, k0 + j], counted over
+    // batches of 64 starts (a lane's binary search over the batch by shuffles)
+    const bool valid = lane < kn;
+    const uint32_t jj = valid ? lane : (uint32_t)(kn - 1);
+    const uint64_t k = k0 + jj;
+    uint64_t c = c0;
+    for (uint64_t cb = c0 + 1;; cb += CAPNP_WAVE) {
+        const uint64_t idx = cb + lane;
+        const uint64_t v = idx <= n ? bstart[idx] : ~0ull;
+        const uint32_t d = v - k0 > CAPNP_WAVE ? CAPNP_WAVE + 1 : (uint32_t)(v - k0);
+        uint32_t cnt = 0;
+        for (uint32_t step = CAPNP_WAVE / 2; step; step >>= 1)
+            if ((uint32_t)__shfl((int)d, (int)(cnt + step - 1)) <= jj) cnt += step;
+        const uint32_t dlast = (uint32_t)__builtin_amdgcn_readlane((int)d, CAPNP_WAVE - 1);
+        if (cnt == CAPNP_WAVE - 1 && dlast <= jj) cnt = CAPNP_WAVE;
+        c += cnt;
+        if (dlast >= CAPNP_WAVE) break;  // this batch reaches past the tile
+    }
+    const uint64_t a = in_off[c], b = in_off[c + 1], bsc = bstart[c];
+    const uint64_t s = a + (k - bsc) * kBlock;
+    const uint64_t e = s + kBlock < b ? s + kBlock : b;
+    const bool cfirst = k == bsc;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staged bytes are in
+    // spec walk (a chunk's first block walks exactly from the chunk start)
+    constexpr uint64_t kNone = ~0ull;
+    uint64_t f, sx, sw = 0;
+    bool serr = false;
+    {
+        uint64_t p = s > a + kLead ? s - kLead : a, w = 0;
+        while (p < s) hop_lds(tbuf, base, p, w, b);
+        if (p > b) {  // the lead-in ran past the chunk: no spec chain
+            f = kNone;
+            sx = b + 1;
+            serr = true;
+        } else {
+            f = p;
+            w = 0;
+            while (p < e) hop_lds(tbuf, base, p, w, b);
+            sx = p;
+            sw = w;
+            serr = p > b;
+        }
+    }
+    // state: entry used, exit, words, own exit (0: none)
+    uint64_t used, ex, wd, own;
+    if (f != kNone && f >= e) {  // spec pass-through
+        used = f;
+        ex = f;
+        wd = 0;
+        own = 0;
+    } else {
+        used = f;
+        ex = sx;
+        wd = sw;
+        own = serr ? 0 : sx;
+    }
+    if (!fix) e0 = uniform64(readlane64(f == kNone ? s : f, 0));  // the spec launch's assumption
+    const uint64_t in_j = lane == 0 ? e0 : (cfirst ? a : 0);
+    for (;;) {
+        uint64_t v = own > in_j ? own : in_j;
+        if (!valid) v = 0;
+        const uint64_t pm = wave_excl_max(v, lane);
+        const uint64_t ent = lane == 0 ? e0 : (cfirst ? a : pm);
+        const bool need = valid && ent != used;
+        if (ballot64(need) == 0) break;
+        if (need) {
+            used = ent;
+            if (ent < s || ent > b) {  // below the block (a chunk's walk failed earlier) or past it
+                ex = b + 1;
+                wd = 0;
+                own = 0;
+            } else if (ent >= e) {  // inside a record that began earlier
+                ex = ent;
+                wd = 0;
+                own = 0;
+            } else {
+                uint64_t pt = ent, wt = 0, ps = f, ws = 0;
+                bool met = false;
+                if (f != kNone && f < e) {
+                    while (pt < e) {
+                        while (ps < pt && ps < e) hop_lds(tbuf, base, ps, ws, b);
+                        if (ps == pt) {
+                            met = true;
+                            break;
+                        }
+                        hop_lds(tbuf, base, pt, wt, b);
+                    }
+                } else {
+                    while (pt < e) hop_lds(tbuf, base, pt, wt, b);
+                }
+                if (met) {
+                    ex = sx;
+                    wd = wt + sw - ws;
+                    own = serr ? 0 : sx;
+                } else {
+                    ex = pt;
+                    wd = wt;
+                    own = pt > b ? 0 : pt;
+                }
+            }
+        }
+    }
+    if (valid) {
+        const uint64_t old = fix ? exit[k] : 0;
+        exit[k] = ex;
+        entry[k] = used;
+        words[k] = wd;
+        if (fix && (uint64_t)lane == kn - 1 && old != ex) flags[2 + pass] = 1;
+    }
+}
+
 __global__ void __launch_bounds__(kThreads)
 k_check(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __restrict__ out_off,
         const uint64_t* __restrict__ bstart, const uint64_t* __restrict__ exit,
@@ -339,6 +565,48 @@ uint64_t blocks_bound(uint64_t n, uint64_t total_bytes) { return total_bytes / k
 
 unsigned grid(uint64_t items) { return (unsigned)((items + kThreads - 1) / kThreads); }
 
+// Spec walks, then fix passes to the fixed point (kPassBatch per flag
+// read-back).  *converged = false after kMaxPasses passes.  Blocking.
+hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, const Ws& w,
+                   uint64_t nbb, hipStream_t s, int* passes, bool* converged) {
+    hipError_t e;
+    *passes = 0;
+    *converged = true;
+    const bool tile = RESYNC_TILE && getenv("CAPNP_RESYNC_BLOCKWALK") == nullptr;
+    const unsigned tgrid = (unsigned)((nbb + kTileBlocks - 1) / kTileBlocks);
+    const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
+    if (tile)
+        k_tile<<<tgrid, CAPNP_WAVE, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
+                                                  w.words, w.flags, 0, 0);
+    else
+        k_spec<<<grid(nbb), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart, w.spec_exit,
+                                                       w.spec_words, w.exit, w.entry, w.words);
+    int pass = 0;
+    for (;;) {
+        if (pass >= kMaxPasses) {
+            *converged = false;
+            break;
+        }
+        for (int i = 0; i < kPassBatch; i++, pass++) {
+            if (tile)
+                k_tile<<<tgrid, CAPNP_WAVE, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
+                                                          w.entry, w.words, w.flags, pass, 1);
+            else
+                k_fix<<<grid(ngroups), kThreads, walk_lds(), s>>>(
+                    d_in, in_off, n, w.bstart, w.spec_exit, w.spec_words, w.exit, w.entry,
+                    w.words, w.flags, pass);
+        }
+        int32_t last = 0;
+        if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
+            hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (!last) break;
+    }
+    *passes = pass;
+    return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" uint32_t capnp_resync_block_bytes(void) { return (uint32_t)kBlock; }
@@ -387,29 +655,10 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
         return e;
-    k_spec<<<grid(nbb), kThreads, walk_lds(), s>>>(d_in, d_in_off, n, w.bstart, w.spec_exit, w.spec_words,
-                                          w.exit, w.entry, w.words);
-    // fix passes, kPassBatch at a time; a pass after one that changed nothing
-    // returns at once, so the flag of a batch's last pass says whether the
-    // fixed point was reached
     int pass = 0;
-    const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
-    for (;;) {
-        if (pass == kMaxPasses) {
-            hflags[1] = 1;  // not converged: let the serial walk decide
-            break;
-        }
-        for (int i = 0; i < kPassBatch; i++, pass++)
-            k_fix<<<grid(ngroups), kThreads, walk_lds(), s>>>(d_in, d_in_off, n, w.bstart, w.spec_exit,
-                                                     w.spec_words, w.exit, w.entry, w.words,
-                                                     w.flags, pass);
-        int32_t last = 0;
-        if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
-            hipSuccess)
-            return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        if (!last) break;
-    }
+    bool conv = true;
+    if ((e = resolve(d_in, d_in_off, n, w, nbb, s, &pass, &conv)) != hipSuccess) return e;
+    if (!conv) hflags[1] = 1;  // not converged: let the serial walk decide
     if (passes) *passes = pass;
     if (!hflags[1]) {
         tb = w.tmp_bytes;
@@ -500,25 +749,52 @@ __global__ void k_valid_words(const int32_t* __restrict__ blk_status, uint64_t n
 // The last block may end in a record the stream cuts short: its unit then
 // ends after its last complete record, and only those words count.
 // tail[0] = that byte, tail[1] = the stream's complete words.
-__global__ void k_tail(const uint8_t* __restrict__ in, uint64_t nbytes,
-                       const uint64_t* __restrict__ exit_, const uint64_t* __restrict__ wbase,
-                       uint64_t nb, uint64_t* __restrict__ tail) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    uint64_t p = nb > 1 ? exit_[nb - 2] : 0, w = 0;
-    while (p < nbytes) {
-        uint64_t q = p, ww = w;
-        hop(in, q, ww, nbytes);
-        if (q > nbytes) break;
-        p = q;
-        w = ww;
-    }
-    tail[0] = p;
-    tail[1] = wbase[nb - 1] + w;
+// The first block whose chain ran past the stream end (a record the stream
+// cuts short): the blocks before it are exact and complete.  *kerr starts at nb.
+__global__ void k_first_err(const uint64_t* __restrict__ exit_, uint64_t nb, uint64_t nbytes,
+                            unsigned long long* __restrict__ kerr) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nb && exit_[k] > nbytes) atomicMin(kerr, (unsigned long long)k);
 }
 
-__global__ void k_set_tail(uint64_t* __restrict__ blk_in, uint64_t nb,
-                           const uint64_t* __restrict__ tail) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) blk_in[nb] = tail[0];
+// The longest prefix of complete records with at most max_words words:
+// cut[0] = its bytes, cut[1] = its words, *cutk = the block it ends in.  The
+// one block where the prefix ends (its words cross max_words, or it is the
+// last trusted block) walks its records from its entry.
+__global__ void k_cut(const uint8_t* __restrict__ in, uint64_t nbytes, uint64_t max_words,
+                      const uint64_t* __restrict__ exit_, const uint64_t* __restrict__ wbase,
+                      const uint64_t* __restrict__ words, uint64_t nb,
+                      const unsigned long long* __restrict__ kerr, uint64_t* __restrict__ cut,
+                      uint64_t* __restrict__ cutk) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t ke = *kerr;
+    if (k >= nb || k > ke) return;
+    const uint64_t lo = wbase[k];
+    if (lo > max_words) return;
+    if (k != ke && k != nb - 1 && lo + words[k] <= max_words) return;
+    uint64_t p = k == 0 ? 0 : exit_[k - 1], w = lo;
+    while (p < nbytes) {
+        uint64_t q = p, dw = 0;
+        hop(in, q, dw, nbytes);
+        if (q > nbytes || w + dw > max_words) break;
+        p = q;
+        w += dw;
+    }
+    cut[0] = p;
+    cut[1] = w;
+    *cutk = k;
+}
+
+// Units after the cut's block are empty at the cut, so a decode of every
+// block stops there (the blocks past a record the stream cuts short hold no
+// trusted chain).
+__global__ void k_set_cut(uint64_t* __restrict__ blk_in, uint64_t* __restrict__ blk_out,
+                          uint64_t nb, const uint64_t* __restrict__ cut,
+                          const uint64_t* __restrict__ cutk) {
+    const uint64_t k = *cutk + 1 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > nb) return;
+    blk_in[k] = cut[0];
+    blk_out[k] = cut[1];
 }
 
 __global__ void k_msg_walk(const uint64_t* __restrict__ words, const uint64_t* __restrict__ res,
@@ -927,18 +1203,22 @@ extern "C" size_t capnp_msg_chain_ws_bytes(uint64_t words_cap) {
     return msg_chain_ws_bytes(words_cap) + 256;
 }
 
-// The longest prefix of complete records of nbytes packed bytes that may
-// end inside a record: *bytes = its packed length, *words = the words it
-// decodes to (the spec / fix / scan resolution above, then k_tail on the
-// last block).  Blocking.  The async stream reader uses it where its inner
-// reader pends or ends: capnp-futures' PackedRead hands out every complete
-// record before it waits or fails (capnp-futures/src/serialize_packed.rs:
+// The longest prefix of complete records of nbytes packed bytes (which may
+// end inside a record) with at most max_words words: *bytes = its packed
+// length, *words = the words it decodes to (the resolution above, then the
+// cut in the one block where the prefix ends), decoded into d_out[0, *words)
+// unless d_out is null.  Blocking.  The stream reader takes its read units
+// this way: whole records, so a unit never ends inside a run (the reference's
+// read() fails there, serialize_packed.rs:166-185), and where its inner
+// reader pends or ends it hands out every complete record first, as
+// capnp-futures' PackedRead does (capnp-futures/src/serialize_packed.rs:
 // 87-225).
-extern "C" hipError_t capnp_resync_prefix(const uint8_t* d_in, uint64_t nbytes, void* d_ws,
-                                          size_t ws_bytes, hipStream_t s, uint64_t* bytes,
-                                          uint64_t* words) {
+extern "C" hipError_t capnp_resync_decode_prefix(const uint8_t* d_in, uint64_t nbytes,
+                                                 uint64_t max_words, uint64_t* d_out, void* d_ws,
+                                                 size_t ws_bytes, hipStream_t s, uint64_t* bytes,
+                                                 uint64_t* words) {
     *bytes = *words = 0;
-    if (nbytes == 0) return hipSuccess;
+    if (nbytes == 0 || max_words == 0) return hipSuccess;
     hipError_t e;
     const uint64_t n = 1;
     const uint64_t nbb = blocks_bound(n, nbytes);
@@ -948,8 +1228,11 @@ extern "C" hipError_t capnp_resync_prefix(const uint8_t* d_in, uint64_t nbytes, 
     uint64_t* aux = (uint64_t*)(base + ((need - (base - (uint8_t*)d_ws) + 255) & ~size_t(255)));
     need = (uint8_t*)(aux + 16) - (uint8_t*)d_ws;
     if (need > ws_bytes) return hipErrorInvalidValue;
-    uint64_t* in_off = aux;      // [2]
-    uint64_t* tail = aux + 8;    // [2]
+    uint64_t* in_off = aux;   // [2]
+    uint64_t* out_off = aux + 2;  // [2]
+    uint64_t* kerr = aux + 4;     // [1]
+    uint64_t* cut = aux + 8;      // [2]
+    uint64_t* cutk = aux + 10;    // [1]
     const uint64_t h_in_off[2] = {0, nbytes};
     if ((e = hipMemcpyAsync(in_off, h_in_off, 16, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(w.flags, 0, 4 * (2 + kMaxPasses), s)) != hipSuccess) return e;
@@ -958,35 +1241,48 @@ extern "C" hipError_t capnp_resync_prefix(const uint8_t* d_in, uint64_t nbytes, 
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
         return e;
-    k_spec<<<grid(nbb), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart, w.spec_exit,
-                                                   w.spec_words, w.exit, w.entry, w.words);
-    const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
-    for (int pass = 0; pass < kMaxPasses;) {
-        for (int i = 0; i < kPassBatch; i++, pass++)
-            k_fix<<<grid(ngroups), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart,
-                                                              w.spec_exit, w.spec_words, w.exit,
-                                                              w.entry, w.words, w.flags, pass);
-        int32_t last = 0;
-        if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
-            hipSuccess)
-            return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        if (!last) break;
-        if (pass >= kMaxPasses) return hipErrorNotReady;  // (not converged)
-    }
+    int pass = 0;
+    bool conv = true;
+    if ((e = resolve(d_in, in_off, n, w, nbb, s, &pass, &conv)) != hipSuccess) return e;
+    if (!conv) return hipErrorNotReady;
     uint64_t nb = 0;
     if ((e = hipMemcpyAsync(&nb, w.bstart + n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     tb = w.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.words, w.wbase, (int)nb, s)) != hipSuccess)
         return e;
-    k_tail<<<1, 64, 0, s>>>(d_in, nbytes, w.exit, w.wbase, nb, tail);
-    uint64_t htail[2] = {0, 0};
-    if ((e = hipMemcpyAsync(htail, tail, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(kerr, &nb, 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    k_first_err<<<grid(nb), kThreads, 0, s>>>(w.exit, nb, nbytes, (unsigned long long*)kerr);
+    k_cut<<<grid(nb), kThreads, 0, s>>>(d_in, nbytes, max_words, w.exit, w.wbase, w.words, nb,
+                                        (const unsigned long long*)kerr, cut, cutk);
+    uint64_t hcut[3] = {0, 0, 0};
+    if ((e = hipMemcpyAsync(hcut, cut, 24, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    *bytes = htail[0];
-    *words = htail[1];
-    return hipSuccess;
+    *bytes = hcut[0];
+    *words = hcut[1];
+    if (!d_out || hcut[1] == 0) return hipSuccess;
+    // decode blocks 0 .. cut[2] as units, the last one ending at the cut
+    const uint64_t nu = hcut[2] + 1;
+    const uint64_t h_out_off[2] = {0, hcut[1]};
+    if ((e = hipMemcpyAsync(out_off, h_out_off, 16, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return e;
+    uint64_t* blk_in = w.spec_exit;
+    uint64_t* blk_out = w.entry;
+    int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
+    k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(in_off, n, out_off, w.bstart, w.exit, w.wbase,
+                                               nullptr, blk_in, blk_out);
+    k_set_cut<<<1, 64, 0, s>>>(blk_in, blk_out, nu, cut, cutk);
+    if ((e = capnp_launch_unpack(d_in, blk_in, nu, 0, d_out, blk_out, blk_status, nullptr, nullptr,
+                                 s)) != hipSuccess)
+        return e;
+    return hipStreamSynchronize(s);
+}
+
+extern "C" hipError_t capnp_resync_prefix(const uint8_t* d_in, uint64_t nbytes, void* d_ws,
+                                          size_t ws_bytes, hipStream_t s, uint64_t* bytes,
+                                          uint64_t* words) {
+    return capnp_resync_decode_prefix(d_in, nbytes, ~0ull, nullptr, d_ws, ws_bytes, s, bytes,
+                                      words);
 }
 
 // The message discovery of capnp_resync_find_messages (below); for
@@ -1039,32 +1335,23 @@ static hipError_t find_messages_impl(const uint8_t* d_in, uint64_t nbytes, uint6
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
         return e;
-    k_spec<<<grid(nbb), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart, w.spec_exit, w.spec_words,
-                                          w.exit, w.entry, w.words);
     int pass = 0;
-    const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
-    for (;;) {
-        if (pass >= kMaxPasses) break;  // (not converged: k_consistent bounds the walk
-                                        // to the exact prefix; the caller continues)
-        for (int i = 0; i < kPassBatch; i++, pass++)
-            k_fix<<<grid(ngroups), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart, w.spec_exit,
-                                                     w.spec_words, w.exit, w.entry, w.words,
-                                                     w.flags, pass);
-        int32_t last = 0;
-        if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
-            hipSuccess)
-            return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        if (!last) break;
-    }
+    bool conv = true;  // (not converged: k_consistent bounds the walk to the exact prefix)
+    if ((e = resolve(d_in, in_off, n, w, nbb, s, &pass, &conv)) != hipSuccess) return e;
     uint64_t nb = 0;
     if ((e = hipMemcpyAsync(&nb, w.bstart + n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     tb = w.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.words, w.wbase, (int)nb, s)) != hipSuccess)
         return e;
+    // the complete-record prefix (a record the stream cuts short ends it)
     uint64_t* tail = aux + 8;  // [2]
-    k_tail<<<1, 64, 0, s>>>(d_in, nbytes, w.exit, w.wbase, nb, tail);
+    uint64_t* cutk = aux + 11;
+    uint64_t* kerr = wout;     // (free until the message chain)
+    if ((e = hipMemcpyAsync(kerr, &nb, 8, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    k_first_err<<<grid(nb), kThreads, 0, s>>>(w.exit, nb, nbytes, (unsigned long long*)kerr);
+    k_cut<<<grid(nb), kThreads, 0, s>>>(d_in, nbytes, ~0ull, w.exit, w.wbase, w.words, nb,
+                                        (const unsigned long long*)kerr, tail, cutk);
     uint64_t htail[2] = {0, 0};
     if ((e = hipMemcpyAsync(htail, tail, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
@@ -1086,7 +1373,7 @@ static hipError_t find_messages_impl(const uint8_t* d_in, uint64_t nbytes, uint6
     int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
     k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(in_off, n, out_off, w.bstart, w.exit, w.wbase,
                                                nullptr, blk_in, blk_out);
-    k_set_tail<<<1, 64, 0, s>>>(blk_in, nb, tail);
+    k_set_cut<<<grid(nb + 1), kThreads, 0, s>>>(blk_in, blk_out, nb, tail, cutk);
     if ((e = capnp_launch_unpack(d_in, blk_in, nb, 0, d_words, blk_out, blk_status, nullptr,
                                  nullptr, s)) != hipSuccess)
         return e;

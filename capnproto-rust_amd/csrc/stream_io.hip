@@ -48,6 +48,9 @@
 
 // capi.hip (internal): the longest prefix of complete records of n host
 // bytes, resolved on the device.
+extern "C" capnp_status capnp_stream_decode_prefix(capnp_ctx* ctx, const uint8_t* host, size_t n,
+                                                   uint64_t max_words, uint64_t* out,
+                                                   uint64_t* bytes, uint64_t* words);
 extern "C" capnp_status capnp_stream_complete_prefix(capnp_ctx* ctx, const uint8_t* host,
                                                      size_t n, uint64_t* bytes, uint64_t* words);
 
@@ -225,13 +228,57 @@ capnp_status reader_lit_head(capnp_packed_reader* r) {
 // kMinUnit words (small reads are served from the decoded surplus), but an
 // inner reader that pends while the caller's own words are staged gets
 // those decoded rather than a pending answer.
-constexpr size_t kMinUnit = 256;
+constexpr size_t kMinUnit = 256;      // (>= the words of any one record: a run is 1 + 255)
+constexpr size_t kWholeUnit = 8192;   // units this long are cut at whole records on the device
+
+// A long unit: the staged input is resolved on the device and cut after the
+// last complete record that fits nw words (capnp_stream_decode_prefix), so
+// the unit ends cleanly (no doubling when a run crosses its end) and its
+// decode keeps the block walk (a unit with spare input bytes would take the
+// serial walk).  The read returns at most nw words: whole records, at least
+// nw - 255 of them unless the stream pends or ends.
+capnp_status reader_fill_whole(capnp_packed_reader* r, size_t nw) {
+    std::vector<uint8_t> out;
+    for (;;) {
+        if (r->ip == r->in.size()) {
+            capnp_status p = reader_pull(r);
+            if (p == CAPNP_NONE) return CAPNP_OK;  // clean end: nothing decoded
+            if (p != CAPNP_OK) return p;
+            continue;
+        }
+        capnp_status p = CAPNP_OK;
+        for (size_t need = nw * 10 + 16; r->in.size() - r->ip < need;)
+            if ((p = reader_pull(r, need - (r->in.size() - r->ip))) != CAPNP_OK) break;
+        out.resize(nw * 8);
+        uint64_t pb = 0, pw = 0;
+        capnp_status e = capnp_stream_decode_prefix(r->ctx, r->in.data() + r->ip,
+                                                    r->in.size() - r->ip, nw,
+                                                    reinterpret_cast<uint64_t*>(out.data()), &pb,
+                                                    &pw);
+        if (e != CAPNP_OK) return e;
+        if (pw > 0) {
+            out.resize(pw * 8);
+            r->ip += pb;
+            r->dec.swap(out);
+            r->dp = 0;
+            return CAPNP_OK;
+        }
+        // the first staged record is incomplete: more input, or pending / end
+        if (p == CAPNP_OK) p = reader_pull(r);
+        if (p == CAPNP_OK) continue;
+        if (p != CAPNP_NONE && p != CAPNP_PENDING) return p;
+        e = reader_lit_head(r);
+        if (e != CAPNP_NONE) return e;
+        return p == CAPNP_PENDING ? CAPNP_PENDING : CAPNP_E_PREMATURE_END_OF_FILE;  // UnexpectedEof
+    }
+}
 
 capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
     want = std::max<size_t>(want, 1);
     size_t nw = std::max(want, kMinUnit);
     std::vector<uint8_t> out;
     if (r->pass_rem) return reader_pass(r);
+    if (nw >= kWholeUnit) return reader_fill_whole(r, nw);
     for (;;) {
         if (r->ip == r->in.size()) {
             capnp_status p = reader_pull(r);

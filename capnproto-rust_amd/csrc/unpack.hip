@@ -1591,12 +1591,16 @@ unpack_ovf_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
 // The overflow tiles of the index-free split launch.  Index-free batches
 // can overflow in bulk -- the resync block decode of config 4 hands over
 // ~10 % of its tiles expanding past the tables (zero-run blocks) -- so the
-// tiles are checked in windows of 64 (one lane each) spread over up to 4096
+// tiles are checked in windows of kOvfWindow (one lane each) spread over up to 8192
 // workgroups, where unpack_ovf_kernel's windows of 256 on at most 1024
 // workgroups left a few hundred of them serialising the overflow tiles
 // (config 4 index-free: 4.3 ms in the overflow kernel; one workgroup per
 // tile instead cost config 2 0.13 ms of empty workgroups).
-constexpr uint32_t kOvfWindow = CAPNP_WAVE;
+#ifndef UNPACK_OVF_WINDOW
+#define UNPACK_OVF_WINDOW 16  // (64: config 4 index-free overflow 1.86 ms on 1155 workgroups)
+#endif
+constexpr uint32_t kOvfWindow = UNPACK_OVF_WINDOW;
+static_assert(kOvfWindow <= CAPNP_WAVE, "one lane per tile of the window");
 
 template <bool SYNC>
 __global__ void __launch_bounds__(kThreads)
@@ -1616,7 +1620,7 @@ unpack_ovf_win_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict
         if (wave == 0) {
             const uint64_t t = base + lane;
             bool o = false;
-            if (t < ntiles) {
+            if (lane < kOvfWindow && t < ntiles) {
                 const uint64_t ca = t * tc;
                 const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
                 o = !tile_fits_lane(in, in_off, out_off, ca, cb);
@@ -2258,7 +2262,7 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
                            UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
                            d_status, d_consumed, d_sync);
         const uint64_t wg = (blocks + kOvfWindow - 1) / kOvfWindow;
-        hipLaunchKernelGGL(unpack_ovf_win_kernel<false>, dim3((uint32_t)(wg < 4096 ? wg : 4096)),
+        hipLaunchKernelGGL(unpack_ovf_win_kernel<false>, dim3((uint32_t)(wg < 8192 ? wg : 8192)),
                            dim3(kThreads), 0, stream, d_in, d_in_off, nchunks, tc, d_out,
                            d_out_off, d_status, d_consumed, d_sync, blocks);
     } else

@@ -13,3 +13,7 @@ cat gpurun_out/${T}_adaptor.json
 timeout -k 10 300 python -u bench.py --no-cpu > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err \
   || { tail -20 gpurun_out/${T}_bench.err; exit 1; }
 python scripts/bench_summary.py default gpurun_out/${T}_bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${T}_c4 -o run --output-format csv \
+  -- python3 bench.py --workload config4 --steps 3 --warmup 1 --no-cpu > gpurun_out/${T}_c4.json 2> gpurun_out/${T}_c4.err \
+  || { tail -20 gpurun_out/${T}_c4.err; exit 1; }
+python scripts/bench_summary.py config4 gpurun_out/${T}_c4.json

@@ -1,0 +1,59 @@
+"""CPU check of the resync tile resolution's logic (tests/emu_resync.py
+restates csrc/resync.hip k_tile): on packed batches from the oracle (config-4
+kinds: ~30 %-zero words, long zero runs, long literal runs; mixed chunk
+sizes) every block resolves to the true chain's entry, exit and words, and a
+literal-run region costs one fix pass per tile it spans."""
+import numpy as np
+
+import emu_resync as E
+import oracle_lib as O
+
+
+def _batch(words, offs):
+    st, packed, poff = O.pack_batch(words, offs)
+    assert st == 0
+    return bytes(packed) + bytes(2100), [int(x) for x in poff]
+
+
+def _check(words, offs, blk, T, max_passes):
+    B, in_off = _batch(words, offs)
+    bl, res, passes, rounds = E.resolve(B, in_off, blk=blk, T=T)
+    truth = E.true_blocks(B, in_off, bl)
+    for k, (r, t) in enumerate(zip(res, truth)):
+        assert t is not None
+        assert r == t, (k, bl[k], r, t)
+    assert passes <= max_passes, passes
+    return passes, rounds
+
+
+def test_tile_resolution_kinds():
+    rng = np.random.default_rng(4)
+    sizes = np.exp(rng.uniform(np.log(8), np.log(1500), 60)).astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+    for kind in (0, 1, 2):
+        words = O.gen_fill(offs, kind0=kind, pz=O.PZ30)
+        _check(words, offs, blk=128, T=16, max_passes=8)
+
+
+def test_tile_resolution_literal_region_passes():
+    # one long literal chunk: 4 KiB tiles (16 blocks of 256 B), ~200 KiB of
+    # 0xFF records: the spec chains never couple, each pass settles a tile
+    n = 25000
+    lit = np.random.default_rng(2).integers(1 << 56, 1 << 63, n, dtype=np.uint64) * 2 + 1
+    offs = np.array([0, n], np.uint64)
+    passes, _ = _check(lit, offs, blk=256, T=16, max_passes=64)
+    assert passes >= 2
+
+
+def test_tile_resolution_runs_across_blocks():
+    n, cw = 40, 300
+    offs = np.arange(0, (n + 1) * cw, cw, dtype=np.uint64)
+    w = np.zeros(n * cw, np.uint64)
+    for c in range(n):
+        k = (c * 37) % 280
+        w[c * cw + 3:c * cw + 3 + k] = 0x1112131415161718
+        w[c * cw + 3 + k::7][:4] = 0x0000000100000001
+    _check(w, offs, blk=64, T=8, max_passes=64)
+    z = np.zeros(n * cw, np.uint64)
+    z[::97] = 5
+    _check(z, offs, blk=64, T=8, max_passes=64)

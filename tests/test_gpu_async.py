@@ -569,3 +569,67 @@ def test_literal_head_while_pending(A):
     assert got == bytes(range(1, 9)) + bytes(range(10, 26))
     assert pends <= 1  # (the pend may be absorbed while the head word is decoded)
     assert pr.read(8) == b""
+
+
+def _mixed_words(seed, n):
+    rng = np.random.default_rng(seed)
+    w = rng.integers(0, 1 << 63, n, dtype=np.uint64)
+    w[rng.random(n) < 0.3] = 0
+    w[n // 7:n // 7 + 3000] = 0  # long zero runs
+    w[n // 3:n // 3 + 4000] |= np.uint64(0x0101010101010101)  # long literal runs
+    sparse = rng.integers(0, 256, n, dtype=np.uint64) << np.uint64(8 * 3)
+    w[n // 2:n // 2 + 5000] = sparse[:5000]
+    return w
+
+
+def test_large_reads_whole_records(A):
+    """Reads of 64 KiB and more take whole-record units resolved on the
+    device (stream_io.hip reader_fill_whole): every read returns 1..n bytes,
+    the bytes are the stream's, a plain and a pending inner reader alike."""
+    from capnp_amd import CapnpError
+    w = _mixed_words(7, 300_000)
+    u = w.tobytes()
+    st, p = O.pack(u)
+    assert st == 0
+    for size in (1 << 20, (1 << 16) + 8, 200_008):
+        for inner in (_Plain(p), A.BlockingRead(p, 70_001)):
+            pr = A.PackedRead(inner)
+            got = bytearray()
+            while True:
+                try:
+                    b = pr.read(size)
+                except CapnpError as e:
+                    assert e.status == 15  # pending
+                    continue
+                if not b:
+                    break
+                assert 0 < len(b) <= size
+                got += b
+            assert bytes(got) == u, size
+
+
+def test_large_reads_truncated_stream(A):
+    """A truncated stream read in 1 MiB reads hands out what the reference's
+    stage machine does before UnexpectedEof (whole records, then a literal
+    run's head word and raw bytes)."""
+    from capnp_amd import CapnpError
+    w = _mixed_words(8, 40_000)
+    st, p = O.pack(w.tobytes())
+    assert st == 0
+    for cut in (len(p) - 1, len(p) - 5, len(p) // 3 + 17, len(p) // 3 + 1000, len(p) // 2 + 1,
+                len(p) // 7 + 3):
+        data = p[:cut]
+        ref, end = _ref_poll_reads(data, 1 << 20)
+        pr = A.PackedRead(_Plain(data))
+        got, err = b"", None
+        while True:
+            try:
+                b = pr.read(1 << 20)
+            except CapnpError as e:
+                err = e.kind
+                break
+            if not b:
+                break
+            got += b
+        assert got == ref, (cut, len(got), len(ref))
+        assert (err == "PrematureEndOfFile") == (end == "EOF"), (cut, err, end)

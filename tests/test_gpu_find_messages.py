@@ -197,3 +197,18 @@ def test_one_pass_matches_discovery(ctx):
                 assert ln == len(rs)
                 assert np.array_equal(w[a:a + ln], np.asarray(rs, np.uint64))
                 a += ln
+
+
+def test_truncated_inside_long_literal_run(ctx):
+    """A stream cut inside a literal run that began several 512-byte blocks
+    earlier: the blocks after the cut record hold no trusted chain, and the
+    messages before it still come back (the complete-record prefix is found
+    from the first block whose chain runs past the end)."""
+    rng = random.Random(21)
+    good = _stream(rng, 6)
+    lit = [np.array([rng.getrandbits(64) | 0x0101010101010101 for _ in range(2000)], np.uint64)]
+    st, b = O.write_message(lit)
+    assert st == 0
+    for cut in (40, 600, 1500, 2100, 5000, len(b) - 3):
+        _check(ctx, good + b[:cut])
+        _check(ctx, good + b + good[:cut % len(good)])
