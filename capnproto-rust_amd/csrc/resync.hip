@@ -234,79 +234,165 @@ k_fix(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint6
 // k_spec + k_fix walk each block from global memory, one lane per block, and
 // a chain that no speculative walk couples with (a literal-run region) moved
 // kGroup blocks per fix pass: config 4 spent 0.9 ms in k_spec and 1.95 ms in
-// 24 fix passes.  Here one wave takes a tile of kTileBlocks consecutive
-// blocks (contiguous packed bytes, <= 32 KiB), stages them in LDS and
-// resolves them among its lanes:
-//   spec   lane j walks from kLead bytes before its block (or from its
+// 24 fix passes.  Here a 256-thread workgroup takes a tile of kTileBlocks
+// consecutive blocks (contiguous packed bytes, <= 32 KiB), stages them in LDS
+// by DMA, and each wave resolves 16 blocks cut into kSegs segments of
+// kSegBytes, one lane each:
+//   spec   lane j walks from kLead bytes before its segment (or from its
 //          chunk's start) to its first record start f >= s, then on to its
 //          exit; the lead-in lets chains from different starts couple before
-//          the block begins, so f is usually the true start;
-//   rounds entries are a prefix max over the lanes' own exits (a block whose
+//          the segment begins, so f is usually the true start;
+//   rounds entries are a prefix max over the lanes' own exits (a segment whose
 //          entry lies past its end -- inside a literal run -- owns none and
 //          passes the entry on; a walk that runs past its chunk owns none
-//          either), with lane 0's entry the tile's and a chunk's first block
-//          entered at the chunk start.  A lane whose entry is not the one its
-//          state derives from walks again from it, in lockstep with its spec
-//          chain until they meet (then its exit stands).  At the fixed point
-//          every block's entry is its predecessor's exit.
-// Lane 0's entry is the previous tile's last exit: the spec launch assumes
-// its own f; fix passes (k_tile with fix = 1) re-resolve a tile whose stored
-// entry differs from the predecessor's exit, and flag a pass whose last exits
-// moved.  A region no walk couples with now costs one tile per pass (32 KiB)
-// instead of kGroup blocks (4 KiB).  The results (exit, entry, words per
-// block) are k_spec + k_fix's, so the scan, check and block decode follow
-// unchanged.
+//          either), with lane 0's entry the wave's and a chunk's first
+//          segment entered at the chunk start.  A lane whose entry is not the
+//          one its state derives from walks again from it, in lockstep with
+//          its spec chain until they meet (then its exit stands; the spec
+//          chain gives up after kCatchUp hops behind, and the walk goes on
+//          alone).  At the fixed point every segment's entry is its
+//          predecessor's exit;
+//   waves  wave w > 0 assumed its lane 0's f; in turn, each takes the previous
+//          wave's last exit and re-runs its rounds if that differs;
+//   blocks a block's entry is its first segment's, its exit its last
+//          segment's, its words the sum.
+// Segments of 128 bytes keep each walk short (a lane whose spec chain missed
+// walks its whole segment; with one lane per 512-byte block that was the
+// critical path, ~100 hops, and four waves share the tile's LDS).  Positions
+// inside the tile are 32-bit offsets from the staged base.
+// The tile's own entry is the previous tile's last exit: the spec launch
+// assumes its first lane's f; fix passes (k_tile with fix = 1) re-resolve a
+// tile whose stored entry differs from the predecessor's exit, and flag a
+// pass whose last exit moved.  A region no walk couples with costs one tile
+// per pass (32 KiB) instead of kGroup blocks (4 KiB).  The results (exit,
+// entry, words per block) are k_spec + k_fix's, so the scan, check and block
+// decode follow unchanged.
 #ifndef RESYNC_TILE
 #define RESYNC_TILE 1
 #endif
-constexpr uint32_t kTileBlocks = CAPNP_WAVE;
+constexpr uint32_t kSegs = 4;                               // segments per block
+constexpr uint32_t kSegBytes = (uint32_t)kBlock / kSegs;    // 128
+constexpr uint32_t kTileWaves = 4;
+constexpr uint32_t kWaveBlocks = CAPNP_WAVE / kSegs;        // 16
+constexpr uint32_t kTileBlocks = kTileWaves * kWaveBlocks;  // 64
+constexpr uint32_t kTileThreads = kTileWaves * CAPNP_WAVE;
 constexpr uint64_t kLead = 48;
+constexpr uint32_t kCatchUp = 16;
 constexpr uint32_t kTileLds = (uint32_t)(kTileBlocks * kBlock + kLead + 64);
+constexpr uint32_t kRelCap = 0xF0000000u;  // chunk ends past this are "far" (tile offsets are < 40 K)
+constexpr uint32_t kNone32 = 0xFFFFFFFFu;
+static_assert(kBlock % kSegs == 0, "segments tile the block");
 
-// hop() on the staged bytes (buf holds in[base ...]).
-__device__ __forceinline__ void hop_lds(const uint8_t* buf, uint64_t base, uint64_t& p,
-                                        uint64_t& w, uint64_t b) {
-    const uint32_t tag = buf[p - base];
-    uint64_t q = p + 1 + __builtin_popcount(tag);
+// hop() on the staged bytes, positions relative to the staged base.
+__device__ __forceinline__ void hop32(const uint8_t* buf, uint32_t& p, uint32_t& w, uint32_t b) {
+    const uint32_t tag = buf[p];
+    uint32_t q = p + 1 + __builtin_popcount(tag);
     w += 1;
     if (tag == 0u || tag == 0xFFu) {
         if (q >= b) {
             p = b + 1;
             return;
         }
-        const uint32_t r = buf[q - base];
+        const uint32_t r = buf[q];
         q += 1;
         w += r;
-        if (tag == 0xFFu) q += 8ull * r;
+        if (tag == 0xFFu) q += 8u * r;
     }
     p = q > b ? b + 1 : q;
 }
 
-__device__ __forceinline__ uint64_t wave_excl_max(uint64_t v, uint32_t lane) {
-    uint64_t x = v;
+__device__ __forceinline__ uint32_t wave_excl_max32(uint32_t v, uint32_t lane) {
+    uint32_t x = v;
 #pragma unroll
     for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
-        const uint64_t y = __shfl_up(x, d);
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
         if (lane >= d && y > x) x = y;
     }
-    const uint64_t e = __shfl_up(x, 1);
-    return lane == 0 ? 0 : e;
+    const uint32_t e = (uint32_t)__shfl_up((int)x, 1);
+    return lane == 0 ? 0u : e;
 }
 
-__global__ void __launch_bounds__(CAPNP_WAVE)
+// One lane's segment state for the rounds.
+struct SegState {
+    uint32_t ss, se, b, a;  // segment [ss, se), chunk end, chunk start (relative)
+    uint32_t f, sx, sw;     // spec chain: first start >= ss (kNone32: none), exit, words
+    bool serr;
+    uint32_t used, ex, own; // entry the state derives from, exit, owned exit (0: none)
+    uint32_t wd;            // words from used to ex
+};
+
+// Rounds to the fixed point for the wave (in_j: lane 0's entry, a chunk's
+// first segment's start, else 0).
+__device__ __forceinline__ void seg_rounds(const uint8_t* buf, SegState& S, bool valid,
+                                           uint32_t in_j, bool fixed_j, uint32_t lane) {
+    for (;;) {
+        uint32_t v = S.own > in_j ? S.own : in_j;
+        if (!valid) v = 0;
+        const uint32_t pm = wave_excl_max32(v, lane);
+        const uint32_t ent = fixed_j ? in_j : pm;
+        const bool need = valid && ent != S.used;
+        if (ballot64(need) == 0) break;
+        if (!need) continue;
+        S.used = ent;
+        if (ent < S.ss || ent > S.b) {  // below the segment (a walk failed earlier) or past the chunk
+            S.ex = S.b + 1;
+            S.wd = 0;
+            S.own = 0;
+        } else if (ent >= S.se && S.se > S.ss) {  // inside a record that began earlier
+            S.ex = ent;
+            S.wd = 0;
+            S.own = 0;
+        } else if (S.se == S.ss) {  // an empty segment (a short block's tail) passes its entry on
+            S.ex = ent;
+            S.wd = 0;
+            S.own = 0;
+        } else {
+            uint32_t pt = ent, wt = 0, ps = S.f, ws = 0, catchup = 0;
+            bool spec = S.f != kNone32 && S.f < S.se, met = false;
+            while (pt < S.se) {
+                if (spec) {
+                    while (ps < pt && ps < S.se && catchup < kCatchUp) {
+                        hop32(buf, ps, ws, S.b);
+                        catchup++;
+                    }
+                    if (ps == pt) {
+                        met = true;
+                        break;
+                    }
+                    if (ps < pt) spec = false;  // too far behind: walk alone
+                }
+                hop32(buf, pt, wt, S.b);
+            }
+            if (met) {
+                S.ex = S.sx;
+                S.wd = wt + S.sw - ws;
+                S.own = S.serr ? 0 : S.sx;
+            } else {
+                S.ex = pt;
+                S.wd = wt;
+                S.own = pt > S.b ? 0 : pt;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kTileThreads)
 k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
        const uint64_t* __restrict__ bstart, uint64_t* exit, uint64_t* __restrict__ entry,
        uint64_t* __restrict__ words, int32_t* flags, int pass, int fix) {
     extern __shared__ __align__(16) uint8_t tbuf[];
+    __shared__ uint32_t wexit[kTileWaves];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & (CAPNP_WAVE - 1);
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid / CAPNP_WAVE));
     const uint64_t nb = uniform64(bstart[n]);
     const uint64_t k0 = (uint64_t)blockIdx.x * kTileBlocks;
     if (k0 >= nb) return;
     if (fix && pass > 0 && __atomic_load_n(&flags[2 + pass - 1], __ATOMIC_RELAXED) == 0) return;
-    const uint32_t lane = threadIdx.x;
     const uint64_t kn = nb - k0 < kTileBlocks ? nb - k0 : kTileBlocks;
-    uint64_t e0 = 0;  // lane 0's entry
+    uint64_t e0 = 0;  // the tile's entry (fix passes)
     if (fix) {
-        e0 = __atomic_load_n(&exit[k0 - 1], __ATOMIC_RELAXED);
+        e0 = uniform64(__atomic_load_n(&exit[k0 - 1], __ATOMIC_RELAXED));
         if (e0 == uniform64(entry[k0])) return;  // consistent
     }
     // c0 = the last chunk with bstart[c0] <= k0: a 64-way search (3 probes
@@ -324,8 +410,7 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     }
     const uint64_t c0 = clo;
     const uint64_t bs0 = uniform64(bstart[c0]), a0 = uniform64(in_off[c0]);
-    // (a tile that starts a chunk is exact since the spec launch)
-    if (fix && bs0 == k0) return;
+    if (fix && bs0 == k0) return;  // a tile that starts a chunk is exact since the spec launch
     // stage [s0 - kLead, s0 + 32 KiB + 16) (clamped to the batch: the tile's
     // blocks are contiguous bytes, at most kBlock each) by LDS DMA, 16 bytes a
     // lane, every load in flight at once
@@ -338,17 +423,19 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     {
         const uint32_t nv = (uint32_t)((hi - base + 15) >> 4);
         const uint8_t* src = in + base;
-        for (uint32_t i0 = 0; i0 < nv; i0 += CAPNP_WAVE) {
+        for (uint32_t i0 = wave * CAPNP_WAVE; i0 < nv; i0 += kTileThreads) {
             if (i0 + lane < nv)
                 __builtin_amdgcn_global_load_lds(
                     (const __attribute__((address_space(1))) void*)(src + 16ull * (i0 + lane)),
                     (__attribute__((address_space(3))) void*)(tbuf + 16u * i0), 16, 0, 0);
         }
     }
-    // lane j's chunk: c0 + the chunk starts in (k0, k0 + j], counted over
-    // batches of 64 starts (a lane's binary search over the batch by shuffles)
-    const bool valid = lane < kn;
-    const uint32_t jj = valid ? lane : (uint32_t)(kn - 1);
+    // this lane's block (offset jb in the tile) and segment q; its chunk: c0 +
+    // the chunk starts in (k0, k0 + jb], counted over batches of 64 starts (a
+    // lane's binary search over the batch by shuffles)
+    const uint32_t jb = wave * kWaveBlocks + lane / kSegs, q = lane % kSegs;
+    const bool valid = jb < kn;
+    const uint32_t jj = valid ? jb : (uint32_t)(kn - 1);
     const uint64_t k = k0 + jj;
     uint64_t c = c0;
     for (uint64_t cb = c0 + 1;; cb += CAPNP_WAVE) {
@@ -366,93 +453,98 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     const uint64_t a = in_off[c], b = in_off[c + 1], bsc = bstart[c];
     const uint64_t s = a + (k - bsc) * kBlock;
     const uint64_t e = s + kBlock < b ? s + kBlock : b;
-    const bool cfirst = k == bsc;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the staged bytes are in
-    // spec walk (a chunk's first block walks exactly from the chunk start)
-    constexpr uint64_t kNone = ~0ull;
-    uint64_t f, sx, sw = 0;
-    bool serr = false;
+    const uint64_t ssa = s + q * kSegBytes < e ? s + q * kSegBytes : e;
+    const uint64_t sea = s + (q + 1) * kSegBytes < e ? s + (q + 1) * kSegBytes : e;
+    const bool cfirst = k == bsc && q == 0;
+    const uint64_t starta = ssa > a + kLead ? ssa - kLead : a;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's staged bytes are in
+    __syncthreads();                                   // ... and every wave's
+    SegState S;
+    S.ss = (uint32_t)(ssa - base);
+    S.se = (uint32_t)(sea - base);
+    S.b = b - base < kRelCap ? (uint32_t)(b - base) : kRelCap;
+    S.a = (uint32_t)(a > base ? a - base : 0);
+    // spec walk (a chunk's first segment walks exactly from the chunk start)
     {
-        uint64_t p = s > a + kLead ? s - kLead : a, w = 0;
-        while (p < s) hop_lds(tbuf, base, p, w, b);
-        if (p > b) {  // the lead-in ran past the chunk: no spec chain
-            f = kNone;
-            sx = b + 1;
-            serr = true;
+        uint32_t p = (uint32_t)(starta - base), w = 0;
+        while (p < S.ss) hop32(tbuf, p, w, S.b);
+        if (p > S.b) {  // the lead-in ran past the chunk: no spec chain
+            S.f = kNone32;
+            S.sx = S.b + 1;
+            S.sw = 0;
+            S.serr = true;
         } else {
-            f = p;
+            S.f = p;
             w = 0;
-            while (p < e) hop_lds(tbuf, base, p, w, b);
-            sx = p;
-            sw = w;
-            serr = p > b;
+            while (p < S.se) hop32(tbuf, p, w, S.b);
+            S.sx = p;
+            S.sw = w;
+            S.serr = p > S.b;
         }
     }
-    // state: entry used, exit, words, own exit (0: none)
-    uint64_t used, ex, wd, own;
-    if (f != kNone && f >= e) {  // spec pass-through
-        used = f;
-        ex = f;
-        wd = 0;
-        own = 0;
+    if (S.f != kNone32 && (S.f >= S.se || S.se == S.ss)) {  // spec pass-through
+        S.used = S.f;
+        S.ex = S.f;
+        S.wd = 0;
+        S.own = 0;
     } else {
-        used = f;
-        ex = sx;
-        wd = sw;
-        own = serr ? 0 : sx;
+        S.used = S.f;
+        S.ex = S.sx;
+        S.wd = S.sw;
+        S.own = S.serr ? 0 : S.sx;
     }
-    if (!fix) e0 = uniform64(readlane64(f == kNone ? s : f, 0));  // the spec launch's assumption
-    const uint64_t in_j = lane == 0 ? e0 : (cfirst ? a : 0);
-    for (;;) {
-        uint64_t v = own > in_j ? own : in_j;
-        if (!valid) v = 0;
-        const uint64_t pm = wave_excl_max(v, lane);
-        const uint64_t ent = lane == 0 ? e0 : (cfirst ? a : pm);
-        const bool need = valid && ent != used;
-        if (ballot64(need) == 0) break;
-        if (need) {
-            used = ent;
-            if (ent < s || ent > b) {  // below the block (a chunk's walk failed earlier) or past it
-                ex = b + 1;
-                wd = 0;
-                own = 0;
-            } else if (ent >= e) {  // inside a record that began earlier
-                ex = ent;
-                wd = 0;
-                own = 0;
-            } else {
-                uint64_t pt = ent, wt = 0, ps = f, ws = 0;
-                bool met = false;
-                if (f != kNone && f < e) {
-                    while (pt < e) {
-                        while (ps < pt && ps < e) hop_lds(tbuf, base, ps, ws, b);
-                        if (ps == pt) {
-                            met = true;
-                            break;
-                        }
-                        hop_lds(tbuf, base, pt, wt, b);
-                    }
-                } else {
-                    while (pt < e) hop_lds(tbuf, base, pt, wt, b);
-                }
-                if (met) {
-                    ex = sx;
-                    wd = wt + sw - ws;
-                    own = serr ? 0 : sx;
-                } else {
-                    ex = pt;
-                    wd = wt;
-                    own = pt > b ? 0 : pt;
-                }
+    // lane 0's entry: the tile's (wave 0 of a fix pass), else its own f
+    const uint32_t f0 = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(S.f == kNone32 ? S.ss : S.f));
+    uint32_t E0;
+    if (fix && wave == 0) {
+        const uint64_t r = e0 - base;
+        E0 = e0 < base ? 0 : (r < kRelCap ? (uint32_t)r : kRelCap + 1);
+    } else {
+        E0 = f0;
+    }
+    const bool first_lane0 =
+        __builtin_amdgcn_readfirstlane((int)cfirst) != 0;  // lane 0 starts a chunk: exact
+    bool fixed_j = lane == 0 || cfirst;
+    uint32_t in_j = lane == 0 ? (first_lane0 ? S.ss : E0) : (cfirst ? S.ss : 0);
+    seg_rounds(tbuf, S, valid, in_j, fixed_j, lane);
+    // the waves in turn: each takes the previous wave's last exit
+    const uint32_t nvalid = kn > (uint64_t)wave * kWaveBlocks
+                                ? (uint32_t)((kn - (uint64_t)wave * kWaveBlocks) < kWaveBlocks
+                                                 ? (kn - (uint64_t)wave * kWaveBlocks) * kSegs
+                                                 : CAPNP_WAVE)
+                                : 0u;
+    if (nvalid && lane == 0) wexit[wave] = 0;
+    if (nvalid) {
+        const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)S.ex, nvalid - 1);
+        if (lane == 0) wexit[wave] = lx;
+    }
+    __syncthreads();
+    for (uint32_t t = 1; t < kTileWaves; t++) {
+        if (wave == t && nvalid && !first_lane0) {
+            const uint32_t E = wexit[t - 1];
+            if (E != E0) {
+                E0 = E;
+                if (lane == 0) in_j = E;
+                seg_rounds(tbuf, S, valid, in_j, fixed_j, lane);
+                const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)S.ex, nvalid - 1);
+                if (lane == 0) wexit[wave] = lx;
             }
         }
+        __syncthreads();
     }
-    if (valid) {
+    // blocks: entry of segment 0, exit of segment 3, words summed
+    uint32_t wsum = S.wd + (uint32_t)__shfl_xor((int)S.wd, 1);
+    wsum += (uint32_t)__shfl_xor((int)wsum, 2);
+    const uint32_t bx = (uint32_t)__shfl((int)S.ex, (int)(lane | (kSegs - 1)));
+    if (valid && q == 0) {
+        const uint64_t xa = bx > S.b ? b + 1 : base + bx;
+        const uint64_t ea = S.used > S.b ? b + 1 : base + S.used;
         const uint64_t old = fix ? exit[k] : 0;
-        exit[k] = ex;
-        entry[k] = used;
-        words[k] = wd;
-        if (fix && (uint64_t)lane == kn - 1 && old != ex) flags[2 + pass] = 1;
+        exit[k] = xa;
+        entry[k] = ea;
+        words[k] = wsum;
+        if (fix && (uint64_t)jb == kn - 1 && old != xa) flags[2 + pass] = 1;
     }
 }
 
@@ -576,8 +668,8 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
     const unsigned tgrid = (unsigned)((nbb + kTileBlocks - 1) / kTileBlocks);
     const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
     if (tile)
-        k_tile<<<tgrid, CAPNP_WAVE, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
-                                                  w.words, w.flags, 0, 0);
+        k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
+                                                    w.words, w.flags, 0, 0);
     else
         k_spec<<<grid(nbb), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart, w.spec_exit,
                                                        w.spec_words, w.exit, w.entry, w.words);
@@ -589,8 +681,8 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
         }
         for (int i = 0; i < kPassBatch; i++, pass++) {
             if (tile)
-                k_tile<<<tgrid, CAPNP_WAVE, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
-                                                          w.entry, w.words, w.flags, pass, 1);
+                k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
+                                                            w.entry, w.words, w.flags, pass, 1);
             else
                 k_fix<<<grid(ngroups), kThreads, walk_lds(), s>>>(
                     d_in, in_off, n, w.bstart, w.spec_exit, w.spec_words, w.exit, w.entry,

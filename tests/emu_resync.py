@@ -1,6 +1,7 @@
-"""Emulation of the resync tile resolution (csrc/resync.hip k_tile: spec
-walks led in by kLead bytes, rounds of a prefix max over owned exits with
-lockstep meet walks, fix passes over tiles) on the CPU: test infrastructure
+"""Emulation of the resync tile resolution (csrc/resync.hip k_tile: blocks
+cut into segments, spec walks led in by kLead bytes, per-wave rounds of a
+prefix max over owned exits with lockstep meet walks, the waves in turn, fix
+passes over tiles) on the CPU: test infrastructure
 that checks its logic against the true record chain before any GPU run.  Not
 a decoder: it returns each block's (entry, exit, words) as the kernel stores
 them (k_spec + k_fix's contract)."""
@@ -35,41 +36,20 @@ def blocks_of(in_off, blk):
     return out
 
 
-def tile(B, in_off, bl, k0, T, lead, E0=None):
-    """One k_tile launch for the tile at block k0 (E0 None: the spec launch)."""
+def _rounds(B, st, E0, catchup):
+    """seg_rounds(): the wave's rounds to the fixed point (st: its lanes)."""
     NONE = -1
-    lanes = bl[k0:k0 + T]
-    st = []
-    for (c, s, e, first) in lanes:
-        a, b = in_off[c], in_off[c + 1]
-        p, w = (s - lead if s > a + lead else a), 0
-        while p < s:
-            p, w = hop(B, p, w, b)
-        if p > b:
-            f, sx, sw, serr = NONE, b + 1, 0, True
-        else:
-            f, w = p, 0
-            while p < e:
-                p, w = hop(B, p, w, b)
-            sx, sw, serr = p, w, p > b
-        if f != NONE and f >= e:
-            used, ex, wd, own = f, f, 0, 0
-        else:
-            used, ex, wd, own = f, sx, sw, (0 if serr else sx)
-        st.append(dict(c=c, a=a, b=b, s=s, e=e, first=first, f=f, sx=sx, sw=sw, serr=serr,
-                       used=used, ex=ex, wd=wd, own=own))
-    if E0 is None:
-        E0 = st[0]["f"] if st[0]["f"] != NONE else st[0]["s"]
     rounds = 0
     while True:
         ins = [E0 if j == 0 else (L["a"] if L["first"] else 0) for j, L in enumerate(st)]
         pm, ents = 0, []
         for j, L in enumerate(st):
-            ents.append(E0 if j == 0 else (L["a"] if L["first"] else pm))
-            pm = max(pm, L["own"], ins[j])
-        need = [ents[j] != L["used"] for j, L in enumerate(st)]
+            ents.append(ins[j] if (j == 0 or L["first"]) else pm)
+            if L["valid"]:
+                pm = max(pm, L["own"], ins[j])
+        need = [L["valid"] and ents[j] != L["used"] for j, L in enumerate(st)]
         if not any(need):
-            break
+            return rounds
         rounds += 1
         for j, L in enumerate(st):
             if not need[j]:
@@ -78,39 +58,104 @@ def tile(B, in_off, bl, k0, T, lead, E0=None):
             s, e, b, f = L["s"], L["e"], L["b"], L["f"]
             if ent < s or ent > b:
                 L["ex"], L["wd"], L["own"] = b + 1, 0, 0
-            elif ent >= e:
+            elif ent >= e or e == s:
                 L["ex"], L["wd"], L["own"] = ent, 0, 0
             else:
-                pt, wt, ps, ws, met = ent, 0, f, 0, False
-                if f != NONE and f < e:
-                    while pt < e:
-                        while ps < pt and ps < e:
+                pt, wt, ps, ws, met, cu = ent, 0, f, 0, False, 0
+                spec = f != NONE and f < e
+                while pt < e:
+                    if spec:
+                        while ps < pt and ps < e and cu < catchup:
                             ps, ws = hop(B, ps, ws, b)
+                            cu += 1
                         if ps == pt:
                             met = True
                             break
-                        pt, wt = hop(B, pt, wt, b)
-                else:
-                    while pt < e:
-                        pt, wt = hop(B, pt, wt, b)
+                        if ps < pt:
+                            spec = False
+                    pt, wt = hop(B, pt, wt, b)
                 if met:
                     L["ex"], L["wd"] = L["sx"], wt + L["sw"] - ws
                     L["own"] = 0 if L["serr"] else L["sx"]
                 else:
                     L["ex"], L["wd"], L["own"] = pt, wt, (0 if pt > b else pt)
-    return [(L["used"], L["ex"], L["wd"]) for L in st], rounds
 
 
-def resolve(B, in_off, blk=512, T=64, lead=48, max_passes=512, snapshot=True):
+def tile(B, in_off, bl, k0, T, lead, E0=None, segs=4, waves=4, catchup=16):
+    """One k_tile launch for the tile at block k0 (E0 None: the spec launch):
+    T blocks, waves x (T / waves) blocks, `segs` segments a block."""
+    NONE = -1
+    kn = min(T, len(bl) - k0)
+    lanes = []
+    for jb in range(T):
+        jj = min(jb, kn - 1)
+        c, s, e, first = bl[k0 + jj]
+        a, b = in_off[c], in_off[c + 1]
+        for q in range(segs):
+            lanes.append((jb < kn, c, a, b, s, e, first and q == 0, q))
+    st = []
+    for (valid, c, a, b, s, e, first, q) in lanes:
+        seg = SEG  # kSegBytes
+        ss, se = min(s + q * seg, e), min(s + (q + 1) * seg, e)
+        p, w = (ss - lead if ss > a + lead else a), 0
+        while p < ss:
+            p, w = hop(B, p, w, b)
+        if p > b:
+            f, sx, sw, serr = NONE, b + 1, 0, True
+        else:
+            f, w = p, 0
+            while p < se:
+                p, w = hop(B, p, w, b)
+            sx, sw, serr = p, w, p > b
+        L = dict(valid=valid, a=a, b=b, s=ss, e=se, first=first, f=f, sx=sx, sw=sw, serr=serr)
+        if f != NONE and (f >= se or se == ss):
+            L.update(used=f, ex=f, wd=0, own=0)
+        else:
+            L.update(used=f, ex=sx, wd=sw, own=(0 if serr else sx))
+        st.append(L)
+    W = len(st) // waves
+    wst = [st[w * W:(w + 1) * W] for w in range(waves)]
+    E0s, rounds = [], 0
+    for w in range(waves):
+        L0 = wst[w][0]
+        e = E0 if (w == 0 and E0 is not None) else (L0["f"] if L0["f"] != NONE else L0["s"])
+        if L0["first"]:
+            e = L0["s"]
+        E0s.append(e)
+        rounds = max(rounds, _rounds(B, wst[w], e, catchup))
+
+    def last_exit(w):
+        v = [L for L in wst[w] if L["valid"]]
+        return v[-1]["ex"] if v else None
+    for w in range(1, waves):
+        if not any(L["valid"] for L in wst[w]) or wst[w][0]["first"]:
+            continue
+        E = last_exit(w - 1)
+        if E != E0s[w]:
+            E0s[w] = E
+            rounds = max(rounds, _rounds(B, wst[w], E, catchup))
+    out = []
+    for jb in range(kn):
+        g = st[jb * segs:(jb + 1) * segs]
+        out.append((g[0]["used"], g[-1]["ex"], sum(x["wd"] for x in g)))
+    return out, rounds
+
+
+SEG = 128
+
+
+def resolve(B, in_off, blk=512, T=64, lead=48, max_passes=512, snapshot=True, segs=4, waves=4):
     """Spec launch + fix passes: per block (entry, exit, words), passes, max rounds.
     snapshot: a pass reads its predecessors' exits as the previous pass left
     them (the GPU's concurrent tiles, the slow case); else in tile order."""
+    global SEG
+    SEG = blk // segs
     bl = blocks_of(in_off, blk)
     nb = len(bl)
     res = [None] * nb
     worst = 0
     for k0 in range(0, nb, T):
-        r, rounds = tile(B, in_off, bl, k0, T, lead)
+        r, rounds = tile(B, in_off, bl, k0, T, lead, None, segs, waves)
         res[k0:k0 + T] = r
         worst = max(worst, rounds)
     passes = 0
@@ -125,7 +170,7 @@ def resolve(B, in_off, blk=512, T=64, lead=48, max_passes=512, snapshot=True):
             if E0 == res[k0][0]:
                 continue
             old = res[min(k0 + T, nb) - 1][1]
-            r, rounds = tile(B, in_off, bl, k0, T, lead, E0)
+            r, rounds = tile(B, in_off, bl, k0, T, lead, E0, segs, waves)
             res[k0:k0 + T] = r
             worst = max(worst, rounds)
             changed |= r[-1][1] != old

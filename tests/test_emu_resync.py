@@ -33,6 +33,7 @@ def test_tile_resolution_kinds():
     for kind in (0, 1, 2):
         words = O.gen_fill(offs, kind0=kind, pz=O.PZ30)
         _check(words, offs, blk=128, T=16, max_passes=8)
+        _check(words, offs, blk=512, T=64, max_passes=8)
 
 
 def test_tile_resolution_literal_region_passes():
