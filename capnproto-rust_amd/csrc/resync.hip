@@ -334,7 +334,15 @@ __device__ __forceinline__ void seg_rounds(const uint8_t* buf, SegState& S, bool
         if (ballot64(need) == 0) break;
         if (!need) continue;
         S.used = ent;
-        if (ent < S.ss || ent > S.b) {  // below the segment (a walk failed earlier) or past the chunk
+        if (ent < S.ss) {
+            // no predecessor reaches this segment yet (one still stands on a
+            // wrong entry, or its chunk failed): the spec chain stands in for
+            // the successors (an error exit marks the segment until an entry
+            // reaches it; at the fixed point of a valid chunk none is left)
+            S.ex = S.b + 1;
+            S.wd = 0;
+            S.own = (S.f != kNone32 && S.f < S.se && !S.serr) ? S.sx : 0;
+        } else if (ent > S.b) {  // past the chunk
             S.ex = S.b + 1;
             S.wd = 0;
             S.own = 0;
@@ -379,7 +387,8 @@ __device__ __forceinline__ void seg_rounds(const uint8_t* buf, SegState& S, bool
 __global__ void __launch_bounds__(kTileThreads)
 k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
        const uint64_t* __restrict__ bstart, uint64_t* exit, uint64_t* __restrict__ entry,
-       uint64_t* __restrict__ words, int32_t* flags, int pass, int fix) {
+       uint64_t* __restrict__ words, uint64_t* __restrict__ blk_c, int32_t* flags, int pass,
+       int fix) {
     extern __shared__ __align__(16) uint8_t tbuf[];
     __shared__ uint32_t wexit[kTileWaves];
     const uint32_t tid = threadIdx.x;
@@ -544,16 +553,30 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
         exit[k] = xa;
         entry[k] = ea;
         words[k] = wsum;
+        if (!fix) blk_c[k] = c;
         if (fix && (uint64_t)jb == kn - 1 && old != xa) flags[2 + pass] = 1;
     }
+}
+
+// Chunks with a block whose resolved chain ran past the chunk end (the tile
+// resolution marks such a block with exit b + 1; a segment that no entry
+// reached keeps that mark): bad[c] = 1.  blk_c[k] = block k's chunk.
+__global__ void __launch_bounds__(kThreads)
+k_mark(const uint64_t* __restrict__ exit, const uint64_t* __restrict__ blk_c,
+       const uint64_t* __restrict__ in_off, const uint64_t* __restrict__ bstart, uint64_t n,
+       int32_t* __restrict__ bad) {
+    const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (k >= bstart[n]) return;
+    const uint64_t c = blk_c[k];
+    if (exit[k] > in_off[c + 1]) bad[c] = 1;
 }
 
 __global__ void __launch_bounds__(kThreads)
 k_check(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __restrict__ out_off,
         const uint64_t* __restrict__ bstart, const uint64_t* __restrict__ exit,
         const uint64_t* __restrict__ words, const uint64_t* __restrict__ wbase,
-        int32_t* __restrict__ ok, int32_t* __restrict__ status, uint64_t* __restrict__ consumed,
-        int32_t* __restrict__ flags) {
+        const int32_t* __restrict__ bad, int32_t* __restrict__ ok, int32_t* __restrict__ status,
+        uint64_t* __restrict__ consumed, int32_t* __restrict__ flags) {
     const uint64_t c = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (c >= n) return;
     const uint64_t a = in_off[c], b = in_off[c + 1];
@@ -565,7 +588,7 @@ k_check(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __restr
         good = false;
     } else {
         const uint64_t f = bstart[c], l = bstart[c + 1] - 1;
-        good = exit[l] == b && wbase[l] + words[l] - wbase[f] == nw;
+        good = exit[l] == b && wbase[l] + words[l] - wbase[f] == nw && !(bad && bad[c]);
     }
     ok[c] = good;
     if (good) {
@@ -657,6 +680,13 @@ uint64_t blocks_bound(uint64_t n, uint64_t total_bytes) { return total_bytes / k
 
 unsigned grid(uint64_t items) { return (unsigned)((items + kThreads - 1) / kThreads); }
 
+// The tile resolution, unless CAPNP_RESYNC_BLOCKWALK selects k_spec + k_fix
+// (diagnostic A/B).
+bool tile_mode() {
+    static const bool v = RESYNC_TILE && getenv("CAPNP_RESYNC_BLOCKWALK") == nullptr;
+    return v;
+}
+
 // Spec walks, then fix passes to the fixed point (kPassBatch per flag
 // read-back).  *converged = false after kMaxPasses passes.  Blocking.
 hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, const Ws& w,
@@ -664,12 +694,12 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
     hipError_t e;
     *passes = 0;
     *converged = true;
-    const bool tile = RESYNC_TILE && getenv("CAPNP_RESYNC_BLOCKWALK") == nullptr;
+    const bool tile = tile_mode();
     const unsigned tgrid = (unsigned)((nbb + kTileBlocks - 1) / kTileBlocks);
     const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
     if (tile)
         k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
-                                                    w.words, w.flags, 0, 0);
+                                                    w.words, w.spec_exit, w.flags, 0, 0);
     else
         k_spec<<<grid(nbb), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart, w.spec_exit,
                                                        w.spec_words, w.exit, w.entry, w.words);
@@ -682,7 +712,8 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
         for (int i = 0; i < kPassBatch; i++, pass++) {
             if (tile)
                 k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
-                                                            w.entry, w.words, w.flags, pass, 1);
+                                                            w.entry, w.words, w.spec_exit, w.flags,
+                                                            pass, 1);
             else
                 k_fix<<<grid(ngroups), kThreads, walk_lds(), s>>>(
                     d_in, in_off, n, w.bstart, w.spec_exit, w.spec_words, w.exit, w.entry,
@@ -757,8 +788,14 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
         if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.words, w.wbase, (int)nbb, s)) !=
             hipSuccess)
             return e;
+        int32_t* bad = nullptr;
+        if (tile_mode()) {  // (blk_c in spec_exit, bad in spec_words: both dead until k_blocks)
+            bad = reinterpret_cast<int32_t*>(w.spec_words);
+            if ((e = hipMemsetAsync(bad, 0, 4 * n, s)) != hipSuccess) return e;
+            k_mark<<<grid(nbb), kThreads, 0, s>>>(w.exit, w.spec_exit, d_in_off, w.bstart, n, bad);
+        }
         k_check<<<grid(n), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit, w.words,
-                                             w.wbase, w.ok, d_status, d_consumed, w.flags);
+                                             w.wbase, bad, w.ok, d_status, d_consumed, w.flags);
         uint64_t nb = 0;
         if ((e = hipMemcpyAsync(hflags, w.flags, 8, hipMemcpyDeviceToHost, s)) != hipSuccess)
             return e;

@@ -56,7 +56,10 @@ def _rounds(B, st, E0, catchup):
                 continue
             ent = L["used"] = ents[j]
             s, e, b, f = L["s"], L["e"], L["b"], L["f"]
-            if ent < s or ent > b:
+            if ent < s:  # not reached yet: the spec chain stands in for the successors
+                L["ex"], L["wd"] = b + 1, 0
+                L["own"] = L["sx"] if (f != NONE and f < e and not L["serr"]) else 0
+            elif ent > b:
                 L["ex"], L["wd"], L["own"] = b + 1, 0, 0
             elif ent >= e or e == s:
                 L["ex"], L["wd"], L["own"] = ent, 0, 0
