@@ -546,8 +546,13 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     uint32_t wsum = S.wd + (uint32_t)__shfl_xor((int)S.wd, 1);
     wsum += (uint32_t)__shfl_xor((int)wsum, 2);
     const uint32_t bx = (uint32_t)__shfl((int)S.ex, (int)(lane | (kSegs - 1)));
+    // a segment left with an error exit (its walk ran past the chunk, or no
+    // entry reached it) marks the whole block, so the chunk fails its check
+    uint32_t berr = S.ex > S.b ? 1u : 0u;
+    berr |= (uint32_t)__shfl_xor((int)berr, 1);
+    berr |= (uint32_t)__shfl_xor((int)berr, 2);
     if (valid && q == 0) {
-        const uint64_t xa = bx > S.b ? b + 1 : base + bx;
+        const uint64_t xa = (berr || bx > S.b) ? b + 1 : base + bx;
         const uint64_t ea = S.used > S.b ? b + 1 : base + S.used;
         const uint64_t old = fix ? exit[k] : 0;
         exit[k] = xa;

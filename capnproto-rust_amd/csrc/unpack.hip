@@ -268,6 +268,146 @@ __device__ UNPACK_GLOBAL_ATTR void unpack_global(const uint8_t* __restrict__ in,
     }
 }
 
+// Global path for one chunk too large for the tile tables (unpack_tile_rest):
+// one wave, windows of kG1Words output words, the descriptor table as one flat
+// array.  Lane 0 walks the records from global memory, writing a descriptor at
+// each record's first word and a continuation at each 64-word group a run
+// enters (positions are 12-bit offsets from the group's first source byte,
+// gpb[g]); then the wave expands the window group by group with coalesced
+// 512-byte stores.  unpack_global's 64-word windows cost a walk round, an
+// 8 KiB table clear and two waits per 64 words: a 512-byte block of zero runs
+// (config 4's index-free block decode, ~600-word runs) spent ~1 us per 64 words.
+// Statuses, consumed bytes and the words written before an error are
+// unpack_global's rules (a window that fails writes nothing).
+constexpr uint32_t kG1Words = CAPNP_WAVE * CAPNP_WAVE;
+
+__device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                               uint64_t c, uint64_t* __restrict__ out,
+                               const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
+                               uint64_t* __restrict__ consumed, uint16_t* desc, uint32_t* gpb,
+                               uint32_t lane) {
+    const uint64_t p_start = uniform64(in_off[c]), in_end = uniform64(in_off[c + 1]);
+    const uint64_t obase = uniform64(out_off[c]), n = uniform64(out_off[c + 1]) - obase;
+    uint64_t p = p_start, w = 0;
+    int32_t st = ST_OK;
+    bool active = n > 0;
+    if (active && p == in_end) {  // read() returns Ok(0): read_exact fails
+        st = ST_FAILED_FILL;
+        active = false;
+    }
+    uint32_t pend_kind = KIND_NONE;
+    uint64_t pend_rem = 0, pend_src = 0;
+    for (uint64_t wbeg = 0; active; wbeg += kG1Words) {
+        {
+            uint4* d4 = reinterpret_cast<uint4*>(desc);
+#pragma unroll
+            for (uint32_t k = 0; k < kG1Words / 8 / CAPNP_WAVE; k++)
+                d4[k * CAPNP_WAVE + lane] = make_uint4(0, 0, 0, 0);
+        }
+        wave_lds_sync();
+        uint64_t pbw = 0;
+        uint32_t cnt_round = 0;
+        if (lane == 0) {
+            const uint64_t wend = (wbeg + kG1Words < n) ? wbeg + kG1Words : n;
+            pbw = pend_kind == KIND_LIT_CONT ? pend_src : p;
+            int32_t gcur = -1;
+            auto put = [&](uint64_t wi, uint32_t kind, uint64_t pos) {
+                const uint32_t i = (uint32_t)(wi - wbeg), g = i / CAPNP_WAVE;
+                if ((int32_t)g != gcur) {
+                    gpb[g] = (uint32_t)(pos - pbw);
+                    gcur = (int32_t)g;
+                }
+                desc[i] = (uint16_t)((kind << 12) | (uint32_t)(pos - pbw - gpb[g]));
+            };
+            // run words [from, from + take): a continuation at each group start among them
+            auto cont = [&](uint64_t from, uint64_t take, uint32_t kind, uint64_t src,
+                            uint64_t after) {
+                const uint64_t r = (from - wbeg) % CAPNP_WAVE;
+                for (uint64_t gs = r ? from + (CAPNP_WAVE - r) : from; gs < from + take;
+                     gs += CAPNP_WAVE)
+                    put(gs, kind, kind == KIND_LIT_CONT ? src + 8 * (gs - from) : after);
+            };
+            if (pend_kind != KIND_NONE) {  // the run carried in from the previous window
+                const uint64_t take = pend_rem < wend - w ? pend_rem : wend - w;
+                cont(w, take, pend_kind, pend_src, p);
+                w += take;
+                pend_rem -= take;
+                if (pend_kind == KIND_LIT_CONT) pend_src += 8 * take;
+                if (pend_rem == 0) pend_kind = KIND_NONE;
+            }
+            while (w < wend) {
+                if (p >= in_end) { st = ST_PREMATURE; break; }
+                const uint32_t tag = in[p];
+                const uint32_t pop = __builtin_popcount(tag);
+                if (p + 1 + pop > in_end) { st = ST_PREMATURE; break; }
+                const uint32_t kind = tag == 0 ? KIND_ZERO : (tag == 0xFF ? KIND_LIT : KIND_NORMAL);
+                put(w, kind, p);
+                uint64_t q = p + 1 + pop;
+                w += 1;
+                if (kind != KIND_NORMAL) {
+                    if (q >= in_end) { st = ST_PREMATURE; break; }
+                    const uint64_t cnt = in[q];
+                    q += 1;
+                    if (cnt > n - w) { st = ST_NOT_CLEAN; break; }
+                    const uint64_t src = q;
+                    if (kind == KIND_LIT) {
+                        if (in_end - q < 8 * cnt) { st = ST_FAILED_FILL; break; }
+                        q += 8 * cnt;
+                    }
+                    const uint64_t take = cnt < wend - w ? cnt : wend - w;
+                    const uint32_t ck = kind == KIND_LIT ? KIND_LIT_CONT : KIND_ZERO_CONT;
+                    cont(w, take, ck, src, q);
+                    w += take;
+                    if (cnt > take) {
+                        pend_kind = ck;
+                        pend_rem = cnt - take;
+                        pend_src = src + 8 * take;
+                    }
+                }
+                p = q;
+            }
+            cnt_round = (uint32_t)(w - wbeg);
+            if (st != ST_OK) { active = false; cnt_round = 0; }
+            else if (w == n) active = false;
+        }
+        active = __builtin_amdgcn_readfirstlane((int)active) != 0;
+        cnt_round = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt_round);
+        pbw = readlane64(pbw, 0);
+        wave_lds_sync();
+        for (uint32_t g = 0; g * CAPNP_WAVE < cnt_round; g++) {
+            const uint32_t i = g * CAPNP_WAVE + lane;
+            const bool valid = i < cnt_round;
+            const uint32_t d = valid ? desc[i] : 0u;
+            const uint64_t heads = ballot64(d != 0);
+            const uint64_t hm = heads & low_mask(lane + 1);
+            const uint32_t h = hm ? 63u - (uint32_t)__builtin_clzll(hm) : 0u;
+            const uint32_t dh = (h == lane) ? d : (uint32_t)desc[g * CAPNP_WAVE + h];
+            const uint32_t kind = dh >> 12;
+            const uint64_t pos = pbw + gpb[g] + (dh & 0xFFFu);
+            uint64_t word = 0;
+            if (valid) {
+                if (kind == KIND_NORMAL) {
+                    const uint32_t tag = in[pos];
+                    word = expand_word(tag, load_bytes(in, pos + 1, __builtin_popcount(tag)));
+                } else if (kind == KIND_LIT) {
+                    const uint64_t src = (h == lane) ? pos + 1 : pos + 10 + 8ull * (lane - h - 1);
+                    word = load_bytes(in, src, 8);
+                } else if (kind == KIND_LIT_CONT) {
+                    word = load_bytes(in, pos + 8ull * (lane - h), 8);
+                }
+                out[obase + wbeg + i] = word;
+            }
+        }
+        wave_lds_sync();
+    }
+    if (lane == 0) {
+        status[c] = st;
+        if (consumed)
+            consumed[c] = st == ST_OK ? p - p_start : (st == ST_NOT_CLEAN ? 0 : in_end - p_start);
+    }
+}
+
+
 constexpr uint32_t kMaxTileChunks = kWaves * CAPNP_WAVE;
 
 // ---------------------------------------------------------------------------
@@ -1432,7 +1572,7 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
 // The tile's chunks [ca, cb) when they do not all fit at once: the longest
 // prefixes that fit, staged in turn, and a chunk too large alone on the
 // global path.
-template <bool SYNC>
+template <bool SYNC, bool G1 = false>
 __device__ void unpack_tile_rest(USmem& sm, const uint8_t* __restrict__ in,
                                  const uint64_t* __restrict__ in_off, uint64_t ca, uint64_t cb,
                                  uint64_t* __restrict__ out, const uint64_t* __restrict__ out_off,
@@ -1462,9 +1602,14 @@ __device__ void unpack_tile_rest(USmem& sm, const uint8_t* __restrict__ in,
 #if UNPACK_PROF
             if (tid == 0 && g_utrace) g_utrace[blockIdx.x * 8 + 4] = 1;
 #endif
-            if (wave == 0)
-                unpack_global<CAPNP_WAVE>(in, in_off, lo, lo + 1, out, out_off, status, consumed,
-                                          sm.desc[0], lane);
+            if (wave == 0) {
+                if (G1)  // (the split overflow kernels; the combined kernels keep their registers)
+                    unpack_global1(in, in_off, lo, out, out_off, status, consumed, &sm.desc[0][0][0],
+                                   reinterpret_cast<uint32_t*>(&sm.desc[1][0][0]), lane);
+                else
+                    unpack_global<CAPNP_WAVE>(in, in_off, lo, lo + 1, out, out_off, status,
+                                              consumed, sm.desc[0], lane);
+            }
             resel = true;
             lo += 1;
             continue;
@@ -1581,8 +1726,8 @@ unpack_ovf_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
             const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
             __syncthreads();
             sm.st.sel[tid] = kExpandTable.s[tid];
-            unpack_tile_rest<SYNC>(sm, in, in_off, ca, cb, out, out_off, status, consumed, sync,
-                                   tid, lane, wave);
+            unpack_tile_rest<SYNC, true>(sm, in, in_off, ca, cb, out, out_off, status, consumed,
+                                         sync, tid, lane, wave);
         }
         __syncthreads();
     }
@@ -1640,8 +1785,8 @@ unpack_ovf_win_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict
                 sm.st.sel[tid] = kExpandTable.s[tid];
                 sel_ok = true;
             }
-            unpack_tile_rest<SYNC>(sm, in, in_off, ca, cb, out, out_off, status, consumed, sync,
-                                   tid, lane, wave);
+            unpack_tile_rest<SYNC, true>(sm, in, in_off, ca, cb, out, out_off, status, consumed,
+                                         sync, tid, lane, wave);
             sel_ok = false;  // (the global path may overlay the selectors)
         }
         __syncthreads();  // ovf_mask is rewritten next window

@@ -140,7 +140,8 @@ def tile(B, in_off, bl, k0, T, lead, E0=None, segs=4, waves=4, catchup=16):
     out = []
     for jb in range(kn):
         g = st[jb * segs:(jb + 1) * segs]
-        out.append((g[0]["used"], g[-1]["ex"], sum(x["wd"] for x in g)))
+        err = any(x["ex"] > x["b"] for x in g)  # any segment's error marks the block
+        out.append((g[0]["used"], g[0]["b"] + 1 if err else g[-1]["ex"], sum(x["wd"] for x in g)))
     return out, rounds
 
 

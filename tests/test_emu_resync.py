@@ -58,3 +58,48 @@ def test_tile_resolution_runs_across_blocks():
     z = np.zeros(n * cw, np.uint64)
     z[::97] = 5
     _check(z, offs, blk=64, T=8, max_passes=64)
+
+
+def test_tile_resolution_malformed_chunks():
+    """Truncated, corrupted and mis-sized chunks: a chunk passes the check
+    (last exit at its end, its word count, no block marked) only if the
+    oracle decodes it cleanly (a failing one must leave for the serial walk;
+    a segment that no entry reached marks its block)."""
+    import random
+    rng = random.Random(23)
+    chunks, lens = [], []
+    for _ in range(200):
+        n = rng.choice([1, 7, 64, 130, 700])
+        w = np.array([rng.getrandbits(64) if rng.random() < 0.6 else 0 for _ in range(n)],
+                     np.uint64)
+        if rng.random() < 0.3:
+            w |= np.uint64(0x0101010101010101)
+        st, k = O.pack(w.tobytes())
+        k = bytearray(k)
+        r = rng.random()
+        if r < 0.15 and len(k) > 1:
+            k = k[:rng.randrange(len(k))]
+        elif r < 0.3 and len(k):
+            k[rng.randrange(len(k))] = rng.choice([0, 0xFF, rng.randrange(256)])
+        elif r < 0.4:
+            n = max(1, n + rng.choice([-3, -1, 1, 4]))
+        chunks.append(bytes(k))
+        lens.append(n)
+    in_offs = np.concatenate([[0], np.cumsum([len(k) for k in chunks])]).astype(np.uint64)
+    out_offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.uint64)
+    packed = np.frombuffer(b"".join(chunks), np.uint8)
+    _, rst, _ = O.unpack_batch(packed, in_offs, out_offs)
+    B = bytes(packed) + bytes(4096)
+    in_off = [int(x) for x in in_offs]
+    bl, res, _, _ = E.resolve(B, in_off, blk=512, T=64)
+    byc = {}
+    for k, (c, s, e, f) in enumerate(bl):
+        byc.setdefault(c, []).append(k)
+    passed = 0
+    for c, ks in byc.items():
+        b = in_off[c + 1]
+        good = (res[ks[-1]][1] == b and sum(res[k][2] for k in ks) == lens[c]
+                and all(res[k][1] <= b for k in ks))
+        assert not (good and rst[c] != 0), c
+        passed += good
+    assert passed > 50 and (rst != 0).sum() > 20
