@@ -230,6 +230,16 @@ k_fix(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint6
     if (changed) flags[2 + pass] = 1;
 }
 
+#ifndef RESYNC_PROF
+#define RESYNC_PROF 0  // diagnostic: per-tile phase timestamps of the spec launch (scripts/resync_prof.py)
+#endif
+#if RESYNC_PROF
+__device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave 0), waves, end
+#define RTRACE(k) do { if (fix == 0 && tid == 0 && g_rtrace) g_rtrace[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define RTRACE(k) ((void)0)
+#endif
+
 // ---- tile resolution (round 3; RESYNC_TILE, the default) ----
 // k_spec + k_fix walk each block from global memory, one lane per block, and
 // a chain that no speculative walk couples with (a literal-run region) moved
@@ -242,20 +252,21 @@ k_fix(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint6
 //          chunk's start) to its first record start f >= s, then on to its
 //          exit; the lead-in lets chains from different starts couple before
 //          the segment begins, so f is usually the true start;
-//   rounds entries are a prefix max over the lanes' own exits (a segment whose
-//          entry lies past its end -- inside a literal run -- owns none and
-//          passes the entry on; a walk that runs past its chunk owns none
-//          either), with lane 0's entry the wave's and a chunk's first
-//          segment entered at the chunk start.  A lane whose entry is not the
-//          one its state derives from walks again from it, in lockstep with
-//          its spec chain until they meet (then its exit stands; the spec
-//          chain gives up after kCatchUp hops behind, and the walk goes on
-//          alone).  At the fixed point every segment's entry is its
-//          predecessor's exit;
-//   waves  wave w > 0 assumed its lane 0's f; in turn, each takes the previous
-//          wave's last exit and re-runs its rounds if that differs;
+//   rounds entries are a prefix max over the lanes' own exits, across the
+//          whole tile (shuffles within a wave, the waves' maxima through LDS):
+//          a segment whose entry lies past its end -- inside a literal run --
+//          owns none and passes the entry on, a walk that runs past its
+//          chunk owns none either, the tile's first lane takes the tile's
+//          entry and a chunk's first segment the chunk start.  A lane whose
+//          entry is not the one its state derives from walks again from it,
+//          in lockstep with its spec chain until they meet (then its exit
+//          stands; the spec chain gives up after kCatchUp hops behind, and
+//          the walk goes on alone); a lane whose entry lies below its
+//          segment (a predecessor not settled yet) lets its spec chain stand
+//          in for its successors.  At the fixed point every segment's entry
+//          is its predecessor's exit;
 //   blocks a block's entry is its first segment's, its exit its last
-//          segment's, its words the sum.
+//          segment's (chunk end + 1 if any segment failed), its words the sum.
 // Segments of 128 bytes keep each walk short (a lane whose spec chain missed
 // walks its whole segment; with one lane per 512-byte block that was the
 // critical path, ~100 hops, and four waves share the tile's LDS).  Positions
@@ -270,9 +281,12 @@ k_fix(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint6
 #ifndef RESYNC_TILE
 #define RESYNC_TILE 1
 #endif
-constexpr uint32_t kSegs = 4;                               // segments per block
+#ifndef RESYNC_SEGS
+#define RESYNC_SEGS 4
+#endif
+constexpr uint32_t kSegs = RESYNC_SEGS;                     // segments per block
 constexpr uint32_t kSegBytes = (uint32_t)kBlock / kSegs;    // 128
-constexpr uint32_t kTileWaves = 4;
+constexpr uint32_t kTileWaves = kSegs;                      // (so a tile stays 64 blocks)
 constexpr uint32_t kWaveBlocks = CAPNP_WAVE / kSegs;        // 16
 constexpr uint32_t kTileBlocks = kTileWaves * kWaveBlocks;  // 64
 constexpr uint32_t kTileThreads = kTileWaves * CAPNP_WAVE;
@@ -301,17 +315,6 @@ __device__ __forceinline__ void hop32(const uint8_t* buf, uint32_t& p, uint32_t&
     p = q > b ? b + 1 : q;
 }
 
-__device__ __forceinline__ uint32_t wave_excl_max32(uint32_t v, uint32_t lane) {
-    uint32_t x = v;
-#pragma unroll
-    for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
-        const uint32_t y = (uint32_t)__shfl_up((int)x, d);
-        if (lane >= d && y > x) x = y;
-    }
-    const uint32_t e = (uint32_t)__shfl_up((int)x, 1);
-    return lane == 0 ? 0u : e;
-}
-
 // One lane's segment state for the rounds.
 struct SegState {
     uint32_t ss, se, b, a;  // segment [ss, se), chunk end, chunk start (relative)
@@ -323,15 +326,34 @@ struct SegState {
 
 // Rounds to the fixed point for the wave (in_j: lane 0's entry, a chunk's
 // first segment's start, else 0).
+// The prefix max runs over the whole tile: within the wave by shuffles,
+// across waves through LDS (wmax: each wave's maximum), two barriers a round;
+// the tile's rounds end together (wneed: whether a wave still has work).
 __device__ __forceinline__ void seg_rounds(const uint8_t* buf, SegState& S, bool valid,
-                                           uint32_t in_j, bool fixed_j, uint32_t lane) {
+                                           uint32_t in_j, bool fixed_j, uint32_t lane,
+                                           uint32_t wave, uint32_t* wmax, uint32_t* wneed) {
     for (;;) {
         uint32_t v = S.own > in_j ? S.own : in_j;
         if (!valid) v = 0;
-        const uint32_t pm = wave_excl_max32(v, lane);
+        uint32_t x = v;
+#pragma unroll
+        for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+            if (lane >= d && y > x) x = y;
+        }
+        if (lane == CAPNP_WAVE - 1) wmax[wave] = x;
+        uint32_t pm = (uint32_t)__shfl_up((int)x, 1);
+        if (lane == 0) pm = 0;
+        __syncthreads();
+        for (uint32_t w2 = 0; w2 < wave; w2++) pm = wmax[w2] > pm ? wmax[w2] : pm;
         const uint32_t ent = fixed_j ? in_j : pm;
         const bool need = valid && ent != S.used;
-        if (ballot64(need) == 0) break;
+        const bool wn = ballot64(need) != 0;
+        if (lane == 0) wneed[wave] = wn;
+        __syncthreads();
+        uint32_t any = 0;
+        for (uint32_t w2 = 0; w2 < kTileWaves; w2++) any |= wneed[w2];
+        if (!any) break;
         if (!need) continue;
         S.used = ent;
         if (ent < S.ss) {
@@ -390,7 +412,7 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
        uint64_t* __restrict__ words, uint64_t* __restrict__ blk_c, int32_t* flags, int pass,
        int fix) {
     extern __shared__ __align__(16) uint8_t tbuf[];
-    __shared__ uint32_t wexit[kTileWaves];
+    __shared__ uint32_t wmax[kTileWaves], wneed[kTileWaves];
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & (CAPNP_WAVE - 1);
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid / CAPNP_WAVE));
@@ -398,6 +420,7 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     const uint64_t k0 = (uint64_t)blockIdx.x * kTileBlocks;
     if (k0 >= nb) return;
     if (fix && pass > 0 && __atomic_load_n(&flags[2 + pass - 1], __ATOMIC_RELAXED) == 0) return;
+    RTRACE(0);
     const uint64_t kn = nb - k0 < kTileBlocks ? nb - k0 : kTileBlocks;
     uint64_t e0 = 0;  // the tile's entry (fix passes)
     if (fix) {
@@ -468,6 +491,7 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     const uint64_t starta = ssa > a + kLead ? ssa - kLead : a;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's staged bytes are in
     __syncthreads();                                   // ... and every wave's
+    RTRACE(1);
     SegState S;
     S.ss = (uint32_t)(ssa - base);
     S.se = (uint32_t)(sea - base);
@@ -502,55 +526,30 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
         S.wd = S.sw;
         S.own = S.serr ? 0 : S.sx;
     }
-    // lane 0's entry: the tile's (wave 0 of a fix pass), else its own f
-    const uint32_t f0 = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)(S.f == kNone32 ? S.ss : S.f));
-    uint32_t E0;
-    if (fix && wave == 0) {
+    RTRACE(2);
+    // the tile's entry (lane 0 of wave 0): the previous tile's last exit in a
+    // fix pass, else its own f
+    uint32_t E0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(S.f == kNone32 ? S.ss : S.f));
+    if (fix) {
         const uint64_t r = e0 - base;
         E0 = e0 < base ? 0 : (r < kRelCap ? (uint32_t)r : kRelCap + 1);
-    } else {
-        E0 = f0;
     }
-    const bool first_lane0 =
-        __builtin_amdgcn_readfirstlane((int)cfirst) != 0;  // lane 0 starts a chunk: exact
-    bool fixed_j = lane == 0 || cfirst;
-    uint32_t in_j = lane == 0 ? (first_lane0 ? S.ss : E0) : (cfirst ? S.ss : 0);
-    seg_rounds(tbuf, S, valid, in_j, fixed_j, lane);
-    // the waves in turn: each takes the previous wave's last exit
-    const uint32_t nvalid = kn > (uint64_t)wave * kWaveBlocks
-                                ? (uint32_t)((kn - (uint64_t)wave * kWaveBlocks) < kWaveBlocks
-                                                 ? (kn - (uint64_t)wave * kWaveBlocks) * kSegs
-                                                 : CAPNP_WAVE)
-                                : 0u;
-    if (nvalid && lane == 0) wexit[wave] = 0;
-    if (nvalid) {
-        const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)S.ex, nvalid - 1);
-        if (lane == 0) wexit[wave] = lx;
-    }
-    __syncthreads();
-    for (uint32_t t = 1; t < kTileWaves; t++) {
-        if (wave == t && nvalid && !first_lane0) {
-            const uint32_t E = wexit[t - 1];
-            if (E != E0) {
-                E0 = E;
-                if (lane == 0) in_j = E;
-                seg_rounds(tbuf, S, valid, in_j, fixed_j, lane);
-                const uint32_t lx = (uint32_t)__builtin_amdgcn_readlane((int)S.ex, nvalid - 1);
-                if (lane == 0) wexit[wave] = lx;
-            }
-        }
-        __syncthreads();
-    }
+    const bool tile_lane0 = wave == 0 && lane == 0;
+    const bool fixed_j = cfirst || tile_lane0;
+    const uint32_t in_j = cfirst ? S.ss : (tile_lane0 ? E0 : 0u);
+    seg_rounds(tbuf, S, valid, in_j, fixed_j, lane, wave, wmax, wneed);
+    RTRACE(3);
+    RTRACE(4);
     // blocks: entry of segment 0, exit of segment 3, words summed
-    uint32_t wsum = S.wd + (uint32_t)__shfl_xor((int)S.wd, 1);
-    wsum += (uint32_t)__shfl_xor((int)wsum, 2);
+    // (a segment left with an error exit -- its walk ran past the chunk, or
+    // no entry reached it -- marks the whole block, so the chunk fails its check)
+    uint32_t wsum = S.wd, berr = S.ex > S.b ? 1u : 0u;
+#pragma unroll
+    for (uint32_t m = 1; m < kSegs; m <<= 1) {
+        wsum += (uint32_t)__shfl_xor((int)wsum, (int)m);
+        berr |= (uint32_t)__shfl_xor((int)berr, (int)m);
+    }
     const uint32_t bx = (uint32_t)__shfl((int)S.ex, (int)(lane | (kSegs - 1)));
-    // a segment left with an error exit (its walk ran past the chunk, or no
-    // entry reached it) marks the whole block, so the chunk fails its check
-    uint32_t berr = S.ex > S.b ? 1u : 0u;
-    berr |= (uint32_t)__shfl_xor((int)berr, 1);
-    berr |= (uint32_t)__shfl_xor((int)berr, 2);
     if (valid && q == 0) {
         const uint64_t xa = (berr || bx > S.b) ? b + 1 : base + bx;
         const uint64_t ea = S.used > S.b ? b + 1 : base + S.used;
@@ -561,6 +560,7 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
         if (!fix) blk_c[k] = c;
         if (fix && (uint64_t)jb == kn - 1 && old != xa) flags[2 + pass] = 1;
     }
+    RTRACE(5);
 }
 
 // Chunks with a block whose resolved chain ran past the chunk end (the tile
@@ -738,6 +738,16 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
 }  // namespace
 
 extern "C" uint32_t capnp_resync_block_bytes(void) { return (uint32_t)kBlock; }
+
+// RESYNC_PROF builds: the per-tile trace buffer (8 words per tile), or null.
+extern "C" int capnp_resync_trace(uint64_t* d_buf) {
+#if RESYNC_PROF
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_rtrace), &d_buf, sizeof(d_buf)) == hipSuccess ? 0 : -1;
+#else
+    (void)d_buf;
+    return -1;
+#endif
+}
 
 // Workspace for capnp_resync_unpack over n chunks holding total_bytes packed bytes.
 extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes) {

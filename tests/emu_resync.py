@@ -1,6 +1,6 @@
 """Emulation of the resync tile resolution (csrc/resync.hip k_tile: blocks
 cut into segments, spec walks led in by kLead bytes, per-wave rounds of a
-prefix max over owned exits with lockstep meet walks, the waves in turn, fix
+prefix max over owned exits across the tile with lockstep meet walks, fix
 passes over tiles) on the CPU: test infrastructure
 that checks its logic against the true record chain before any GPU run.  Not
 a decoder: it returns each block's (entry, exit, words) as the kernel stores
@@ -116,27 +116,12 @@ def tile(B, in_off, bl, k0, T, lead, E0=None, segs=4, waves=4, catchup=16):
         else:
             L.update(used=f, ex=sx, wd=sw, own=(0 if serr else sx))
         st.append(L)
-    W = len(st) // waves
-    wst = [st[w * W:(w + 1) * W] for w in range(waves)]
-    E0s, rounds = [], 0
-    for w in range(waves):
-        L0 = wst[w][0]
-        e = E0 if (w == 0 and E0 is not None) else (L0["f"] if L0["f"] != NONE else L0["s"])
-        if L0["first"]:
-            e = L0["s"]
-        E0s.append(e)
-        rounds = max(rounds, _rounds(B, wst[w], e, catchup))
-
-    def last_exit(w):
-        v = [L for L in wst[w] if L["valid"]]
-        return v[-1]["ex"] if v else None
-    for w in range(1, waves):
-        if not any(L["valid"] for L in wst[w]) or wst[w][0]["first"]:
-            continue
-        E = last_exit(w - 1)
-        if E != E0s[w]:
-            E0s[w] = E
-            rounds = max(rounds, _rounds(B, wst[w], E, catchup))
+    # rounds over the whole tile (the kernel's prefix max spans its waves)
+    L0 = st[0]
+    e = E0 if E0 is not None else (L0["f"] if L0["f"] != NONE else L0["s"])
+    if L0["first"]:
+        e = L0["s"]
+    rounds = _rounds(B, st, e, catchup)
     out = []
     for jb in range(kn):
         g = st[jb * segs:(jb + 1) * segs]
