@@ -80,6 +80,22 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+// Four 64-bit scalar loads in one round trip (uniform addresses).  The
+// compiler otherwise waits after each load whose value a compare or branch
+// uses before the next load is issued.
+__device__ __forceinline__ void sload4(const uint64_t* p0, const uint64_t* p1, const uint64_t* p2,
+                                       const uint64_t* p3, uint64_t& a, uint64_t& b, uint64_t& c,
+                                       uint64_t& d) {
+    asm volatile(
+        "s_load_dwordx2 %0, %4, 0x0\n\t"
+        "s_load_dwordx2 %1, %5, 0x0\n\t"
+        "s_load_dwordx2 %2, %6, 0x0\n\t"
+        "s_load_dwordx2 %3, %7, 0x0\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&s"(a), "=&s"(b), "=&s"(c), "=&s"(d)
+        : "s"(p0), "s"(p1), "s"(p2), "s"(p3));
+}
+
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
     const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);

@@ -1132,7 +1132,7 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
 }
 
 // Wave 0: global byte offset of tile t (aggregate already published).
-__device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, uint32_t lane) {
+[[maybe_unused]] __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, uint32_t lane) {
 #if PACK_ABLATE == 1 || PACK_ABLATE == 4
     return t * agg;  // timing-only: fake, in-bounds prefix; output is wrong
 #endif
@@ -1218,6 +1218,112 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
     (void)n_win;
 #endif
     return gexcl + within;
+}
+
+// Multi-level aggregate look-back (PACK_LB=2).  Level k holds one record per
+// block of 64^k tiles (level 0 = ts, level 1 = gs, deeper levels follow gs in
+// the state).  Tile t's offset is, at every level k, the sum of the records
+// of its level-k node's earlier siblings: the mixed-radix digits of t.  All
+// levels are polled at once (one round trip when everything is published),
+// and no record ever carries an inclusive prefix, so there is no chain of
+// look-backs: the last tile of a level-(k+1) block publishes that block's
+// aggregate as soon as levels 0..k of its own look-back are summed.
+// (PACK_LB=1, `lookback`: the group's tiles, then windows of group records
+// back to the nearest inclusive one: >= 2 dependent round trips.)
+#ifndef PACK_LB
+#define PACK_LB 1
+#endif
+
+__device__ __forceinline__ uint64_t* level_records(const LookbackArgs& A, uint32_t k) {
+    if (k == 0) return A.ts;
+    uint64_t* p = A.gs;
+    uint64_t n = (A.ntiles + kGroup - 1) / kGroup;
+    for (uint32_t m = 1; m < k; m++) {
+        p += n;
+        n = (n + kGroup - 1) / kGroup;
+    }
+    return p;
+}
+
+// Aggregate of tiles [t0, t1) from their records (missing ones computed from
+// the input): the bounded-wait fallback of every level.
+__device__ uint64_t tiles_aggregate(const LookbackArgs& A, uint64_t t0, uint64_t t1,
+                                    uint32_t lane) {
+    uint64_t sum = 0;
+    for (uint64_t b = t0; b < t1; b += kGroup) {
+        uint64_t st = b + lane < t1 ? poll_agent(&A.ts[b + lane]) : kFlagAgg;
+        uint64_t miss = ballot64((st >> 62) == 0);
+        while (miss) {
+            const uint32_t j = ctz64(miss);
+            const uint64_t a = tile_aggregate(A, b + j, lane);
+            if (lane == 0) publish_agent(&A.ts[b + j], kFlagAgg | a);
+            if (lane == j) st = kFlagAgg | a;
+            miss &= miss - 1;
+        }
+        uint64_t v = st & kValMask;
+        for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        sum += v;
+    }
+    return sum;
+}
+
+// Wave 0: global byte offset of tile t (aggregate already published).
+[[maybe_unused]] __device__ uint64_t lookback_ml(const LookbackArgs& A, uint64_t t, uint64_t agg, uint32_t lane) {
+#if PACK_ABLATE == 1 || PACK_ABLATE == 4
+    return t * agg;  // timing-only: fake, in-bounds prefix; output is wrong
+#endif
+    // levels 0..K: K = the first level whose node index is < 64
+    uint32_t K = 0;
+    while ((t >> (6 * K)) >= kGroup) K++;
+    // the first three levels' polls go out together (<= 262144 tiles: all)
+    uint64_t pre[3];
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++) {
+        const uint64_t i = t >> (6 * k);
+        const uint32_t r = (uint32_t)(i & (kGroup - 1));
+        const uint64_t* rec = level_records(A, k) + (i - r);
+        pre[k] = (k <= K && lane < r) ? poll_agent(const_cast<uint64_t*>(rec + lane)) : kFlagAgg;
+    }
+    uint64_t below = 0;  // sum of levels 0..k-1
+    for (uint32_t k = 0; k <= K; k++) {
+        const uint64_t i = t >> (6 * k);
+        const uint32_t r = (uint32_t)(i & (kGroup - 1));
+        uint64_t* rec = level_records(A, k) + (i - r);
+        uint64_t st = k == 0 ? pre[0] : k == 1 ? pre[1] : k == 2 ? pre[2]
+                                        : (lane < r ? poll_agent(rec + lane) : kFlagAgg);
+        for (uint32_t spins = 0;;) {
+            const uint64_t miss = ballot64((st >> 62) == 0);
+            if (!miss) break;
+            if (++spins >= kSpinLimit) {
+                if (lane == 0) PROF_ADD(2, 1);
+                const uint32_t j = ctz64(miss);
+                const uint64_t n0 = (i - r + j) << (6 * k), n1 = n0 + (1ull << (6 * k));
+                const uint64_t a = tiles_aggregate(A, n0, n1 < A.ntiles ? n1 : A.ntiles, lane);
+                if (lane == 0) publish_agent(rec + j, kFlagAgg | a);
+                if (lane == j) st = kFlagAgg | a;
+                continue;
+            }
+            __builtin_amdgcn_s_sleep(PACK_SLEEP);
+            st = ((miss >> lane) & 1) ? poll_agent(rec + lane) : st;
+        }
+        uint64_t v = st & kValMask;
+        for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        below += v;
+        // t closes its level-(k+1) block: publish that block's aggregate
+        const uint64_t span = 1ull << (6 * (k + 1));
+        if (((t + 1) & (span - 1)) == 0 && lane == 0)
+            publish_agent(level_records(A, k + 1) + (t >> (6 * (k + 1))), kFlagAgg | (below + agg));
+    }
+    return below;
+}
+
+__device__ __forceinline__ uint64_t tile_offset(const LookbackArgs& A, uint64_t t, uint64_t agg,
+                                                uint32_t lane) {
+#if PACK_LB == 2
+    return lookback_ml(A, t, agg, lane);
+#else
+    return lookback(A, t, agg, lane);
+#endif
 }
 
 // Wave 0: exclusive scan of the tile's chunk sizes (<= 64) into chunk_pos
@@ -1552,7 +1658,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         }
 #endif
         if (wave == 0) {
-            const uint64_t excl = lookback(LA, tile, agg, lane);
+            const uint64_t excl = tile_offset(LA, tile, agg, lane);
             if (lane == 0) TRACE(tile, 2, RT());
             if (lane < nc) sm.chunk_pos[lane] += excl;
             if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
@@ -1592,7 +1698,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         if (wave == 0) {
             const uint64_t agg = scan_chunks(sm, nc, lane);
             publish(LA, tile, agg, lane);
-            const uint64_t excl = lookback(LA, tile, agg, lane);
+            const uint64_t excl = tile_offset(LA, tile, agg, lane);
             if (lane < nc) sm.chunk_pos[lane] += excl;
             if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
         }
@@ -1855,7 +1961,7 @@ pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ c
         if (wave == 0) {
             const uint64_t agg = scan_chunks(sm, nc, lane);
             publish(LA, tile, agg, lane);
-            const uint64_t excl = lookback(LA, tile, agg, lane);
+            const uint64_t excl = tile_offset(LA, tile, agg, lane);
             if (lane < nc) sm.chunk_pos[lane] += excl;
             if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
             if (lane == 0) ovf[tile] = 1;
@@ -1942,7 +2048,7 @@ pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ c
         }
     }
     if (wave == 0) {
-        const uint64_t excl = lookback(LA, tile, agg, lane);
+        const uint64_t excl = tile_offset(LA, tile, agg, lane);
         if (lane < nc) sm.chunk_pos[lane] += excl;
         if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
     }
@@ -1975,6 +2081,9 @@ pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ c
 // kCsSteps chunks of its tile.  Tiles with a longer chunk (or more chunks per
 // wave) take the streaming size pass and leave their bytes to
 // pack_ovf_kernel.
+#ifndef PACK_CS_SPEC
+#define PACK_CS_SPEC 1  // one-round-trip prologues: speculative step loads etc. (below)
+#endif
 constexpr uint32_t kCsSteps = 4;   // chunks (steps) per wave
 constexpr uint32_t kCsWords = 128; // words per step
 
@@ -2127,36 +2236,95 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     const uint64_t c1 = (c0 + tc < nchunks) ? c0 + tc : nchunks;
     const uint32_t nc = (uint32_t)(c1 - c0);
     const uint64_t* __restrict__ toff = chunk_off + c0;
-    const uint64_t TW0 = uniform64(chunk_off[c0]);
-    const uint64_t TW1 = uniform64(chunk_off[c1]);
-    for (uint32_t i = tid; i <= kSelCopy; i += kThreads) sm.sel[i] = kSel8Table.e[i];
     uint8_t* region = sm.stage[wave];
-
-    // wave w: chunks [wc0, wc1), one per step; lane s < kCsSteps + 1 holds
-    // the tile-relative word offset of chunk wc0 + s
+    // wave w: chunks [wc0, wc1), one per step
     const uint32_t q = (nc + kWaves - 1) / kWaves;
     const uint32_t wc0 = wave * q < nc ? wave * q : nc;
     const uint32_t wc1 = wc0 + q < nc ? wc0 + q : nc;
     const uint32_t nw = wc1 - wc0;
-    const uint32_t d_off = lane < nw ? (uint32_t)(toff[wc0 + lane] - TW0) : 0u;
-    const uint32_t d_len = lane < nw ? (uint32_t)(toff[wc0 + lane + 1] - TW0) - d_off : 0u;
-    const bool ok = nw <= kCsSteps && ballot64(lane < nw && d_len > kCsWords) == 0;
-    if (lane == 0) sm.wave_steps[wave] = ok ? 0u : 1u;
+    const uint64_t TW0 = uniform64(chunk_off[c0]);
+#if PACK_CS_SPEC
+    const uint64_t WS0 = uniform64(toff[wc0]);
+#endif
+    const uint64_t TW1 = uniform64(chunk_off[c1]);
     const uint32_t tile_bytes = (uint32_t)((TW1 - TW0) * 8);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
     uint64_t clo[kCsSteps], chi[kCsSteps];
+#if PACK_CS_SPEC
+    // Every load of the prologue is issued in one round trip: the scalar
+    // offsets (TW0, TW1, the wave's first chunk WS0), the wave's chunk offsets
+    // (one buffer load, lane l <= nw: toff[wc0 + l]; lanes past them read 0,
+    // so no branch and no wait at its join), the selector table entry (written
+    // to LDS after the word loads), and the words themselves, speculatively:
+    // chunk s of the wave at WS0 + 128 s.  That is the step layout exactly
+    // when every chunk of the wave but its last holds 128 words (1 KiB
+    // segments); otherwise the steps load again once the offsets are in.
+    // (The compiler had waited for the table entry, then for each of the two
+    // offset loads, before the word loads: four round trips.)
+    // (the offsets' low words: lengths and tile offsets fit 32 bits)
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint64_t*>(toff + wc0), 0, (int)((nw + 1) * 8), 0x00020000);
+    const uint32_t o = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(lane * 8u), 0, 0);
+    const Sel8 selv = kSel8Table.e[tid];
+    const uint32_t sb = (uint32_t)(WS0 - TW0);
 #pragma unroll
     for (uint32_t s = 0; s < kCsSteps; s++) {
-        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)d_off, s);
-        const uint32_t n = s < nw ? (uint32_t)__builtin_amdgcn_readlane((int)d_len, s) : 0u;
-        const uint32_t vlo = lane < n ? (a + lane) * 8u : 0x80000000u;
-        const uint32_t vhi = lane + 64u < n ? (a + lane + 64u) * 8u : 0x80000000u;
+        const uint32_t vlo = s < nw ? (sb + kCsWords * s + lane) * 8u : 0x80000000u;
+        const uint32_t vhi = s < nw ? (sb + kCsWords * s + 64u + lane) * 8u : 0x80000000u;
         const auto x = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vlo, 0, 0);
         const auto y = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vhi, 0, 0);
         clo[s] = ((uint64_t)x[1] << 32) | x[0];
         chi[s] = ((uint64_t)y[1] << 32) | y[0];
     }
+    const uint32_t onext = (uint32_t)__shfl_down((int)o, 1, 64);
+    const uint32_t d_off = lane < nw ? o - (uint32_t)TW0 : 0u;
+    const uint32_t d_len = lane < nw ? onext - o : 0u;
+#else
+    for (uint32_t i = tid; i <= kSelCopy; i += kThreads) sm.sel[i] = kSel8Table.e[i];
+    const uint32_t d_off = lane < nw ? (uint32_t)(toff[wc0 + lane] - TW0) : 0u;
+    const uint32_t d_len = lane < nw ? (uint32_t)(toff[wc0 + lane + 1] - TW0) - d_off : 0u;
+#endif
+    const bool ok = nw <= kCsSteps && ballot64(lane < nw && d_len > kCsWords) == 0;
+    if (lane == 0) sm.wave_steps[wave] = ok ? 0u : 1u;
+#if PACK_CS_SPEC
+    if (ballot64(lane + 1u < nw && d_len != kCsWords) != 0) {
+        // (the speculative values enter the reloaded ones through an opaque
+        // zero, so the compiler keeps their loads ahead of this branch)
+        uint64_t z;
+        asm volatile("s_mov_b64 %0, 0" : "=s"(z));
+#else
+    {
+        const uint64_t z = 0;
+#endif
+#pragma unroll
+        for (uint32_t s = 0; s < kCsSteps; s++) {
+            const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)d_off, s);
+            const uint32_t n = s < nw ? (uint32_t)__builtin_amdgcn_readlane((int)d_len, s) : 0u;
+            const uint32_t vlo = lane < n ? (a + lane) * 8u : 0x80000000u;
+            const uint32_t vhi = lane + 64u < n ? (a + lane + 64u) * 8u : 0x80000000u;
+            const auto x = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vlo, 0, 0);
+            const auto y = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vhi, 0, 0);
+            clo[s] = (((uint64_t)x[1] << 32) | x[0]) | (clo[s] & z);
+            chi[s] = (((uint64_t)y[1] << 32) | y[0]) | (chi[s] & z);
+        }
+    }
+#if PACK_CS_SPEC
+    else {
+        // the wave's last chunk may be short: its step's words past it are
+        // the next wave's (pass 1 takes words past n as zero)
+        const uint32_t nl = nw ? (uint32_t)__builtin_amdgcn_readlane((int)d_len, nw - 1) : 0u;
+#pragma unroll
+        for (uint32_t s = 0; s < kCsSteps; s++) {
+            if (s + 1 == nw) {
+                clo[s] = lane < nl ? clo[s] : 0ull;
+                chi[s] = lane + 64u < nl ? chi[s] : 0ull;
+            }
+        }
+    }
+    sm.sel[tid] = selv;
+    if (tid == 0) sm.sel[kSelCopy] = kSel8Table.e[kSelCopy];
+#endif
     for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
     __syncthreads();
     bool staged = true;
@@ -2191,7 +2359,7 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         if (wave == 0) {
             const uint64_t agg = scan_chunks(sm, nc, lane);
             publish(LA, tile, agg, lane);
-            const uint64_t excl = lookback(LA, tile, agg, lane);
+            const uint64_t excl = tile_offset(LA, tile, agg, lane);
             if (lane < nc) sm.chunk_pos[lane] += excl;
             if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
             if (lane == 0) ovf[tile] = 1;
@@ -2263,7 +2431,7 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         wave_lds_sync();
         if (lane == 0) TRACE(tile, 3, RT());
 #endif
-        const uint64_t excl = lookback(LA, tile, agg, lane);
+        const uint64_t excl = tile_offset(LA, tile, agg, lane);
 #if PACK_PROF == 3
         if (lane == 0) TRACE(tile, 4, RT());
 #endif
@@ -2430,7 +2598,11 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     const uint64_t R1 = !have ? R0 : (R0 + kWtRange < Tb ? R0 + kWtRange : Tb);
     const uint32_t nw = (uint32_t)(R1 - R0);
     const bool lastr = have && R1 == whi;
+#if PACK_CS_SPEC
+    const Sel8 selv = kSel8Table.e[tid];  // (written after the word loads are issued)
+#else
     for (uint32_t i = tid; i <= kSelCopy; i += kThreads) sm.sel[i] = kSel8Table.e[i];
+#endif
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
     uint8_t* const outa = out - mis;
@@ -2448,6 +2620,10 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             cache[s] = ((uint64_t)v[1] << 32) | v[0];
         }
     }
+#if PACK_CS_SPEC
+    sm.sel[tid] = selv;
+    if (tid == 0) sm.sel[kSelCopy] = kSel8Table.e[kSelCopy];
+#endif
     // the range's first chunks (their offsets are written after the
     // look-back; loaded now, off that path)
     const uint64_t cA = have ? uniform64(map[tile * kWaves + wave]) : nchunks;
@@ -2569,7 +2745,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         }
     }
     if (wave == 0) {
-        const uint64_t excl = PACK_WT_ABL == 5 ? tile * 8192 : lookback(LA, tile, agg, lane);
+        const uint64_t excl = PACK_WT_ABL == 5 ? tile * 8192 : tile_offset(LA, tile, agg, lane);
         if (lane == 0) {
             wm.excl = excl;
             tile_off[tile] = excl;
@@ -2620,11 +2796,31 @@ pack_wt_plan(const uint64_t* __restrict__ in, const uint64_t* __restrict__ cbits
     const uint64_t b64 = wlo >> 6;
     uint32_t rec = 0;
     if (R < whi && R > wlo) {
+#if PACK_CS_SPEC
+        // every load in one round trip: clamped addresses and selects instead
+        // of guarded loads (the compiler waited at each guard's join)
+        const uint64_t ib = R - 64 + lane >= wlo ? R - 64 + lane : wlo;
+        const uint64_t ia = R + lane < whi ? R + lane : whi - 1;
+        // (word R - 65 as a lane's load, so it is not deferred to its use)
+        const uint64_t ip = R - 65 + lane >= wlo ? R - 65 + lane : wlo;
+        const uint64_t xb = in[ib], xa = in[ia];
+        const uint64_t xp = readlane64(in[ip], 0);
+        const uint64_t qa = 1 + (R >> 6) - b64, qb = R >= 64 ? qa - 1 : qa;
+        const uint32_t rr = (uint32_t)(R & 63);
+        const uint64_t ca0 = uniform64(cbits[qa]), ca1 = uniform64(cbits[qa + 1]);
+        const uint64_t cb0 = uniform64(cbits[qb]), cb1 = uniform64(cbits[qb + 1]);
+        const uint64_t wb = R >= wlo + 64 - lane ? xb : 0ull;
+        const uint64_t wp = R >= wlo + 65 ? xp : 0ull;
+        const uint64_t wa = R + lane < whi ? xa : 0ull;
+        const uint64_t bb = R >= 64 ? (rr ? (cb0 >> rr) | (cb1 << (64 - rr)) : cb0) : 0ull;
+        const uint64_t ba = rr ? (ca0 >> rr) | (ca1 << (64 - rr)) : ca0;
+#else
         const uint64_t wb = R >= wlo + 64 - lane ? in[R - 64 + lane] : 0ull;
         const uint64_t wp = R >= wlo + 65 ? in[R - 65] : 0ull;
         const uint64_t wa = R + lane < whi ? in[R + lane] : 0ull;
         const uint64_t bb = R >= 64 ? start_bits(cbits, b64, R - 64) : 0ull;
         const uint64_t ba = start_bits(cbits, b64, R);
+#endif
         if (!(ba & 1)) {  // R inside a chunk
             const Carry c = carry_in_b(in, cbits, b64, wlo, R, lane, wb, wp, bb);
             const uint32_t ext = run_ext_b(in, cbits, b64, whi, R, c, lane, wa, ba);
@@ -2685,15 +2881,25 @@ extern "C" uint32_t capnp_pack_tile_words(void) { return kWaves * 64 * kStageSte
 
 // Workspace layout (zeroed every call; uncached memory, capi.hip):
 // ts[ntiles] tile records, then gs[ngroups] group records.
-extern "C" size_t capnp_pack_state_bytes(uint64_t nchunks, uint32_t tc) {
-    const uint64_t ntiles = (nchunks + tc - 1) / tc;
-    const uint64_t ngroups = (ntiles + kGroup - 1) / kGroup;
-    return ((ntiles + ngroups) * 8 + ntiles + 15) & ~size_t(15);  // + overflow flags
+// Look-back records above the tiles': level 1 (groups of 64 tiles), then the
+// deeper levels of lookback_ml (blocks of 64^k tiles) up to one record.
+static uint64_t level_record_count(uint64_t ntiles) {
+    uint64_t total = 0;
+    for (uint64_t n = ntiles; n > 1;) {
+        n = (n + kGroup - 1) / kGroup;
+        total += n;
+    }
+    return total ? total : 1;
 }
 
-// The tiles' overflow flags follow the tile and group records in the state.
+extern "C" size_t capnp_pack_state_bytes(uint64_t nchunks, uint32_t tc) {
+    const uint64_t ntiles = (nchunks + tc - 1) / tc;
+    return ((ntiles + level_record_count(ntiles)) * 8 + ntiles + 15) & ~size_t(15);  // + overflow flags
+}
+
+// The tiles' overflow flags follow the tile and level records in the state.
 static uint8_t* pack_ovf_flags(uint64_t* d_state, uint64_t ntiles) {
-    return reinterpret_cast<uint8_t*>(d_state + ntiles + (ntiles + kGroup - 1) / kGroup);
+    return reinterpret_cast<uint8_t*>(d_state + ntiles + level_record_count(ntiles));
 }
 static dim3 pack_ovf_grid(uint64_t ntiles) {
     const uint64_t g = (ntiles + kThreads - 1) / kThreads;

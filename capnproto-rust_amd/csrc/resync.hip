@@ -132,6 +132,13 @@ struct Ws {
     int32_t* flags;        // [1] chunk failed, [2 + i] fix pass i changed an exit
     void* tmp;
     size_t tmp_bytes;
+    // RESYNC_SEGUNITS: the resolved segments (kSegs per block) as decode units
+    uint64_t* seg_exit = nullptr;  // [kSegs nbb] exit of each segment
+    uint32_t* seg_wrel = nullptr;  // [kSegs nbb] words of the block's earlier segments
+    uint64_t* u_in = nullptr;      // [kSegs nbb + 1] unit packed starts
+    uint64_t* u_out = nullptr;     // [kSegs nbb + 1] unit first words
+    int32_t* u_st = nullptr;       // [kSegs nbb]
+    uint64_t* u_cons = nullptr;    // [kSegs nbb]
 };
 
 // (a chunk with no packed bytes but a nonzero word count owns one empty
@@ -281,6 +288,9 @@ __device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave
 #ifndef RESYNC_TILE
 #define RESYNC_TILE 1
 #endif
+#ifndef RESYNC_SEGUNITS
+#define RESYNC_SEGUNITS 0  // 1: decode the resolved segments as units (k_units)
+#endif
 #ifndef RESYNC_SEGS
 #define RESYNC_SEGS 4
 #endif
@@ -410,7 +420,7 @@ __global__ void __launch_bounds__(kTileThreads)
 k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
        const uint64_t* __restrict__ bstart, uint64_t* exit, uint64_t* __restrict__ entry,
        uint64_t* __restrict__ words, uint64_t* __restrict__ blk_c, int32_t* flags, int pass,
-       int fix) {
+       int fix, uint64_t* __restrict__ seg_exit, uint32_t* __restrict__ seg_wrel) {
     extern __shared__ __align__(16) uint8_t tbuf[];
     __shared__ uint32_t wmax[kTileWaves], wneed[kTileWaves];
     const uint32_t tid = threadIdx.x;
@@ -544,6 +554,18 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     // (a segment left with an error exit -- its walk ran past the chunk, or
     // no entry reached it -- marks the whole block, so the chunk fails its check)
     uint32_t wsum = S.wd, berr = S.ex > S.b ? 1u : 0u;
+    if (seg_exit && valid) {
+        // the segment as a decode unit: its exit, and the words of the block's
+        // earlier segments (an exclusive scan over the block's kSegs lanes)
+        uint32_t pre = S.wd;
+#pragma unroll
+        for (uint32_t m = 1; m < kSegs; m <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)pre, m);
+            if (q >= m) pre += y;
+        }
+        seg_exit[k * kSegs + q] = S.ex > S.b ? b + 1 : base + S.ex;
+        seg_wrel[k * kSegs + q] = pre - S.wd;
+    }
 #pragma unroll
     for (uint32_t m = 1; m < kSegs; m <<= 1) {
         wsum += (uint32_t)__shfl_xor((int)wsum, (int)m);
@@ -639,20 +661,52 @@ k_blocks(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __rest
     blk_out[k] = out_off[c] + (out_off[c + 1] == out_off[c] ? 0 : wbase[k] - wbase[f]);
 }
 
+// The same at segment granularity (RESYNC_SEGUNITS): every resolved segment
+// is a read unit -- its records run from the previous segment's exit to its
+// own and decode to exactly its words -- so the decode's walkers follow ~30
+// words each instead of a block's ~120.  Unit u = kSegs k + q (block k,
+// segment q); a chunk that failed its check is one unit, its last.
+__global__ void __launch_bounds__(kThreads)
+k_units(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __restrict__ out_off,
+        const uint64_t* __restrict__ bstart, const uint64_t* __restrict__ seg_exit,
+        const uint32_t* __restrict__ seg_wrel, const uint64_t* __restrict__ wbase,
+        const int32_t* __restrict__ ok, uint64_t* __restrict__ u_in, uint64_t* __restrict__ u_out) {
+    const uint64_t u = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    const uint64_t nu = kSegs * bstart[n];
+    if (u > nu) return;
+    if (u == nu) {
+        u_in[u] = in_off[n];
+        u_out[u] = out_off[n];
+        return;
+    }
+    const uint64_t k = u / kSegs;
+    const uint64_t c = chunk_of(bstart, n, k);
+    const uint64_t f = bstart[c];
+    if (ok && !ok[c]) {
+        u_in[u] = in_off[c];
+        u_out[u] = out_off[c];
+        return;
+    }
+    u_in[u] = u == kSegs * f ? in_off[c] : seg_exit[u - 1];
+    u_out[u] = out_off[c] +
+               (out_off[c + 1] == out_off[c] ? 0 : wbase[k] - wbase[f] + seg_wrel[u]);
+}
+
 // Status and consumed bytes of the chunks that failed their check: those of
-// the unit that spans the chunk (its last block).
+// the unit that spans the chunk (its last block, or its last segment: `per`
+// units per block).
 __global__ void __launch_bounds__(kThreads)
 k_fail(uint64_t n, const uint64_t* __restrict__ bstart, const int32_t* __restrict__ ok,
        const int32_t* __restrict__ blk_status, const uint64_t* __restrict__ blk_consumed,
-       int32_t* __restrict__ status, uint64_t* __restrict__ consumed) {
+       int32_t* __restrict__ status, uint64_t* __restrict__ consumed, uint32_t per = 1) {
     const uint64_t c = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (c >= n || ok[c]) return;
-    const uint64_t l = bstart[c + 1] - 1;  // (a failing chunk owns at least one block)
+    const uint64_t l = per * bstart[c + 1] - 1;  // (a failing chunk owns at least one block)
     status[c] = blk_status[l];
     if (consumed) consumed[c] = blk_consumed[l];
 }
 
-size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes) {
+size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes, bool segs = false) {
     size_t off = 0;
     auto take = [&](size_t bytes) {
         uint8_t* p = base ? base + off : nullptr;
@@ -671,6 +725,15 @@ size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes) {
     w->flags = (int32_t*)take(4 * (2 + kMaxPasses));
     w->tmp = take(tmp_bytes);
     w->tmp_bytes = tmp_bytes;
+    if (segs) {
+        const uint64_t nu = kSegs * nbb;
+        w->seg_exit = (uint64_t*)take(8 * nu);
+        w->seg_wrel = (uint32_t*)take(4 * nu);
+        w->u_in = (uint64_t*)take(8 * (nu + 1));
+        w->u_out = (uint64_t*)take(8 * (nu + 1));
+        w->u_st = (int32_t*)take(4 * nu);
+        w->u_cons = (uint64_t*)take(8 * nu);
+    }
     return off;
 }
 
@@ -704,7 +767,8 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
     const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
     if (tile)
         k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
-                                                    w.words, w.spec_exit, w.flags, 0, 0);
+                                                    w.words, w.spec_exit, w.flags, 0, 0,
+                                                    w.seg_exit, w.seg_wrel);
     else
         k_spec<<<grid(nbb), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart, w.spec_exit,
                                                        w.spec_words, w.exit, w.entry, w.words);
@@ -718,7 +782,7 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
             if (tile)
                 k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
                                                             w.entry, w.words, w.spec_exit, w.flags,
-                                                            pass, 1);
+                                                            pass, 1, w.seg_exit, w.seg_wrel);
             else
                 k_fix<<<grid(ngroups), kThreads, walk_lds(), s>>>(
                     d_in, in_off, n, w.bstart, w.spec_exit, w.spec_words, w.exit, w.entry,
@@ -754,7 +818,7 @@ extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes) {
     const uint64_t nbb = blocks_bound(n, total_bytes);
     const uint64_t m = nbb > n + 1 ? nbb : n + 1;
     Ws w;
-    return carve(&w, nullptr, n, nbb, scan_tmp_bytes(m)) + 256;
+    return carve(&w, nullptr, n, nbb, scan_tmp_bytes(m), RESYNC_SEGUNITS) + 256;
 }
 
 // Blocking (the fix passes read a flag back).  On return, *passes = fix passes
@@ -784,7 +848,8 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
     const uint64_t m = nbb > n + 1 ? nbb : n + 1;
     Ws w;
     uint8_t* base = (uint8_t*)(((uintptr_t)d_ws + 255) & ~uintptr_t(255));
-    if (carve(&w, base, n, nbb, scan_tmp_bytes(m)) + (base - (uint8_t*)d_ws) > ws_bytes)
+    if (carve(&w, base, n, nbb, scan_tmp_bytes(m), RESYNC_SEGUNITS) + (base - (uint8_t*)d_ws) >
+        ws_bytes)
         return hipErrorInvalidValue;
     int32_t hflags[2] = {0, 0};
     if ((e = hipMemsetAsync(w.flags, 0, 4 * (2 + kMaxPasses), s)) != hipSuccess) return e;
@@ -824,15 +889,27 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
         uint64_t* blk_out = w.entry;
         int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
         uint64_t* blk_consumed = w.words;  // (dead after the wbase scan and the check)
-        k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit,
-                                                   w.wbase, w.ok, blk_in, blk_out);
-        if ((e = capnp_launch_unpack(d_in, blk_in, nb, 0, d_out, blk_out, blk_status,
+        uint32_t per = 1;
+        if (RESYNC_SEGUNITS && w.seg_exit) {
+            per = kSegs;
+            blk_in = w.u_in;
+            blk_out = w.u_out;
+            blk_status = w.u_st;
+            blk_consumed = w.u_cons;
+            k_units<<<grid(per * nb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart,
+                                                            w.seg_exit, w.seg_wrel, w.wbase,
+                                                            w.ok, blk_in, blk_out);
+        } else {
+            k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit,
+                                                       w.wbase, w.ok, blk_in, blk_out);
+        }
+        if ((e = capnp_launch_unpack(d_in, blk_in, per * nb, 0, d_out, blk_out, blk_status,
                                      hflags[1] ? blk_consumed : nullptr, nullptr, s)) != hipSuccess)
             return e;
         if (hflags[1]) {
             if (serial) *serial = 3;
             k_fail<<<grid(n), kThreads, 0, s>>>(n, w.bstart, w.ok, blk_status, blk_consumed,
-                                                d_status, d_consumed);
+                                                d_status, d_consumed, per);
         }
     } else {
         if (serial) *serial = 1;

@@ -1398,18 +1398,24 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
 // One staged sub-tile: chunks [ca, cb) whose packed bytes, output words and
 // count fit the LDS tables (stage, walk, expand).  All threads of the
 // workgroup call it; it ends after its last LDS access of the expansion.
-template <bool SYNC>
-__device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __restrict__ in,
-                                              const uint64_t* __restrict__ in_off, uint64_t ca,
-                                              uint64_t cb, uint64_t* __restrict__ out,
-                                              const uint64_t* __restrict__ out_off,
-                                              int32_t* __restrict__ status,
-                                              uint64_t* __restrict__ consumed,
-                                              const uint32_t* __restrict__ sync, uint32_t tid,
-                                              uint32_t lane, uint32_t wave) {
+#ifndef UNPACK_PRO
+#define UNPACK_PRO 1  // every staging load in one round trip (below)
+#endif
+
+// SELW: the selector table is written here too, its load issued with the
+// staging loads (the caller's copy had waited for it before any of them).
+// The tile [ca, cb) whose packed bytes are [B0, B1) and words [W0, W1).
+template <bool SYNC, bool SELW = false>
+__device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __restrict__ in,
+                                                 const uint64_t* __restrict__ in_off, uint64_t ca,
+                                                 uint64_t cb, uint64_t* __restrict__ out,
+                                                 const uint64_t* __restrict__ out_off,
+                                                 int32_t* __restrict__ status,
+                                                 uint64_t* __restrict__ consumed,
+                                                 const uint32_t* __restrict__ sync, uint32_t tid,
+                                                 uint32_t lane, uint32_t wave, uint64_t B0,
+                                                 uint64_t B1, uint64_t W0, uint64_t W1) {
     const uint32_t nc = (uint32_t)(cb - ca);
-    const uint64_t B0 = uniform64(in_off[ca]), B1 = uniform64(in_off[cb]);
-    const uint64_t W0 = uniform64(out_off[ca]), W1 = uniform64(out_off[cb]);
     const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
     UPROF_T(t0);
     const uint32_t nbytes = (uint32_t)(B1 - B0) + off0;
@@ -1418,6 +1424,75 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
     const uint64_t kf = W0 / kSyncWords + 1;
     const uint32_t nseg =
         W1 > W0 ? 1u + (uint32_t)((W1 - 1) / kSyncWords + 1 - kf) : 0u;
+#if UNPACK_PRO
+    // stage the tile: every load in one round trip, then the LDS writes.  The
+    // chunk tables and sync entries come by buffer loads (lanes past them
+    // read 0: no branch, so no wait at a join), ahead of the byte loads, so
+    // their LDS writes wait only for them (loads return in order); the
+    // selector table entry likewise.  (Loads under `if (tid <= nc)` had each
+    // waited for everything before them: with the table copy, ~4 dependent
+    // round trips before the walk.)
+    {
+        constexpr uint32_t kLoads = (kTileBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
+        const uint64_t selv = SELW ? kExpandTable.s[tid] : 0;
+        uint32_t t_w = 0, t_wz = 0, t_p = 0, e_a = 0, e_b = 0;
+        if (SYNC || UNPACK_SPEC) {
+            const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint64_t*>(out_off + ca), 0, (int)((nc + 1) * 8), 0x00020000);
+            const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint64_t*>(in_off + ca), 0, (int)((nc + 1) * 8), 0x00020000);
+            // (low words: tile-relative offsets fit 32 bits)
+            t_w = __builtin_amdgcn_raw_buffer_load_b32(ors, (int)(tid * 8u), 0, 0);
+            t_wz = __builtin_amdgcn_raw_buffer_load_b32(ors, (int)(tid * 8u + 8u), 0, 0);
+            t_p = __builtin_amdgcn_raw_buffer_load_b32(irs, (int)(tid * 8u), 0, 0);
+        }
+        if constexpr (SYNC) {
+            // entry of segment b >= 1 = sync[kf + b - 1]: b = tid and b = tid + 256
+            const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint32_t*>(sync + (kf - 1)), 0, (int)(nseg * 4), 0x00020000);
+            e_a = __builtin_amdgcn_raw_buffer_load_b32(srs, (int)(tid * 4u), 0, 0);
+            e_b = __builtin_amdgcn_raw_buffer_load_b32(srs, (int)((tid + kThreads) * 4u), 0, 0);
+        }
+        const uint4* src = reinterpret_cast<const uint4*>(in + B0 - off0);
+        uint4* dst = reinterpret_cast<uint4*>(S.bytes);
+        const uint32_t nblk = (nbytes + 15) / 16;
+        uint4 r[kLoads];
+#pragma unroll
+        for (uint32_t k = 0; k < kLoads; k++) {
+            const uint32_t idx = tid + k * kThreads;
+            r[k] = nblk ? src[idx < nblk ? idx : nblk - 1] : make_uint4(0, 0, 0, 0);
+        }
+        uint4* dd = reinterpret_cast<uint4*>(S.dpos);
+        const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
+        for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
+        if (SELW) S.sel[tid] = selv;
+        if (SYNC || UNPACK_SPEC) {
+            if (tid <= nc) {
+                const uint32_t wa = t_w - (uint32_t)W0;
+                S.cw[tid] = wa;
+                S.cp[tid] = t_p - (uint32_t)B0 + off0;
+                if constexpr (SYNC) {
+                    // segments whose first word (max(0, b G - r0)) lies in this chunk
+                    const uint32_t wz = tid < nc ? t_wz - (uint32_t)W0 : wa;
+                    const uint32_t r0 = (uint32_t)(W0 % kSyncWords);
+                    if (wz > wa) {
+                        const uint32_t blo = wa == 0 ? 0u : (wa + r0 + kSyncWords - 1) / kSyncWords;
+                        const uint32_t bhi = (wz + r0 + kSyncWords - 1) / kSyncWords;
+                        for (uint32_t bb = blo; bb < bhi; bb++) S.segc[bb] = (uint8_t)tid;
+                    }
+                }
+            }
+            if (tid < kStageChunks) S.badc[tid] = 0;
+        }
+        if constexpr (SYNC) {
+            if (tid >= 1 && tid < nseg) S.ent[tid] = e_a;
+            if (tid + kThreads < nseg) S.ent[tid + kThreads] = e_b;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kLoads; k++)
+            if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
+    }
+#else
     // stage the tile's packed bytes: every load issued before any LDS write
     // (aligned 16-byte blocks holding at least one byte of the range never
     // cross a page), and clear the descriptors
@@ -1465,6 +1540,7 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
         for (uint32_t k = 0; k < kLoads; k++)
             if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
     }
+#endif
     __syncthreads();
     UPROF_T(t1);
     // walk: lane j of one wave follows chunk j.  The walking wave rotates
@@ -1565,6 +1641,20 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
 #endif
 }
 
+template <bool SYNC, bool SELW = false>
+__device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __restrict__ in,
+                                              const uint64_t* __restrict__ in_off, uint64_t ca,
+                                              uint64_t cb, uint64_t* __restrict__ out,
+                                              const uint64_t* __restrict__ out_off,
+                                              int32_t* __restrict__ status,
+                                              uint64_t* __restrict__ consumed,
+                                              const uint32_t* __restrict__ sync, uint32_t tid,
+                                              uint32_t lane, uint32_t wave) {
+    unpack_staged_at<SYNC, SELW>(S, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid,
+                                 lane, wave, uniform64(in_off[ca]), uniform64(in_off[cb]),
+                                 uniform64(out_off[ca]), uniform64(out_off[cb]));
+}
+
 // One workgroup per tile of `tc` chunks.  The tile is cut into sub-tiles
 // that fit the LDS tables (normally one: the whole tile), each staged,
 // walked and expanded in turn; a single chunk too large for the tables
@@ -1631,8 +1721,14 @@ __device__ __forceinline__ bool tile_fits(const uint8_t* __restrict__ in,
                                           uint64_t cb) {
     const uint64_t B0 = uniform64(in_off[ca]), W0 = uniform64(out_off[ca]);
     const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
+#if UNPACK_PRO
+    // (all four loads in one round trip: no short-circuit branches between them)
+    const uint64_t B1 = uniform64(in_off[cb]), W1 = uniform64(out_off[cb]);
+    return (cb - ca <= kStageChunks) & (B1 - B0 <= kTileBytes - off0) & (W1 - W0 <= kTileWords);
+#else
     return cb - ca <= kStageChunks && uniform64(in_off[cb]) - B0 <= kTileBytes - off0 &&
            uniform64(out_off[cb]) - W0 <= kTileWords;
+#endif
 }
 
 // The same test for a per-lane tile (the overflow kernel's scan).
@@ -1690,10 +1786,19 @@ unpack_fit_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     const uint64_t ca = (uint64_t)blockIdx.x * tc;
     const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
+#if UNPACK_PRO
+    uint64_t B0, B1, W0, W1;
+    sload4(in_off + ca, in_off + cb, out_off + ca, out_off + cb, B0, B1, W0, W1);
+    const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
+    if (cb - ca > kStageChunks || B1 - B0 > kTileBytes - off0 || W1 - W0 > kTileWords) return;
+    unpack_staged_at<SYNC, true>(S, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid,
+                                 lane, wave, B0, B1, W0, W1);
+#else
     if (!tile_fits(in, in_off, out_off, ca, cb)) return;
     S.sel[tid] = kExpandTable.s[tid];
     unpack_staged<SYNC>(S, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid, lane,
                         wave);
+#endif
 }
 
 template <bool SYNC>
@@ -2052,6 +2157,75 @@ unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
     const uint64_t kf = Wa / kSyncWords + 1;
     const uint32_t nseg = 1u + (uint32_t)((Wb - 1) / kSyncWords + 1 - kf);
     const uint32_t r0 = (uint32_t)(Wa % kSyncWords);
+#if UNPACK_PRO
+    // every staging load in one round trip (as unpack_staged_at): the chunk
+    // tables and sync entries by buffer loads ahead of the byte loads, the
+    // selector entry written after them
+    {
+        constexpr uint32_t kLoads = (kWtBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
+        const uint64_t selv = kExpandTable.s[tid];
+        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint64_t*>(out_off + ca), 0, (int)((nc + 1) * 8), 0x00020000);
+        const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint64_t*>(in_off + ca), 0, (int)((nc + 1) * 8), 0x00020000);
+        const auto wov = __builtin_amdgcn_raw_buffer_load_b64(ors, (int)(tid * 8u), 0, 0);
+        const auto wnv = __builtin_amdgcn_raw_buffer_load_b64(ors, (int)(tid * 8u + 8u), 0, 0);
+        const uint32_t t_p = __builtin_amdgcn_raw_buffer_load_b32(irs, (int)(tid * 8u), 0, 0);
+        const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t*>(sync + (kf - 1)), 0, (int)(nseg * 4), 0x00020000);
+        const uint32_t e_a = __builtin_amdgcn_raw_buffer_load_b32(srs, (int)(tid * 4u), 0, 0);
+        const uint32_t e_b = __builtin_amdgcn_raw_buffer_load_b32(srs, (int)((tid + kThreads) * 4u), 0, 0);
+        const uint4* src = reinterpret_cast<const uint4*>(in + Bs - off0);
+        uint4* dst = reinterpret_cast<uint4*>(S.bytes);
+        const uint32_t nblk = (nbytes + 15) / 16;
+        uint4 r[kLoads];
+#pragma unroll
+        for (uint32_t k = 0; k < kLoads; k++) {
+            const uint32_t idx = tid + k * kThreads;
+            r[k] = nblk ? src[idx < nblk ? idx : nblk - 1] : make_uint4(0, 0, 0, 0);
+        }
+        // descriptors: none, or the raw words of a literal run carried in
+        const uint32_t litn = uniform(Pp->litn), litp = uniform(Pp->litp) + off0;
+        if (litn == 0) {
+            uint4* dd = reinterpret_cast<uint4*>(S.dpos);
+            const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
+            for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
+        } else {
+            for (uint32_t i = tid; i < ((Wt + 7) & ~7u); i += kThreads)
+                S.dpos[i] = i < litn ? (uint16_t)(kRaw | (litp + 8 * i)) : kNone;
+        }
+        S.sel[tid] = selv;
+        if (tid <= nc) {
+            const uint64_t wo = ((uint64_t)wov[1] << 32) | wov[0];
+            const uint32_t wa = wo < Wa ? 0u : (uint32_t)(wo - Wa);
+            S.cw[tid] = wa;  // (the end of a partial last chunk lies past Wt)
+            S.cp[tid] = t_p - (uint32_t)Bs + off0;  // (wraps for a partial first)
+            if (tid < nc) {
+                const uint64_t wn = ((uint64_t)wnv[1] << 32) | wnv[0];
+                const uint32_t wz = wn - Wa < Wt ? (uint32_t)(wn - Wa) : Wt;
+                if (wz > wa) {
+                    const uint32_t blo = wa == 0 ? 0u : (wa + r0 + kSyncWords - 1) / kSyncWords;
+                    const uint32_t bhi = (wz + r0 + kSyncWords - 1) / kSyncWords;
+                    for (uint32_t bb = blo; bb < bhi; bb++) S.segc[bb] = (uint8_t)tid;
+                }
+            }
+        }
+        if (tid >= 1 && tid < nseg) S.ent[tid] = e_a;
+        if (tid + kThreads < nseg) S.ent[tid + kThreads] = e_b;
+        if (tid < kStageChunks) S.badc[tid] = 0;
+        if (tid == 0) {
+            S.wt_q0 = uniform(Pp->q0) + off0;
+            S.wt_w0 = uniform(Pp->w0);
+            S.wt_qB = uniform(Pp->qB) + off0;
+            S.wt_wB = uniform(Pp->wB);
+            S.wt_pre = uniform(Pp->pre);
+            S.wt_pl = pl ? 1u : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kLoads; k++)
+            if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
+    }
+#else
     S.sel[tid] = kExpandTable.s[tid];
     {
         constexpr uint32_t kLoads = (kWtBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
@@ -2104,6 +2278,7 @@ unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
         for (uint32_t k = 0; k < kLoads; k++)
             if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
     }
+#endif
     __syncthreads();
     bool marked = false;
     for (uint32_t b = tid; b < nseg; b += kThreads) {
