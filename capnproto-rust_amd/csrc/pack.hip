@@ -1166,6 +1166,9 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
         for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
         within = v;
     }
+#if PACK_PROF == 3
+    if (lane == 0) TRACE(t, 7, RT());  // (the group's earlier tiles are summed)
+#endif
     const bool group_last = (r == kGroup - 1) || (t + 1 == A.ntiles);
     if (group_last && lane == 0) publish_agent(&A.gs[g], kFlagAgg | (within + agg));
     // exclusive prefix of the group: 64 groups per round; a group contributes

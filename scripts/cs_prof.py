@@ -100,6 +100,11 @@ def main():
         print("   phase us : " + "  ".join(f"{p} {m:.2f}" for p, m in zip(ph, means)))
         print("   in flight: " + "  ".join(f"{p} {x:.0f}" for p, x in zip(ph, inflight))
               + f"  (total {sum(inflight):.0f})")
+        if not a.pipe and (T[:, 7] > 0).all():  # look-back split: own group, then groups
+            w = (T[:, 7] - T[:, 3]) / 100.0
+            g = (T[:, 4] - T[:, 7]) / 100.0
+            print(f"   lookback: own group {w.mean():.2f} (p90 {np.percentile(w, 90):.2f})  "
+                  f"group records {g.mean():.2f} (p90 {np.percentile(g, 90):.2f}) us")
         q = np.percentile(T[:, 5] - T[:, order[0]], [10, 50, 90]) / 100.0
         print(f"   lifetime p10/p50/p90 {q[0]:.2f}/{q[1]:.2f}/{q[2]:.2f} us; "
               f"first start->last start {starts[-1] - starts[0]:.1f} us")
