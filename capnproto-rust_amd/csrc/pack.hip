@@ -1132,7 +1132,8 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
 }
 
 // Wave 0: global byte offset of tile t (aggregate already published).
-[[maybe_unused]] __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, uint32_t lane) {
+[[maybe_unused]] __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, uint32_t lane,
+                                              bool early_group = false) {
 #if PACK_ABLATE == 1 || PACK_ABLATE == 4
     return t * agg;  // timing-only: fake, in-bounds prefix; output is wrong
 #endif
@@ -1170,7 +1171,7 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
     if (lane == 0) TRACE(t, 7, RT());  // (the group's earlier tiles are summed)
 #endif
     const bool group_last = (r == kGroup - 1) || (t + 1 == A.ntiles);
-    if (group_last && lane == 0) publish_agent(&A.gs[g], kFlagAgg | (within + agg));
+    if (group_last && !early_group && lane == 0) publish_agent(&A.gs[g], kFlagAgg | (within + agg));
     // exclusive prefix of the group: 64 groups per round; a group contributes
     // its inclusive record (and ends the scan), else its aggregate
     uint64_t gexcl = 0;
@@ -1321,12 +1322,48 @@ __device__ uint64_t tiles_aggregate(const LookbackArgs& A, uint64_t t0, uint64_t
 }
 
 __device__ __forceinline__ uint64_t tile_offset(const LookbackArgs& A, uint64_t t, uint64_t agg,
-                                                uint32_t lane) {
+                                                uint32_t lane, bool early_group = false) {
 #if PACK_LB == 2
+    (void)early_group;
     return lookback_ml(A, t, agg, lane);
 #else
-    return lookback(A, t, agg, lane);
+    return lookback(A, t, agg, lane, early_group);
 #endif
+}
+
+// The group aggregate, published by the group's last tile from a wave that
+// polls the group's earlier tile records right after pass 1 (PACK_EARLYG):
+// in `lookback` it is published by wave 0 only after its pass 2 and that
+// poll, and the next group's tiles wait on it.  (A compare-and-swap from
+// empty: it never overwrites the inclusive record wave 0 publishes later.)
+#ifndef PACK_EARLYG
+#define PACK_EARLYG 0
+#endif
+__device__ void publish_group_early(const LookbackArgs& A, uint64_t t, uint64_t agg,
+                                    uint32_t lane) {
+    const uint64_t g = t / kGroup;
+    const uint32_t r = (uint32_t)(t % kGroup);
+    uint64_t st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
+    for (uint32_t spins = 0;;) {
+        const uint64_t miss = ballot64((st >> 62) == 0);
+        if (!miss) break;
+        if (++spins >= kSpinLimit) {
+            const uint64_t j = g * kGroup + ctz64(miss);
+            const uint64_t a = tile_aggregate(A, j, lane);
+            if (lane == 0) publish_agent(&A.ts[j], kFlagAgg | a);
+        } else {
+            __builtin_amdgcn_s_sleep(PACK_SLEEP);
+        }
+        st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
+    }
+    uint64_t v = st & kValMask;
+    for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    if (lane == 0) {
+        uint64_t expected = 0;
+        __hip_atomic_compare_exchange_strong(&A.gs[g], &expected, kFlagAgg | (v + agg),
+                                             __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // Wave 0: exclusive scan of the tile's chunk sizes (<= 64) into chunk_pos
@@ -2408,6 +2445,17 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         if (lane == 0) TRACE(tile, 2, RT());
 #endif
     }
+#if PACK_EARLYG
+    const bool early_group = (tile % kGroup) == kGroup - 1;
+    if (early_group && wave == kWaves - 1) {
+        uint32_t a = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; w++) a += (uint32_t)lds_u64(&sm.wave_bytes[w]);
+        publish_group_early(LA, tile, a, lane);
+    }
+#else
+    const bool early_group = false;
+#endif
     // ---- pass 2: the bytes (the look-back loads are in flight)
     if (fits) {
         uint8_t* const region_m1 = region - 1;
@@ -2434,7 +2482,7 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         wave_lds_sync();
         if (lane == 0) TRACE(tile, 3, RT());
 #endif
-        const uint64_t excl = tile_offset(LA, tile, agg, lane);
+        const uint64_t excl = tile_offset(LA, tile, agg, lane, early_group);
 #if PACK_PROF == 3
         if (lane == 0) TRACE(tile, 4, RT());
 #endif

@@ -288,9 +288,6 @@ __device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave
 #ifndef RESYNC_TILE
 #define RESYNC_TILE 1
 #endif
-#ifndef RESYNC_BLKC
-#define RESYNC_BLKC 0  // 1: block -> chunk map before the tiles (k_blkc): no searches in k_tile
-#endif
 #ifndef RESYNC_SEGUNITS
 #define RESYNC_SEGUNITS 0  // 1: decode the resolved segments as units (k_units)
 #endif
@@ -419,14 +416,6 @@ __device__ __forceinline__ void seg_rounds(const uint8_t* buf, SegState& S, bool
     }
 }
 
-// blk_c[k] = the chunk that owns block k (the last c with bstart[c] <= k).
-__global__ void __launch_bounds__(kThreads)
-k_blkc(const uint64_t* __restrict__ bstart, uint64_t n, uint64_t* __restrict__ blk_c) {
-    const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (k >= bstart[n]) return;
-    blk_c[k] = chunk_of(bstart, n, k);
-}
-
 __global__ void __launch_bounds__(kTileThreads)
 k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
        const uint64_t* __restrict__ bstart, uint64_t* exit, uint64_t* __restrict__ entry,
@@ -448,19 +437,6 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
         e0 = uniform64(__atomic_load_n(&exit[k0 - 1], __ATOMIC_RELAXED));
         if (e0 == uniform64(entry[k0])) return;  // consistent
     }
-    const uint32_t jb = wave * kWaveBlocks + lane / kSegs, q = lane % kSegs;
-    const bool valid = jb < kn;
-    const uint32_t jj = valid ? jb : (uint32_t)(kn - 1);
-    const uint64_t k = k0 + jj;
-#if RESYNC_BLKC
-    // the chunks of the tile's first block and of this lane's block from the
-    // block -> chunk map (k_blkc), and the lane's chunk bounds, all before the
-    // staging DMA: two round trips where the searches took ~6 (each vector
-    // load after the DMA also waited for it: loads complete in order)
-    const uint64_t c0 = uniform64(blk_c[k0]);
-    const uint64_t c = blk_c[k];
-    const uint64_t a = in_off[c], b = in_off[c + 1], bsc = bstart[c];
-#else
     // c0 = the last chunk with bstart[c0] <= k0: a 64-way search (3 probes
     // deep for 10^5 chunks, where one lane's binary search was 17 dependent
     // loads)
@@ -475,7 +451,6 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
         chi = nhi;
     }
     const uint64_t c0 = clo;
-#endif
     const uint64_t bs0 = uniform64(bstart[c0]), a0 = uniform64(in_off[c0]);
     if (fix && bs0 == k0) return;  // a tile that starts a chunk is exact since the spec launch
     // stage [s0 - kLead, s0 + 32 KiB + 16) (clamped to the batch: the tile's
@@ -497,10 +472,13 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
                     (__attribute__((address_space(3))) void*)(tbuf + 16u * i0), 16, 0, 0);
         }
     }
-#if !RESYNC_BLKC
     // this lane's block (offset jb in the tile) and segment q; its chunk: c0 +
     // the chunk starts in (k0, k0 + jb], counted over batches of 64 starts (a
     // lane's binary search over the batch by shuffles)
+    const uint32_t jb = wave * kWaveBlocks + lane / kSegs, q = lane % kSegs;
+    const bool valid = jb < kn;
+    const uint32_t jj = valid ? jb : (uint32_t)(kn - 1);
+    const uint64_t k = k0 + jj;
     uint64_t c = c0;
     for (uint64_t cb = c0 + 1;; cb += CAPNP_WAVE) {
         const uint64_t idx = cb + lane;
@@ -515,7 +493,6 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
         if (dlast >= CAPNP_WAVE) break;  // this batch reaches past the tile
     }
     const uint64_t a = in_off[c], b = in_off[c + 1], bsc = bstart[c];
-#endif
     const uint64_t s = a + (k - bsc) * kBlock;
     const uint64_t e = s + kBlock < b ? s + kBlock : b;
     const uint64_t ssa = s + q * kSegBytes < e ? s + q * kSegBytes : e;
@@ -602,7 +579,7 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
         exit[k] = xa;
         entry[k] = ea;
         words[k] = wsum;
-        if (!fix && !RESYNC_BLKC) blk_c[k] = c;
+        if (!fix) blk_c[k] = c;
         if (fix && (uint64_t)jb == kn - 1 && old != xa) flags[2 + pass] = 1;
     }
     RTRACE(5);
@@ -788,7 +765,6 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
     const bool tile = tile_mode();
     const unsigned tgrid = (unsigned)((nbb + kTileBlocks - 1) / kTileBlocks);
     const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
-    if (tile && RESYNC_BLKC) k_blkc<<<grid(nbb), kThreads, 0, s>>>(w.bstart, n, w.spec_exit);
     if (tile)
         k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
                                                     w.words, w.spec_exit, w.flags, 0, 0,
