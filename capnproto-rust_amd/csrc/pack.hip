@@ -878,19 +878,34 @@ __device__ __forceinline__ uint64_t start_bits(const uint64_t* __restrict__ cb, 
     return r ? (lo >> r) | (cb[q + 1] << (64 - r)) : lo;
 }
 
+// start_bits for a signed first word p > 64 (b64 - 1) - 64 (a window that
+// may begin before word 0).
+__device__ __forceinline__ uint64_t start_bits_s(const uint64_t* __restrict__ cb, uint64_t b64,
+                                                 int64_t p) {
+    const uint64_t q = (uint64_t)(1 + (p >> 6) - (int64_t)b64);  // (p >> 6: floor)
+    const uint32_t r = (uint32_t)(p & 63);
+    const uint64_t lo = cb[q];
+    return r ? (lo >> r) | (cb[q + 1] << (64 - r)) : lo;
+}
+
 // The run state entering word R from the 64 words before it (w = word
 // R - 64 + lane, wp = word R - 65, bits = their chunk-start bits): the last
 // sure head or chunk start s before R, then heads every 256 words through an
 // all-zero / all-0xFF stretch, or one resolved step.  Deeper stretches load
 // eight windows (words and bits) per round.
+// W: the words examined first are R - W .. R - 1 (lanes 64 - W ..; wp = word
+// R - W - 1): with random data nearly every word is a sure head, so a short
+// window decides almost every range and the deep search takes the rest.
+template <uint32_t W = 64>
 __device__ __forceinline__ Carry carry_in_b(const uint64_t* __restrict__ in,
                                             const uint64_t* __restrict__ cb, uint64_t b64,
                                             uint64_t wlo, uint64_t R, uint32_t lane, uint64_t w,
                                             uint64_t wp, uint64_t bits) {
-    const bool v = R + lane >= 64 + wlo;  // word R - 64 + lane is at or past wlo
+    // word R - 64 + lane is in the window and at or past wlo
+    const bool v = (int)lane >= 64 - (int)W && R + lane >= 64 + wlo;
     const uint32_t tag = v ? tag_of(w) : 0u;
     const uint32_t up = (uint32_t)__shfl_up((int)tag, 1, 64);
-    const uint32_t ptag = lane ? up : tag_of(wp);
+    const uint32_t ptag = lane != 64u - W ? up : tag_of(wp);  // (W = 64: lane 0)
     const uint64_t G = ballot64(v && (((bits >> lane) & 1) || sure_head(tag, ptag)));
     if (G) {
         const uint32_t j = 63u - (uint32_t)__builtin_clzll(G);
@@ -906,8 +921,8 @@ __device__ __forceinline__ Carry carry_in_b(const uint64_t* __restrict__ in,
         return resolve_step_s(ballot64(tag == 0) & Vj, ballot64(pop >= 7) & Vj,
                               ballot64(tag == 0xFF) & Vj, 1ull << j, 64, Carry{0, 0}).next;
     }
-    bool allz = ballot64(tag != 0) == 0, allf = ballot64(tag != 0xFF) == 0;
-    for (uint64_t hi = R - 64; hi > wlo; hi = hi > wlo + 512 ? hi - 512 : wlo) {
+    bool allz = ballot64(v && tag != 0) == 0, allf = ballot64(v && tag != 0xFF) == 0;
+    for (uint64_t hi = R - W; hi > wlo; hi = hi > wlo + 512 ? hi - 512 : wlo) {
         uint32_t t[8];
         uint64_t bk[8];
         {
@@ -918,8 +933,13 @@ __device__ __forceinline__ Carry carry_in_b(const uint64_t* __restrict__ in,
                 const bool inb = hi >= wlo + 64ull * (k + 1) - lane;  // lo + lane >= wlo
                 x[k] = inb ? in[lo + lane] : 0ull;
                 // (words lo .. lo + 63 reach the batch: lo >= 0 and lo + 64 > wlo)
-                bk[k] = (hi >= 64ull * (k + 1) && hi + 64 > wlo + 64ull * (k + 1))
-                            ? start_bits(cb, b64, lo) : 0ull;
+                // (signed: with W < 64 the windows are not 64-aligned, so one
+                // can start below word 0 and still hold valid words; cb[0]
+                // is the zero guard for the 64 words before the batch's first
+                // 64-word block, so any window overlapping the batch is
+                // covered)
+                const int64_t slo = (int64_t)hi - 64ll * (k + 1);
+                bk[k] = slo + 64 <= (int64_t)wlo ? 0ull : start_bits_s(cb, b64, slo);
             }
 #pragma unroll
             for (int k = 0; k < 8; k++) t[k] = tag_of(x[k]);
@@ -2712,6 +2732,32 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
 #endif
     // the range's first chunks (their offsets are written after the
     // look-back; loaded now, off that path)
+#if PACK_CS_SPEC
+    // (unconditional loads at in-bounds indexes, selected afterwards: map and
+    // plan have an entry past the last range, and the steps' chunk-start
+    // bits are one vector load; guarded loads had each waited at its join)
+    const uint64_t r = tile * kWaves + wave;
+    const uint64_t cAr = uniform64(map[r]);
+    const uint32_t pinr = uniform(plan[r]), poutr = uniform(plan[r + 1]);
+    const uint64_t q0 = have ? 1 + (R0 >> 6) - b64 : 0;
+    const uint64_t cbv = cbits[q0 + (lane < kStageSteps ? lane : kStageSteps)];
+    const uint64_t cA = have ? cAr : nchunks;
+    // the run states at both ends (pack_wt_plan)
+    const uint32_t pin = have ? pinr : 0u;
+    const uint32_t pout = (have && !lastr) ? poutr : 0u;
+    const uint64_t stv = chunk_off[cA + lane < nchunks ? cA + lane : nchunks];
+    const uint64_t st0 = cA + lane < nchunks ? stv : ~0ull;
+    // chunk starts (forced heads) of the steps
+    uint64_t smk[kStageSteps];
+    const uint32_t rr = (uint32_t)(R0 & 63);
+#pragma unroll
+    for (uint32_t s = 0; s < kStageSteps; s++) {
+        const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
+        const uint64_t lo = readlane64(cbv, s), hi = readlane64(cbv, s + 1);
+        const uint64_t bits = rr ? (lo >> rr) | (hi << (64 - rr)) : lo;
+        smk[s] = nv ? bits & low_mask(nv) : 0ull;
+    }
+#else
     const uint64_t cA = have ? uniform64(map[tile * kWaves + wave]) : nchunks;
     const uint64_t st0 = cA + lane < nchunks ? chunk_off[cA + lane] : ~0ull;
     // the run states at both ends (pack_wt_plan)
@@ -2725,6 +2771,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
         smk[s] = nv ? start_bits(cbits, b64, R0 + 64u * s) & low_mask(nv) : 0ull;
     }
+#endif
     for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
         *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
     wave_lds_sync();
@@ -2866,6 +2913,10 @@ pack_wt_bits(const uint64_t* __restrict__ chunk_off, uint64_t nchunks, uint64_t 
     if (st < whi) atomicOr(&cb[1 + (st >> 6) - b64], 1ull << (st & 63));
 }
 
+#ifndef PACK_PLAN_WIN
+#define PACK_PLAN_WIN 64  // words before a range examined first (16: 254 vs 190 us, more deep searches)
+#endif
+static_assert(PACK_PLAN_WIN >= 2 && PACK_PLAN_WIN <= 64, "plan window");
 // Run state at every wave range's first word, one wave per range: plan[r] =
 // type | rem << 2 | ext << 10, ext = the words from R0 on that the run open
 // there absorbs (run_ext_b).  The pack kernel reads its own entry and the
@@ -2882,34 +2933,39 @@ pack_wt_plan(const uint64_t* __restrict__ in, const uint64_t* __restrict__ cbits
     const uint64_t b64 = wlo >> 6;
     uint32_t rec = 0;
     if (R < whi && R > wlo) {
-#if PACK_CS_SPEC
-        // every load in one round trip: clamped addresses and selects instead
-        // of guarded loads (the compiler waited at each guard's join)
-        const uint64_t ib = R - 64 + lane >= wlo ? R - 64 + lane : wlo;
-        const uint64_t ia = R + lane < whi ? R + lane : whi - 1;
-        // (word R - 65 as a lane's load, so it is not deferred to its use)
-        const uint64_t ip = R - 65 + lane >= wlo ? R - 65 + lane : wlo;
-        const uint64_t xb = in[ib], xa = in[ia];
-        const uint64_t xp = readlane64(in[ip], 0);
-        const uint64_t qa = 1 + (R >> 6) - b64, qb = R >= 64 ? qa - 1 : qa;
+        // Every load in one round trip: clamped addresses and selects instead
+        // of guarded loads (the compiler waited at each guard's join).  The
+        // W words before R (lanes 64 - W ..) and the word before them; the
+        // words after R only when the run state at R is an open run.
+        constexpr uint32_t W = PACK_PLAN_WIN;
+        // (a buffer load over words [B, R), B = max(R - W - 1, wlo): lanes
+        // outside it read 0 without a fetch, and no branch means no wait at
+        // a join before the scalar loads below)
+        const uint64_t B = R - W - 1 >= wlo ? R - W - 1 : wlo;
+        const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint64_t*>(in + B), 0, (int)((R - B) * 8), 0x00020000);
+        const uint64_t wi = R - 64 + lane;
+        const uint32_t vo = wi >= B ? (uint32_t)(wi - B) * 8u : 0x80000000u;
+        const auto xv = __builtin_amdgcn_raw_buffer_load_b64(wrs, (int)vo, 0, 0);
+        const uint64_t x = ((uint64_t)xv[1] << 32) | xv[0];
+        // (the words after R: with the full window they load with the rest)
+        const uint64_t xa = W == 64 ? in[R + lane < whi ? R + lane : whi - 1] : 0ull;
+        const uint64_t qa = uniform64(1 + (R >> 6) - b64), qb = uniform64(R >= 64 ? qa - 1 : qa);
         const uint32_t rr = (uint32_t)(R & 63);
-        const uint64_t ca0 = uniform64(cbits[qa]), ca1 = uniform64(cbits[qa + 1]);
-        const uint64_t cb0 = uniform64(cbits[qb]), cb1 = uniform64(cbits[qb + 1]);
-        const uint64_t wb = R >= wlo + 64 - lane ? xb : 0ull;
-        const uint64_t wp = R >= wlo + 65 ? xp : 0ull;
-        const uint64_t wa = R + lane < whi ? xa : 0ull;
+        uint64_t ca0, ca1, cb0, cb1;
+        sload4(cbits + qa, cbits + qa + 1, cbits + qb, cbits + qb + 1, ca0, ca1, cb0, cb1);
+        const uint64_t wb = R >= wlo + 64 - lane ? x : 0ull;
+        const uint64_t xp = W < 64 ? readlane64(x, 63u - W) : in[R - 65 >= wlo ? R - 65 : wlo];
+        const uint64_t wp = R >= wlo + W + 1 ? xp : 0ull;  // word R - W - 1
         const uint64_t bb = R >= 64 ? (rr ? (cb0 >> rr) | (cb1 << (64 - rr)) : cb0) : 0ull;
         const uint64_t ba = rr ? (ca0 >> rr) | (ca1 << (64 - rr)) : ca0;
-#else
-        const uint64_t wb = R >= wlo + 64 - lane ? in[R - 64 + lane] : 0ull;
-        const uint64_t wp = R >= wlo + 65 ? in[R - 65] : 0ull;
-        const uint64_t wa = R + lane < whi ? in[R + lane] : 0ull;
-        const uint64_t bb = R >= 64 ? start_bits(cbits, b64, R - 64) : 0ull;
-        const uint64_t ba = start_bits(cbits, b64, R);
-#endif
         if (!(ba & 1)) {  // R inside a chunk
-            const Carry c = carry_in_b(in, cbits, b64, wlo, R, lane, wb, wp, bb);
-            const uint32_t ext = run_ext_b(in, cbits, b64, whi, R, c, lane, wa, ba);
+            const Carry c = carry_in_b<W>(in, cbits, b64, wlo, R, lane, wb, wp, bb);
+            uint32_t ext = 0;
+            if (c.type != 0 && c.rem != 0) {
+                const uint64_t wa = R + lane < whi ? (W == 64 ? xa : in[R + lane]) : 0ull;
+                ext = run_ext_b(in, cbits, b64, whi, R, c, lane, wa, ba);
+            }
             rec = c.type | (c.rem << 2) | (ext << 10);
         }
     }
