@@ -705,6 +705,56 @@ __device__ __forceinline__ void copy_out(const uint8_t* region, uint8_t* __restr
     if (lane < hi - b) out[b + lane] = region[(b - D0) + lane];
 }
 
+// copy_out for a region of at most 1024 MAXIT bytes: every LDS read of the
+// wave first, then the stores (the passes' registers are dead by the
+// copy-out, so the reads need no extra occupancy), instead of one LDS round
+// trip per 1 KiB store.
+template <int MAXIT>
+__device__ __forceinline__ void copy_out_pre(const uint8_t* region, uint8_t* __restrict__ out,
+                                             uint64_t D0, uint64_t len, uint64_t cap,
+                                             uint32_t lane) {
+    const uint64_t lo = D0;
+    const uint64_t hi = (D0 + len < cap) ? D0 + len : cap;
+    if (hi <= lo) return;
+    const uint64_t a = (lo + 15) & ~15ull, b = hi & ~15ull;
+    if (a > b) {
+        if (lane < hi - lo) out[lo + lane] = region[lane];
+        return;
+    }
+    if (lane < a - lo) out[lo + lane] = region[lane];
+    const uint32_t m = (uint32_t)((a - D0) & 15);  // source misalignment (uniform)
+    const uint32_t q = m >> 2, sb = m & 3;
+    uint4 A[MAXIT], B[MAXIT];
+#pragma unroll
+    for (int it = 0; it < MAXIT; it++) {
+        const uint64_t blk = a + 16ull * lane + 1024ull * it;
+        const uint32_t s = (uint32_t)(blk - D0) & ~15u;
+        if (blk < b) {
+            A[it] = *reinterpret_cast<const uint4*>(region + s);
+            B[it] = *reinterpret_cast<const uint4*>(region + s + 16);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < MAXIT; it++) {
+        const uint64_t blk = a + 16ull * lane + 1024ull * it;
+        if (blk < b) {
+            const uint32_t w[8] = {A[it].x, A[it].y, A[it].z, A[it].w,
+                                   B[it].x, B[it].y, B[it].z, B[it].w};
+            const uint32_t w0 = q == 0 ? w[0] : q == 1 ? w[1] : q == 2 ? w[2] : w[3];
+            const uint32_t w1 = q == 0 ? w[1] : q == 1 ? w[2] : q == 2 ? w[3] : w[4];
+            const uint32_t w2 = q == 0 ? w[2] : q == 1 ? w[3] : q == 2 ? w[4] : w[5];
+            const uint32_t w3 = q == 0 ? w[3] : q == 1 ? w[4] : q == 2 ? w[5] : w[6];
+            const uint32_t w4 = q == 0 ? w[4] : q == 1 ? w[5] : q == 2 ? w[6] : w[7];
+            const uint4 o = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sb),
+                                       __builtin_amdgcn_alignbyte(w2, w1, sb),
+                                       __builtin_amdgcn_alignbyte(w3, w2, sb),
+                                       __builtin_amdgcn_alignbyte(w4, w3, sb));
+            *reinterpret_cast<uint4*>(out + blk) = o;
+        }
+    }
+    if (lane < hi - b) out[b + lane] = region[(b - D0) + lane];
+}
+
 // Streaming path: wave w owns chunks w, w+4, ...  MODE_SIZE fills
 // chunk_size; MODE_RING re-reads and writes at chunk_pos.
 template <int MODE>
@@ -2176,6 +2226,9 @@ pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ c
 // kCsSteps chunks of its tile.  Tiles with a longer chunk (or more chunks per
 // wave) take the streaming size pass and leave their bytes to
 // pack_ovf_kernel.
+#ifndef PACK_COPY_PRE
+#define PACK_COPY_PRE 0  // 1: the chunk-step kernel's copy-out reads its LDS region first
+#endif
 #ifndef PACK_CS_SPEC
 #define PACK_CS_SPEC 1  // one-round-trip prologues: speculative step loads etc. (below)
 #endif
@@ -2550,7 +2603,13 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         if (nw) {
             const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
             const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
+#if PACK_COPY_PRE
+            copy_out_pre<(kStageRegion + 1023) / 1024>(region, out - mis, D0,
+                                                       lds_u64(&sm.wave_bytes[wave]), out_cap + mis,
+                                                       lane);
+#else
             copy_out(region, out - mis, D0, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
+#endif
         }
 #if PACK_PROF == 3
         __syncthreads();

@@ -1248,6 +1248,9 @@ __device__ __forceinline__ void spec_tile(SM& S, uint64_t ca, uint32_t nc,
 #define UNPACK_SEG_OVERLAP 48  // config 2 nosync: 0 -> 724 us, 16 -> 699, 32 -> 646, 48 -> 614, 64 -> 640
 #endif
 constexpr uint32_t kSegOverlap = UNPACK_SEG_OVERLAP;  // spec walk lead-in (bytes)
+#ifndef UNPACK_DESC_MASK
+#define UNPACK_DESC_MASK 0  // 1: descriptors from the spec walk's record-start mask (below)
+#endif
 constexpr uint32_t kSegChunks = 16;  // tiles of at most this many chunks take the segment walk
 
 // One record hop (the walk's loops stop once p >= the segment end, so a
@@ -1286,7 +1289,18 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
     uint32_t p = s0, w = 0;
     while (act && p < sb) seg_hop(S.bytes, p, w);
     const uint32_t f = p, wf = w;
+#if UNPACK_DESC_MASK
+    // the spec chain's record starts in the segment, bit p - f (a segment
+    // whose starts reach past 64 bytes keeps the walk below)
+    uint64_t smask = 0;
+    while (act && p < se) {
+        smask |= (p - f < 64u) ? (1ull << (p - f)) : 0ull;
+        seg_hop(S.bytes, p, w);
+    }
+    const bool mask_ok = se - f <= 64u;
+#else
     while (act && p < se) seg_hop(S.bytes, p, w);
+#endif
     const bool serr = p > pe;  // (a record past the chunk end: garbage, or j = 0's error)
     const uint32_t xs = serr ? 0u : p, ws = w - wf;
 #if UNPACK_PROF
@@ -1357,6 +1371,39 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
     const bool chunk_ok = act && (bad_m & gm) == 0 && tot == n && xl == pe && n > 0 && pe > cs;
     if (act && j == 0) S.badc[c] = chunk_ok ? 0 : 1;
     // 3. descriptors of the good chunks: records from the entry to the exit
+#if UNPACK_DESC_MASK
+    if (chunk_ok && e == f && mask_ok) {
+        // the segment kept its spec chain: its record starts are the mask's
+        // bits, so the tag reads do not wait on each other (two records a
+        // round, their reads issued together)
+        uint32_t ww = S.cw[c] + incl - wd;
+        uint64_t m = smask;
+        while (m) {
+            const uint32_t q0 = f + (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            const bool two = m != 0;
+            const uint32_t q1 = two ? f + (uint32_t)__builtin_ctzll(m) : q0;
+            if (two) m &= m - 1;
+            uint32_t t0, a1, a9, t1, c1, c9;
+            rec_bytes(S.bytes, q0 + 1u, t0, a1, a9);
+            rec_bytes(S.bytes, q1 + 1u, t1, c1, c9);
+            {
+                const bool isz = t0 == 0, isf = t0 == 0xFF;
+                const uint32_t cnt = isz ? a1 : (isf ? a9 : 0u);
+                S.dpos[ww] = (uint16_t)q0;
+                if (isf && cnt) lit_entries(S, ww, q0, cnt);
+                ww += 1u + cnt;
+            }
+            if (two) {
+                const bool isz = t1 == 0, isf = t1 == 0xFF;
+                const uint32_t cnt = isz ? c1 : (isf ? c9 : 0u);
+                S.dpos[ww] = (uint16_t)q1;
+                if (isf && cnt) lit_entries(S, ww, q1, cnt);
+                ww += 1u + cnt;
+            }
+        }
+    } else
+#endif
     if (chunk_ok) {
         uint32_t q = e, ww = S.cw[c] + incl - wd;
         while (q < x) {
