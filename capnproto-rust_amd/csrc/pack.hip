@@ -1164,7 +1164,10 @@ __device__ uint64_t tile_aggregate(const LookbackArgs& A, uint64_t j, uint32_t l
 // Every wait is bounded: on timeout the waiter computes the missing aggregate
 // itself from the input (records are idempotent), so the kernel finishes with
 // the right answer under any workgroup dispatch order.
-constexpr uint32_t kGroup = 64;
+#ifndef PACK_GROUP
+#define PACK_GROUP 64  // tiles per look-back group (<= 64: one lane per tile)
+#endif
+constexpr uint32_t kGroup = PACK_GROUP;
 #ifndef PACK_SLEEP
 #define PACK_SLEEP 2  // s_sleep between look-back polls (x 64 cycles)
 #endif
