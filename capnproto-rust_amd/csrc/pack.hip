@@ -1409,6 +1409,9 @@ __device__ __forceinline__ uint64_t tile_offset(const LookbackArgs& A, uint64_t 
 // in `lookback` it is published by wave 0 only after its pass 2 and that
 // poll, and the next group's tiles wait on it.  (A compare-and-swap from
 // empty: it never overwrites the inclusive record wave 0 publishes later.)
+#ifndef PACK_WT_EARLYG
+#define PACK_WT_EARLYG 0  // the word-tile kernel's early group aggregate (A/B)
+#endif
 #ifndef PACK_EARLYG
 #define PACK_EARLYG 1  // measured (config 2): 508.6 -> 502.4 us; 2: the inclusive record too
 #endif
@@ -2882,6 +2885,14 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         agg += b;
     }
     if (wave == 0) publish(LA, tile, agg, lane);
+#if PACK_EARLYG && PACK_WT_EARLYG
+    // (the group's last tile publishes the group aggregate from its last
+    // wave now, as the chunk-step kernel does)
+    const bool early_group = (tile % kGroup) == kGroup - 1;
+    if (early_group && wave == kWaves - 1) publish_group_early(LA, tile, agg, lane);
+#else
+    const bool early_group = false;
+#endif
     // pass 2: the bytes
     wave_lds_sync();
     {
@@ -2940,7 +2951,8 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         }
     }
     if (wave == 0) {
-        const uint64_t excl = PACK_WT_ABL == 5 ? tile * 8192 : tile_offset(LA, tile, agg, lane);
+        const uint64_t excl =
+            PACK_WT_ABL == 5 ? tile * 8192 : tile_offset(LA, tile, agg, lane, early_group);
         if (lane == 0) {
             wm.excl = excl;
             tile_off[tile] = excl;
