@@ -300,8 +300,14 @@ constexpr uint32_t kTileWaves = kSegs;                      // (so a tile stays 
 constexpr uint32_t kWaveBlocks = CAPNP_WAVE / kSegs;        // 16
 constexpr uint32_t kTileBlocks = kTileWaves * kWaveBlocks;  // 64
 constexpr uint32_t kTileThreads = kTileWaves * CAPNP_WAVE;
-constexpr uint64_t kLead = 48;
-constexpr uint32_t kCatchUp = 16;
+#ifndef RESYNC_LEAD
+#define RESYNC_LEAD 48  // spec walk lead-in (bytes)
+#endif
+#ifndef RESYNC_CATCHUP
+#define RESYNC_CATCHUP 16  // hops a re-walk lets its spec chain catch up per step
+#endif
+constexpr uint64_t kLead = RESYNC_LEAD;
+constexpr uint32_t kCatchUp = RESYNC_CATCHUP;
 constexpr uint32_t kTileLds = (uint32_t)(kTileBlocks * kBlock + kLead + 64);
 constexpr uint32_t kRelCap = 0xF0000000u;  // chunk ends past this are "far" (tile offsets are < 40 K)
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
