@@ -24,8 +24,9 @@ collectives are the barrier and the max-over-ranks of the timing only.
 The JSON line also carries
   roofline      the dominant kernel's algorithmic bytes per launch / its mean
                 launch time (HIP events on the launch stream) vs 8 TB/s;
-  cpu_baseline  the CPU oracle (C restatement of the reference codec) timed
-                on a bounded sample of the same workload on this host.
+  cpu_baseline  the reference's CPU codec loops (oracle/refloop_oracle.c, a C
+                restatement; the reference is Rust and cannot be built here)
+                timed on a bounded sample of the same workload on this host.
 """
 import argparse
 import json
@@ -144,13 +145,17 @@ def config1_baseline(threads, target_words=1 << 25, reps=3):
     mo = msg_off[:m + 1]
     ww = words[:int(mo[-1])]
     um = 8 * len(ww)
-    runs = [O.messages_roundtrip_mt(ww, mo, threads) for _ in range(reps)]
+    runs = [O.refloop_messages_roundtrip_mt(ww, mo, threads) for _ in range(reps)]
     assert all(r[3] for r in runs)
     bm = min(runs, key=lambda r: r[0] + r[1])
     m1 = max(1, m // 16)
-    b1 = min((O.messages_roundtrip_mt(words[:int(msg_off[m1])], msg_off[:m1 + 1], 1)
+    b1 = min((O.refloop_messages_roundtrip_mt(words[:int(msg_off[m1])], msg_off[:m1 + 1], 1)
               for _ in range(2)), key=lambda r: r[0] + r[1])
     u1 = 8 * int(msg_off[m1])
+    # the parity oracle's branchy loops on the same requests (the round-3 figure)
+    ro = min((O.messages_roundtrip_mt(ww, mo, threads) for _ in range(2)),
+             key=lambda r: r[0] + r[1])
+    assert ro[3] and ro[2] == bm[2]
     return {
         "workload": "config1: benchmark carsales bytes reuse packed, codec calls "
                     "(write_message + read_message per request)",
@@ -161,9 +166,13 @@ def config1_baseline(threads, target_words=1 << 25, reps=3):
         "requests_per_s": round(m / (bm[0] + bm[1]), 1),
         "single_thread_roundtrip_gibps": round(u1 / (b1[0] + b1[1]) / GiB, 3),
         "single_thread_requests_per_s": round(m1 / (b1[0] + b1[1]), 1),
+        "oracle_roundtrip_gibps": round(um / (ro[0] + ro[1]) / GiB, 3),
         "kind": "port",
         "note": f"best of {reps}; {m} requests ({um / GiB:.3f} GiB) of the reference "
-                f"benchmark's chain; single thread on the first {m1}",
+                f"benchmark's chain, the reference's loops (oracle/refloop_oracle.c; "
+                f"read_message zeroes the body as allocate_zeroed_vec does); single "
+                f"thread on the first {m1}; oracle_roundtrip_gibps: the parity oracle's "
+                f"branchy loops",
     }
 
 
@@ -189,24 +198,47 @@ def cpu_baseline(args, threads):
         words = O.gen_fill(offs, kind0=0, pz=PZ.get(args.workload, PZ["config2"]))
 
     def timed(nn, thr, reps):
+        """The reference's loops (oracle/refloop_oracle.c): buffers allocated
+        and mapped before the clock, bytes checked against the parity oracle
+        after it."""
+        o = offs[:nn + 1]
+        w = words[:int(o[-1])]
+        b = O.RefloopBatch(w, o, thr)
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            st = b.pack()
+            t1 = time.perf_counter()
+            b.unpack()
+            t2 = time.perf_counter()
+            assert st == 0 and (b.status == 0).all() and np.array_equal(b.back[:len(w)], w)
+            if best is None or t2 - t0 < best[0]:
+                best = (t2 - t0, t1 - t0, t2 - t1)
+        stream, soffs = b.packed_stream()
+        st, ref, ref_offs = O.pack_batch(w, o)
+        assert st == 0 and np.array_equal(stream, ref) and np.array_equal(soffs, ref_offs)
+        return best
+
+    def timed_oracle(nn, thr, reps):
+        """The parity oracle's branchy loops (round 3's baseline), same sample."""
         o = offs[:nn + 1]
         w = words[:int(o[-1])]
         best = None
         for _ in range(reps):
             t0 = time.perf_counter()
             st, packed, poffs = O.pack_batch(w, o, threads=thr)
-            t1 = time.perf_counter()
             back, status, _ = O.unpack_batch(packed, poffs, o, threads=thr)
-            t2 = time.perf_counter()
+            t1 = time.perf_counter()
             assert st == 0 and (status == 0).all() and np.array_equal(back, w)
-            if best is None or t2 - t0 < best[0]:
-                best = (t2 - t0, t1 - t0, t2 - t1)
+            best = t1 - t0 if best is None else min(best, t1 - t0)
         return best
 
     best = timed(n, threads, args.cpu_reps)
     n1 = max(1, n // 16)
     one = timed(n1, 1, 2)
     u, u1 = int(offs[n]) * 8, int(offs[n1]) * 8
+    orc = timed_oracle(n, threads, 2)
+    orc1 = timed_oracle(n1, 1, 1)
     shape = (f"{n} segments of 64 B - 64 KiB" if args.workload == "config4"
              else f"{n} segments x {cw * 8} B")
     share = cpu_share()
@@ -217,12 +249,19 @@ def cpu_baseline(args, threads):
         **share,
         "kind": "port",
         "sample": f"{shape} ({u / GiB:.3f} GiB) of the same workload, "
-                  f"pack+unpack per segment, best of {args.cpu_reps}, {threads} threads "
-                  f"(oracle/packed_oracle.c, gcc -O3; cores = threads used = the affinity "
-                  f"mask's CPUs capped by the cgroup quota and OMP_NUM_THREADS)",
+                  f"pack+unpack per segment, best of {args.cpu_reps}, {threads} threads, "
+                  f"the reference's branch-free loops (oracle/refloop_oracle.c, gcc -O3: "
+                  f"serialize_packed.rs:304-439 / :80-228, outputs mapped before timing, "
+                  f"bytes checked against the parity oracle); cores = threads used = the "
+                  f"affinity mask's CPUs capped by the cgroup quota and OMP_NUM_THREADS",
         "pack_gibps": round(u / best[1] / GiB, 3),
         "unpack_gibps": round(u / best[2] / GiB, 3),
         "single_thread_gibps": round(u1 / one[0] / GiB, 3),
+        "single_thread_pack_gibps": round(u1 / one[1] / GiB, 3),
+        "single_thread_unpack_gibps": round(u1 / one[2] / GiB, 3),
+        # round 3's baseline: the parity oracle (oracle/packed_oracle.c), branchy loops
+        "oracle_gibps": round(u / orc / GiB, 3),
+        "oracle_single_thread_gibps": round(u1 / orc1 / GiB, 3),
     }
     # BASELINE configs[0] rides on every line (the driver runs the default
     # workload only)

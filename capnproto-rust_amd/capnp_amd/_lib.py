@@ -48,8 +48,9 @@ EXPORTS = [
     "capnp_packed_reader_free", "capnp_packed_reader_read", "capnp_packed_reader_read_exact",
     "capnp_packed_reader_read_message", "capnp_packed_reader_buffered",
     "capnp_gpu_find_messages",
-    "capnp_gpu_read_message_stream",
+    "capnp_gpu_read_message_stream", "capnp_abi_version", "capnp_resync_max_passes",
 ]
+ABI_VERSION = 4  # include/capnp_packed.h CAPNP_ABI_VERSION
 
 
 class ReaderOptionsC(C.Structure):
@@ -82,6 +83,12 @@ def lib():
         build()
     L = C.CDLL(LIB_PATH)
     vp, sz, u64, u32, i32 = C.c_void_p, C.c_size_t, C.c_uint64, C.c_uint32, C.c_int
+    L.capnp_abi_version.restype = u32
+    if L.capnp_abi_version() != ABI_VERSION:  # (signatures below are this revision's)
+        raise ImportError(f"{LIB_PATH}: ABI {L.capnp_abi_version()}, binding expects "
+                          f"{ABI_VERSION}")
+    L.capnp_resync_max_passes.argtypes = [C.c_int]
+    L.capnp_resync_max_passes.restype = C.c_int
     L.capnp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int)]
     L.capnp_ctx_create.restype = vp
     L.capnp_ctx_destroy.argtypes = [vp]

@@ -184,7 +184,9 @@ class Context:
         import torch
         nmsg = msg_seg_off.numel() - 1
         nseg = seg_word_off.numel() - 1
-        total_words = int(seg_word_off[-1].item() - seg_word_off[0].item()) if nseg else 0
+        # (the words `words` holds up to the last segment: the bound the
+        # library checks every segment offset against)
+        total_words = int(seg_word_off[-1].item()) if nseg else 0
         if out is None:
             cap = self.batch_bound_bytes(total_words + 2 * nmsg + nseg // 2, 2 * nmsg + nseg)
             out = torch.empty(max(cap, 1), dtype=torch.uint8, device=words.device)
@@ -327,7 +329,9 @@ class Context:
         stops short of a clean end, the next message is read as the loop's
         next try_read_message (capnp_gpu_read_messages), which fails as the
         reference does, or succeeds and the loop goes on after it.
-        max_msgs caps the messages one pass lists (None: no cap)."""
+        max_msgs caps the messages one pass lists (None: no cap): a pass that
+        finds more hands out the first max_msgs and the next pass decodes the
+        stream again from the message after them."""
         import torch
         nb = int(packed.numel())
         out, start = [], 0
@@ -338,13 +342,17 @@ class Context:
                 view, limit=limit, msgs_cap=max_msgs, stream=stream)
             mbo_h, bwo_h, mso_h = mbo.cpu().tolist(), bwo.cpu().tolist(), mso.cpu().tolist()
             seg_h = segw.cpu().tolist()
-            for k in range(n):
+            take = n if max_msgs is None else min(n, int(max_msgs))
+            for k in range(take):
                 a, p = bwo_h[k], []
                 for j in range(mso_h[k], mso_h[k + 1]):
                     ln = seg_h[j]
                     p.append(words[a:a + ln])
                     a += ln
                 out.append((p, mbo_h[k + 1] - mbo_h[k]))
+            if take < n:  # the cap: the next pass starts at message `take`
+                start += mbo_h[take]
+                continue
             stop = mbo_h[n]
             if clean or stop >= rest:
                 break

@@ -436,6 +436,8 @@ extern "C" {
 
 const char* capnp_version(void) { return "capnp-packed-mi355x 0.1.0 (gfx950)"; }
 
+uint32_t capnp_abi_version(void) { return CAPNP_ABI_VERSION; }
+
 capnp_reader_options capnp_default_reader_options(void) {
     capnp_reader_options o;
     o.traversal_limit_in_words = 8ull * 1024 * 1024;
@@ -999,9 +1001,12 @@ capnp_status capnp_gpu_write_messages(capnp_ctx* ctx, const uint64_t* d_words,
     if (total_segs < nmsg || (total_words && !d_words)) return CAPNP_E_INVALID_ARGUMENT;
     {
         // message m's segments [msg_seg_off[m], msg_seg_off[m+1]) within
-        // [0, total_segs]; segment offsets non-decreasing
-        capnp_status vst = check_offsets(
-            ctx, s, {{d_msg_seg_off, nmsg, (uint64_t)total_segs}, {d_seg_word_off, total_segs, ~0ull}});
+        // [0, total_segs]; segment offsets non-decreasing and within the
+        // total_words words of d_words (both paths read the segments at these
+        // offsets before anything else would notice)
+        capnp_status vst = check_offsets(ctx, s,
+                                         {{d_msg_seg_off, nmsg, (uint64_t)total_segs},
+                                          {d_seg_word_off, total_segs, (uint64_t)total_words}});
         if (vst != CAPNP_OK) return vst;
     }
     // Gap path: the segments are packed in place as the chunks, each

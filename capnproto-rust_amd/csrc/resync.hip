@@ -81,6 +81,7 @@ static uint32_t walk_lds() {
 constexpr uint32_t kThreads = 256;
 constexpr uint64_t kGroup = 8;  // blocks per fix lane
 constexpr int kMaxPasses = 512;  // fix passes before giving up to the serial path
+int g_max_passes = kMaxPasses;   // (capnp_resync_max_passes: tests drive the fallbacks)
 constexpr int kPassBatch = 8;    // fix passes enqueued per flag read-back
 constexpr uint64_t kShortChunk = 2 * kBlock;  // mean packed bytes per chunk below which
                                               // the batch goes straight to the batch unpack
@@ -129,7 +130,8 @@ struct Ws {
     uint64_t* words;       // [nbb]
     uint64_t* wbase;       // [nbb] exclusive scan of words
     int32_t* ok;           // [n]
-    int32_t* flags;        // [1] chunk failed, [2 + i] fix pass i changed an exit
+    int32_t* flags;        // [0] a tile hit the round cap, [1] chunk failed,
+                           // [2 + i] fix pass i changed an exit
     void* tmp;
     size_t tmp_bytes;
     // RESYNC_SEGUNITS: the resolved segments (kSegs per block) as decode units
@@ -345,10 +347,24 @@ struct SegState {
 // The prefix max runs over the whole tile: within the wave by shuffles,
 // across waves through LDS (wmax: each wave's maximum), two barriers a round;
 // the tile's rounds end together (wneed: whether a wave still has work).
-__device__ __forceinline__ void seg_rounds(const uint8_t* buf, SegState& S, bool valid,
+// Termination: lane i's entry is a function of the owned exits of lanes < i
+// only, and a lane's owned exit is a function of its entry.  So lane 0 (whose
+// entry is fixed) is settled after round 1, and by induction lane i after
+// round i + 1: the tile reaches its fixed point within kTileThreads + 1
+// rounds.  kMaxRounds caps the loop anyway; a tile that reaches the cap (which
+// the argument rules out) marks every segment with an error exit and returns
+// false, and the caller flags the resolution as unreliable (the batch then
+// takes the serial decode).
+constexpr uint32_t kMaxRounds = kTileThreads + 2;
+__device__ __forceinline__ bool seg_rounds(const uint8_t* buf, SegState& S, bool valid,
                                            uint32_t in_j, bool fixed_j, uint32_t lane,
                                            uint32_t wave, uint32_t* wmax, uint32_t* wneed) {
-    for (;;) {
+    for (uint32_t round = 0;; round++) {
+        if (round == kMaxRounds) {  // (uniform: every wave counts the same rounds)
+            S.ex = S.b + 1;
+            S.wd = 0;
+            return false;
+        }
         uint32_t v = S.own > in_j ? S.own : in_j;
         if (!valid) v = 0;
         uint32_t x = v;
@@ -369,7 +385,7 @@ __device__ __forceinline__ void seg_rounds(const uint8_t* buf, SegState& S, bool
         __syncthreads();
         uint32_t any = 0;
         for (uint32_t w2 = 0; w2 < kTileWaves; w2++) any |= wneed[w2];
-        if (!any) break;
+        if (!any) return true;
         if (!need) continue;
         S.used = ent;
         if (ent < S.ss) {
@@ -440,8 +456,18 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     const uint64_t kn = nb - k0 < kTileBlocks ? nb - k0 : kTileBlocks;
     uint64_t e0 = 0;  // the tile's entry (fix passes)
     if (fix) {
-        e0 = uniform64(__atomic_load_n(&exit[k0 - 1], __ATOMIC_RELAXED));
-        if (e0 == uniform64(entry[k0])) return;  // consistent
+        if (k0 == 0) return;  // (block 0 starts chunk 0: exact since the spec launch)
+        // One read of the predecessor's exit for the whole workgroup.  The
+        // predecessor tile may rewrite exit[k0 - 1] during this same pass; when
+        // each wave read it for itself, waves that read it before and after
+        // the write disagreed on returning here, and the waves left in
+        // seg_rounds polled round flags (wneed) that the returned waves never
+        // wrote -- the timing-dependent hang of two resync tests in round 3.
+        __shared__ uint64_t s_e0;
+        if (tid == 0) s_e0 = __atomic_load_n(&exit[k0 - 1], __ATOMIC_RELAXED);
+        __syncthreads();
+        e0 = uniform64(s_e0);
+        if (e0 == uniform64(entry[k0])) return;  // consistent (entry[k0] is this tile's own)
     }
     // c0 = the last chunk with bstart[c0] <= k0: a 64-way search (3 probes
     // deep for 10^5 chunks, where one lane's binary search was 17 dependent
@@ -553,7 +579,8 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     const bool tile_lane0 = wave == 0 && lane == 0;
     const bool fixed_j = cfirst || tile_lane0;
     const uint32_t in_j = cfirst ? S.ss : (tile_lane0 ? E0 : 0u);
-    seg_rounds(tbuf, S, valid, in_j, fixed_j, lane, wave, wmax, wneed);
+    if (!seg_rounds(tbuf, S, valid, in_j, fixed_j, lane, wave, wmax, wneed) && tid == 0)
+        flags[0] = 1;  // resolution unreliable: the caller decodes serially
     RTRACE(3);
     RTRACE(4);
     // blocks: entry of segment 0, exit of segment 3, words summed
@@ -780,11 +807,11 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
                                                        w.spec_words, w.exit, w.entry, w.words);
     int pass = 0;
     for (;;) {
-        if (pass >= kMaxPasses) {
+        if (pass >= g_max_passes) {
             *converged = false;
             break;
         }
-        for (int i = 0; i < kPassBatch; i++, pass++) {
+        for (int i = 0; i < kPassBatch && pass < g_max_passes; i++, pass++) {
             if (tile)
                 k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
                                                             w.entry, w.words, w.spec_exit, w.flags,
@@ -794,11 +821,17 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
                     d_in, in_off, n, w.bstart, w.spec_exit, w.spec_words, w.exit, w.entry,
                     w.words, w.flags, pass);
         }
-        int32_t last = 0;
+        int32_t last = 0, capped = 0;
         if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
             hipSuccess)
             return e;
+        if ((e = hipMemcpyAsync(&capped, w.flags, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+            return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (capped) {  // a tile hit the round cap (never, by seg_rounds' argument)
+            *converged = false;
+            break;
+        }
         if (!last) break;
     }
     *passes = pass;
@@ -808,6 +841,12 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
 }  // namespace
 
 extern "C" uint32_t capnp_resync_block_bytes(void) { return (uint32_t)kBlock; }
+
+extern "C" int capnp_resync_max_passes(int passes) {
+    const int old = g_max_passes;
+    g_max_passes = passes <= 0 ? kMaxPasses : (passes > kMaxPasses ? kMaxPasses : passes);
+    return old;
+}
 
 // RESYNC_PROF builds: the per-tile trace buffer (8 words per tile), or null.
 extern "C" int capnp_resync_trace(uint64_t* d_buf) {
@@ -1010,6 +1049,24 @@ __global__ void k_cut(const uint8_t* __restrict__ in, uint64_t nbytes, uint64_t 
     cut[0] = p;
     cut[1] = w;
     *cutk = k;
+}
+
+// The same prefix by one lane walking from the stream start: the fallback
+// when the resolution did not settle (fix passes past kMaxPasses, e.g. a
+// literal-run region longer than kMaxPasses tiles, which no speculative chain
+// couples with).
+__global__ void k_cut_serial(const uint8_t* __restrict__ in, uint64_t nbytes, uint64_t max_words,
+                             uint64_t* __restrict__ cut) {
+    uint64_t p = 0, w = 0;
+    while (p < nbytes) {
+        uint64_t q = p, dw = 0;
+        hop(in, q, dw, nbytes);
+        if (q > nbytes || w + dw > max_words) break;
+        p = q;
+        w += dw;
+    }
+    cut[0] = p;
+    cut[1] = w;
 }
 
 // Units after the cut's block are empty at the cut, so a decode of every
@@ -1471,7 +1528,22 @@ extern "C" hipError_t capnp_resync_decode_prefix(const uint8_t* d_in, uint64_t n
     int pass = 0;
     bool conv = true;
     if ((e = resolve(d_in, in_off, n, w, nbb, s, &pass, &conv)) != hipSuccess) return e;
-    if (!conv) return hipErrorNotReady;
+    if (!conv) {  // exact serial walk for the cut, one unit for the decode
+        k_cut_serial<<<1, 1, 0, s>>>(d_in, nbytes, max_words, cut);
+        uint64_t hc[2] = {0, 0};
+        if ((e = hipMemcpyAsync(hc, cut, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        *bytes = hc[0];
+        *words = hc[1];
+        if (!d_out || hc[1] == 0) return hipSuccess;
+        const uint64_t h_off[4] = {0, hc[0], 0, hc[1]};
+        if ((e = hipMemcpyAsync(in_off, h_off, 32, hipMemcpyHostToDevice, s)) != hipSuccess)
+            return e;
+        if ((e = capnp_launch_unpack(d_in, in_off, 1, 0, d_out, out_off, w.ok, nullptr, nullptr,
+                                     s)) != hipSuccess)
+            return e;
+        return hipStreamSynchronize(s);
+    }
     uint64_t nb = 0;
     if ((e = hipMemcpyAsync(&nb, w.bstart + n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;

@@ -115,6 +115,12 @@ void* capnp_ctx_stream(capnp_ctx* ctx);
 const char* capnp_ctx_last_error(capnp_ctx* ctx);
 /* Library / ABI version and the gfx target the kernels were built for. */
 const char* capnp_version(void);
+/* The ABI revision this header describes.  It changes whenever an exported
+   signature changes in place (round 3 inserted buf_len into
+   capnp_gpu_read_flat_messages under the same name); a binding checks
+   capnp_abi_version() == CAPNP_ABI_VERSION once, before any other call. */
+#define CAPNP_ABI_VERSION 4u
+uint32_t capnp_abi_version(void);
 /* Default ReaderOptions (message.rs:117-120). */
 capnp_reader_options capnp_default_reader_options(void);
 
@@ -304,13 +310,15 @@ capnp_status capnp_stream_unpack_batch(capnp_ctx* ctx, const uint8_t* packed,
    back to back into d_out, message m at d_msg_byte_off[m] (nmsg+1 entries,
    the last is the total): each is exactly the byte stream write_message
    produces (the segment table's word 0, the rest of the table, then every
-   segment, each packed by its own write_all).  total_segs and total_words
-   are the batch's segment count and segment words (host-side sizes).  The
+   segment, each packed by its own write_all).  total_segs is the batch's
+   segment count and total_words the words d_words holds (host-side sizes):
+   every d_seg_word_off entry must lie in [0, total_words].  The
    segments are packed in place with a gap before each message's first
    segment that then receives the packed table; a batch whose message offsets
    do not span [0, total_segs) goes through a staging copy instead.
    d_msg_seg_off must be non-decreasing and end at or before total_segs, and
-   d_seg_word_off non-decreasing: checked on the device first
+   d_seg_word_off non-decreasing and end at or before total_words: checked
+   on the device first, before any segment word is read
    (CAPNP_E_INVALID_ARGUMENT otherwise).  Synchronises the stream twice (the
    check; then to choose the path, or to size the staging pack); out_cap as
    in capnp_gpu_pack_batch. */

@@ -59,6 +59,13 @@ capnp_status capnp_resync_stats(capnp_ctx* ctx, int* passes, int* serial);
 /* Packed bytes per lane of the index-free decode. */
 uint32_t capnp_resync_block_bytes(void);
 
+/* Diagnostic: the fix passes the index-free decode runs before it gives up
+ * to its serial fallbacks (process-wide; 1 .. 512, 0 restores the default
+ * 512).  Returns the previous cap.  Lets the tests drive the non-converging
+ * paths (capnp_gpu_unpack_batch_resync's serial batch decode, the stream
+ * reader's serial whole-record cut) without a 16 MiB adversarial stream. */
+int capnp_resync_max_passes(int passes);
+
 /* Pre-sizes the context workspace for batches of up to max_chunks chunks so
  * that later calls allocate nothing (required before HIP graph capture). */
 capnp_status capnp_ctx_reserve(capnp_ctx* ctx, size_t max_chunks);

@@ -75,6 +75,15 @@ def lib():
         L.carsales_stream.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64,
                                       C.c_void_p, C.c_size_t]
         L.carsales_stream.restype = C.c_size_t
+        # oracle/refloop_oracle.c: the reference's own loop shapes (timing)
+        L.refloop_pack.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, szp]
+        L.refloop_read_exact.argtypes = [C.c_void_p, C.c_size_t, szp, C.c_void_p, C.c_size_t]
+        L.refloop_pack_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.refloop_unpack_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.refloop_write_messages_mt.argtypes = L.oracle_write_messages_mt.argtypes
+        L.refloop_read_messages_mt.argtypes = L.oracle_read_messages_mt.argtypes
         _lib = L
     return _lib
 
@@ -306,6 +315,103 @@ def messages_roundtrip_mt(words, msg_off, threads=1):
     ok = bool((st == 0).all())
     lib().oracle_read_messages_mt(out.ctypes.data, slot.ctypes.data, sizes.ctypes.data, n,
                                   body.ctypes.data, msg_off.ctypes.data, st.ctypes.data, threads)
+    t2 = time.perf_counter()
+    ok = ok and bool((st == 0).all()) and np.array_equal(body[:len(words)], words)
+    return t1 - t0, t2 - t1, int(sizes.sum()), ok
+
+
+# ---- the reference's loop shapes (oracle/refloop_oracle.c): the timed CPU
+# baseline.  Outputs are allocated and their pages mapped before the clock
+# starts; bytes are checked against the parity oracle by the caller.
+
+def refloop_pack(data):
+    a = _buf(data)
+    cap = lib().oracle_bound(len(a) // 8) + 16
+    out = np.zeros(cap, np.uint8)
+    n = C.c_size_t(0)
+    st = lib().refloop_pack(a.ctypes.data, len(a), out.ctypes.data, cap, C.byref(n))
+    return st, out[:n.value].tobytes()
+
+
+def refloop_read_exact(packed, out_len):
+    a = _buf(packed)
+    out = np.zeros(max(out_len, 1), np.uint8)
+    used = C.c_size_t(0)
+    st = lib().refloop_read_exact(a.ctypes.data if len(a) else None, len(a), C.byref(used),
+                                  out.ctypes.data, out_len)
+    return st, out[:out_len].tobytes(), used.value
+
+
+class RefloopBatch:
+    """Chunk-level pack + unpack of one batch on `threads` threads with the
+    reference's loops: each thread packs its contiguous chunk range into its
+    own output region (one independent write_all per chunk, as the
+    reference's callers do per segment), then reads every chunk back with
+    read_exact.  All buffers are allocated and mapped here, outside any timed
+    region; pack() and unpack() are what the caller times."""
+
+    def __init__(self, words, offs, threads):
+        self.words = np.ascontiguousarray(words, np.uint64)
+        self.offs = np.ascontiguousarray(offs, np.uint64)
+        self.n = len(self.offs) - 1
+        self.threads = max(1, int(threads))
+        t = self.threads
+        cuts = [self.n * i // t for i in range(t + 1)]
+        w = self.offs[cuts].astype(np.int64)
+        nw = np.diff(w)
+        nc = np.diff(np.array(cuts, np.int64))
+        bound = 8 * nw + (nw + 1) // 2 + 2 * nc + 64  # >= the sum of the chunks' bounds
+        self.region = np.concatenate([[0], np.cumsum(bound)]).astype(np.uint64)
+        self.out = np.ones(int(self.region[-1]) + 16, np.uint8)  # (ones: pages mapped)
+        self.pos = np.ones(self.n, np.uint64)
+        self.size = np.ones(self.n, np.uint64)
+        self.back = np.ones(max(int(self.offs[-1]), 1), np.uint64)
+        self.status = np.ones(self.n, np.int32)
+
+    def pack(self):
+        return lib().refloop_pack_batch(self.words.ctypes.data, self.offs.ctypes.data, self.n,
+                                        self.out.ctypes.data, self.region.ctypes.data,
+                                        self.pos.ctypes.data, self.size.ctypes.data,
+                                        self.threads)
+
+    def unpack(self):
+        return lib().refloop_unpack_batch(self.out.ctypes.data, self.pos.ctypes.data,
+                                          self.size.ctypes.data, self.n, self.back.ctypes.data,
+                                          self.offs.ctypes.data, self.status.ctypes.data,
+                                          self.threads)
+
+    def packed_stream(self):
+        """The chunks' packed bytes concatenated in chunk order (the stream
+        successive write_all calls produce) and its byte offsets."""
+        parts = [self.out[int(p):int(p) + int(s)] for p, s in zip(self.pos, self.size)]
+        stream = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+        offs = np.concatenate([[0], np.cumsum(self.size)]).astype(np.uint64)
+        return stream, offs
+
+
+def refloop_messages_roundtrip_mt(words, msg_off, threads=1):
+    """messages_roundtrip_mt with the reference's loops (write_message +
+    read_message of one-segment messages, read_message zeroing the body as
+    allocate_zeroed_vec does) -> (seconds write, seconds read, packed bytes,
+    ok)."""
+    import time
+    words = np.ascontiguousarray(words, np.uint64)
+    msg_off = np.ascontiguousarray(msg_off, np.uint64)
+    n = len(msg_off) - 1
+    lens = np.diff(msg_off).astype(np.int64)
+    slot = np.zeros(n + 1, np.uint64)
+    slot[1:] = np.cumsum(8 * lens + (lens + 1) // 2 + 48)
+    out = np.ones(int(slot[-1]) + 16, np.uint8)
+    sizes = np.zeros(n, np.uint64)
+    st = np.ones(n, np.int32)
+    body = np.ones(max(int(msg_off[-1]), 1), np.uint64)
+    t0 = time.perf_counter()
+    lib().refloop_write_messages_mt(words.ctypes.data, msg_off.ctypes.data, n, out.ctypes.data,
+                                    slot.ctypes.data, sizes.ctypes.data, st.ctypes.data, threads)
+    t1 = time.perf_counter()
+    ok = bool((st == 0).all())
+    lib().refloop_read_messages_mt(out.ctypes.data, slot.ctypes.data, sizes.ctypes.data, n,
+                                   body.ctypes.data, msg_off.ctypes.data, st.ctypes.data, threads)
     t2 = time.perf_counter()
     ok = ok and bool((st == 0).all()) and np.array_equal(body[:len(words)], words)
     return t1 - t0, t2 - t1, int(sizes.sum()), ok

@@ -103,3 +103,36 @@ def test_tile_resolution_malformed_chunks():
         assert not (good and rst[c] != 0), c
         passed += good
     assert passed > 50 and (rst != 0).sum() > 20
+
+
+def test_tile_rounds_bounded():
+    """seg_rounds' termination argument (csrc/resync.hip): lane i's entry
+    depends only on the owned exits of lanes < i, so lane i is settled after
+    round i + 1 and a tile needs at most lanes + 1 rounds (the kernel caps
+    them at kTileThreads + 2 and sends a capped tile to the serial decode).
+    Checked on garbage byte streams, literal regions and malformed chunks,
+    where the spec chains couple least."""
+    rng = np.random.default_rng(11)
+    T, segs = 16, 4
+    worst = 0
+    for trial in range(12):
+        n = int(rng.integers(2000, 9000))
+        if trial % 3 == 0:  # random bytes: no record structure at all
+            B = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        elif trial % 3 == 1:  # 0xFF-heavy garbage: long fake literal runs
+            b = rng.integers(0, 256, n, dtype=np.uint8)
+            b[rng.random(n) < 0.3] = 0xFF
+            B = b.tobytes()
+        else:  # a real literal region with corrupted bytes
+            lit = rng.integers(1 << 56, 1 << 63, n // 8, dtype=np.uint64) * 2 + 1
+            st, k = O.pack(lit.tobytes())
+            k = bytearray(k)
+            for i in rng.integers(0, len(k), 20):
+                k[int(i)] = int(rng.integers(0, 256))
+            B = bytes(k)
+        cut = sorted(set(int(x) for x in rng.integers(1, len(B), 5)))
+        in_off = [0] + cut + [len(B)]
+        _, _, _, rounds = E.resolve(B + bytes(4096), in_off, blk=128, T=T, segs=segs)
+        assert rounds <= T * segs + 1, (trial, rounds)
+        worst = max(worst, rounds)
+    assert worst >= 2

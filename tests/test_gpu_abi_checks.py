@@ -149,6 +149,13 @@ def test_messages_checked(env):
     dm = _dev(torch, [0, 1, 3], np.int64)
     assert L.capnp_gpu_write_messages(ctx.handle, _p(w), _p(swo_bad), _p(dm), 2, 3, 30, _p(out),
                                       out.numel(), _p(mbo), s) == BAD
+    # segment offsets past the words d_words holds (total_words): rejected
+    # before any segment is read
+    swo_past = _dev(torch, [0, 10, 20, 4000], np.int64)
+    assert L.capnp_gpu_write_messages(ctx.handle, _p(w), _p(swo_past), _p(dm), 2, 3, 30,
+                                      _p(out), out.numel(), _p(mbo), s) == BAD
+    assert L.capnp_gpu_write_messages(ctx.handle, _p(w), _p(swo), _p(dm), 2, 3, 29, _p(out),
+                                      out.numel(), _p(mbo), s) == BAD
     assert L.capnp_gpu_write_messages(ctx.handle, _p(w), _p(swo), _p(dm), 2, 3, 30, _p(out),
                                       out.numel(), _p(mbo), s) == 0
     torch.cuda.synchronize()

@@ -132,7 +132,9 @@ def test_many_tiny_messages(ctx):
 
 
 def test_small_discovery_rounds(ctx):
-    """The same loop with a cap of 3 messages per discovery round."""
+    """The same loop with a cap of 3 messages per pass: ~14 passes, each
+    decoding the stream again from the message after the previous pass's
+    last (read_message_stream honours max_msgs)."""
     import torch
     rng = random.Random(12)
     stream = _stream(rng, 40)
@@ -141,6 +143,10 @@ def test_small_discovery_rounds(ctx):
     got, end = ctx.read_message_stream(dev, max_msgs=3)
     assert end == ref_end and len(got) == len(ref)
     assert [u for _, u in got] == [u for _, u in ref]
+    for (gs, _), (rs, _) in zip(got, ref):
+        assert len(gs) == len(rs)
+        for g, r in zip(gs, rs):
+            assert np.array_equal(g.cpu().numpy().view(np.uint64), r)
 
 
 def test_zero_heavy_stream(ctx):
