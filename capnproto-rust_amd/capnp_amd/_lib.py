@@ -49,6 +49,7 @@ EXPORTS = [
     "capnp_packed_reader_read_message", "capnp_packed_reader_buffered",
     "capnp_gpu_find_messages",
     "capnp_gpu_read_message_stream", "capnp_abi_version", "capnp_resync_max_passes",
+    "capnp_unpack_prefix",
 ]
 ABI_VERSION = 4  # include/capnp_packed.h CAPNP_ABI_VERSION
 
@@ -129,6 +130,8 @@ def lib():
     L.capnp_unpack_tile_words.restype = C.c_uint32
     L.capnp_pack.argtypes = [vp, vp, sz, vp, sz, C.POINTER(C.c_size_t)]
     L.capnp_unpack.argtypes = [vp, vp, sz, C.POINTER(C.c_size_t), vp, sz]
+    L.capnp_unpack_prefix.argtypes = [vp, vp, sz, u64, vp, C.POINTER(C.c_size_t),
+                                      C.POINTER(C.c_uint64)]
     L.capnp_pack_batch_host.argtypes = [vp, vp, vp, sz, vp, sz, vp]
     L.capnp_unpack_batch_host.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp]
     L.capnp_stream_pack_batch.argtypes = [vp, vp, vp, sz, vp, sz, vp, sz]

@@ -15,11 +15,12 @@ Same names, argument meaning and error behaviour as the reference:
 `BufReader` over any raw reader, whose fill_buf() hands out one buffer at a
 time and refills after consume() — as PackedRead's refresh_buffer!
 (serialize_packed.rs:59-74) does, a read unit that runs past the current
-buffer consumes it and continues in the next one.  A successful read
-consumes exactly the bytes the message used, so a stream of messages is
-read by calling try_read_message until it returns None; a failed one leaves
-the reader where the reference leaves it (every buffer it had to look past
-consumed).  Errors raise CapnpError whose `.kind` is the capnp::ErrorKind
+buffer consumes it and continues in the next one (_read_unit: each buffer is
+decoded once; only an incomplete record is carried to the next).  A
+successful read consumes exactly the bytes the message used, so a stream of
+messages is read by calling try_read_message until it returns None; a
+failed one leaves the reader where the reference leaves it (every buffer it
+had to look past consumed).  Errors raise CapnpError whose `.kind` is the capnp::ErrorKind
 name.  Every transform runs in the HIP kernels; nothing here touches bytes.
 """
 import ctypes as C
@@ -72,102 +73,91 @@ class SliceRead:
 class BufReader:
     """std::io::BufReader over a raw reader (`.read(n) -> bytes`, b"" at the
     end): fill_buf() returns the current buffer of up to `capacity` bytes,
-    reading the next one only once it is consumed.  `unread(bufs)` puts
-    whole buffers back in front (in order), so _refilling can look ahead and
-    still leave the reader exactly where the reference's PackedRead would."""
+    reading the next one only once it is consumed."""
 
     def __init__(self, raw, capacity=8192):
         self.raw = raw
         self.capacity = capacity
         self.buf = b""
         self.pos = 0
-        self.back = []  # buffers put back by unread, next first
 
     def fill_buf(self):
         if self.pos >= len(self.buf):
-            self.buf = self.back.pop() if self.back else bytes(self.raw.read(self.capacity))
+            self.buf = bytes(self.raw.read(self.capacity))
             self.pos = 0
         return memoryview(self.buf)[self.pos:]
 
     def consume(self, n):
         self.pos = min(self.pos + n, len(self.buf))
 
-    def unread(self, bufs):
-        """Puts `bufs` back; the current buffer's unconsumed rest follows them."""
-        rest = self.buf[self.pos:]
-        if rest:
-            self.back.append(rest)
-        self.back.extend(reversed([b for b in bufs if b]))
-        self.buf, self.pos = b"", 0
-
 
 # statuses that mean "the unit ran past the bytes in hand"
 _NEEDS_MORE = (2, 4, 5)  # PrematureEndOfPackedInput, FailedToFill, PrematureEndOfFile
+_EMPTY = -1              # _read_unit: read() found the input empty at entry (Ok(0))
 
 
-def _refilling(r, attempt):
-    """Runs attempt(data) on the reader's current buffer; while it fails for
-    lack of input and the reader has more, consumes that buffer (the
-    reference's refresh_buffer!, serialize_packed.rs:59-74) and retries over
-    everything seen so far.  On success consumes exactly the bytes used:
-    `attempt` returns (status, used, result).
+def _unpack(ctx, data, out):
+    """capnp_unpack: PackedRead::read_exact of len(out) bytes (a np.uint8
+    view) from the slice `data` -> (status, consumed)."""
+    a = _np_u8(data)
+    used = C.c_size_t(0)
+    st = _lib.lib().capnp_unpack(ctx.handle, a.ctypes.data, len(data), C.byref(used),
+                                 out.ctypes.data if len(out) else None, len(out))
+    return st, used.value
 
-    The reference streams, so the result is the outcome at the first buffer
-    boundary where the unit stops needing input.  Retrying at every boundary
-    re-decodes everything seen each time (O(k^2) for a unit spanning k
-    buffers); with a reader that can put buffers back (`unread`) the retries
-    happen only once the bytes in hand have doubled, and the first boundary
-    whose outcome is final is then found by bisection over the buffers taken
-    since the last retry (a decode is left to right, so once the outcome over
-    a prefix is final it is the same over every longer prefix); the buffers
-    past that boundary are put back."""
-    bufs = []           # buffers taken so far; all consumed but maybe the last
-    plen = [0]          # plen[j] = bytes in bufs[:j]
-    lookahead = hasattr(r, "unread")
-    tried = 0           # the outcome over bufs[:tried] is known to need more
-    last = None
+
+def _prefix(ctx, data, max_words, out):
+    """capnp_unpack_prefix: the whole records of `data` decoding to at most
+    max_words words, decoded into `out` -> (bytes, words)."""
+    a = _np_u8(data)
+    nb, nw = C.c_size_t(0), C.c_uint64(0)
+    _check(_lib.lib().capnp_unpack_prefix(ctx.handle, a.ctypes.data, len(data), max_words,
+                                          out.ctypes.data, C.byref(nb), C.byref(nw)), ctx)
+    return nb.value, nw.value
+
+
+def _read_unit(r, ctx, out, exact):
+    """One PackedRead::read (exact False) or read_exact (exact True) of
+    len(out) bytes into `out` (np.uint8, a word multiple) from the BufRead
+    `r`, streaming over its buffers as the reference does
+    (serialize_packed.rs:80-228; refresh_buffer!, :59-74: a unit that runs
+    past the current buffer consumes it and continues in the next).
+
+    Each buffer is decoded once: the input in hand is the current buffer
+    plus `tail`, the bytes of the one record the previous buffer ended in.
+    If the unit completes, exactly the bytes it used are consumed.  If it
+    fails for a reason the bytes in hand already decide (a run past the
+    unit's end), the current buffer stays unconsumed, as in the reference.
+    If it needs more input, its whole records are final (the decode is left
+    to right), so they are kept in `out`, only the incomplete record is
+    carried, and the buffer is consumed.  At the end of the input the
+    failure over what was seen stands.  Returns the status, or _EMPTY for a
+    read() at an empty input (Ok(0), :96-98)."""
+    n = len(out)
+    if n == 0:
+        return _lib.OK
+    tail, done, first = b"", 0, True
     while True:
         cur = bytes(r.fill_buf())
-        if not cur:  # the reader has nothing more (or was empty at entry)
-            if not bufs:
-                st, used, res = attempt(b"")
-                return st, res
-            if len(bufs) == tried:
-                return last  # the failure stands over all the bytes seen, all consumed
-            j, cur_taken = len(bufs), True
-            st, used, res = attempt(b"".join(bufs))
-            if st in _NEEDS_MORE:
-                return st, res
-            break
-        bufs.append(cur)
-        plen.append(plen[-1] + len(cur))
-        j = len(bufs)
-        if lookahead and tried and plen[j] < 2 * plen[tried]:
-            r.consume(len(cur))  # not worth a retry yet: take the next buffer too
-            continue
-        st, used, res = attempt(b"".join(bufs))
-        if st in _NEEDS_MORE:
-            r.consume(len(cur))
-            tried, last = j, (st, res)
-            continue
-        cur_taken = False
-        break
-    # the outcome over bufs[:j] is final; the reference stopped at the first
-    # such boundary in (tried, j], with that boundary's buffer current
-    lo, hi = tried, j
-    while hi - lo > 1:
-        mid = (lo + hi) // 2
-        s2, u2, r2 = attempt(b"".join(bufs[:mid]))
-        if s2 in _NEEDS_MORE:
-            lo = mid
-        else:
-            hi, st, used, res = mid, s2, u2, r2
-    if cur_taken or hi < j:
-        r.unread(bufs[hi - 1:j] if cur_taken else bufs[hi - 1:j - 1])
-        r.fill_buf()
-    if st == _lib.OK:
-        r.consume(used - plen[hi - 1])
-    return st, res
+        if not cur:
+            if first:  # read() of an empty input is Ok(0); read_exact fails (io.rs:26-28)
+                return 4 if exact else _EMPTY
+            if not tail:  # the next record's tag: refresh_buffer! finds nothing (:59-74)
+                return 2
+            st, _ = _unpack(ctx, tail, out[done:])  # the record cut short stands
+            return st
+        first = False
+        data = tail + cur if tail else cur
+        st, used = _unpack(ctx, data, out[done:])
+        if st == _lib.OK:
+            r.consume(used - len(tail))
+            return st
+        if st not in _NEEDS_MORE:
+            return st
+        nb, nw = _prefix(ctx, data, (n - done) // 8, out[done:].view(np.uint64))
+        done += 8 * nw
+        tail = data[nb:]
+        r.consume(len(cur))
 
 
 class OwnedSegments:
@@ -258,15 +248,7 @@ class PackedRead:
 
     def _read_exact(self, n):
         out = np.empty(n, np.uint8)
-
-        def attempt(data):
-            used = C.c_size_t(0)
-            a = _np_u8(data)
-            st = _lib.lib().capnp_unpack(self.ctx.handle, a.ctypes.data, len(data),
-                                         C.byref(used), out.ctypes.data, n)
-            return st, used.value, None
-
-        st, _ = _refilling(self.inner, attempt)
+        st = _read_unit(self.inner, self.ctx, out, exact=True)
         _check(st, self.ctx)
         return out.tobytes()
 
@@ -314,10 +296,32 @@ def write_message(write, segments, ctx=None):
     _write(write, out[:n.value].tobytes())
 
 
+def _fast(r, attempt):
+    """The message within the reader's current buffer, in one device call:
+    (status, result) when it is there whole (or the input is at a clean
+    end), else None, and the caller reads the message unit by unit
+    (nothing has been consumed): a message past the buffer, and every
+    failure, whose stream position then comes out as the reference leaves
+    it (the units before the failing one consumed)."""
+    cur = bytes(r.fill_buf())
+    st, used, res = attempt(cur)
+    if st == _lib.OK:
+        r.consume(used)
+        return st, res
+    if st == _lib.NONE:
+        return st, res
+    return None
+
+
+def _u32(b, i):
+    return int.from_bytes(bytes(b[i:i + 4]), "little")
+
+
 def _read(read, options, try_mode, ctx):
     ctx = ctx or default_context()
     r = _as_reader(read)
-    opts = (options or DEFAULT_READER_OPTIONS)._c()
+    options = options or DEFAULT_READER_OPTIONS
+    opts = options._c()
 
     def attempt(data):
         a = _np_u8(data)
@@ -335,15 +339,39 @@ def _read(read, options, try_mode, ctx):
                 if need > cap:
                     cap = need
                     continue
-            return st, used.value, (body, segs, nseg.value)
+            return st, used.value, (body, segs[:nseg.value])
 
-    st, res = _refilling(r, attempt)
-    if st == _lib.NONE:
-        return None
+    fast = _fast(r, attempt)
+    if fast is not None:
+        st, res = fast
+        if st == _lib.NONE:
+            return None
+        _check(st, ctx)
+        body, segs = res
+        return OwnedSegments(body[:int(segs.astype(np.uint64).sum())], segs)
+    # read_segment_table + read_segments unit by unit (serialize.rs:448-524)
+    w0 = np.empty(8, np.uint8)
+    st = _read_unit(r, ctx, w0, exact=False)
+    if st == _EMPTY:  # :456-462
+        if try_mode:
+            return None
+        raise CapnpError(5, "PrematureEndOfFile")
     _check(st, ctx)
-    body, segs, nseg = res
-    total = int(segs[:nseg].astype(np.uint64).sum())
-    return OwnedSegments(body[:total], segs[:nseg])
+    nseg = (_u32(w0, 0) + 1) & 0xFFFFFFFF
+    if nseg == 0 or nseg >= SEGMENTS_COUNT_LIMIT:  # :467-473
+        raise CapnpError(6)
+    lens = [_u32(w0, 4)]
+    if nseg > 1:  # :476-496
+        t = np.empty(8 if nseg < 4 else (nseg & ~1) * 4, np.uint8)
+        _check(_read_unit(r, ctx, t, exact=True), ctx)
+        lens += [_u32(t, 4 * i) for i in range(nseg - 1)]
+    total = sum(lens)
+    limit = options.traversal_limit_in_words
+    if limit is not None and total > limit:  # :501-507
+        raise CapnpError(8)
+    body = np.empty(max(total, 1), np.uint64)
+    _check(_read_unit(r, ctx, body.view(np.uint8)[:8 * total], exact=True), ctx)  # :514-524
+    return OwnedSegments(body[:total], np.array(lens, np.uint32))
 
 
 def read_message(read, options=None, ctx=None):
@@ -363,7 +391,8 @@ def _read_no_alloc(read, buffer, options, try_mode, ctx):
     nb = np.frombuffer(buffer, dtype=np.uint8) if not isinstance(buffer, np.ndarray) else \
         buffer.view(np.uint8)
     nseg, tb, bb = C.c_uint32(0), C.c_size_t(0), C.c_size_t(0)
-    opts = (options or DEFAULT_READER_OPTIONS)._c()
+    options = options or DEFAULT_READER_OPTIONS
+    opts = options._c()
 
     def attempt(data):
         a = _np_u8(data)
@@ -373,16 +402,53 @@ def _read_no_alloc(read, buffer, options, try_mode, ctx):
             nb.nbytes, C.byref(nseg), C.byref(tb), C.byref(bb), C.byref(used))
         return st, used.value, None
 
-    st, _ = _refilling(r, attempt)
-    if st == _lib.NONE:
-        return None
+    def result(table_bytes, body_bytes, n):
+        t = nb[:table_bytes].view(np.uint32)
+        return OwnedSegments(nb[table_bytes:table_bytes + body_bytes].view(np.uint64),
+                             [int(t[1 + i]) for i in range(n)])
+
+    fast = _fast(r, attempt)
+    if fast is not None:
+        st, _ = fast
+        if st == _lib.NONE:
+            return None
+        _check(st, ctx)
+        return result(tb.value, bb.value, nseg.value)
+    # serialize.rs:333-420 unit by unit: read(8), the table rest 8 bytes at
+    # a time into the buffer (:371-395), then the body after the table
+    if nb.ctypes.data % 8:  # :341-343
+        raise CapnpError(10)
+    if nb.nbytes < 8:  # :345-347
+        raise CapnpError(9)
+    st = _read_unit(r, ctx, nb[:8], exact=False)
+    if st == _EMPTY:
+        if try_mode:
+            return None
+        raise CapnpError(5, "PrematureEndOfFile")
     _check(st, ctx)
-    body = nb[tb.value:tb.value + bb.value].view(np.uint64)
-    lens = []
-    t = nb[:tb.value].view(np.uint32)
-    for i in range(nseg.value):
-        lens.append(int(t[1 + i]))
-    return OwnedSegments(body, lens)
+    n = (_u32(nb, 0) + 1) & 0xFFFFFFFF
+    if n == 0 or n >= SEGMENTS_COUNT_LIMIT:
+        raise CapnpError(6)
+    total = _u32(nb, 4)
+    got = 1
+    while got < n:
+        start = (got + 1) * 4
+        if nb.nbytes < start + 8:  # :374-376
+            raise CapnpError(9)
+        _check(_read_unit(r, ctx, nb[start:start + 8], exact=True), ctx)
+        total += _u32(nb, start)
+        got += 1
+        if got < n:
+            total += _u32(nb, start + 4)
+        got += 1
+    limit = options.traversal_limit_in_words
+    if limit is not None and total > limit:
+        raise CapnpError(8)
+    start = (got + 1) * 4
+    if nb.nbytes < start + 8 * total:  # :407-409
+        raise CapnpError(9)
+    _check(_read_unit(r, ctx, nb[start:start + 8 * total], exact=True), ctx)
+    return result(start, 8 * total, n)
 
 
 def read_message_no_alloc(read, buffer, options=None, ctx=None):

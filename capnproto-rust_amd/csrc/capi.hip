@@ -121,6 +121,8 @@ size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
 }  // namespace
 
 constexpr size_t kTablePrefixBytes = 4096;  // >= 10 bytes x (1 + 256) table words
+// message bodies of at least this many words decode in parallel (read_body)
+constexpr uint64_t kParallelBodyWords = 4096;
 
 struct capnp_ctx {
     int device = 0;
@@ -1301,30 +1303,40 @@ capnp_status capnp_stream_complete_prefix(capnp_ctx* ctx, const uint8_t* host, s
 }
 
 // ... and decoded: the longest prefix of complete records of n host bytes
-// with at most max_words words, its words into out[0, *words) (host).
+// with at most max_words words, its words into out[0, *words) (host; NULL:
+// the lengths only).
 capnp_status capnp_stream_decode_prefix(capnp_ctx* ctx, const uint8_t* host, size_t n,
                                         uint64_t max_words, uint64_t* out, uint64_t* bytes,
                                         uint64_t* words) {
-    if (!ctx || !bytes || !words || (n && !host) || (max_words && !out))
-        return CAPNP_E_INVALID_ARGUMENT;
+    if (!ctx || !bytes || !words || (n && !host)) return CAPNP_E_INVALID_ARGUMENT;
     *bytes = *words = 0;
     if (n == 0 || max_words == 0) return CAPNP_OK;
     const size_t o_out = round16(n) + 64;
-    capnp_status st = ensure_stage(ctx, o_out + max_words * 8 + 16);
+    capnp_status st = ensure_stage(ctx, o_out + (out ? max_words * 8 : 0) + 16);
     if (st != CAPNP_OK) return st;
     const size_t ws = capnp_resync_ws_bytes(1, n) + 4096;
     st = ensure_buf(ctx, &ctx->d_resync, &ctx->resync_cap, ws);
     if (st != CAPNP_OK) return st;
     hipStream_t s = ctx->stream;
-    uint64_t* d_out = reinterpret_cast<uint64_t*>(ctx->d_stage + o_out);
+    uint64_t* d_out = out ? reinterpret_cast<uint64_t*>(ctx->d_stage + o_out) : nullptr;
     HIP_TRY(hipMemcpyAsync(ctx->d_stage, host, n, hipMemcpyHostToDevice, s));
     HIP_TRY(capnp_resync_decode_prefix(ctx->d_stage, n, max_words, d_out, ctx->d_resync,
                                        ctx->resync_cap, s, bytes, words));
-    if (*words) {
+    if (out && *words) {
         HIP_TRY(hipMemcpyAsync(out, d_out, *words * 8, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
     }
     return CAPNP_OK;
+}
+
+capnp_status capnp_unpack_prefix(capnp_ctx* ctx, const uint8_t* in, size_t in_len,
+                                 uint64_t max_words, uint64_t* out, size_t* bytes,
+                                 uint64_t* words) {
+    if (!bytes || !words) return CAPNP_E_INVALID_ARGUMENT;
+    uint64_t b = 0;
+    capnp_status st = capnp_stream_decode_prefix(ctx, in, in_len, max_words, out, &b, words);
+    *bytes = (size_t)b;
+    return st;
 }
 
 capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf, size_t buf_len,
@@ -1455,6 +1467,27 @@ static capnp_status read_body(capnp_ctx* ctx, const FrameResult& fr, const uint8
     const uint64_t offs[4] = {0, take, 0, fr.total_words};
     if (take) HIP_TRY(hipMemcpyAsync(di + o_in, in + fr.table_consumed, take,
                                      hipMemcpyHostToDevice, s));
+    if (fr.total_words >= kParallelBodyWords && take) {
+        // A long body decodes in parallel: the whole records of the staged
+        // bytes up to the body's words, resolved block by block
+        // (capnp_resync_decode_prefix) instead of one lane walking the unit.
+        // If they fill the body exactly, that is the read: read_exact stops
+        // right after the record that fills its buffer
+        // (serialize_packed.rs:222-225).  Otherwise the read fails, and the
+        // exact unit decode below gives its status.
+        st = ensure_buf(ctx, &ctx->d_resync, &ctx->resync_cap, capnp_resync_ws_bytes(1, take) + 4096);
+        if (st != CAPNP_OK) return st;
+        uint64_t pb = 0, pw = 0;
+        HIP_TRY(capnp_resync_decode_prefix(di + o_in, take, fr.total_words,
+                                           reinterpret_cast<uint64_t*>(d), ctx->d_resync,
+                                           ctx->resync_cap, s, &pb, &pw));
+        if (pw == fr.total_words) {
+            HIP_TRY(hipMemcpyAsync(host_out, d, fr.total_words * 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            *body_consumed = pb;
+            return CAPNP_OK;
+        }
+    }
     HIP_TRY(hipMemcpyAsync(di + o_off, offs, sizeof(offs), hipMemcpyHostToDevice, s));
     HIP_TRY(capnp_launch_unpack(di + o_in, reinterpret_cast<uint64_t*>(di + o_off), 1, 0,
                                 reinterpret_cast<uint64_t*>(d),

@@ -42,13 +42,7 @@
 #include <stdlib.h>
 #include "../../include/capnp_packed.h"
 
-#ifndef PACK_EMIT_SKIP0
-#define PACK_EMIT_SKIP0 1  // emit: no LDS OR of zero dwords (0: every lane ORs four dwords)
-#endif
 
-#ifndef PACK_ABLATE
-#define PACK_ABLATE 0  // diagnostic builds only (scripts/ablate.py); 0 = product
-#endif
 
 #ifndef PACK_PROF
 #define PACK_PROF 0  // look-back counters (scripts/pack_prof.py); 0 = product
@@ -73,25 +67,16 @@ __device__ uint64_t* g_trace;
 
 namespace {
 
-#ifndef PACK_WAVES
-#define PACK_WAVES 4  // waves per workgroup (tile = PACK_WAVES x kStageSteps x 64 words)
-#endif
-constexpr int kWaves = PACK_WAVES;
+constexpr int kWaves = 4;  // waves per workgroup (tile = kWaves x kStageSteps x 64 words)
 constexpr int kThreads = kWaves * CAPNP_WAVE;
-#ifndef PACK_RING
-#define PACK_RING 4096
-#endif
-constexpr uint32_t kRing = PACK_RING;      // streaming path: per-wave ring (bytes)
+constexpr uint32_t kRing = 4096;           // streaming path: per-wave ring (bytes)
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr int kMaxTileChunks = 64;
 constexpr uint32_t kZeroAhead = 1024;      // ring bytes zeroed per refill
 constexpr uint32_t kStepMax = 64 * 10 + 16;
 
 // Staged path capacity: kStageSteps steps of 64 words per wave.
-#ifndef PACK_STAGE_STEPS
-#define PACK_STAGE_STEPS 8
-#endif
-constexpr uint32_t kStageSteps = PACK_STAGE_STEPS;
+constexpr uint32_t kStageSteps = 8;
 constexpr uint32_t kStageWords = 64 * kStageSteps;
 // >= the packed bytes of a wave's range: at most 8.5 bytes per word (a 0xFF
 // head of 10 bytes needs a word of <= 7 bytes before the next one) plus 1.5
@@ -110,10 +95,7 @@ constexpr uint32_t kRegion = (kStageBytesMax + kGapSlack + 32 + 15) & ~15u;
 // smaller regions and the 8-byte selector entries fit 8 workgroups per CU
 // (20.3 KB each) where the worst-case layout fit 6 (23.8 KB): 608 -> 570 us
 // at config 2 in a trial build.
-#ifndef PACK_STAGE_BYTES
-#define PACK_STAGE_BYTES 4192
-#endif
-constexpr uint32_t kStageBytes = PACK_STAGE_BYTES;
+constexpr uint32_t kStageBytes = 4192;
 static_assert(kStageBytes <= kStageBytesMax && kStageBytes % 16 == 0, "stage capacity");
 constexpr uint32_t kStageRegion = (kStageBytes + 32 + 15) & ~15u;
 // per-wave LDS region of the chunk tiles: the staged bytes, or the
@@ -521,7 +503,7 @@ struct StageState {
     pk.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
 }
 
-// size_step with less scalar work (PACK_LEAN_STEP, the default).  The
+// size_step with less scalar work.  The
 // scalar unit (one per CU, shared by the four SIMDs) was the pack kernel's
 // busiest pipe: ~95 SALU ops per 64-word step in pass 1, and one more SALU op
 // per step cost ~2.1 us per launch against ~1.0 us for one more VALU op
@@ -572,9 +554,6 @@ __device__ __forceinline__ void size_step_lean(StageState& pk, uint64_t w, uint3
     pk.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
 }
 
-#ifndef PACK_LEAN_STEP
-#define PACK_LEAN_STEP 1  // 0: size_step (mask tests in scalar code, per-step LDS bookkeeping)
-#endif
 
 // Pass 2 of one staged step.  With `tab` (record sync index), every head
 // lane also writes the entries of the sync points its record covers: words
@@ -619,18 +598,10 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
     // and lanes past the step's words would otherwise all OR into the next
     // record's dword, same-address LDS atomics that serialise; long zero runs
     // made that the larger part of the emit)
-#if PACK_EMIT_SKIP0
     if (e0) __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     if (e1) __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     if (e2) __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     if (e3) __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#else
-    __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#endif
-#if PACK_ABLATE != 5
     if constexpr (SYNC) {
         // sync points m = hw + d, d = (t0 - hw) mod kSyncWords, d <= cnt, of
         // the record headed at word hw = g + lane; m - t0 is a multiple of
@@ -654,7 +625,6 @@ __device__ __forceinline__ void emit_step(uint64_t w, const StepInfo& si, uint32
             }
         }
     }
-#endif
 }
 
 // Copies region bytes [0, len) to out[D0 .. D0+len) (16-aligned coordinates),
@@ -1164,17 +1134,10 @@ __device__ uint64_t tile_aggregate(const LookbackArgs& A, uint64_t j, uint32_t l
 // Every wait is bounded: on timeout the waiter computes the missing aggregate
 // itself from the input (records are idempotent), so the kernel finishes with
 // the right answer under any workgroup dispatch order.
-#ifndef PACK_GROUP
-#define PACK_GROUP 64  // tiles per look-back group (<= 64: one lane per tile)
-#endif
-constexpr uint32_t kGroup = PACK_GROUP;
-#ifndef PACK_SLEEP
-#define PACK_SLEEP 2  // s_sleep between look-back polls (x 64 cycles)
-#endif
-#ifndef PACK_GWIN
-#define PACK_GWIN 16  // measured: 64 -> 564 us, 16 -> 552, 4 -> 555, 1 -> 603
-#endif
-constexpr uint32_t kGroupWindow = PACK_GWIN;  // group records per poll
+constexpr uint32_t kGroup = 64;  // tiles per look-back group (<= 64: one lane per tile)
+constexpr int kSleep = 2;        // s_sleep between look-back polls (x 64 cycles)
+// group records per poll; measured: 64 -> 564 us, 16 -> 552, 4 -> 555, 1 -> 603
+constexpr uint32_t kGroupWindow = 16;
 constexpr uint32_t kSpinLimit = 4096;
 
 __device__ uint64_t group_aggregate(const LookbackArgs& A, uint64_t g, uint32_t lane) {
@@ -1199,17 +1162,12 @@ __device__ uint64_t group_aggregate(const LookbackArgs& A, uint64_t g, uint32_t 
 // Wave 0: publishes tile t's aggregate.
 __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint64_t agg,
                                         uint32_t lane) {
-#if PACK_ABLATE != 1 && PACK_ABLATE != 4
     if (lane == 0) publish_agent(&A.ts[t], kFlagAgg | agg);
-#endif
 }
 
 // Wave 0: global byte offset of tile t (aggregate already published).
 [[maybe_unused]] __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, uint32_t lane,
                                               bool early_group = false) {
-#if PACK_ABLATE == 1 || PACK_ABLATE == 4
-    return t * agg;  // timing-only: fake, in-bounds prefix; output is wrong
-#endif
     const uint64_t g = t / kGroup;
     const uint32_t r = (uint32_t)(t % kGroup);
 #if PACK_PROF
@@ -1231,7 +1189,7 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
             const uint64_t a = tile_aggregate(A, j, lane);
             if (lane == 0) publish_agent(&A.ts[j], kFlagAgg | a);
         } else {
-            __builtin_amdgcn_s_sleep(PACK_SLEEP);
+            __builtin_amdgcn_s_sleep(kSleep);
         }
         st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
     }
@@ -1269,7 +1227,7 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
                 const uint64_t a = group_aggregate(A, jg, lane);
                 if (lane == 0) publish_agent(&A.gs[jg], kFlagAgg | a);
             } else {
-                __builtin_amdgcn_s_sleep(PACK_SLEEP);
+                __builtin_amdgcn_s_sleep(kSleep);
             }
             continue;
         }
@@ -1297,124 +1255,16 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
     return gexcl + within;
 }
 
-// Multi-level aggregate look-back (PACK_LB=2).  Level k holds one record per
-// block of 64^k tiles (level 0 = ts, level 1 = gs, deeper levels follow gs in
-// the state).  Tile t's offset is, at every level k, the sum of the records
-// of its level-k node's earlier siblings: the mixed-radix digits of t.  All
-// levels are polled at once (one round trip when everything is published),
-// and no record ever carries an inclusive prefix, so there is no chain of
-// look-backs: the last tile of a level-(k+1) block publishes that block's
-// aggregate as soon as levels 0..k of its own look-back are summed.
-// (PACK_LB=1, `lookback`: the group's tiles, then windows of group records
-// back to the nearest inclusive one: >= 2 dependent round trips.)
-#ifndef PACK_LB
-#define PACK_LB 1
-#endif
-
-__device__ __forceinline__ uint64_t* level_records(const LookbackArgs& A, uint32_t k) {
-    if (k == 0) return A.ts;
-    uint64_t* p = A.gs;
-    uint64_t n = (A.ntiles + kGroup - 1) / kGroup;
-    for (uint32_t m = 1; m < k; m++) {
-        p += n;
-        n = (n + kGroup - 1) / kGroup;
-    }
-    return p;
-}
-
-// Aggregate of tiles [t0, t1) from their records (missing ones computed from
-// the input): the bounded-wait fallback of every level.
-__device__ uint64_t tiles_aggregate(const LookbackArgs& A, uint64_t t0, uint64_t t1,
-                                    uint32_t lane) {
-    uint64_t sum = 0;
-    for (uint64_t b = t0; b < t1; b += kGroup) {
-        uint64_t st = b + lane < t1 ? poll_agent(&A.ts[b + lane]) : kFlagAgg;
-        uint64_t miss = ballot64((st >> 62) == 0);
-        while (miss) {
-            const uint32_t j = ctz64(miss);
-            const uint64_t a = tile_aggregate(A, b + j, lane);
-            if (lane == 0) publish_agent(&A.ts[b + j], kFlagAgg | a);
-            if (lane == j) st = kFlagAgg | a;
-            miss &= miss - 1;
-        }
-        uint64_t v = st & kValMask;
-        for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-        sum += v;
-    }
-    return sum;
-}
-
-// Wave 0: global byte offset of tile t (aggregate already published).
-[[maybe_unused]] __device__ uint64_t lookback_ml(const LookbackArgs& A, uint64_t t, uint64_t agg, uint32_t lane) {
-#if PACK_ABLATE == 1 || PACK_ABLATE == 4
-    return t * agg;  // timing-only: fake, in-bounds prefix; output is wrong
-#endif
-    // levels 0..K: K = the first level whose node index is < 64
-    uint32_t K = 0;
-    while ((t >> (6 * K)) >= kGroup) K++;
-    // the first three levels' polls go out together (<= 262144 tiles: all)
-    uint64_t pre[3];
-#pragma unroll
-    for (uint32_t k = 0; k < 3; k++) {
-        const uint64_t i = t >> (6 * k);
-        const uint32_t r = (uint32_t)(i & (kGroup - 1));
-        const uint64_t* rec = level_records(A, k) + (i - r);
-        pre[k] = (k <= K && lane < r) ? poll_agent(const_cast<uint64_t*>(rec + lane)) : kFlagAgg;
-    }
-    uint64_t below = 0;  // sum of levels 0..k-1
-    for (uint32_t k = 0; k <= K; k++) {
-        const uint64_t i = t >> (6 * k);
-        const uint32_t r = (uint32_t)(i & (kGroup - 1));
-        uint64_t* rec = level_records(A, k) + (i - r);
-        uint64_t st = k == 0 ? pre[0] : k == 1 ? pre[1] : k == 2 ? pre[2]
-                                        : (lane < r ? poll_agent(rec + lane) : kFlagAgg);
-        for (uint32_t spins = 0;;) {
-            const uint64_t miss = ballot64((st >> 62) == 0);
-            if (!miss) break;
-            if (++spins >= kSpinLimit) {
-                if (lane == 0) PROF_ADD(2, 1);
-                const uint32_t j = ctz64(miss);
-                const uint64_t n0 = (i - r + j) << (6 * k), n1 = n0 + (1ull << (6 * k));
-                const uint64_t a = tiles_aggregate(A, n0, n1 < A.ntiles ? n1 : A.ntiles, lane);
-                if (lane == 0) publish_agent(rec + j, kFlagAgg | a);
-                if (lane == j) st = kFlagAgg | a;
-                continue;
-            }
-            __builtin_amdgcn_s_sleep(PACK_SLEEP);
-            st = ((miss >> lane) & 1) ? poll_agent(rec + lane) : st;
-        }
-        uint64_t v = st & kValMask;
-        for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-        below += v;
-        // t closes its level-(k+1) block: publish that block's aggregate
-        const uint64_t span = 1ull << (6 * (k + 1));
-        if (((t + 1) & (span - 1)) == 0 && lane == 0)
-            publish_agent(level_records(A, k + 1) + (t >> (6 * (k + 1))), kFlagAgg | (below + agg));
-    }
-    return below;
-}
-
 __device__ __forceinline__ uint64_t tile_offset(const LookbackArgs& A, uint64_t t, uint64_t agg,
                                                 uint32_t lane, bool early_group = false) {
-#if PACK_LB == 2
-    (void)early_group;
-    return lookback_ml(A, t, agg, lane);
-#else
     return lookback(A, t, agg, lane, early_group);
-#endif
 }
 
 // The group aggregate, published by the group's last tile from a wave that
-// polls the group's earlier tile records right after pass 1 (PACK_EARLYG):
+// polls the group's earlier tile records right after pass 1:
 // in `lookback` it is published by wave 0 only after its pass 2 and that
 // poll, and the next group's tiles wait on it.  (A compare-and-swap from
 // empty: it never overwrites the inclusive record wave 0 publishes later.)
-#ifndef PACK_WT_EARLYG
-#define PACK_WT_EARLYG 0  // the word-tile kernel's early group aggregate (A/B)
-#endif
-#ifndef PACK_EARLYG
-#define PACK_EARLYG 1  // measured (config 2): 508.6 -> 502.4 us; 2: the inclusive record too
-#endif
 
 __device__ void publish_group_early(const LookbackArgs& A, uint64_t t, uint64_t agg,
                                     uint32_t lane) {
@@ -1429,7 +1279,7 @@ __device__ void publish_group_early(const LookbackArgs& A, uint64_t t, uint64_t 
             const uint64_t a = tile_aggregate(A, j, lane);
             if (lane == 0) publish_agent(&A.ts[j], kFlagAgg | a);
         } else {
-            __builtin_amdgcn_s_sleep(PACK_SLEEP);
+            __builtin_amdgcn_s_sleep(kSleep);
         }
         st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
     }
@@ -1441,40 +1291,6 @@ __device__ void publish_group_early(const LookbackArgs& A, uint64_t t, uint64_t 
                                              __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
     }
-#if PACK_EARLYG == 2
-    // ... and the group's inclusive record as well: the group part of the
-    // look-back (windows of group records back to an inclusive one), so the
-    // next groups find it before this tile's wave 0 gets there (which then
-    // publishes the same value again)
-    uint64_t gexcl = 0;
-    int64_t idx = (int64_t)g - 1;
-    for (uint32_t spins = 0; idx >= 0;) {
-        const int64_t j = idx - (int64_t)lane;
-        const bool in_win = lane < kGroupWindow;
-        const uint64_t rec = !in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc);
-        const uint64_t inc = ballot64((rec & kFlagInc) != 0);
-        const uint32_t first_inc = ctz64(inc);
-        const uint64_t need = first_inc < 64 ? low_mask(first_inc) : low_mask(kGroupWindow);
-        const uint64_t missing = ballot64((rec >> 62) == 0) & need;
-        if (missing) {
-            if (++spins >= kSpinLimit) {
-                const uint64_t jg = (uint64_t)(idx - (int64_t)ctz64(missing));
-                const uint64_t a = group_aggregate(A, jg, lane);
-                if (lane == 0) publish_agent(&A.gs[jg], kFlagAgg | a);
-            } else {
-                __builtin_amdgcn_s_sleep(PACK_SLEEP);
-            }
-            continue;
-        }
-        uint64_t val = (lane <= first_inc) ? (rec & kValMask) : 0;
-        for (uint32_t d = 32; d >= 1; d >>= 1) val += __shfl_xor(val, d, 64);
-        gexcl += val;
-        if (first_inc < 64) break;
-        idx -= kGroupWindow;
-        spins = 0;
-    }
-    if (lane == 0) publish_agent(&A.gs[g], kFlagInc | (gexcl + v + agg));
-#endif
 }
 
 // Wave 0: exclusive scan of the tile's chunk sizes (<= 64) into chunk_pos
@@ -1502,15 +1318,14 @@ __device__ __forceinline__ uint64_t scan_chunks(SM& sm, uint32_t nc, uint32_t la
 }
 
 // One workgroup per tile (tile = blockIdx.x), 4 waves.
-#ifndef PACK_MIN_WAVES
-#define PACK_MIN_WAVES 8  // per SIMD (LDS 19.7 KB: 8 workgroups per CU; 6 before the selector table left LDS)
-#endif
+// (8 waves per SIMD: LDS 19.7 KB, 8 workgroups per CU; 6 before the
+// selector table left LDS)
 
 // GAP: chunk c is preceded by gap[c] bytes of the output that the kernel
 // leaves zero (out_off[c] is the gap's start; capnp_gpu_write_messages puts
 // each message's segment table there).
 template <bool SYNC, bool GAP>
-__global__ void __launch_bounds__(kThreads, GAP ? 7 : PACK_MIN_WAVES)  // (GAP: 20.6 KB of LDS)
+__global__ void __launch_bounds__(kThreads, GAP ? 7 : 8)  // (GAP: 20.6 KB of LDS)
 pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
             uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
             uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts,
@@ -1563,12 +1378,9 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
     uint8_t* const outa = out - mis;
-#ifndef PACK_ONE_BARRIER
-#define PACK_ONE_BARRIER 1
-#endif
     // (the ranges below read only chunk_off, so without gaps the barrier
     // after them also covers the table writes above)
-    if (GAP || !PACK_ONE_BARRIER) __syncthreads();
+    if (GAP) __syncthreads();
 #if PACK_PROF == 2
     if (tid == 0) TRACE(tile, 5, RT());  // (2: prelude timeline instead of look-back counters)
 #endif
@@ -1579,43 +1391,32 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
     const uint32_t q = (nc + kWaves - 1) / kWaves;
     const uint32_t wc0 = wave * q < nc ? wave * q : nc;
     const uint32_t wc1 = wc0 + q < nc ? wc0 + q : nc;
-#ifndef PACK_SPEC_LOAD
-#define PACK_SPEC_LOAD 1
-#endif
-    // The range's words go out to registers before its steps are known
-    // (PACK_SPEC_LOAD): step s loads the 64 words from the range start
-    // + 64 s.  That is the staged layout exactly when every chunk of the
-    // range is a whole number of steps (checked in the walk; otherwise the
-    // steps are loaded again), and the load latency then overlaps the walk.
-    // Interleaved A/B on three boxes (us): config 2 583 / 584 vs 597 / 587 /
-    // 593, carsales 591 / 596 vs 610 / 609; equal chunks of 100 words pay
-    // 1.8-3 % (every step loaded twice).  PACK_SPEC_LOAD=2 speculates only
-    // when the range's first chunk is whole steps and the range is that many
-    // of it: ragged batches then pay ~1.5 % (code), config 2 gains the same.
+    // The range's words go out to registers before its steps are known:
+    // step s loads the 64 words from the range start + 64 s.  That is the
+    // staged layout exactly when every chunk of the range is a whole number
+    // of steps (checked in the walk; otherwise the steps are loaded again),
+    // and the load latency then overlaps the walk.  Interleaved A/B on three
+    // boxes (us): config 2 583 / 584 vs 597 / 587 / 593, carsales 591 / 596
+    // vs 610 / 609; equal chunks of 100 words pay 1.8-3 % (every step loaded
+    // twice).
     const uint32_t tile_bytes = (uint32_t)((TW1 - TW0) * 8);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
     uint64_t cache[kStageSteps];
     // (messages with segment tables, GAP, have ragged segments: no speculation)
-    constexpr bool kSpec = PACK_SPEC_LOAD && !GAP;
+    constexpr bool kSpec = !GAP;
     uint64_t ragged = 63;  // OR of the range's chunk lengths (| 63: not speculated): low bits = load
     if (kSpec && wc1 > wc0) {
-        // speculate when the range's chunks look whole steps: its first chunk
-        // is, and the range is as long as that many of it (a batch of equal
-        // chunks of 100 words loads once, after the walk, as before)
         const uint64_t a = uniform64(toff[wc0]);
-        const uint64_t l0 = uniform64(toff[wc0 + 1]) - a;
         const uint32_t r0 = (uint32_t)(a - TW0);
         const uint32_t r1 = (uint32_t)(uniform64(toff[wc1]) - TW0);
-        if (PACK_SPEC_LOAD == 1 || ((l0 & 63u) == 0 && (uint64_t)(r1 - r0) == l0 * (wc1 - wc0))) {
-            ragged = 0;
+        ragged = 0;
 #pragma unroll
-            for (uint32_t s = 0; s < kStageSteps; s++) {
-                const uint32_t w = r0 + 64 * s + lane;
-                const uint32_t vo = w < r1 ? w * 8u : 0x80000000u;
-                const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vo, 0, 0);
-                cache[s] = ((uint64_t)v[1] << 32) | v[0];
-            }
+        for (uint32_t s = 0; s < kStageSteps; s++) {
+            const uint32_t w = r0 + 64 * s + lane;
+            const uint32_t vo = w < r1 ? w * 8u : 0x80000000u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vo, 0, 0);
+            cache[s] = ((uint64_t)v[1] << 32) | v[0];
         }
     }
 
@@ -1678,15 +1479,7 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 #endif
         // pass 1: sizes and positions
         StepInfo si[kStageSteps];
-#ifndef PACK_HBITS
-#define PACK_HBITS 1  // 1: pass 2 rebuilds each step's head mask from bit s of one VGPR
-                      // (not the SGPR pair kept, i.e. spilled, from pass 1); 2: and its meta
-#endif
-        uint32_t hbits = 0;  // PACK_HBITS: bit s = this lane heads a record in step s
-        uint32_t kin_l = 0;  // PACK_HBITS 2: lane s = step s's carried-run words (meta >> 16)
-        (void)hbits;
-        (void)kin_l;
-#if PACK_LEAN_STEP
+        uint32_t hbits = 0;  // bit s = this lane heads a record in step s
         {
             // (each step's chunk start and running size go to lane s of two
             // registers; the chunk tables are written once after the loop)
@@ -1703,21 +1496,8 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                     if constexpr (GAP) local += uniform(sm.chunk_gap[wc0 + (meta >> 9)]);
                     pk.begin(local);
                 }
-#if PACK_ABLATE == 3 || PACK_ABLATE == 4
-                asm volatile("" ::"v"(cache[s]));  // timing-only: skip the arithmetic
-                pk.total += 34 * (meta & 127u) / 8;
-                si[s].H = 0;
-                si[s].pos = 0;
-                si[s].tag = 0;
-#else
                 size_step_lean(pk, cache[s], meta & 127u, lane, si[s]);
-#endif
-#if PACK_HBITS
                 hbits |= mask_sel(si[s].H, 1u << s, 0u);
-#endif
-#if PACK_HBITS >= 2
-                kin_l = lane == s ? (si[s].meta >> 16) : kin_l;
-#endif
                 rec_oc = lane == s ? pk.o_c : rec_oc;
                 rec_sz = lane == s ? pk.total : rec_sz;
                 if ((meta >> 8) & 1) local += pk.total;
@@ -1733,41 +1513,6 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
             }
             if (lane == 0) sm.wave_bytes[wave] = local;
         }
-#else
-        {
-            StageState pk;
-            pk.begin(0);
-            uint32_t local = 0;
-#pragma unroll
-            for (uint32_t s = 0; s < kStageSteps; s++) {
-                const uint32_t meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s);
-                si[s].meta = meta;
-                if ((meta >> 7) & 1) {
-                    if constexpr (GAP) local += uniform(sm.chunk_gap[wc0 + (meta >> 9)]);
-                    pk.begin(local);
-                    if (lane == 0) sm.chunk_oc[wc0 + (meta >> 9)] = (uint32_t)local;
-                }
-#if PACK_ABLATE == 3 || PACK_ABLATE == 4
-                asm volatile("" ::"v"(cache[s]));  // timing-only: skip the arithmetic
-                pk.total += 34 * (meta & 127u) / 8;
-                si[s].H = 0;
-                si[s].pos = 0;
-                si[s].tag = 0;
-#else
-                size_step(pk, cache[s], meta & 127u, lane, si[s]);
-#endif
-                if ((meta >> 8) & 1) {
-                    if (lane == 0) {
-                        uint32_t g = 0;
-                        if constexpr (GAP) g = uniform(sm.chunk_gap[wc0 + (meta >> 9)]);
-                        sm.chunk_size[wc0 + (meta >> 9)] = pk.total + g;
-                    }
-                    local += pk.total;
-                }
-            }
-            if (lane == 0) sm.wave_bytes[wave] = local;
-        }
-#endif
         __syncthreads();
         // every range's bytes (gaps included) must fit its region
         bool fits = true;
@@ -1782,20 +1527,13 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         }
         // pass 2: assemble the bytes (the look-back loads are in flight)
         uint8_t* const region_m1 = region - 1;
-#if PACK_ABLATE != 3 && PACK_ABLATE != 4
         wave_lds_sync();
         if (fits) {
             uint32_t ext = 0;  // words the run open at the step end absorbs later
 #pragma unroll
             for (int s = (int)kStageSteps - 1; s >= 0; s--) {
                 StepInfo sj = si[s];
-#if PACK_HBITS
                 sj.H = ballot64(((hbits >> s) & 1u) != 0);
-#endif
-#if PACK_HBITS >= 2
-                sj.meta = (uint32_t)__builtin_amdgcn_readlane((int)d_meta, s) |
-                          ((uint32_t)__builtin_amdgcn_readlane((int)kin_l, s) << 16);
-#endif
                 const uint32_t meta = sj.meta;
                 const uint32_t e = ((meta >> 8) & 1) ? 0u : ext;
                 emit_step<SYNC>(cache[s], sj, e, lane, region_m1, sm.sel,
@@ -1807,7 +1545,6 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
                 ext = ((meta >> 7) & 1) ? 0u : (meta >> 16) + (sj.H == 0 ? e : 0u);
             }
         }
-#endif
         if (wave == 0) {
             const uint64_t excl = tile_offset(LA, tile, agg, lane);
             if (lane == 0) TRACE(tile, 2, RT());
@@ -1816,9 +1553,6 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         }
         __syncthreads();
         for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
-#if PACK_ABLATE == 2
-        return;  // timing-only: no output stores
-#endif
         if (fits) {
             if (wc1 > wc0) {
                 const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
@@ -1855,9 +1589,6 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
         }
         __syncthreads();
         for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
-#if PACK_ABLATE == 2
-        return;
-#endif
         run_streaming<MODE_RING>(in, toff, sm.chunk_size, sm.chunk_pos, nc, wave, lane,
                                  region, sm.sel, outa, mis, out_cap,
                                  GAP ? sm.chunk_gap : nullptr);
@@ -1893,12 +1624,6 @@ pack_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_
 // streaming size pass, take part in the look-back, and leave their bytes to
 // pack_ovf_kernel (as tiles whose staged bytes overflow their regions do).
 
-#ifndef LEAN_EXP
-#define LEAN_EXP 0  // diagnostic variants (1: no streaming fallback)
-#endif
-#ifndef LEAN_SCHED
-#define LEAN_SCHED 1  // scheduling barrier between steps
-#endif
 
 struct LeanCarry {
     uint32_t type;   // run open at the step start: 0 none, 1 zero run, 2 literal run
@@ -2101,7 +1826,7 @@ pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ c
     for (int w = 0; w < kWaves; w++) staged &= sm.wave_steps[w] <= kStageSteps;
     staged = __builtin_amdgcn_readfirstlane((int)staged) != 0;
 
-    if (LEAN_EXP != 1 && !staged) {
+    if (!staged) {
         // sizes by the streaming size pass, offsets by the look-back; the
         // bytes come from pack_ovf_kernel
         if constexpr (SYNC)
@@ -2162,9 +1887,7 @@ pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ c
             rec_oc = lane == s ? oc : rec_oc;
             rec_sz = lane == s ? c.total : rec_sz;
             if ((meta >> 8) & 1) local += c.total;
-#if LEAN_SCHED
             __builtin_amdgcn_sched_barrier(0);  // one step at a time: registers
-#endif
         }
         if (lane < kStageSteps && ((d_meta >> 8) & 1))
             sm.chunk_size[wc0 + ((d_meta >> 9) & 63u)] = rec_sz;
@@ -2193,9 +1916,7 @@ pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ c
                                  (uint32_t)__builtin_amdgcn_readlane((int)rec_oc, s),
                                  (uint32_t)__builtin_amdgcn_readlane((int)d_g, s), t0);
             ext = ((meta >> 7) & 1) ? 0u : (kin & 0xFFu) + ((kin & 0x100u) ? e : 0u);
-#if LEAN_SCHED
             __builtin_amdgcn_sched_barrier(0);
-#endif
         }
     }
     if (wave == 0) {
@@ -2232,11 +1953,8 @@ pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ c
 // kCsSteps chunks of its tile.  Tiles with a longer chunk (or more chunks per
 // wave) take the streaming size pass and leave their bytes to
 // pack_ovf_kernel.
-#ifndef PACK_COPY_PRE
-#define PACK_COPY_PRE 0  // 1: the chunk-step kernel's copy-out reads its LDS region first
-#endif
-#ifndef PACK_CS_SPEC
-#define PACK_CS_SPEC 1  // one-round-trip prologues: speculative step loads etc. (below)
+#ifndef PACK_PF
+#define PACK_PF 0  // chunk-step kernel: L2 prefetch distance in tiles (a multiple of 8: same XCD)
 #endif
 constexpr uint32_t kCsSteps = 4;   // chunks (steps) per wave
 constexpr uint32_t kCsWords = 128; // words per step
@@ -2397,15 +2115,20 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     const uint32_t wc1 = wc0 + q < nc ? wc0 + q : nc;
     const uint32_t nw = wc1 - wc0;
     const uint64_t TW0 = uniform64(chunk_off[c0]);
-#if PACK_CS_SPEC
     const uint64_t WS0 = uniform64(toff[wc0]);
-#endif
     const uint64_t TW1 = uniform64(chunk_off[c1]);
+#if PACK_PF
+    // the words of tile + PACK_PF (dealt to this XCD too: blocks go round
+    // robin over the 8 XCDs), touched once per 64 bytes so that its loads
+    // hit L2 when that tile runs
+    const uint64_t pt = tile + PACK_PF < gridDim.x ? tile + PACK_PF : tile;
+    const uint64_t pc0 = pt * tc, pc1 = pc0 + tc < nchunks ? pc0 + tc : nchunks;
+    const uint64_t PW0 = uniform64(chunk_off[pc0]), PW1 = uniform64(chunk_off[pc1]);
+#endif
     const uint32_t tile_bytes = (uint32_t)((TW1 - TW0) * 8);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
     uint64_t clo[kCsSteps], chi[kCsSteps];
-#if PACK_CS_SPEC
     // Every load of the prologue is issued in one round trip: the scalar
     // offsets (TW0, TW1, the wave's first chunk WS0), the wave's chunk offsets
     // (one buffer load, lane l <= nw: toff[wc0 + l]; lanes past them read 0,
@@ -2431,26 +2154,21 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         clo[s] = ((uint64_t)x[1] << 32) | x[0];
         chi[s] = ((uint64_t)y[1] << 32) | y[0];
     }
+#if PACK_PF
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint64_t*>(in + PW0), 0, pt == tile ? 0 : (int)((PW1 - PW0) * 8), 0x00020000);
+    const uint32_t pfv = __builtin_amdgcn_raw_buffer_load_b32(prs, (int)(tid * 64u), 0, 0);
+#endif
     const uint32_t onext = (uint32_t)__shfl_down((int)o, 1, 64);
     const uint32_t d_off = lane < nw ? o - (uint32_t)TW0 : 0u;
     const uint32_t d_len = lane < nw ? onext - o : 0u;
-#else
-    for (uint32_t i = tid; i <= kSelCopy; i += kThreads) sm.sel[i] = kSel8Table.e[i];
-    const uint32_t d_off = lane < nw ? (uint32_t)(toff[wc0 + lane] - TW0) : 0u;
-    const uint32_t d_len = lane < nw ? (uint32_t)(toff[wc0 + lane + 1] - TW0) - d_off : 0u;
-#endif
     const bool ok = nw <= kCsSteps && ballot64(lane < nw && d_len > kCsWords) == 0;
     if (lane == 0) sm.wave_steps[wave] = ok ? 0u : 1u;
-#if PACK_CS_SPEC
     if (ballot64(lane + 1u < nw && d_len != kCsWords) != 0) {
         // (the speculative values enter the reloaded ones through an opaque
         // zero, so the compiler keeps their loads ahead of this branch)
         uint64_t z;
         asm volatile("s_mov_b64 %0, 0" : "=s"(z));
-#else
-    {
-        const uint64_t z = 0;
-#endif
 #pragma unroll
         for (uint32_t s = 0; s < kCsSteps; s++) {
             const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)d_off, s);
@@ -2463,7 +2181,6 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             chi[s] = (((uint64_t)y[1] << 32) | y[0]) | (chi[s] & z);
         }
     }
-#if PACK_CS_SPEC
     else {
         // the wave's last chunk may be short: its step's words past it are
         // the next wave's (pass 1 takes words past n as zero)
@@ -2478,7 +2195,6 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     }
     sm.sel[tid] = selv;
     if (tid == 0) sm.sel[kSelCopy] = kSel8Table.e[kSelCopy];
-#endif
     for (uint32_t i = tid; i < nc; i += kThreads) sm.chunk_size[i] = 0;
     __syncthreads();
     bool staged = true;
@@ -2520,6 +2236,9 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         }
         __syncthreads();
         for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
+#if PACK_PF
+        asm volatile("" ::"v"(pfv));
+#endif
         return;
     }
 
@@ -2541,9 +2260,7 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         rec_oc = lane == s ? local : rec_oc;
         if (lane == s && s < nw) sm.chunk_size[wc0 + s] = sz;
         local += sz;
-#if LEAN_SCHED
         __builtin_amdgcn_sched_barrier(0);
-#endif
     }
     if (lane == 0) sm.wave_bytes[wave] = local;
     __syncthreads();
@@ -2559,7 +2276,6 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         if (lane == 0) TRACE(tile, 2, RT());
 #endif
     }
-#if PACK_EARLYG
     const bool early_group = (tile % kGroup) == kGroup - 1;
     if (early_group && wave == kWaves - 1) {
         uint32_t a = 0;
@@ -2567,9 +2283,6 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         for (int w = 0; w < kWaves; w++) a += (uint32_t)lds_u64(&sm.wave_bytes[w]);
         publish_group_early(LA, tile, a, lane);
     }
-#else
-    const bool early_group = false;
-#endif
     // ---- pass 2: the bytes (the look-back loads are in flight)
     if (fits) {
         uint8_t* const region_m1 = region - 1;
@@ -2586,9 +2299,7 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             cs_emit_word<SYNC>(clo[s], ilo[s], region_m1, sm.sel, srs, oc, d, b);
             cs_emit_word<SYNC>(chi[s], ihi[s], region_m1, sm.sel, srs, oc, d,
                                b + 64u / (kSyncWords / 4u));
-#if LEAN_SCHED
             __builtin_amdgcn_sched_barrier(0);
-#endif
         }
     }
     if (wave == 0) {
@@ -2609,13 +2320,7 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         if (nw) {
             const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
             const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
-#if PACK_COPY_PRE
-            copy_out_pre<(kStageRegion + 1023) / 1024>(region, out - mis, D0,
-                                                       lds_u64(&sm.wave_bytes[wave]), out_cap + mis,
-                                                       lane);
-#else
             copy_out(region, out - mis, D0, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
-#endif
         }
 #if PACK_PROF == 3
         __syncthreads();
@@ -2626,6 +2331,9 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
         if (tid == 0) ovf[tile] = 1;
     }
+#if PACK_PF
+    asm volatile("" ::"v"(pfv));
+#endif
 }
 
 // Tiles whose staged ranges overflowed (ovf[t] set by pack_kernel, after its
@@ -2686,9 +2394,6 @@ pack_ovf_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ ch
 // chunk's own start is unknown here, so the entry holds the record's position
 // relative to the tile (24-bit two's complement) and pack_wt_fix_sync adds
 // tile offset - chunk offset once every tile is placed.
-#ifndef PACK_WT_ABL
-#define PACK_WT_ABL 0  // diagnostic timing variants (scripts/wt_ablate.py); 0 = product
-#endif
 
 struct WtSmem {
     Sel8 sel[kSelCopy + 1];                // record assembly per tag (s0, s1)
@@ -2721,20 +2426,9 @@ __device__ __forceinline__ void size_step_s(StageState& pk, uint64_t w, uint32_t
     pk.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
 }
 
-#ifndef PACK_WT_DEBUG
-#define PACK_WT_DEBUG 0
-#endif
-#if PACK_WT_DEBUG
-__device__ uint32_t g_pwt_dbg[4096 * 8];
-#endif
-#ifndef PACK_WT_PIN
-#define PACK_WT_PIN 1
-#endif
-#ifndef PACK_WT_MIN_WAVES
-#define PACK_WT_MIN_WAVES 6  // the LDS (24.3 KB) allows 6 workgroups per CU
-#endif
+// (6 waves per SIMD: the LDS, 24.3 KB, allows 6 workgroups per CU)
 template <bool SYNC>
-__global__ void __launch_bounds__(kThreads, PACK_WT_MIN_WAVES)
+__global__ void __launch_bounds__(kThreads, 6)
 pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
                uint64_t nchunks, uint8_t* __restrict__ out, uint64_t out_cap,
                uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts, uint64_t* __restrict__ gs,
@@ -2769,11 +2463,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     const uint64_t R1 = !have ? R0 : (R0 + kWtRange < Tb ? R0 + kWtRange : Tb);
     const uint32_t nw = (uint32_t)(R1 - R0);
     const bool lastr = have && R1 == whi;
-#if PACK_CS_SPEC
     const Sel8 selv = kSel8Table.e[tid];  // (written after the word loads are issued)
-#else
-    for (uint32_t i = tid; i <= kSelCopy; i += kThreads) sm.sel[i] = kSel8Table.e[i];
-#endif
     uint8_t* region = sm.stage[wave];
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
     uint8_t* const outa = out - mis;
@@ -2791,13 +2481,10 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             cache[s] = ((uint64_t)v[1] << 32) | v[0];
         }
     }
-#if PACK_CS_SPEC
     sm.sel[tid] = selv;
     if (tid == 0) sm.sel[kSelCopy] = kSel8Table.e[kSelCopy];
-#endif
     // the range's first chunks (their offsets are written after the
     // look-back; loaded now, off that path)
-#if PACK_CS_SPEC
     // (unconditional loads at in-bounds indexes, selected afterwards: map and
     // plan have an entry past the last range, and the steps' chunk-start
     // bits are one vector load; guarded loads had each waited at its join)
@@ -2822,31 +2509,14 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         const uint64_t bits = rr ? (lo >> rr) | (hi << (64 - rr)) : lo;
         smk[s] = nv ? bits & low_mask(nv) : 0ull;
     }
-#else
-    const uint64_t cA = have ? uniform64(map[tile * kWaves + wave]) : nchunks;
-    const uint64_t st0 = cA + lane < nchunks ? chunk_off[cA + lane] : ~0ull;
-    // the run states at both ends (pack_wt_plan)
-    const uint64_t r = tile * kWaves + wave;
-    const uint32_t pin = have ? uniform(plan[r]) : 0u;
-    const uint32_t pout = (have && !lastr) ? uniform(plan[r + 1]) : 0u;
-    // chunk starts (forced heads) of the steps and of both windows
-    uint64_t smk[kStageSteps];
-#pragma unroll
-    for (uint32_t s = 0; s < kStageSteps; s++) {
-        const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
-        smk[s] = nv ? start_bits(cbits, b64, R0 + 64u * s) & low_mask(nv) : 0ull;
-    }
-#endif
     for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
         *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
     wave_lds_sync();
     const Carry cin{pin & 3u, (pin >> 2) & 0xFFu};
     // (pin the words here: nothing of pass 1 is computed ahead of the carry,
     // which would keep eight steps' worth of values live through it)
-#if PACK_WT_PIN
 #pragma unroll
     for (uint32_t s = 0; s < kStageSteps; s++) asm volatile("" : "+v"(cache[s]));
-#endif
     __syncthreads();
     // pass 1: sizes and positions
     StepInfo si[kStageSteps];
@@ -2867,14 +2537,6 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     if (lane == 0) {
         sm.wave_bytes[wave] = pk.total;
         wm.lastcs[wave] = lastcs;
-#if PACK_WT_DEBUG
-        const uint64_t r = tile * kWaves + wave;
-        if (r < 4096) {
-            uint32_t* d = g_pwt_dbg + 8 * r;
-            d[0] = cin.type; d[1] = cin.rem; d[2] = rext; d[3] = pk.carry.type; d[4] = pk.carry.rem;
-            d[5] = (uint32_t)R0; d[6] = (uint32_t)R1; d[7] = pk.total;
-        }
-#endif
     }
     __syncthreads();
     uint32_t woff = 0, agg = 0;
@@ -2885,15 +2547,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         agg += b;
     }
     if (wave == 0) publish(LA, tile, agg, lane);
-#if PACK_EARLYG && PACK_WT_EARLYG
-    // (the group's last tile publishes the group aggregate from its last
-    // wave now, as the chunk-step kernel does)
-    const bool early_group = (tile % kGroup) == kGroup - 1;
-    if (early_group && wave == kWaves - 1) publish_group_early(LA, tile, agg, lane);
-#else
-    const bool early_group = false;
-#endif
-    // pass 2: the bytes
+        // pass 2: the bytes
     wave_lds_sync();
     {
         uint8_t* const region_m1 = region - 1;
@@ -2901,12 +2555,11 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
 #pragma unroll
         for (int s = (int)kStageSteps - 1; s >= 0; s--) {
             const uint32_t e = ext;
-            if (PACK_WT_ABL != 6)
-                emit_step<false>(cache[s], si[s], e, lane, region_m1, sm.sel, nullptr, 0, 0, 0);
+            emit_step<false>(cache[s], si[s], e, lane, region_m1, sm.sel, nullptr, 0, 0, 0);
             ext = (si[s].meta >> 16) + (si[s].H == 0 ? e : 0u);
         }
     }
-    if (SYNC && PACK_WT_ABL != 3) {
+    if (SYNC) {
         // the chunk open at R0 started at tile position oc (0: before the tile)
         uint32_t oc = 0;
         for (int w = (int)wave - 1; w >= 0; w--) {
@@ -2951,8 +2604,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         }
     }
     if (wave == 0) {
-        const uint64_t excl =
-            PACK_WT_ABL == 5 ? tile * 8192 : tile_offset(LA, tile, agg, lane, early_group);
+        const uint64_t excl = tile_offset(LA, tile, agg, lane);
         if (lane == 0) {
             wm.excl = excl;
             tile_off[tile] = excl;
@@ -2963,7 +2615,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     const uint64_t excl = lds_u64(&wm.excl);
     // offsets of the chunks that start in the range (in the batch's last
     // range also the empty chunks at its end)
-    if (have && PACK_WT_ABL != 4) {
+    if (have) {
         for (uint64_t c0 = cA;; c0 += CAPNP_WAVE) {
             const uint64_t c = c0 + lane;
             const uint64_t st = c0 == cA ? st0 : (c < nchunks ? chunk_off[c] : ~0ull);
@@ -2972,7 +2624,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             if (ballot64(inr) != ~0ull) break;
         }
     }
-    if (have && PACK_WT_ABL != 7)
+    if (have)
         copy_out(region, outa, excl + woff + mis, lds_u64(&sm.wave_bytes[wave]), out_cap + mis,
                  lane);
 }
@@ -2987,10 +2639,9 @@ pack_wt_bits(const uint64_t* __restrict__ chunk_off, uint64_t nchunks, uint64_t 
     if (st < whi) atomicOr(&cb[1 + (st >> 6) - b64], 1ull << (st & 63));
 }
 
-#ifndef PACK_PLAN_WIN
-#define PACK_PLAN_WIN 64  // words before a range examined first (16: 254 vs 190 us, more deep searches)
-#endif
-static_assert(PACK_PLAN_WIN >= 2 && PACK_PLAN_WIN <= 64, "plan window");
+// words before a range examined first (16: 254 vs 190 us, more deep searches)
+constexpr uint32_t kPlanWin = 64;
+static_assert(kPlanWin >= 2 && kPlanWin <= 64, "plan window");
 // Run state at every wave range's first word, one wave per range: plan[r] =
 // type | rem << 2 | ext << 10, ext = the words from R0 on that the run open
 // there absorbs (run_ext_b).  The pack kernel reads its own entry and the
@@ -3011,7 +2662,7 @@ pack_wt_plan(const uint64_t* __restrict__ in, const uint64_t* __restrict__ cbits
         // of guarded loads (the compiler waited at each guard's join).  The
         // W words before R (lanes 64 - W ..) and the word before them; the
         // words after R only when the run state at R is an open run.
-        constexpr uint32_t W = PACK_PLAN_WIN;
+        constexpr uint32_t W = kPlanWin;
         // (a buffer load over words [B, R), B = max(R - W - 1, wlo): lanes
         // outside it read 0 without a fetch, and no branch means no wait at
         // a join before the scalar loads below)
@@ -3122,24 +2773,6 @@ static dim3 pack_ovf_grid(uint64_t ntiles) {
     return dim3((uint32_t)(g < 1024 ? g : 1024));
 }
 
-// CAPNP_PACK_LEAN=0 selects pack_kernel for the chunk tiles (A/B builds).
-static bool pack_lean_enabled() {
-    static const bool v = [] {
-        const char* e = getenv("CAPNP_PACK_LEAN");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
-// CAPNP_PACK_CS=0 leaves 128-word-chunk batches to pack_lean_kernel (A/B).
-static bool pack_cs_enabled() {
-    static const bool v = [] {
-        const char* e = getenv("CAPNP_PACK_CS");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
 extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_chunk_off,
                                         uint64_t nchunks, uint32_t tc, uint8_t* d_out,
                                         uint64_t out_cap, uint64_t* d_out_off,
@@ -3153,7 +2786,7 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_
     hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(nchunks, tc), stream);
     if (e != hipSuccess) return e;
     uint8_t* ovf = pack_ovf_flags(d_state, ntiles);
-    if (pack_cs_enabled() && tc == kWaves * kCsSteps) {
+    if (tc == kWaves * kCsSteps) {
         // chunks of at most 128 words (tc chosen for a mean of 65-128 words;
         // a tile with a longer chunk takes the streaming size pass)
         if (d_sync)
@@ -3164,23 +2797,15 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_
             hipLaunchKernelGGL((pack_cs_kernel<false>), dim3((uint32_t)ntiles), dim3(kThreads),
                                0, stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap,
                                d_out_off, d_state, d_state + ntiles, d_sync, ovf);
-    } else if (pack_lean_enabled()) {
-        if (d_sync)
-            hipLaunchKernelGGL((pack_lean_kernel<true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
-                               stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
-                               d_state, d_state + ntiles, d_sync, ovf);
-        else
-            hipLaunchKernelGGL((pack_lean_kernel<false>), dim3((uint32_t)ntiles), dim3(kThreads),
-                               0, stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap,
-                               d_out_off, d_state, d_state + ntiles, d_sync, ovf);
-    } else if (d_sync)
-        hipLaunchKernelGGL((pack_kernel<true, false>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
+    } else if (d_sync) {
+        hipLaunchKernelGGL((pack_lean_kernel<true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
                            stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
-                           d_state, d_state + ntiles, d_sync, nullptr, ovf);
-    else
-        hipLaunchKernelGGL((pack_kernel<false, false>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
+                           d_state, d_state + ntiles, d_sync, ovf);
+    } else {
+        hipLaunchKernelGGL((pack_lean_kernel<false>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
                            stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
-                           d_state, d_state + ntiles, d_sync, nullptr, ovf);
+                           d_state, d_state + ntiles, d_sync, ovf);
+    }
     hipLaunchKernelGGL((pack_ovf_kernel<false>), pack_ovf_grid(ntiles), dim3(kThreads), 0, stream,
                        d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, ovf, ntiles,
                        nullptr);
@@ -3230,12 +2855,8 @@ extern "C" size_t capnp_pack_wt_ws_bytes(uint64_t wlo, uint64_t whi) {
 extern "C" uint32_t capnp_pack_wt_words(void) { return kWtTile; }
 
 extern "C" int capnp_pack_wt_dbg(uint32_t* out) {
-#if PACK_WT_DEBUG
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pwt_dbg), sizeof(g_pwt_dbg)) == hipSuccess ? 0 : -1;
-#else
     (void)out;
     return -1;
-#endif
 }
 
 extern "C" hipError_t capnp_launch_pack_wt(const uint64_t* d_in, const uint64_t* d_chunk_off,

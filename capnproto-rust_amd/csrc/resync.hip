@@ -7,37 +7,28 @@
 // The decode of a read unit is a serial tag chain: where record k+1 starts
 // depends on record k's tag and run count.  The batch unpack without an index
 // gives one lane per chunk, so a long chunk is one long dependent chain.
-// Here each chunk's packed bytes are cut into kBlock-byte blocks, one lane
-// per block, and the chain is resynchronised speculatively:
+// Here each chunk's packed bytes are cut into kBlock-byte blocks and the
+// chain is resynchronised speculatively, tile by tile (k_tile, below):
 //
-//   spec   lane k walks its block from the block's first byte as if a record
-//          started there; its exit (first record position at or past the
-//          block end) and word count are kept.  A chunk's first block starts
-//          at a real record, so its walk is exact.
-//   fix    lane k takes its true entry, the exit of block k-1, and walks from
-//          it in lockstep with the speculative chain until both land on the
-//          same byte (tag chains couple within a few records: record lengths
-//          are 1..10 bytes).  From the meet on the speculative walk is exact,
-//          so the exit stands and only the word count changes.  No meet (or an
-//          entry past the block end, as inside a literal run that spans
-//          blocks) means the block is re-walked from the entry and its exit
-//          changes; the pass repeats until no exit changes.  A fix lane owns
-//          8 consecutive blocks and fixes them in order, so inside a literal
-//          run region (long records no speculative walk couples with) the
-//          true chain advances 8 blocks per pass; passes are enqueued 8 at a
-//          time and skip themselves after a pass that changed nothing.  At that fixed
-//          point every block's entry is its predecessor's exit and the first
-//          block's entry is the chunk start, so by induction every exit is
-//          the one the serial walk produces.
-//   scan   exclusive scan of the block word counts: each block's first
-//          output word.
-//   check  lane per chunk: the chain must end exactly at the chunk's packed
-//          end with exactly the chunk's word count (then no record ran short,
-//          and no run overran the output: the word count is monotone).
-//   decode each resolved block is a read unit of its own (its records run
-//          from its entry to its exit): the blocks go to the batch unpack
-//          kernel as a batch of ~120-word units (staged LDS tiles, coalesced
-//          stores).
+//   resolve  every block's entry (its first record start), exit (the first
+//            record start at or past its end) and word count, from
+//            speculative walks that meet the true chain (tag chains couple
+//            within a few records: record lengths are 1..10 bytes), then
+//            fix passes over the tiles whose entry was not their
+//            predecessor's exit, until no exit changes.  At that fixed
+//            point every block's entry is its predecessor's exit and the
+//            first block's entry is the chunk start, so by induction every
+//            exit is the one the serial walk produces.
+//   scan     exclusive scan of the block word counts: each block's first
+//            output word.
+//   check    lane per chunk: the chain must end exactly at the chunk's packed
+//            end with exactly the chunk's word count (then no record ran
+//            short, and no run overran the output: the word count is
+//            monotone).
+//   decode   each resolved block is a read unit of its own (its records run
+//            from its entry to its exit): the blocks go to the batch unpack
+//            kernel as a batch of ~120-word units (staged LDS tiles,
+//            coalesced stores).
 //
 // A chunk that fails the check (a malformed stream, or a valid unit followed
 // by spare bytes in its range) is decoded serially as one unit of that same
@@ -48,12 +39,6 @@
 #include "common.h"
 #include "../../include/capnp_packed.h"
 
-#ifndef RESYNC_WALK_LDS
-#define RESYNC_WALK_LDS 32768  // 4 workgroups per CU (config 4 index-free: 5.81 -> 4.93 ms; 64 KiB: 5.31)
-#endif
-#ifndef RESYNC_BLOCK
-#define RESYNC_BLOCK 512
-#endif
 
 extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d_in_off,
                                           size_t nchunks, uint32_t tc, uint64_t* d_out,
@@ -63,23 +48,8 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
 
 namespace {
 
-constexpr uint64_t kBlock = RESYNC_BLOCK;  // packed bytes per lane
-
-// Dynamic LDS the block walks reserve (unused) to cap their workgroups per
-// CU: each lane walks its own block byte by byte from global memory, so the
-// working set is one cache line per lane; at full occupancy (2048 lanes per
-// CU) it is 256 KB per CU, beyond L1 and the CU's share of L2, and every
-// hop refetched its line from HBM (config 4: 11.4 GB read for 0.57 GB of
-// packed bytes).  CAPNP_RESYNC_LDS overrides (bytes; diagnostic).
-static uint32_t walk_lds() {
-    static const uint32_t v = [] {
-        const char* e = getenv("CAPNP_RESYNC_LDS");
-        return e ? (uint32_t)atoi(e) : (uint32_t)RESYNC_WALK_LDS;
-    }();
-    return v;
-}
+constexpr uint64_t kBlock = 512;  // packed bytes per block
 constexpr uint32_t kThreads = 256;
-constexpr uint64_t kGroup = 8;  // blocks per fix lane
 constexpr int kMaxPasses = 512;  // fix passes before giving up to the serial path
 int g_max_passes = kMaxPasses;   // (capnp_resync_max_passes: tests drive the fallbacks)
 constexpr int kPassBatch = 8;    // fix passes enqueued per flag read-back
@@ -123,8 +93,8 @@ __device__ __forceinline__ uint64_t chunk_of(const uint64_t* __restrict__ bstart
 struct Ws {
     uint64_t* nblk;        // [n+1] blocks per chunk
     uint64_t* bstart;      // [n+1] exclusive scan of nblk
-    uint64_t* spec_exit;   // [nbb]
-    uint32_t* spec_words;  // [nbb]
+    uint64_t* spec_exit;   // [nbb] (k_tile: each block's chunk; then decode units' starts)
+    uint32_t* spec_words;  // [nbb] (the chunks' error marks; then the units' statuses)
     uint64_t* exit;        // [nbb]
     uint64_t* entry;       // [nbb] entry the current exit/words were derived from
     uint64_t* words;       // [nbb]
@@ -134,13 +104,6 @@ struct Ws {
                            // [2 + i] fix pass i changed an exit
     void* tmp;
     size_t tmp_bytes;
-    // RESYNC_SEGUNITS: the resolved segments (kSegs per block) as decode units
-    uint64_t* seg_exit = nullptr;  // [kSegs nbb] exit of each segment
-    uint32_t* seg_wrel = nullptr;  // [kSegs nbb] words of the block's earlier segments
-    uint64_t* u_in = nullptr;      // [kSegs nbb + 1] unit packed starts
-    uint64_t* u_out = nullptr;     // [kSegs nbb + 1] unit first words
-    int32_t* u_st = nullptr;       // [kSegs nbb]
-    uint64_t* u_cons = nullptr;    // [kSegs nbb]
 };
 
 // (a chunk with no packed bytes but a nonzero word count owns one empty
@@ -158,87 +121,6 @@ __global__ void __launch_bounds__(kThreads) k_count(const uint64_t* __restrict__
     nblk[c] = len == 0 ? (out_off[c + 1] != out_off[c] ? 1 : 0) : (len + kBlock - 1) / kBlock;
 }
 
-__global__ void __launch_bounds__(kThreads)
-k_spec(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
-       const uint64_t* __restrict__ bstart, uint64_t* __restrict__ spec_exit,
-       uint32_t* __restrict__ spec_words, uint64_t* __restrict__ exit, uint64_t* __restrict__ entry,
-       uint64_t* __restrict__ words) {
-    const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (k >= bstart[n]) return;
-    const uint64_t c = chunk_of(bstart, n, k);
-    const uint64_t b = in_off[c + 1];
-    const uint64_t s = in_off[c] + (k - bstart[c]) * kBlock;
-    const uint64_t end = s + kBlock < b ? s + kBlock : b;
-    uint64_t p = s, w = 0;
-    while (p < end) hop(in, p, w, b);
-    spec_exit[k] = p;
-    spec_words[k] = (uint32_t)w;
-    exit[k] = p;
-    entry[k] = s;
-    words[k] = w;
-}
-
-// Fix pass `pass`: lane = group of kGroup consecutive blocks of the batch,
-// fixed in order, so a lane's own blocks take their entries from exits it has
-// just computed (a literal run that spans blocks, which no speculative walk
-// couples with, then costs one pass per group rather than per block).  The
-// group's first block reads its predecessor's exit as the last pass left it.
-// The pass does nothing if the previous pass changed no exit.
-__global__ void __launch_bounds__(kThreads)
-k_fix(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
-      const uint64_t* __restrict__ bstart, const uint64_t* __restrict__ spec_exit,
-      const uint32_t* __restrict__ spec_words, uint64_t* exit, uint64_t* __restrict__ entry,
-      uint64_t* __restrict__ words, int32_t* flags, int pass) {
-    if (pass > 0 && __atomic_load_n(&flags[2 + pass - 1], __ATOMIC_RELAXED) == 0) return;
-    const uint64_t k0 = ((uint64_t)blockIdx.x * kThreads + threadIdx.x) * kGroup;
-    const uint64_t nb = bstart[n];
-    if (k0 >= nb) return;
-    uint64_t c = chunk_of(bstart, n, k0);
-    bool changed = false;
-    for (uint64_t k = k0; k < k0 + kGroup && k < nb; k++) {
-        while (k >= bstart[c + 1]) c++;
-        if (k == bstart[c]) continue;  // a chunk's first block starts at its first record
-        // (a predecessor in another group may be rewritten by its own lane
-        // during this pass; either value is fine, a later pass sees the last)
-        const uint64_t e = __atomic_load_n(&exit[k - 1], __ATOMIC_RELAXED);
-        if (e == entry[k]) continue;
-        const uint64_t b = in_off[c + 1];
-        const uint64_t s = in_off[c] + (k - bstart[c]) * kBlock;
-        const uint64_t end = s + kBlock < b ? s + kBlock : b;
-        uint64_t nx, nw;
-        if (e >= end) {  // the block lies inside a record that began earlier
-            nx = e;
-            nw = 0;
-        } else {
-            uint64_t ps = s, ws = 0;  // speculative chain
-            uint64_t pt = e, wt = 0;  // true chain
-            bool met = false;
-            while (pt < end) {
-                while (ps < pt && ps < end) hop(in, ps, ws, b);
-                if (ps == pt) {
-                    met = true;
-                    break;
-                }
-                hop(in, pt, wt, b);
-            }
-            if (met) {
-                nx = spec_exit[k];
-                nw = wt + spec_words[k] - ws;
-            } else {
-                nx = pt;
-                nw = wt;
-            }
-        }
-        entry[k] = e;
-        words[k] = nw;
-        if (nx != exit[k]) {
-            __atomic_store_n(&exit[k], nx, __ATOMIC_RELAXED);
-            changed = true;
-        }
-    }
-    if (changed) flags[2 + pass] = 1;
-}
-
 #ifndef RESYNC_PROF
 #define RESYNC_PROF 0  // diagnostic: per-tile phase timestamps of the spec launch (scripts/resync_prof.py)
 #endif
@@ -249,14 +131,11 @@ __device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave
 #define RTRACE(k) ((void)0)
 #endif
 
-// ---- tile resolution (round 3; RESYNC_TILE, the default) ----
-// k_spec + k_fix walk each block from global memory, one lane per block, and
-// a chain that no speculative walk couples with (a literal-run region) moved
-// kGroup blocks per fix pass: config 4 spent 0.9 ms in k_spec and 1.95 ms in
-// 24 fix passes.  Here a 256-thread workgroup takes a tile of kTileBlocks
-// consecutive blocks (contiguous packed bytes, <= 32 KiB), stages them in LDS
-// by DMA, and each wave resolves 16 blocks cut into kSegs segments of
-// kSegBytes, one lane each:
+// ---- tile resolution (k_tile) ----
+// A 256-thread workgroup takes a tile of kTileBlocks consecutive blocks
+// (contiguous packed bytes, <= 32 KiB), stages them in LDS by DMA, and each
+// wave resolves 16 blocks cut into kSegs segments of kSegBytes, one lane
+// each:
 //   spec   lane j walks from kLead bytes before its segment (or from its
 //          chunk's start) to its first record start f >= s, then on to its
 //          exit; the lead-in lets chains from different starts couple before
@@ -276,6 +155,9 @@ __device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave
 //          is its predecessor's exit;
 //   blocks a block's entry is its first segment's, its exit its last
 //          segment's (chunk end + 1 if any segment failed), its words the sum.
+// (Round 2 walked each 512-byte block from global memory, one lane per block,
+// and a literal-run region moved 8 blocks per fix pass: config 4 spent
+// 0.9 ms in the spec walks and 1.95 ms in 24 fix passes; 2.4 ms in all now.)
 // Segments of 128 bytes keep each walk short (a lane whose spec chain missed
 // walks its whole segment; with one lane per 512-byte block that was the
 // critical path, ~100 hops, and four waves share the tile's LDS).  Positions
@@ -284,32 +166,21 @@ __device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave
 // assumes its first lane's f; fix passes (k_tile with fix = 1) re-resolve a
 // tile whose stored entry differs from the predecessor's exit, and flag a
 // pass whose last exit moved.  A region no walk couples with costs one tile
-// per pass (32 KiB) instead of kGroup blocks (4 KiB).  The results (exit,
-// entry, words per block) are k_spec + k_fix's, so the scan, check and block
-// decode follow unchanged.
-#ifndef RESYNC_TILE
-#define RESYNC_TILE 1
-#endif
-#ifndef RESYNC_SEGUNITS
-#define RESYNC_SEGUNITS 0  // 1: decode the resolved segments as units (k_units)
-#endif
-#ifndef RESYNC_SEGS
-#define RESYNC_SEGS 4
-#endif
-constexpr uint32_t kSegs = RESYNC_SEGS;                     // segments per block
+// at most one tile per pass (32 KiB); tiles later in a pass often read an
+// exit their predecessor wrote in the same pass.
+// Segments per block re-checked in round 3 (2 / 4 / 8: 2574 / 2367 / 2497 us,
+// config 4 index-free): 4.
+constexpr uint32_t kSegs = 4;                               // segments per block
 constexpr uint32_t kSegBytes = (uint32_t)kBlock / kSegs;    // 128
 constexpr uint32_t kTileWaves = kSegs;                      // (so a tile stays 64 blocks)
 constexpr uint32_t kWaveBlocks = CAPNP_WAVE / kSegs;        // 16
 constexpr uint32_t kTileBlocks = kTileWaves * kWaveBlocks;  // 64
 constexpr uint32_t kTileThreads = kTileWaves * CAPNP_WAVE;
-#ifndef RESYNC_LEAD
-#define RESYNC_LEAD 64  // spec walk lead-in (bytes); 48 -> 64: config 4 index-free -2.7 % on two boxes
-#endif
-#ifndef RESYNC_CATCHUP
-#define RESYNC_CATCHUP 16  // hops a re-walk lets its spec chain catch up per step
-#endif
-constexpr uint64_t kLead = RESYNC_LEAD;
-constexpr uint32_t kCatchUp = RESYNC_CATCHUP;
+// spec walk lead-in (bytes); 48 -> 64: config 4 index-free -2.7 % on two
+// boxes (32 / 80 / 96: 2478 / 2340 / 2295 us against 2311-2329)
+constexpr uint64_t kLead = 64;
+// hops a re-walk lets its spec chain catch up per step (32: 2439 us, slower)
+constexpr uint32_t kCatchUp = 16;
 constexpr uint32_t kTileLds = (uint32_t)(kTileBlocks * kBlock + kLead + 64);
 constexpr uint32_t kRelCap = 0xF0000000u;  // chunk ends past this are "far" (tile offsets are < 40 K)
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
@@ -442,7 +313,7 @@ __global__ void __launch_bounds__(kTileThreads)
 k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
        const uint64_t* __restrict__ bstart, uint64_t* exit, uint64_t* __restrict__ entry,
        uint64_t* __restrict__ words, uint64_t* __restrict__ blk_c, int32_t* flags, int pass,
-       int fix, uint64_t* __restrict__ seg_exit, uint32_t* __restrict__ seg_wrel) {
+       int fix) {
     extern __shared__ __align__(16) uint8_t tbuf[];
     __shared__ uint32_t wmax[kTileWaves], wneed[kTileWaves];
     const uint32_t tid = threadIdx.x;
@@ -587,18 +458,6 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     // (a segment left with an error exit -- its walk ran past the chunk, or
     // no entry reached it -- marks the whole block, so the chunk fails its check)
     uint32_t wsum = S.wd, berr = S.ex > S.b ? 1u : 0u;
-    if (seg_exit && valid) {
-        // the segment as a decode unit: its exit, and the words of the block's
-        // earlier segments (an exclusive scan over the block's kSegs lanes)
-        uint32_t pre = S.wd;
-#pragma unroll
-        for (uint32_t m = 1; m < kSegs; m <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)pre, m);
-            if (q >= m) pre += y;
-        }
-        seg_exit[k * kSegs + q] = S.ex > S.b ? b + 1 : base + S.ex;
-        seg_wrel[k * kSegs + q] = pre - S.wd;
-    }
 #pragma unroll
     for (uint32_t m = 1; m < kSegs; m <<= 1) {
         wsum += (uint32_t)__shfl_xor((int)wsum, (int)m);
@@ -694,52 +553,20 @@ k_blocks(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __rest
     blk_out[k] = out_off[c] + (out_off[c + 1] == out_off[c] ? 0 : wbase[k] - wbase[f]);
 }
 
-// The same at segment granularity (RESYNC_SEGUNITS): every resolved segment
-// is a read unit -- its records run from the previous segment's exit to its
-// own and decode to exactly its words -- so the decode's walkers follow ~30
-// words each instead of a block's ~120.  Unit u = kSegs k + q (block k,
-// segment q); a chunk that failed its check is one unit, its last.
-__global__ void __launch_bounds__(kThreads)
-k_units(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __restrict__ out_off,
-        const uint64_t* __restrict__ bstart, const uint64_t* __restrict__ seg_exit,
-        const uint32_t* __restrict__ seg_wrel, const uint64_t* __restrict__ wbase,
-        const int32_t* __restrict__ ok, uint64_t* __restrict__ u_in, uint64_t* __restrict__ u_out) {
-    const uint64_t u = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-    const uint64_t nu = kSegs * bstart[n];
-    if (u > nu) return;
-    if (u == nu) {
-        u_in[u] = in_off[n];
-        u_out[u] = out_off[n];
-        return;
-    }
-    const uint64_t k = u / kSegs;
-    const uint64_t c = chunk_of(bstart, n, k);
-    const uint64_t f = bstart[c];
-    if (ok && !ok[c]) {
-        u_in[u] = in_off[c];
-        u_out[u] = out_off[c];
-        return;
-    }
-    u_in[u] = u == kSegs * f ? in_off[c] : seg_exit[u - 1];
-    u_out[u] = out_off[c] +
-               (out_off[c + 1] == out_off[c] ? 0 : wbase[k] - wbase[f] + seg_wrel[u]);
-}
-
 // Status and consumed bytes of the chunks that failed their check: those of
-// the unit that spans the chunk (its last block, or its last segment: `per`
-// units per block).
+// the unit that spans the chunk (its last block).
 __global__ void __launch_bounds__(kThreads)
 k_fail(uint64_t n, const uint64_t* __restrict__ bstart, const int32_t* __restrict__ ok,
        const int32_t* __restrict__ blk_status, const uint64_t* __restrict__ blk_consumed,
-       int32_t* __restrict__ status, uint64_t* __restrict__ consumed, uint32_t per = 1) {
+       int32_t* __restrict__ status, uint64_t* __restrict__ consumed) {
     const uint64_t c = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (c >= n || ok[c]) return;
-    const uint64_t l = per * bstart[c + 1] - 1;  // (a failing chunk owns at least one block)
+    const uint64_t l = bstart[c + 1] - 1;  // (a failing chunk owns at least one block)
     status[c] = blk_status[l];
     if (consumed) consumed[c] = blk_consumed[l];
 }
 
-size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes, bool segs = false) {
+size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes) {
     size_t off = 0;
     auto take = [&](size_t bytes) {
         uint8_t* p = base ? base + off : nullptr;
@@ -758,15 +585,6 @@ size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes, b
     w->flags = (int32_t*)take(4 * (2 + kMaxPasses));
     w->tmp = take(tmp_bytes);
     w->tmp_bytes = tmp_bytes;
-    if (segs) {
-        const uint64_t nu = kSegs * nbb;
-        w->seg_exit = (uint64_t*)take(8 * nu);
-        w->seg_wrel = (uint32_t*)take(4 * nu);
-        w->u_in = (uint64_t*)take(8 * (nu + 1));
-        w->u_out = (uint64_t*)take(8 * (nu + 1));
-        w->u_st = (int32_t*)take(4 * nu);
-        w->u_cons = (uint64_t*)take(8 * nu);
-    }
     return off;
 }
 
@@ -781,13 +599,6 @@ uint64_t blocks_bound(uint64_t n, uint64_t total_bytes) { return total_bytes / k
 
 unsigned grid(uint64_t items) { return (unsigned)((items + kThreads - 1) / kThreads); }
 
-// The tile resolution, unless CAPNP_RESYNC_BLOCKWALK selects k_spec + k_fix
-// (diagnostic A/B).
-bool tile_mode() {
-    static const bool v = RESYNC_TILE && getenv("CAPNP_RESYNC_BLOCKWALK") == nullptr;
-    return v;
-}
-
 // Spec walks, then fix passes to the fixed point (kPassBatch per flag
 // read-back).  *converged = false after kMaxPasses passes.  Blocking.
 hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, const Ws& w,
@@ -795,32 +606,19 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
     hipError_t e;
     *passes = 0;
     *converged = true;
-    const bool tile = tile_mode();
     const unsigned tgrid = (unsigned)((nbb + kTileBlocks - 1) / kTileBlocks);
-    const uint64_t ngroups = (nbb + kGroup - 1) / kGroup;
-    if (tile)
-        k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
-                                                    w.words, w.spec_exit, w.flags, 0, 0,
-                                                    w.seg_exit, w.seg_wrel);
-    else
-        k_spec<<<grid(nbb), kThreads, walk_lds(), s>>>(d_in, in_off, n, w.bstart, w.spec_exit,
-                                                       w.spec_words, w.exit, w.entry, w.words);
+    k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
+                                                w.words, w.spec_exit, w.flags, 0, 0);
     int pass = 0;
     for (;;) {
         if (pass >= g_max_passes) {
             *converged = false;
             break;
         }
-        for (int i = 0; i < kPassBatch && pass < g_max_passes; i++, pass++) {
-            if (tile)
-                k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
-                                                            w.entry, w.words, w.spec_exit, w.flags,
-                                                            pass, 1, w.seg_exit, w.seg_wrel);
-            else
-                k_fix<<<grid(ngroups), kThreads, walk_lds(), s>>>(
-                    d_in, in_off, n, w.bstart, w.spec_exit, w.spec_words, w.exit, w.entry,
-                    w.words, w.flags, pass);
-        }
+        for (int i = 0; i < kPassBatch && pass < g_max_passes; i++, pass++)
+            k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
+                                                        w.entry, w.words, w.spec_exit, w.flags,
+                                                        pass, 1);
         int32_t last = 0, capped = 0;
         if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
             hipSuccess)
@@ -863,7 +661,7 @@ extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes) {
     const uint64_t nbb = blocks_bound(n, total_bytes);
     const uint64_t m = nbb > n + 1 ? nbb : n + 1;
     Ws w;
-    return carve(&w, nullptr, n, nbb, scan_tmp_bytes(m), RESYNC_SEGUNITS) + 256;
+    return carve(&w, nullptr, n, nbb, scan_tmp_bytes(m)) + 256;
 }
 
 // Blocking (the fix passes read a flag back).  On return, *passes = fix passes
@@ -893,7 +691,7 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
     const uint64_t m = nbb > n + 1 ? nbb : n + 1;
     Ws w;
     uint8_t* base = (uint8_t*)(((uintptr_t)d_ws + 255) & ~uintptr_t(255));
-    if (carve(&w, base, n, nbb, scan_tmp_bytes(m), RESYNC_SEGUNITS) + (base - (uint8_t*)d_ws) >
+    if (carve(&w, base, n, nbb, scan_tmp_bytes(m)) + (base - (uint8_t*)d_ws) >
         ws_bytes)
         return hipErrorInvalidValue;
     int32_t hflags[2] = {0, 0};
@@ -913,12 +711,10 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
         if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.words, w.wbase, (int)nbb, s)) !=
             hipSuccess)
             return e;
-        int32_t* bad = nullptr;
-        if (tile_mode()) {  // (blk_c in spec_exit, bad in spec_words: both dead until k_blocks)
-            bad = reinterpret_cast<int32_t*>(w.spec_words);
-            if ((e = hipMemsetAsync(bad, 0, 4 * n, s)) != hipSuccess) return e;
-            k_mark<<<grid(nbb), kThreads, 0, s>>>(w.exit, w.spec_exit, d_in_off, w.bstart, n, bad);
-        }
+        // (blk_c in spec_exit, bad in spec_words: both dead until k_blocks)
+        int32_t* bad = reinterpret_cast<int32_t*>(w.spec_words);
+        if ((e = hipMemsetAsync(bad, 0, 4 * n, s)) != hipSuccess) return e;
+        k_mark<<<grid(nbb), kThreads, 0, s>>>(w.exit, w.spec_exit, d_in_off, w.bstart, n, bad);
         k_check<<<grid(n), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit, w.words,
                                              w.wbase, bad, w.ok, d_status, d_consumed, w.flags);
         uint64_t nb = 0;
@@ -934,27 +730,15 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
         uint64_t* blk_out = w.entry;
         int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
         uint64_t* blk_consumed = w.words;  // (dead after the wbase scan and the check)
-        uint32_t per = 1;
-        if (RESYNC_SEGUNITS && w.seg_exit) {
-            per = kSegs;
-            blk_in = w.u_in;
-            blk_out = w.u_out;
-            blk_status = w.u_st;
-            blk_consumed = w.u_cons;
-            k_units<<<grid(per * nb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart,
-                                                            w.seg_exit, w.seg_wrel, w.wbase,
-                                                            w.ok, blk_in, blk_out);
-        } else {
-            k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit,
-                                                       w.wbase, w.ok, blk_in, blk_out);
-        }
-        if ((e = capnp_launch_unpack(d_in, blk_in, per * nb, 0, d_out, blk_out, blk_status,
+        k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit,
+                                                   w.wbase, w.ok, blk_in, blk_out);
+        if ((e = capnp_launch_unpack(d_in, blk_in, nb, 0, d_out, blk_out, blk_status,
                                      hflags[1] ? blk_consumed : nullptr, nullptr, s)) != hipSuccess)
             return e;
         if (hflags[1]) {
             if (serial) *serial = 3;
             k_fail<<<grid(n), kThreads, 0, s>>>(n, w.bstart, w.ok, blk_status, blk_consumed,
-                                                d_status, d_consumed, per);
+                                                d_status, d_consumed);
         }
     } else {
         if (serial) *serial = 1;

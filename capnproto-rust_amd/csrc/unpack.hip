@@ -33,27 +33,6 @@
 #include <stdlib.h>
 #include "../../include/capnp_packed.h"
 
-#ifndef UNPACK_SYNC_WAVES
-#define UNPACK_SYNC_WAVES 0  // 1: wave-autonomous sync kernel (measured slower)
-#endif
-#ifndef UNPACK_GROUPS
-#define UNPACK_GROUPS 2  // expansion groups in flight per wave
-#endif
-#ifndef UNPACK_MIN_WAVES
-#define UNPACK_MIN_WAVES 8  // __launch_bounds__ waves per SIMD of the tile kernel
-#endif
-#ifndef UNPACK_HOPIF
-#define UNPACK_HOPIF 1  // phase A hop under an exec mask (0: branch-free selects)
-#endif
-#ifndef UNPACK_PHASEA_UNROLL
-#define UNPACK_PHASEA_UNROLL 1
-#endif
-#ifndef UNPACK_EXP3
-#define UNPACK_EXP3 1  // expand reads three aligned dwords (0: two aligned qwords)
-#endif
-#ifndef UNPACK_EXP
-#define UNPACK_EXP 0  // diagnostic variants of the segment walk (scripts/uvar.py)
-#endif
 #ifndef UNPACK_PROF
 #define UNPACK_PROF 0  // phase timers (scripts/unpack_prof.py); 0 = product
 #endif
@@ -65,27 +44,6 @@ __device__ unsigned long long g_uprof[8];
 #define UPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
 #else
 #define UPROF_T(v)
-#endif
-
-#ifndef UNPACK_WT_DEBUG
-#define UNPACK_WT_DEBUG 0
-#endif
-#if UNPACK_WT_DEBUG
-__device__ unsigned long long g_wt_ev_n;
-__device__ uint32_t g_wt_ev[64 * 12];
-__device__ __forceinline__ void wt_event(uint32_t kind, uint32_t b, uint32_t c, uint32_t q,
-                                         uint32_t w, uint32_t c2, uint32_t q2, uint32_t w2,
-                                         uint32_t err, uint32_t x, uint32_t y) {
-    const unsigned long long k = atomicAdd(&g_wt_ev_n, 1ull);
-    if (k < 64) {
-        uint32_t* e = g_wt_ev + 12 * k;
-        e[0] = blockIdx.x; e[1] = kind; e[2] = b; e[3] = c; e[4] = q; e[5] = w;
-        e[6] = c2; e[7] = q2; e[8] = w2; e[9] = err; e[10] = x; e[11] = y;
-    }
-}
-#define WT_EVENT(...) wt_event(__VA_ARGS__)
-#else
-#define WT_EVENT(...) ((void)0)
 #endif
 
 namespace {
@@ -131,16 +89,8 @@ __device__ __forceinline__ uint64_t expand_word(uint32_t tag, uint64_t packed) {
 
 // Global path: lane l < NL of the wave decodes chunk c0 + l (c < c_end);
 // `desc` is this wave's NL x 64 descriptor table (NL * 128 bytes of LDS).
-#ifndef UNPACK_GLOBAL_NOINLINE
-#define UNPACK_GLOBAL_NOINLINE 0
-#endif
-#if UNPACK_GLOBAL_NOINLINE
-#define UNPACK_GLOBAL_ATTR __attribute__((noinline))
-#else
-#define UNPACK_GLOBAL_ATTR
-#endif
 template <uint32_t NL>
-__device__ UNPACK_GLOBAL_ATTR void unpack_global(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+__device__ void unpack_global(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                               uint64_t c0, uint64_t c_end, uint64_t* __restrict__ out,
                               const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
                               uint64_t* __restrict__ consumed, uint16_t (*desc)[CAPNP_WAVE],
@@ -413,20 +363,15 @@ constexpr uint32_t kMaxTileChunks = kWaves * CAPNP_WAVE;
 // ---------------------------------------------------------------------------
 // Staged path.
 
-// Tile tables sized for UNPACK_TILE_WORDS output words (~5.8 packed bytes per
+// Tile tables sized for kTileWords output words (~5.8 packed bytes per
 // word of capacity: P/U up to 0.72; a tile with more is cut into sub-tiles).  The walk and the expansion are latency
 // chains, so throughput scales with resident workgroups: smaller tiles, more
 // of them per CU (2048 words: ~16 KB of LDS, 9 workgroups per CU).
-#ifndef UNPACK_TILE_WORDS
-#define UNPACK_TILE_WORDS 2048
-#endif
-constexpr uint32_t kTileWords = UNPACK_TILE_WORDS;   // descriptor capacity (output words)
+constexpr uint32_t kTileWords = 2048;
+constexpr uint32_t kGroups = 2;  // expansion groups in flight per wave   // descriptor capacity (output words)
 // LDS capacity for packed bytes: 5.8 bytes per word of capacity (carsales
 // segments pack to 5.6), what is left of 20 KiB per workgroup (8 per CU)
-#ifndef UNPACK_TILE_BYTES
-#define UNPACK_TILE_BYTES (kTileWords * 93 / 16)
-#endif
-constexpr uint32_t kTileBytes = UNPACK_TILE_BYTES;
+constexpr uint32_t kTileBytes = kTileWords * 93 / 16;
 // The global path (tiles that do not fit) runs on as many waves as the
 // staged tables' LDS can hold descriptor tables for (8 KiB each).
 constexpr uint32_t kGlobalWaves = kTileWords >= 4096 ? 4 : 2;
@@ -473,24 +418,12 @@ __device__ __forceinline__ uint64_t expand_desc(const uint8_t* B, const uint64_t
     // off 8-byte alignment is replayed at 64 LDS cycles, MI355X_MICROARCH.md
     // §LDS, and was half the LDS time of this kernel)
     const uint32_t src = raw ? pos : pos + 1;
-#if UNPACK_EXP3
     // three naturally aligned dwords from src & ~3 (never misaligned) and a
     // funnel shift by src & 3 (alignbyte reads only the low two bits)
     const uint32_t* q4 = reinterpret_cast<const uint32_t*>(B + (src & ~3u));
     const uint32_t x0 = q4[0], x1 = q4[1], x2 = q4[2];
     const uint64_t v = ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, src) << 32) |
                        __builtin_amdgcn_alignbyte(x1, x0, src);
-#else
-    const uint64_t* q8 = reinterpret_cast<const uint64_t*>(B + (src & ~7u));
-    const uint64_t a = q8[0], b = q8[1];
-    const uint32_t o = src & 7u, sh = o & 3u;
-    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32);
-    const uint32_t b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
-    const bool up = o >= 4;
-    const uint32_t x0 = up ? a1 : a0, x1 = up ? b0 : a1, x2 = up ? b1 : b0;
-    const uint64_t v = ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, sh) << 32) |
-                       __builtin_amdgcn_alignbyte(x1, x0, sh);
-#endif
     const uint32_t t = none ? 0u : (raw ? 0xFFu : tag);
     const uint64_t sv = sel[t];
     const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
@@ -503,21 +436,6 @@ __device__ __forceinline__ uint64_t expand_desc(const uint8_t* B, const uint64_t
 constexpr uint32_t kSyncWords = CAPNP_SYNC_WORDS;
 constexpr uint32_t kSyncNone = 0xFFFFFFFFu;
 
-// Block walk without the index (UNPACK_SPEC): a chunk's packed bytes are cut
-// into kSpecBlk-byte blocks, one thread each.  Tables live over the selector
-// table (reloaded before the expansion) and the sync-walk tables.
-constexpr uint32_t kSpecBlk = 64;
-struct SpecTabs {
-    uint16_t bpos[kThreads];             // block start (LDS position)
-    uint16_t bend[kThreads];             // block end
-    uint8_t bchk[kThreads];              // chunk of the block
-    uint16_t bfirst[kStageChunks + 1];   // first block of each chunk
-};
-struct SpecOut {
-    uint16_t bx[kThreads];  // exit of the block's walk (first record boundary at or past its end)
-    uint16_t bw[kThreads];  // words the walk decoded
-};
-
 // The staged tables for tiles of up to TW output words and TB packed bytes
 // (chunk tiles: kTileWords / kTileBytes; word tiles: kWtWords / kWtBytes).
 template <uint32_t TW, uint32_t TB>
@@ -526,7 +444,6 @@ struct StageSmemT {
     static constexpr uint32_t kSeg = TW / kSyncWords + 2;
     union {
         uint64_t sel[256];  // expand_selector(tag): 0x00 -> zeros, 0xFF -> identity
-        SpecTabs sp;
     };
     uint8_t badc[kStageChunks];     // 1 = the chunk needs the exact walk
     uint32_t cw[kStageChunks + 1];  // chunk word offsets (tile-relative)
@@ -536,13 +453,11 @@ struct StageSmemT {
             uint32_t ent[kSeg];             // sync walk: entry of segment b (b >= 1)
             uint8_t segc[kSeg];             // sync walk: chunk that holds segment b's first word
         };
-        SpecOut so;
     };
     // word tiles (unpack_wt_kernel): walk start of segment 0 (position + 1,
     // word), the state the last walker must reach at the tile end when the
     // last chunk continues, words of the first chunk before the tile, flags
     uint32_t wt_q0, wt_w0, wt_qB, wt_wB, wt_pre, wt_pl;
-    uint32_t spec_nb;  // block walk: blocks in the tile
     alignas(16) uint8_t bytes[TB + 16];
     alignas(16) uint16_t dpos[TW + 2 * CAPNP_WAVE];  // [TW + 2 lane]: dummy slots
 };
@@ -560,26 +475,16 @@ union USmem {
 // address is a misaligned LDS access: replayed, and SQ_LDS_UNALIGNED_STALL
 // was half of this kernel's LDS cycles.  The tag is extracted from its
 // aligned dword instead (32-bit reads are never misaligned).
-// UNPACK_RECB=1: three ds_read_u8 kept apart by volatile (a byte read is
-// never misaligned): all three share q's address register through the
-// offset field, so the hop spends no VALU on addressing.
-#ifndef UNPACK_RECB
-#define UNPACK_RECB 0  // measured slower (volatile pins the reads' order): 427 vs 403 us
-#endif
+// (Three ds_read_u8 kept apart by volatile -- a byte read is never
+// misaligned, and all three share q's address register -- measured slower:
+// 427 vs 403 us; volatile pins the reads' order.)
 __device__ __forceinline__ void rec_bytes(const uint8_t* B, uint32_t q, uint32_t& tag,
                                           uint32_t& b1, uint32_t& b9) {
-#if UNPACK_RECB
-    const volatile uint8_t* V = B;
-    tag = V[q - 1u];
-    b1 = V[q];
-    b9 = V[q + 8u];
-#else
     const uint32_t p = q - 1u;
     const uint32_t dw = *reinterpret_cast<const uint32_t*>(B + (p & ~3u));
     tag = __builtin_amdgcn_ubfe(dw, (p & 3u) * 8u, 8u);
     b1 = B[q];
     b9 = B[q + 8];
-#endif
 }
 
 // Exact status of a record that failed the fast check in walk_chunk, in the
@@ -766,7 +671,6 @@ __device__ __forceinline__ void seg_start(SM& S, uint32_t nc, uint32_t b, uint32
         w = wn;
     }
     if (!ok) {
-        if constexpr (WT) if (mark) WT_EVENT(4, b, c, q, w, e, off, d, 0, sb, cwe);
         if (mark) mark_bad(S, c, marked);
         q = cpe1;
         w = cwe;
@@ -808,12 +712,11 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     // word, so a lane reaches stopw within kSyncWords hops; a lane already
     // there only sends its store to the dummy slot).  Phase B below handles
     // chunk ends and whatever is left.
-#if UNPACK_HOPIF
-    // (UNPACK_HOPIF: the hop runs under the exec mask of the lanes still
+    // (the hop runs under the exec mask of the lanes still
     // below stopw, so the state updates need no selects and the record
     // checks collect in a wave mask)
     uint64_t errm = 0;
-#pragma unroll UNPACK_PHASEA_UNROLL
+#pragma unroll 1  // (x2 / x4 / x8 measured within noise)
     for (uint32_t it = 0; it < kSyncWords; it++) {
         if (w < stopw) {
             const bool isz = tag == 0, isf = tag == 0xFF;
@@ -841,31 +744,6 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
 #if UNPACK_PROF
     const uint64_t lt1 = __builtin_amdgcn_s_memtime();
 #endif
-#else
-#pragma unroll UNPACK_PHASEA_UNROLL
-    for (uint32_t it = 0; it < kSyncWords; it++) {
-        const bool hop = w < stopw;
-        const bool isz = tag == 0, isf = tag == 0xFF;
-        const uint32_t fx = isf ? 8u * b9 + 1u : 0u;
-        const uint32_t qe = __builtin_popcount(tag) + q + (isz ? 1u : 0u) + fx + 1u;
-        const uint32_t qn = qe < cpe1 ? qe : cpe1;
-        uint32_t ntag, nb1, nb9;
-        rec_bytes(B, qn, ntag, nb1, nb9);
-        const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
-        const uint32_t wn0 = w + 1u + cnt;
-        err = err || (hop && (qe > cpe1 || wn0 > cwe));
-        const uint32_t wn = wn0 < cwe ? wn0 : cwe;
-        S.dpos[hop ? w : dummy] = (uint16_t)(q - 1u);
-        if (ballot64(hop && isf && wn > w + 1)) {  // literal-run words (rare)
-            if (hop && isf) lit_entries(S, w, q - 1u, (WT && wn > wlim ? wlim : wn) - w - 1);
-        }
-        q = hop ? qn : q;
-        w = hop ? wn : w;
-        tag = hop ? ntag : tag;
-        b1 = hop ? nb1 : b1;
-        b9 = hop ? nb9 : b9;
-    }
-#endif
     // Fast end: when every lane reached its segment end within phase A (no
     // chunk ends inside a segment: aligned chunk sizes, the usual case) the
     // state "end of chunk c" already equals "start of chunk c + 1", so the
@@ -873,10 +751,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     // chunks, which only costs an extra exact walk); only the last segment's
     // lane steps past the tile's last chunk.  Phase B's one bookkeeping
     // round cost ~2500 cycles per wave (UNPACK_PROF).
-#ifndef UNPACK_FASTEND
-#define UNPACK_FASTEND 1
-#endif
-    const bool fastend = UNPACK_FASTEND && ballot64(!(w >= eb || c >= nc)) == 0;
+    const bool fastend = ballot64(!(w >= eb || c >= nc)) == 0;
     if (fastend) {
         if (last && c < nc && w == cwe) {
             if (err || (S.cw[c] < cwe && q != cpe1)) mark_bad(S, c, marked);
@@ -896,7 +771,6 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
                 if (w == cwe) {
                     // a non-empty chunk must end exactly at its packed end
                     if (err || (S.cw[c] < cwe && q != cpe1)) {
-                        if constexpr (WT) WT_EVENT(5, b, c, q, w, cpe1, cwe, S.cw[c], err, sb, eb);
                         mark_bad(S, c, marked);
                     }
                     err = false;
@@ -920,24 +794,16 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
         const uint32_t fx = isf ? 8u * b9 + 1u : 0u;
         const uint32_t qe = __builtin_popcount(tag) + q + (isz ? 1u : 0u) + fx + 1u;
         const uint32_t qn = qe < cpe1 ? qe : cpe1;
-#if UNPACK_EXP == 2  // one unaligned 16-byte read per record
-        typedef uint4 u4u __attribute__((aligned(1)));
-        const uint4 nv = *reinterpret_cast<const u4u*>(B + qn - 1);
-        const uint32_t ntag = nv.x & 0xFFu, nb1 = (nv.x >> 8) & 0xFFu, nb9 = (nv.z >> 8) & 0xFFu;
-#else
         uint32_t ntag, nb1, nb9;
         rec_bytes(B, qn, ntag, nb1, nb9);
-#endif
         const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
         const uint32_t wn0 = w + 1u + cnt;
         err = err || (hop && (qe > cpe1 || wn0 > cwe));
         const uint32_t wn = wn0 < cwe ? wn0 : cwe;  // (an overrun ends the chunk)
-#if UNPACK_EXP != 1  // 1: timing only, no descriptors
         S.dpos[hop ? w : dummy] = (uint16_t)(q - 1u);
         if (ballot64(hop && isf && wn > w + 1)) {  // literal-run words (rare)
             if (hop && isf) lit_entries(S, w, q - 1u, (WT && wn > wlim ? wlim : wn) - w - 1);
         }
-#endif
         q = hop ? qn : q;
         w = hop ? wn : w;
         tag = ntag;
@@ -948,9 +814,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     if (lane_id() == 0 && g_utrace) {
         g_utrace[blockIdx.x * 8 + 5] = iters;
         g_utrace[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memtime() - lt0;
-#if UNPACK_HOPIF
         g_utrace[blockIdx.x * 8 + 7] = lt1 - lt0;
-#endif
     }
 #endif
     // the walks must meet
@@ -962,11 +826,9 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
                 // (c == nc: the walk reached the chunk's end exactly, just past
                 // the tile, and passed its end check)
                 if (c + 1 < nc || q != S.wt_qB || w != S.wt_wB || err) {
-                    WT_EVENT(1, b, c, q, w, nc, S.wt_qB, S.wt_wB, err, sb, eb);
                     mark_bad(S, nc - 1, marked);
                 }
         } else if (c < nc) {
-            if constexpr (WT) WT_EVENT(2, b, c, q, w, nc, 0, 0, err, sb, eb);
             mark_bad(S, c, marked);
         }
     } else {
@@ -975,7 +837,6 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
         // (positions and words decide: "end of chunk c" and "start of chunk
         // c+1" are the same state)
         if (q2 != q || w2 != w || err) {
-            if constexpr (WT) WT_EVENT(3, b, c, q, w, c2, q2, w2, err, sb, eb);
             if (c < nc) mark_bad(S, c, marked);
             mark_bad(S, c2, marked);
         }
@@ -983,246 +844,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     return marked;
 }
 
-#ifndef UNPACK_SPEC
-// index-free tiles: 1 = block walk (spec_tile), 0 = one walker lane per chunk.
-// Measured at config 2: walk phase 23.3 vs 25.0 us per tile, 986 vs 997 us
-// per launch: the block walk shortens the chain 3x but walks every record
-// twice (plus a confirming round) on 10x the lanes, so the tile's total hop
-// work grows 3.4x and the CU saturates; kept as an option, off.
-#define UNPACK_SPEC 2  // 2 = segment walk (spec_seg_tile, below)
-#endif
-#ifndef UNPACK_SPEC_ROUNDS
-#define UNPACK_SPEC_ROUNDS 8  // fix-up rounds before a chunk falls to the exact walk
-#endif
-
-// Block walk: from p while p < be inside a chunk whose bytes end at pe ->
-// the exit (first record boundary at or past be), the words decoded, and
-// whether a record ran past the chunk (then the chunk takes the exact walk).
-__device__ __forceinline__ void spec_walk(const uint8_t* B, uint32_t p, uint32_t be, uint32_t pe,
-                                          uint32_t& x, uint32_t& words, bool& err) {
-    uint32_t w = 0;
-    err = false;
-    while (p < be) {
-        uint32_t tag, b1, b9;
-        rec_bytes(B, p + 1, tag, b1, b9);
-        const bool isz = tag == 0, isf = tag == 0xFF;
-        const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
-        const uint32_t q = p + 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) +
-                           (isf ? 8u * cnt : 0u);
-        if (q > pe) {
-            err = true;
-            break;
-        }
-        w += 1u + cnt;
-        p = q;
-    }
-    x = p;
-    words = w;
-}
-
-// spec_walk that also marks every record start it visits in `M` (bit
-// p - s; the block [s, be) is at most 64 bytes).
-__device__ __forceinline__ void spec_walk_m(const uint8_t* B, uint32_t s, uint32_t be,
-                                            uint32_t pe, uint64_t& M, uint32_t& x,
-                                            uint32_t& words, bool& err) {
-    uint32_t w = 0, p = s;
-    uint64_t m = 0;
-    err = false;
-    while (p < be) {
-        uint32_t tag, b1, b9;
-        rec_bytes(B, p + 1, tag, b1, b9);
-        m |= 1ull << (p - s);
-        const bool isz = tag == 0, isf = tag == 0xFF;
-        const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
-        const uint32_t q = p + 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) +
-                           (isf ? 8u * cnt : 0u);
-        if (q > pe) {
-            err = true;
-            break;
-        }
-        w += 1u + cnt;
-        p = q;
-    }
-    M = m;
-    x = p;
-    words = w;
-}
-
-// The descriptors of a block whose walk is final: records from p to x, the
-// first at tile word w; false if a run overruns the chunk's words (wend).
-template <class SM>
-__device__ __forceinline__ bool spec_desc(SM& S, uint32_t p, uint32_t x, uint32_t w,
-                                          uint32_t wend) {
-    while (p < x) {
-        uint32_t tag, b1, b9;
-        rec_bytes(S.bytes, p + 1, tag, b1, b9);
-        const bool isz = tag == 0, isf = tag == 0xFF;
-        const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
-        if (w + 1u + cnt > wend) return false;
-        S.dpos[w] = (uint16_t)p;
-        if (isf && cnt) lit_entries(S, w, p, cnt);
-        w += 1u + cnt;
-        p += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) + (isf ? 8u * cnt : 0u);
-    }
-    return true;
-}
-
-// Index-free walk of a staged tile, one thread per kSpecBlk-byte block of a
-// chunk ("resync" inside a tile).  Round 0 walks every block from its first
-// byte (the chunk's first block from the chunk start: exact); then each
-// block's entry becomes the furthest exit of the blocks before it in its
-// chunk, and blocks whose entry moved walk again, until no entry moves.  At
-// that fixed point every block starts where its predecessor ended, so the
-// walks chain exactly from the chunk start; a chunk is fast-path only if its
-// last block ends exactly at its packed end with exactly its words and no
-// record ran past it.  Then the descriptors are written from the final
-// entries (word offsets from the blocks' word counts), and every other chunk
-// takes the exact serial walk.  Speculation changes the speed only.
-template <class SM>
-__device__ __forceinline__ void spec_tile(SM& S, uint64_t ca, uint32_t nc,
-                                          int32_t* __restrict__ status,
-                                          uint64_t* __restrict__ consumed, uint32_t tid,
-                                          uint32_t lane, uint32_t wave) {
-    if (wave == 0) {  // block table, lane = chunk
-        uint32_t nb = 0, len = 0, n = 0;
-        if (lane < nc) {
-            len = S.cp[lane + 1] - S.cp[lane];
-            n = S.cw[lane + 1] - S.cw[lane];
-            nb = (n && len) ? (len + kSpecBlk - 1) / kSpecBlk : 0u;
-            if (n && !len) S.badc[lane] = 1;  // (FailedToFill: the exact walk says so)
-        }
-        uint32_t incl = nb;
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)incl, d, 64);
-            if (lane >= d) incl += t;
-        }
-        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        const uint32_t first = incl - nb;
-        if (lane < nc) S.sp.bfirst[lane] = (uint16_t)first;
-        if (total <= kThreads && lane < nc)
-            for (uint32_t j = 0; j < nb; j++) {
-                const uint32_t b = S.cp[lane] + j * kSpecBlk;
-                const uint32_t e = b + kSpecBlk < S.cp[lane + 1] ? b + kSpecBlk : S.cp[lane + 1];
-                S.sp.bpos[first + j] = (uint16_t)b;
-                S.sp.bend[first + j] = (uint16_t)e;
-                S.sp.bchk[first + j] = (uint8_t)lane;
-            }
-        if (lane == 0) S.spec_nb = total;
-    }
-    __syncthreads();
-    const uint32_t NB = S.spec_nb;
-    if (NB > kThreads) {  // (cannot happen: <= kTileBytes / 64 + 64 blocks)
-        if (tid < nc) S.badc[tid] = 1;
-    } else {
-        const bool act = tid < NB;
-        uint32_t c = 0, sb = 0, be = 0, pe = 0, first = 0;
-        if (act) {
-            c = S.sp.bchk[tid];
-            first = S.sp.bfirst[c];
-            sb = tid == first ? S.cp[c] : S.sp.bpos[tid];
-            be = S.sp.bend[tid];
-            pe = S.cp[c + 1];
-        }
-        // round 0: every block walks from its first byte (a chunk's first
-        // block from the chunk start: exact), marking the record starts it
-        // visits
-        uint64_t M = 0;
-        uint32_t x0 = sb, w0 = 0;
-        bool err0 = false;
-        if (act) spec_walk_m(S.bytes, sb, be, pe, M, x0, w0, err0);
-        uint32_t e = sb, x = x0, w = w0;
-        bool err = err0;
-        if (act) {
-            S.so.bx[tid] = (uint16_t)x;
-            S.so.bw[tid] = (uint16_t)(w < 0xFFFFu ? w : 0xFFFFu);
-        }
-        // Then each block takes its predecessor's exit as its entry.  The
-        // walks are deterministic, so if the round-0 walk visited that entry
-        // it is the exact walk from there on: same exit, words less those
-        // decoded before the entry (a short walk), and no re-walk.  Otherwise
-        // it walks again from the entry.  Repeat until no entry moves: then
-        // every block starts where its predecessor ended and, by induction
-        // from the chunk start, every walk is exact.
-        for (uint32_t r = 0;; r++) {
-            __syncthreads();
-            bool ch = false;
-            if (act && tid != first) {
-                const uint32_t xp = S.so.bx[tid - 1];
-                if (xp != e) {
-                    ch = true;
-                    e = xp;
-                    if (xp >= be) {  // a record from an earlier block covers this one
-                        x = xp;
-                        w = 0;
-                        err = false;
-                    } else if (xp >= sb && ((M >> (xp - sb)) & 1u)) {
-                        uint32_t xb, wb;
-                        bool eb;
-                        spec_walk(S.bytes, sb, xp, pe, xb, wb, eb);
-                        x = x0;
-                        w = w0 - wb;
-                        err = err0;
-                    } else {
-                        spec_walk(S.bytes, xp, be, pe, x, w, err);
-                    }
-                }
-            }
-            const bool any = __syncthreads_or(ch);
-            if (!any) break;
-            if (r + 1 >= UNPACK_SPEC_ROUNDS) {  // not settled: the exact walk decides
-                if (ch) S.badc[c] = 1;
-                break;
-            }
-            if (ch) {
-                S.so.bx[tid] = (uint16_t)x;
-                S.so.bw[tid] = (uint16_t)(w < 0xFFFFu ? w : 0xFFFFu);
-            }
-        }
-        if (act && err) S.badc[c] = 1;
-        __syncthreads();
-        // chunk check: its last block ends at its end with exactly its words
-        if (tid < nc && !S.badc[tid]) {
-            const uint32_t n = S.cw[tid + 1] - S.cw[tid];
-            if (n && S.cp[tid + 1] > S.cp[tid]) {
-                const uint32_t f = S.sp.bfirst[tid];
-                const uint32_t l = f + (S.cp[tid + 1] - S.cp[tid] + kSpecBlk - 1) / kSpecBlk - 1;
-                uint32_t sw = 0;
-                for (uint32_t j = f; j <= l; j++) sw += S.so.bw[j];
-                if (S.so.bx[l] != S.cp[tid + 1] || sw != n) S.badc[tid] = 1;
-            }
-        }
-        __syncthreads();
-        if (act && !S.badc[c]) {
-            uint32_t wa = S.cw[c];
-            for (uint32_t j = first; j < tid; j++) wa += S.so.bw[j];
-            if (!spec_desc(S, e, S.so.bx[tid], wa, S.cw[c + 1])) S.badc[c] = 1;
-        }
-    }
-    __syncthreads();
-    if (tid < nc) {
-        const uint64_t cc = ca + tid;
-        if (S.badc[tid]) {  // exact serial walk of the chunk
-#if UNPACK_PROF
-            atomicAdd(&g_uprof[0], 1ull);
-#endif
-            const uint32_t wa = S.cw[tid], wz = S.cw[tid + 1];
-            for (uint32_t i = wa; i < wz; i++) S.dpos[i] = kNone;
-            int32_t st;
-            uint32_t used;
-            walk_chunk(S, S.cp[tid], S.cp[tid + 1], wa, wz - wa, st, used);
-            status[cc] = st;
-            if (consumed) consumed[cc] = used;
-        } else {
-            status[cc] = ST_OK;
-            if (consumed)
-                consumed[cc] = S.cw[tid + 1] > S.cw[tid] ? S.cp[tid + 1] - S.cp[tid] : 0u;
-        }
-    }
-    __syncthreads();
-    S.sel[tid] = kExpandTable.s[tid];  // (the block tables overlaid it)
-}
-
-// Index-free walk of a staged tile on every thread (UNPACK_SPEC 2, tiles of
+// Index-free walk of a staged tile on every thread (tiles of
 // at most 16 chunks): each chunk's packed bytes are cut into S = 16 equal
 // byte segments, one thread each, so a chunk's ~117-record
 // chain becomes S chains of ~117 / S records and all four waves walk
@@ -1244,13 +866,9 @@ __device__ __forceinline__ void spec_tile(SM& S, uint64_t ca, uint32_t nc,
 //   3. desc: word bases by a scan of the segment words; each thread writes
 //      the descriptors of its records, from its entry to its exit.
 // Speculation changes the speed only, never the result.
-#ifndef UNPACK_SEG_OVERLAP
-#define UNPACK_SEG_OVERLAP 48  // config 2 nosync: 0 -> 724 us, 16 -> 699, 32 -> 646, 48 -> 614, 64 -> 640
-#endif
-constexpr uint32_t kSegOverlap = UNPACK_SEG_OVERLAP;  // spec walk lead-in (bytes)
-#ifndef UNPACK_DESC_MASK
-#define UNPACK_DESC_MASK 0  // 1: descriptors from the spec walk's record-start mask (below)
-#endif
+// spec walk lead-in (bytes); config 2 nosync: 0 -> 724 us, 16 -> 699,
+// 32 -> 646, 48 -> 614, 64 -> 640 (re-checked in round 3: 40-64 within noise)
+constexpr uint32_t kSegOverlap = 48;
 constexpr uint32_t kSegChunks = 16;  // tiles of at most this many chunks take the segment walk
 
 // One record hop (the walk's loops stop once p >= the segment end, so a
@@ -1289,18 +907,7 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
     uint32_t p = s0, w = 0;
     while (act && p < sb) seg_hop(S.bytes, p, w);
     const uint32_t f = p, wf = w;
-#if UNPACK_DESC_MASK
-    // the spec chain's record starts in the segment, bit p - f (a segment
-    // whose starts reach past 64 bytes keeps the walk below)
-    uint64_t smask = 0;
-    while (act && p < se) {
-        smask |= (p - f < 64u) ? (1ull << (p - f)) : 0ull;
-        seg_hop(S.bytes, p, w);
-    }
-    const bool mask_ok = se - f <= 64u;
-#else
     while (act && p < se) seg_hop(S.bytes, p, w);
-#endif
     const bool serr = p > pe;  // (a record past the chunk end: garbage, or j = 0's error)
     const uint32_t xs = serr ? 0u : p, ws = w - wf;
 #if UNPACK_PROF
@@ -1371,39 +978,6 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
     const bool chunk_ok = act && (bad_m & gm) == 0 && tot == n && xl == pe && n > 0 && pe > cs;
     if (act && j == 0) S.badc[c] = chunk_ok ? 0 : 1;
     // 3. descriptors of the good chunks: records from the entry to the exit
-#if UNPACK_DESC_MASK
-    if (chunk_ok && e == f && mask_ok) {
-        // the segment kept its spec chain: its record starts are the mask's
-        // bits, so the tag reads do not wait on each other (two records a
-        // round, their reads issued together)
-        uint32_t ww = S.cw[c] + incl - wd;
-        uint64_t m = smask;
-        while (m) {
-            const uint32_t q0 = f + (uint32_t)__builtin_ctzll(m);
-            m &= m - 1;
-            const bool two = m != 0;
-            const uint32_t q1 = two ? f + (uint32_t)__builtin_ctzll(m) : q0;
-            if (two) m &= m - 1;
-            uint32_t t0, a1, a9, t1, c1, c9;
-            rec_bytes(S.bytes, q0 + 1u, t0, a1, a9);
-            rec_bytes(S.bytes, q1 + 1u, t1, c1, c9);
-            {
-                const bool isz = t0 == 0, isf = t0 == 0xFF;
-                const uint32_t cnt = isz ? a1 : (isf ? a9 : 0u);
-                S.dpos[ww] = (uint16_t)q0;
-                if (isf && cnt) lit_entries(S, ww, q0, cnt);
-                ww += 1u + cnt;
-            }
-            if (two) {
-                const bool isz = t1 == 0, isf = t1 == 0xFF;
-                const uint32_t cnt = isz ? c1 : (isf ? c9 : 0u);
-                S.dpos[ww] = (uint16_t)q1;
-                if (isf && cnt) lit_entries(S, ww, q1, cnt);
-                ww += 1u + cnt;
-            }
-        }
-    } else
-#endif
     if (chunk_ok) {
         uint32_t q = e, ww = S.cw[c] + incl - wd;
         while (q < x) {
@@ -1445,9 +1019,6 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
 // One staged sub-tile: chunks [ca, cb) whose packed bytes, output words and
 // count fit the LDS tables (stage, walk, expand).  All threads of the
 // workgroup call it; it ends after its last LDS access of the expansion.
-#ifndef UNPACK_PRO
-#define UNPACK_PRO 1  // every staging load in one round trip (below)
-#endif
 
 // SELW: the selector table is written here too, its load issued with the
 // staging loads (the caller's copy had waited for it before any of them).
@@ -1471,7 +1042,6 @@ __device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __
     const uint64_t kf = W0 / kSyncWords + 1;
     const uint32_t nseg =
         W1 > W0 ? 1u + (uint32_t)((W1 - 1) / kSyncWords + 1 - kf) : 0u;
-#if UNPACK_PRO
     // stage the tile: every load in one round trip, then the LDS writes.  The
     // chunk tables and sync entries come by buffer loads (lanes past them
     // read 0: no branch, so no wait at a join), ahead of the byte loads, so
@@ -1482,17 +1052,15 @@ __device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __
     {
         constexpr uint32_t kLoads = (kTileBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
         const uint64_t selv = SELW ? kExpandTable.s[tid] : 0;
-        uint32_t t_w = 0, t_wz = 0, t_p = 0, e_a = 0, e_b = 0;
-        if (SYNC || UNPACK_SPEC) {
-            const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint64_t*>(out_off + ca), 0, (int)((nc + 1) * 8), 0x00020000);
-            const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint64_t*>(in_off + ca), 0, (int)((nc + 1) * 8), 0x00020000);
-            // (low words: tile-relative offsets fit 32 bits)
-            t_w = __builtin_amdgcn_raw_buffer_load_b32(ors, (int)(tid * 8u), 0, 0);
-            t_wz = __builtin_amdgcn_raw_buffer_load_b32(ors, (int)(tid * 8u + 8u), 0, 0);
-            t_p = __builtin_amdgcn_raw_buffer_load_b32(irs, (int)(tid * 8u), 0, 0);
-        }
+        uint32_t e_a = 0, e_b = 0;
+        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint64_t*>(out_off + ca), 0, (int)((nc + 1) * 8), 0x00020000);
+        const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint64_t*>(in_off + ca), 0, (int)((nc + 1) * 8), 0x00020000);
+        // (low words: tile-relative offsets fit 32 bits)
+        const uint32_t t_w = __builtin_amdgcn_raw_buffer_load_b32(ors, (int)(tid * 8u), 0, 0);
+        const uint32_t t_wz = __builtin_amdgcn_raw_buffer_load_b32(ors, (int)(tid * 8u + 8u), 0, 0);
+        const uint32_t t_p = __builtin_amdgcn_raw_buffer_load_b32(irs, (int)(tid * 8u), 0, 0);
         if constexpr (SYNC) {
             // entry of segment b >= 1 = sync[kf + b - 1]: b = tid and b = tid + 256
             const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
@@ -1513,24 +1081,22 @@ __device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __
         const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
         for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
         if (SELW) S.sel[tid] = selv;
-        if (SYNC || UNPACK_SPEC) {
-            if (tid <= nc) {
-                const uint32_t wa = t_w - (uint32_t)W0;
-                S.cw[tid] = wa;
-                S.cp[tid] = t_p - (uint32_t)B0 + off0;
-                if constexpr (SYNC) {
-                    // segments whose first word (max(0, b G - r0)) lies in this chunk
-                    const uint32_t wz = tid < nc ? t_wz - (uint32_t)W0 : wa;
-                    const uint32_t r0 = (uint32_t)(W0 % kSyncWords);
-                    if (wz > wa) {
-                        const uint32_t blo = wa == 0 ? 0u : (wa + r0 + kSyncWords - 1) / kSyncWords;
-                        const uint32_t bhi = (wz + r0 + kSyncWords - 1) / kSyncWords;
-                        for (uint32_t bb = blo; bb < bhi; bb++) S.segc[bb] = (uint8_t)tid;
-                    }
+        if (tid <= nc) {
+            const uint32_t wa = t_w - (uint32_t)W0;
+            S.cw[tid] = wa;
+            S.cp[tid] = t_p - (uint32_t)B0 + off0;
+            if constexpr (SYNC) {
+                // segments whose first word (max(0, b G - r0)) lies in this chunk
+                const uint32_t wz = tid < nc ? t_wz - (uint32_t)W0 : wa;
+                const uint32_t r0 = (uint32_t)(W0 % kSyncWords);
+                if (wz > wa) {
+                    const uint32_t blo = wa == 0 ? 0u : (wa + r0 + kSyncWords - 1) / kSyncWords;
+                    const uint32_t bhi = (wz + r0 + kSyncWords - 1) / kSyncWords;
+                    for (uint32_t bb = blo; bb < bhi; bb++) S.segc[bb] = (uint8_t)tid;
                 }
             }
-            if (tid < kStageChunks) S.badc[tid] = 0;
         }
+        if (tid < kStageChunks) S.badc[tid] = 0;
         if constexpr (SYNC) {
             if (tid >= 1 && tid < nseg) S.ent[tid] = e_a;
             if (tid + kThreads < nseg) S.ent[tid + kThreads] = e_b;
@@ -1539,68 +1105,12 @@ __device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __
         for (uint32_t k = 0; k < kLoads; k++)
             if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
     }
-#else
-    // stage the tile's packed bytes: every load issued before any LDS write
-    // (aligned 16-byte blocks holding at least one byte of the range never
-    // cross a page), and clear the descriptors
-    {
-        constexpr uint32_t kLoads = (kTileBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
-        const uint4* src = reinterpret_cast<const uint4*>(in + B0 - off0);
-        uint4* dst = reinterpret_cast<uint4*>(S.bytes);
-        const uint32_t nblk = (nbytes + 15) / 16;
-        uint4 r[kLoads];
-#pragma unroll
-        for (uint32_t k = 0; k < kLoads; k++) {
-            const uint32_t idx = tid + k * kThreads;
-            r[k] = nblk ? src[idx < nblk ? idx : nblk - 1] : make_uint4(0, 0, 0, 0);
-        }
-        uint4* dd = reinterpret_cast<uint4*>(S.dpos);
-        const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
-        for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
-        if constexpr (SYNC) {
-            // chunk tables and the tile's sync entries (segment b >= 1 starts
-            // at global word 32 (kf + b - 1))
-            if (tid <= nc) {
-                const uint32_t wa = (uint32_t)(out_off[ca + tid] - W0);
-                S.cw[tid] = wa;
-                S.cp[tid] = (uint32_t)(in_off[ca + tid] - B0) + off0;
-                // segments whose first word (max(0, b G - r0)) lies in this chunk
-                const uint32_t wz = tid < nc ? (uint32_t)(out_off[ca + tid + 1] - W0) : wa;
-                const uint32_t r0 = (uint32_t)(W0 % kSyncWords);
-                if (wz > wa) {
-                    const uint32_t blo = wa == 0 ? 0u : (wa + r0 + kSyncWords - 1) / kSyncWords;
-                    const uint32_t bhi = (wz + r0 + kSyncWords - 1) / kSyncWords;
-                    for (uint32_t bb = blo; bb < bhi; bb++) S.segc[bb] = (uint8_t)tid;
-                }
-            }
-            for (uint32_t b = tid; b < nseg; b += kThreads)
-                if (b >= 1) S.ent[b] = sync[kf + b - 1];
-            if (tid < kStageChunks) S.badc[tid] = 0;
-        } else if (UNPACK_SPEC) {
-            if (tid <= nc) {
-                S.cw[tid] = (uint32_t)(out_off[ca + tid] - W0);
-                S.cp[tid] = (uint32_t)(in_off[ca + tid] - B0) + off0;
-            }
-            if (tid < kStageChunks) S.badc[tid] = 0;
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kLoads; k++)
-            if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
-    }
-#endif
     __syncthreads();
     UPROF_T(t1);
     // walk: lane j of one wave follows chunk j.  The walking wave rotates
     // with the tile so that the walks of the workgroups sharing a CU spread
     // over its four SIMDs instead of all landing on wave 0's.
-#ifndef UNPACK_ROTATE_WALKER
-#define UNPACK_ROTATE_WALKER 1
-#endif
-#if UNPACK_ROTATE_WALKER
     const uint32_t walker = (blockIdx.x + (uint32_t)ca) & (kWaves - 1);
-#else
-    const uint32_t walker = 0;
-#endif
     if constexpr (SYNC) {
         const uint32_t wrel = (wave - walker) & (kWaves - 1);
         bool marked = false;
@@ -1629,10 +1139,8 @@ __device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __
             }
         }
         if (anybad) __syncthreads();
-    } else if (UNPACK_SPEC == 2 && nc <= kSegChunks) {
+    } else if (nc <= kSegChunks) {
         spec_seg_tile(S, ca, nc, status, consumed, tid, lane);
-    } else if (UNPACK_SPEC == 1) {
-        spec_tile(S, ca, nc, status, consumed, tid, lane, wave);
     } else if (wave == walker && lane < nc) {
         // (many short chunks -- the resync blocks, ~120 words -- keep 64
         // serial walkers busy; the segment walk is for few long chunks:
@@ -1643,32 +1151,27 @@ __device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __
         const uint64_t ow = out_off[c], oe = out_off[c + 1];
         int32_t st;
         uint32_t used;
-#ifndef UNPACK_WALK_PRIO
-#define UNPACK_WALK_PRIO 0  // s_setprio of the walker wave (its hops are a latency chain)
-#endif
-        if (UNPACK_WALK_PRIO) __builtin_amdgcn_s_setprio(UNPACK_WALK_PRIO);
         walk_wave(S, (uint32_t)(gp - B0) + off0, (uint32_t)(ge - B0) + off0,
                   (uint32_t)(ow - W0), (uint32_t)(oe - ow), st, used);
-        if (UNPACK_WALK_PRIO) __builtin_amdgcn_s_setprio(0);
         status[c] = st;
         if (consumed) consumed[c] = used;
     }
     if constexpr (!SYNC) __syncthreads();
     UPROF_T(t2);
     // expand: lane = output word (a plain descriptor lookup, no head
-    // search); 64-word groups interleaved over waves, UNPACK_GROUPS per iteration so
+    // search); 64-word groups interleaved over waves, kGroups per iteration so
     // that their LDS round trips overlap; coalesced 512-byte stores.
     {
         const uint32_t ng = (Wt + CAPNP_WAVE - 1) / CAPNP_WAVE;
-        for (uint32_t g0 = wave; g0 < ng; g0 += UNPACK_GROUPS * kWaves) {
-            uint32_t d[UNPACK_GROUPS];
+        for (uint32_t g0 = wave; g0 < ng; g0 += kGroups * kWaves) {
+            uint32_t d[kGroups];
 #pragma unroll
-            for (int u = 0; u < UNPACK_GROUPS; u++) {
+            for (int u = 0; u < kGroups; u++) {
                 const uint32_t i = (g0 + u * kWaves) * CAPNP_WAVE + lane;
                 d[u] = i < Wt ? S.dpos[i] : kNone;
             }
 #pragma unroll
-            for (int u = 0; u < UNPACK_GROUPS; u++) {
+            for (int u = 0; u < kGroups; u++) {
                 const uint32_t i = (g0 + u * kWaves) * CAPNP_WAVE + lane;
                 const uint64_t word = expand_desc(S.bytes, S.sel, d[u]);
                 if (i < Wt) out[W0 + i] = word;
@@ -1761,24 +1264,8 @@ __device__ void unpack_tile_rest(USmem& sm, const uint8_t* __restrict__ in,
     }
 }
 
-// Whether tile [ca, cb) fits the LDS tables at once (the usual case).
-__device__ __forceinline__ bool tile_fits(const uint8_t* __restrict__ in,
-                                          const uint64_t* __restrict__ in_off,
-                                          const uint64_t* __restrict__ out_off, uint64_t ca,
-                                          uint64_t cb) {
-    const uint64_t B0 = uniform64(in_off[ca]), W0 = uniform64(out_off[ca]);
-    const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
-#if UNPACK_PRO
-    // (all four loads in one round trip: no short-circuit branches between them)
-    const uint64_t B1 = uniform64(in_off[cb]), W1 = uniform64(out_off[cb]);
-    return (cb - ca <= kStageChunks) & (B1 - B0 <= kTileBytes - off0) & (W1 - W0 <= kTileWords);
-#else
-    return cb - ca <= kStageChunks && uniform64(in_off[cb]) - B0 <= kTileBytes - off0 &&
-           uniform64(out_off[cb]) - W0 <= kTileWords;
-#endif
-}
-
-// The same test for a per-lane tile (the overflow kernel's scan).
+// Whether tile [ca, cb) fits the LDS tables at once (the overflow kernels'
+// per-lane scan; unpack_fit_kernel makes the same test from its offsets).
 __device__ __forceinline__ bool tile_fits_lane(const uint8_t* __restrict__ in,
                                                const uint64_t* __restrict__ in_off,
                                                const uint64_t* __restrict__ out_off, uint64_t ca,
@@ -1789,31 +1276,9 @@ __device__ __forceinline__ bool tile_fits_lane(const uint8_t* __restrict__ in,
            out_off[cb] - out_off[ca] <= kTileWords;
 }
 
-// One workgroup per tile of `tc` chunks.  The tile is cut into sub-tiles
-// that fit the LDS tables (normally one: the whole tile), each staged,
-// walked and expanded in turn; a single chunk too large for the tables
-// takes the global path.
-template <bool SYNC>
-__global__ void __launch_bounds__(kThreads, UNPACK_MIN_WAVES)
-unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-              uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
-              const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
-              uint64_t* __restrict__ consumed, const uint32_t* __restrict__ sync) {
-    __shared__ USmem sm;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-    const uint64_t ca = (uint64_t)blockIdx.x * tc;
-    const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
-    sm.st.sel[tid] = kExpandTable.s[tid];  // (read only by the staged expansions)
-    if (tile_fits(in, in_off, out_off, ca, cb)) {  // the usual case, kept straight-line
-        unpack_staged<SYNC>(sm.st, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid,
-                            lane, wave);
-        return;
-    }
-    unpack_tile_rest<SYNC>(sm, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid, lane,
-                           wave);
-}
+#ifndef UNPACK_PF
+#define UNPACK_PF 0  // unpack_fit_kernel: L2 prefetch distance in tiles (a multiple of 8)
+#endif
 
 // Split launch: unpack_fit_kernel stages the tiles that fit and returns on
 // the others; unpack_ovf_kernel finds those by the same test (two offsets a
@@ -1822,7 +1287,7 @@ unpack_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_of
 // global walk, so it does not spill at 8 waves per SIMD (the combined
 // kernel spilled 44 B per lane).
 template <bool SYNC>
-__global__ void __launch_bounds__(kThreads, UNPACK_MIN_WAVES)
+__global__ void __launch_bounds__(kThreads, 8)
 unpack_fit_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                   uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
                   const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
@@ -1833,18 +1298,32 @@ unpack_fit_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     const uint64_t ca = (uint64_t)blockIdx.x * tc;
     const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
-#if UNPACK_PRO
     uint64_t B0, B1, W0, W1;
     sload4(in_off + ca, in_off + cb, out_off + ca, out_off + cb, B0, B1, W0, W1);
+#if UNPACK_PF
+    // the packed bytes of tile + UNPACK_PF (same XCD: blocks go round robin
+    // over the 8 XCDs), touched once per 64 bytes so that its staging loads
+    // hit L2 when that tile runs
+    const uint64_t pt = (uint64_t)blockIdx.x + UNPACK_PF < gridDim.x ? blockIdx.x + UNPACK_PF
+                                                                      : blockIdx.x;
+    const uint64_t pa = pt * tc, pb = pa + tc < nchunks ? pa + tc : nchunks;
+    uint64_t PB0, PB1, PW0, PW1;
+    sload4(in_off + pa, in_off + pb, out_off + pa, out_off + pb, PB0, PB1, PW0, PW1);
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(in + PB0), 0, pt == blockIdx.x ? 0 : (int)(PB1 - PB0), 0x00020000);
+    const uint32_t pfv = __builtin_amdgcn_raw_buffer_load_b32(prs, (int)(tid * 64u), 0, 0);
+#endif
     const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
-    if (cb - ca > kStageChunks || B1 - B0 > kTileBytes - off0 || W1 - W0 > kTileWords) return;
+    if (cb - ca > kStageChunks || B1 - B0 > kTileBytes - off0 || W1 - W0 > kTileWords) {
+#if UNPACK_PF
+        asm volatile("" ::"v"(pfv));
+#endif
+        return;
+    }
     unpack_staged_at<SYNC, true>(S, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid,
                                  lane, wave, B0, B1, W0, W1);
-#else
-    if (!tile_fits(in, in_off, out_off, ca, cb)) return;
-    S.sel[tid] = kExpandTable.s[tid];
-    unpack_staged<SYNC>(S, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid, lane,
-                        wave);
+#if UNPACK_PF
+    asm volatile("" ::"v"(pfv));
 #endif
 }
 
@@ -1893,10 +1372,7 @@ unpack_ovf_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
 // workgroups left a few hundred of them serialising the overflow tiles
 // (config 4 index-free: 4.3 ms in the overflow kernel; one workgroup per
 // tile instead cost config 2 0.13 ms of empty workgroups).
-#ifndef UNPACK_OVF_WINDOW
-#define UNPACK_OVF_WINDOW 16  // (64: config 4 index-free overflow 1.86 ms on 1155 workgroups)
-#endif
-constexpr uint32_t kOvfWindow = UNPACK_OVF_WINDOW;
+constexpr uint32_t kOvfWindow = 16;  // (64: config 4 index-free overflow 1.86 ms on 1155 workgroups)
 static_assert(kOvfWindow <= CAPNP_WAVE, "one lane per tile of the window");
 
 template <bool SYNC>
@@ -1968,10 +1444,7 @@ unpack_ovf_win_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict
 // be planned (an unusable index entry, more than kStageChunks chunks, or
 // bytes beyond the LDS table).  unpack_wt_plan (one thread per tile) resolves
 // the tile's chunks and both ends from global memory up front.
-#ifndef UNPACK_WT_WORDS
-#define UNPACK_WT_WORDS 1536
-#endif
-constexpr uint32_t kWtWords = UNPACK_WT_WORDS;
+constexpr uint32_t kWtWords = 1536;
 static_assert(kWtWords % kSyncWords == 0 && kWtWords <= kMaxTileChunks * CAPNP_WAVE,
               "word tile size");
 // Packed bytes a word tile stages: 8.125 per word, so that runs of literal
@@ -1982,22 +1455,15 @@ static_assert(kWtWords % kSyncWords == 0 && kWtWords <= kMaxTileChunks * CAPNP_W
 // (half of the 256 walkers had no segment) 730; in their own tables 1280 ->
 // 649, 1536 -> 632 (7 workgroups per CU), 1792 -> 660, 2048 -> 677 (5 per
 // CU).
-#ifndef UNPACK_WT_BYTES
-#define UNPACK_WT_BYTES ((kWtWords * 65 / 8 + 2064 + 15) & ~15u)
-#endif
-constexpr uint32_t kWtBytes = UNPACK_WT_BYTES;
+constexpr uint32_t kWtBytes = (kWtWords * 65 / 8 + 2064 + 15) & ~15u;
 using WtStageSmem = StageSmemT<kWtWords, kWtBytes>;
-#ifndef UNPACK_WT_MIN_WAVES
-#define UNPACK_WT_MIN_WAVES 7  // the LDS (21.8 KB at 1536 words) allows 7 workgroups per CU
-#endif
+// (7 waves per SIMD: the LDS, 21.8 KB at 1536 words, allows 7 workgroups per CU)
 // plan flags
 constexpr uint32_t kWtPf = 1, kWtPl = 2, kWtFallback = 4;
 
 // Diagnostics (capnp_unpack_wt_stats): [0] tiles planned as fallback, [1]
 // pieces that failed in a tile, [2] chunks the finish kernel decoded serially.
 __device__ unsigned long long g_wt_stats[4];
-// first failing tiles: tile id, badc mask (UNPACK_WT_DEBUG builds)
-__device__ unsigned long long g_wt_dbg[2 * 256];
 
 struct alignas(16) WtPlan {
     uint64_t ca, cb;  // chunks [ca, cb) overlap the tile
@@ -2168,7 +1634,7 @@ __device__ __forceinline__ void serial_chunk_at(const uint8_t* __restrict__ in,
     if (consumed) consumed[c] = used;
 }
 
-__global__ void __launch_bounds__(kThreads, UNPACK_WT_MIN_WAVES)
+__global__ void __launch_bounds__(kThreads, 7)
 unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                  uint64_t* __restrict__ out, const uint64_t* __restrict__ out_off,
                  int32_t* __restrict__ status, uint64_t* __restrict__ consumed,
@@ -2204,7 +1670,6 @@ unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
     const uint64_t kf = Wa / kSyncWords + 1;
     const uint32_t nseg = 1u + (uint32_t)((Wb - 1) / kSyncWords + 1 - kf);
     const uint32_t r0 = (uint32_t)(Wa % kSyncWords);
-#if UNPACK_PRO
     // every staging load in one round trip (as unpack_staged_at): the chunk
     // tables and sync entries by buffer loads ahead of the byte loads, the
     // selector entry written after them
@@ -2272,60 +1737,6 @@ unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
         for (uint32_t k = 0; k < kLoads; k++)
             if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
     }
-#else
-    S.sel[tid] = kExpandTable.s[tid];
-    {
-        constexpr uint32_t kLoads = (kWtBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
-        const uint4* src = reinterpret_cast<const uint4*>(in + Bs - off0);
-        uint4* dst = reinterpret_cast<uint4*>(S.bytes);
-        const uint32_t nblk = (nbytes + 15) / 16;
-        uint4 r[kLoads];
-#pragma unroll
-        for (uint32_t k = 0; k < kLoads; k++) {
-            const uint32_t idx = tid + k * kThreads;
-            r[k] = nblk ? src[idx < nblk ? idx : nblk - 1] : make_uint4(0, 0, 0, 0);
-        }
-        // descriptors: none, or the raw words of a literal run carried in
-        const uint32_t litn = uniform(Pp->litn), litp = uniform(Pp->litp) + off0;
-        if (litn == 0) {
-            uint4* dd = reinterpret_cast<uint4*>(S.dpos);
-            const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
-            for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
-        } else {
-            for (uint32_t i = tid; i < ((Wt + 7) & ~7u); i += kThreads)
-                S.dpos[i] = i < litn ? (uint16_t)(kRaw | (litp + 8 * i)) : kNone;
-        }
-        if (tid <= nc) {
-            const uint64_t wo = out_off[ca + tid];
-            const uint32_t wa = wo < Wa ? 0u : (uint32_t)(wo - Wa);
-            S.cw[tid] = wa;  // (the end of a partial last chunk lies past Wt)
-            S.cp[tid] = (uint32_t)(in_off[ca + tid] - Bs) + off0;  // (wraps for a partial first)
-            if (tid < nc) {
-                const uint64_t wn = out_off[ca + tid + 1];
-                const uint32_t wz = wn - Wa < Wt ? (uint32_t)(wn - Wa) : Wt;
-                if (wz > wa) {
-                    const uint32_t blo = wa == 0 ? 0u : (wa + r0 + kSyncWords - 1) / kSyncWords;
-                    const uint32_t bhi = (wz + r0 + kSyncWords - 1) / kSyncWords;
-                    for (uint32_t bb = blo; bb < bhi; bb++) S.segc[bb] = (uint8_t)tid;
-                }
-            }
-        }
-        for (uint32_t b = tid; b < nseg; b += kThreads)
-            if (b >= 1) S.ent[b] = sync[kf + b - 1];
-        if (tid < kStageChunks) S.badc[tid] = 0;
-        if (tid == 0) {
-            S.wt_q0 = uniform(Pp->q0) + off0;
-            S.wt_w0 = uniform(Pp->w0);
-            S.wt_qB = uniform(Pp->qB) + off0;
-            S.wt_wB = uniform(Pp->wB);
-            S.wt_pre = uniform(Pp->pre);
-            S.wt_pl = pl ? 1u : 0u;
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < kLoads; k++)
-            if (tid + k * kThreads < nblk) dst[tid + k * kThreads] = r[k];
-    }
-#endif
     __syncthreads();
     bool marked = false;
     for (uint32_t b = tid; b < nseg; b += kThreads) {
@@ -2357,15 +1768,7 @@ unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
     if (tid == 0) {
         const uint32_t f = ((pf && S.badc[0]) ? 1u : 0u) | ((pl && S.badc[nc - 1]) ? 2u : 0u);
         flags[s] = f;
-        if (f) {
-            const unsigned long long k = atomicAdd(&g_wt_stats[1], 1ull);
-            if (k < 256) {
-                unsigned long long m = 0;
-                for (uint32_t i = 0; i < nc && i < 64; i++) m |= (unsigned long long)(S.badc[i] != 0) << i;
-                g_wt_dbg[2 * k] = s;
-                g_wt_dbg[2 * k + 1] = m;
-            }
-        }
+        if (f) atomicAdd(&g_wt_stats[1], 1ull);
     }
     if (anybad) __syncthreads();
     for (uint32_t i = tid; i < Wt; i += kThreads) out[Wa + i] = expand_desc(S.bytes, S.sel, S.dpos[i]);
@@ -2397,159 +1800,6 @@ unpack_wt_finish(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
     }
 }
 
-// ---------------------------------------------------------------------------
-// Sync kernel (the record sync index is given): every wave is autonomous.  A
-// sub-tile = `tc` consecutive chunks of about kSubWords output words; wave w
-// of workgroup g takes sub-tile 4 g + w, stages its packed bytes in its own
-// LDS region, walks its kSyncWords-word segments (walk_segment, one lane each),
-// re-walks chunks whose segments did not meet, and expands - with no
-// workgroup barrier after the selector table, so the 16-32 resident waves of
-// a CU overlap each other's load latency, walks and expansions freely.
-#ifndef UNPACK_SUB_WORDS
-#define UNPACK_SUB_WORDS 1024
-#endif
-constexpr uint32_t kSubWords = UNPACK_SUB_WORDS;
-constexpr uint32_t kSubBytes = kSubWords * 9 / 2;
-constexpr uint32_t kSubChunks = 64;
-constexpr uint32_t kSubSeg = kSubWords / kSyncWords + 2;
-constexpr uint32_t kSubGlobalLanes = 16;  // fallback walkers (desc table in the byte area)
-
-struct WaveSmem {
-    static constexpr uint32_t kDummy = kSubWords;  // dpos[kDummy + 2 lane]: dummy slots
-    uint8_t badc[kSubChunks];
-    uint32_t cw[kSubChunks + 1];
-    uint32_t cp[kSubChunks + 1];
-    uint32_t ent[kSubSeg];
-    uint8_t segc[kSubSeg];
-    alignas(16) uint8_t bytes[kSubBytes + 16];
-    alignas(16) uint16_t dpos[kSubWords + 2 * CAPNP_WAVE];
-};
-static_assert(sizeof(uint16_t) * kSubGlobalLanes * CAPNP_WAVE <= kSubBytes,
-              "fallback descriptor table must fit the byte area");
-
-struct SyncSmem {
-    uint64_t sel[256];
-    WaveSmem w[kWaves];
-};
-
-__global__ void __launch_bounds__(kThreads)
-unpack_sync_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
-                   uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
-                   const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
-                   uint64_t* __restrict__ consumed, const uint32_t* __restrict__ sync) {
-    __shared__ SyncSmem sm;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63u;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-    sm.sel[tid] = kExpandTable.s[tid];
-    __syncthreads();
-    const uint64_t ca = ((uint64_t)blockIdx.x * kWaves + wave) * tc;
-    if (ca >= nchunks) return;
-    const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
-    const uint32_t nc = (uint32_t)(cb - ca);
-    WaveSmem& S = sm.w[wave];
-    const uint64_t B0 = uniform64(in_off[ca]), B1 = uniform64(in_off[cb]);
-    const uint64_t W0 = uniform64(out_off[ca]), W1 = uniform64(out_off[cb]);
-    const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
-    const bool fits = nc <= kSubChunks && B1 - B0 <= kSubBytes - off0 && W1 - W0 <= kSubWords;
-    if (!fits) {
-        for (uint64_t c0 = ca; c0 < cb; c0 += kSubGlobalLanes)
-            unpack_global<kSubGlobalLanes>(in, in_off, c0, cb, out, out_off, status, consumed,
-                                           reinterpret_cast<uint16_t(*)[CAPNP_WAVE]>(S.bytes),
-                                           lane);
-        return;
-    }
-    const uint32_t nbytes = (uint32_t)(B1 - B0) + off0;
-    const uint32_t Wt = (uint32_t)(W1 - W0);
-    const uint64_t kf = W0 / kSyncWords + 1;
-    const uint32_t nseg = W1 > W0 ? 1u + (uint32_t)((W1 - 1) / kSyncWords + 1 - kf) : 0u;
-    // stage: every global load issued before any LDS write
-    {
-        constexpr uint32_t kLoads = (kSubBytes + 15 + 16 * CAPNP_WAVE - 1) / (16 * CAPNP_WAVE);
-        const uint4* src = reinterpret_cast<const uint4*>(in + B0 - off0);
-        const uint32_t nblk = (nbytes + 15) / 16;
-        uint4 r[kLoads];
-#pragma unroll
-        for (uint32_t k = 0; k < kLoads; k++) {
-            const uint32_t idx = lane + k * CAPNP_WAVE;
-            r[k] = nblk ? src[idx < nblk ? idx : nblk - 1] : make_uint4(0, 0, 0, 0);
-        }
-        uint32_t wa = 0, wz = 0, pa = 0;
-        if (lane <= nc) {
-            wa = (uint32_t)(out_off[ca + lane] - W0);
-            pa = (uint32_t)(in_off[ca + lane] - B0) + off0;
-            wz = lane < nc ? (uint32_t)(out_off[ca + lane + 1] - W0) : wa;
-        }
-        uint32_t e0 = 0, e1 = 0;
-        if (lane + 1 < nseg) e0 = sync[kf + lane];
-        if (lane + 65 < nseg) e1 = sync[kf + lane + 64];
-        uint4* dd = reinterpret_cast<uint4*>(S.dpos);
-        const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
-        for (uint32_t k = lane; k < (Wt + 7) / 8; k += CAPNP_WAVE) dd[k] = none;
-        if (lane < kSubChunks) S.badc[lane] = 0;
-        if (lane <= nc) {
-            S.cw[lane] = wa;
-            S.cp[lane] = pa;
-            // segments whose first word (max(0, b G - r0)) lies in this chunk
-            const uint32_t r0 = (uint32_t)(W0 % kSyncWords);
-            if (wz > wa) {
-                const uint32_t blo = wa == 0 ? 0u : (wa + r0 + kSyncWords - 1) / kSyncWords;
-                const uint32_t bhi = (wz + r0 + kSyncWords - 1) / kSyncWords;
-                for (uint32_t bb = blo; bb < bhi; bb++) S.segc[bb] = (uint8_t)lane;
-            }
-        }
-        if (lane + 1 < nseg) S.ent[lane + 1] = e0;
-        if (lane + 65 < nseg) S.ent[lane + 65] = e1;
-        uint4* dst = reinterpret_cast<uint4*>(S.bytes);
-#pragma unroll
-        for (uint32_t k = 0; k < kLoads; k++)
-            if (lane + k * CAPNP_WAVE < nblk) dst[lane + k * CAPNP_WAVE] = r[k];
-    }
-    wave_lds_sync();
-    // walk: lane b = segment b (and b + 64 when the sub-tile has more)
-    bool marked = false;
-    for (uint32_t b = lane; b < nseg; b += CAPNP_WAVE) {
-        const uint32_t sb = b == 0 ? 0u : (uint32_t)((kf + b - 1) * kSyncWords - W0);
-        const bool last = b + 1 == nseg;
-        const uint32_t eb = last ? Wt : (uint32_t)((kf + b) * kSyncWords - W0);
-        marked |= walk_segment(S, nc, b, sb, eb, last);
-    }
-    wave_lds_sync();
-    const bool anybad = ballot64(marked) != 0;
-    if (lane < nc) {
-        const uint64_t c = ca + lane;
-        if (anybad && S.badc[lane]) {  // exact serial walk of the chunk
-            const uint32_t wa = S.cw[lane], wz = S.cw[lane + 1];
-            for (uint32_t i = wa; i < wz; i++) S.dpos[i] = kNone;
-            int32_t st;
-            uint32_t used;
-            walk_chunk(S, S.cp[lane], S.cp[lane + 1], wa, wz - wa, st, used);
-            status[c] = st;
-            if (consumed) consumed[c] = used;
-        } else {
-            status[c] = ST_OK;
-            if (consumed)
-                consumed[c] = S.cw[lane + 1] > S.cw[lane] ? S.cp[lane + 1] - S.cp[lane] : 0u;
-        }
-    }
-    wave_lds_sync();
-    // expand: lane = output word, four 64-word groups per iteration
-    for (uint32_t g0 = 0; g0 * CAPNP_WAVE < Wt; g0 += 4) {
-        uint32_t d[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint32_t i = (g0 + u) * CAPNP_WAVE + lane;
-            d[u] = i < Wt ? S.dpos[i] : kNone;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint32_t i = (g0 + u) * CAPNP_WAVE + lane;
-            const uint64_t word = expand_desc(S.bytes, sm.sel, d[u]);
-            if (i < Wt) out[W0 + i] = word;
-        }
-    }
-}
-
 }  // namespace
 
 // Output words per unpack tile the staged path is sized for; the host picks
@@ -2558,26 +1808,7 @@ extern "C" uint32_t capnp_unpack_tile_words(void) { return kTileWords; }
 
 // Output words per wave sub-tile of the sync kernel (chunks_per_tile for the
 // record-sync-index calls ~ this / mean chunk words).
-extern "C" uint32_t capnp_unpack_sync_tile_words(void) {
-    return UNPACK_SYNC_WAVES ? kSubWords : kTileWords;
-}
-
-extern "C" hipError_t capnp_launch_unpack_stream(const uint8_t* d_in, const uint64_t* d_in_off,
-                                                 uint64_t nchunks, uint32_t cpw, uint64_t* d_out,
-                                                 const uint64_t* d_out_off, int32_t* d_status,
-                                                 uint64_t* d_consumed, hipStream_t stream);
-
-// Which kernel decodes a batch without the record sync index: the staged
-// tile kernel (default) or the streaming lane-per-chunk kernel (ustream.hip,
-// CAPNP_UNPACK_KERNEL=stream; measured slower: 1.11 vs 0.95 ms at config 2,
-// its per-hop instruction count is the limit).
-static bool use_stream_kernel() {
-    static const int v = [] {
-        const char* e = getenv("CAPNP_UNPACK_KERNEL");
-        return (e && e[0] == 's') ? 1 : 0;
-    }();
-    return v != 0;
-}
+extern "C" uint32_t capnp_unpack_sync_tile_words(void) { return kTileWords; }
 
 extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d_in_off,
                                           uint64_t nchunks, uint32_t tc, uint64_t* d_out,
@@ -2585,57 +1816,30 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
                                           uint64_t* d_consumed, const uint32_t* d_sync,
                                           hipStream_t stream) {
     if (nchunks == 0) return hipSuccess;
-    if (!d_sync && use_stream_kernel() && !(reinterpret_cast<uintptr_t>(d_out) & 15u)) {
-        // chunks per wave ~ 16 tiles' worth (tc ~ 2048 words / mean chunk)
-        const uint32_t cpw = tc ? (tc * 16 < 256 ? tc * 16 : 256) : 256;
-        return capnp_launch_unpack_stream(d_in, d_in_off, nchunks, cpw, d_out, d_out_off,
-                                          d_status, d_consumed, stream);
-    }
-    if (tc == 0) tc = ((d_sync && UNPACK_SYNC_WAVES) ? kSubWords : kTileWords) / 128;
+    if (tc == 0) tc = kTileWords / 128;
     if (tc > kMaxTileChunks) return hipErrorInvalidValue;  // global path: 4 waves x 64
     const uint64_t blocks = (nchunks + tc - 1) / tc;
-#ifndef UNPACK_EXTRA_LDS
-#define UNPACK_EXTRA_LDS 0  // diagnostic: dynamic LDS padding to cap workgroups per CU
-#endif
-    if (d_sync && UNPACK_SYNC_WAVES) {
-        if (tc > kSubChunks) return hipErrorInvalidValue;
-        const uint64_t subs = (nchunks + tc - 1) / tc;
-        hipLaunchKernelGGL(unpack_sync_kernel, dim3((uint32_t)((subs + kWaves - 1) / kWaves)),
-                           dim3(kThreads), UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc,
-                           d_out, d_out_off, d_status, d_consumed, d_sync);
-        return hipGetLastError();
-    }
-#ifndef UNPACK_SPLIT
-#define UNPACK_SPLIT 1  // sync path: fitting tiles and overflow tiles in two kernels
-                        // (index-free: measured 985 vs 930 us split, so kept whole)
-#endif
-    const uint64_t og = (blocks + kThreads - 1) / kThreads;
-    const dim3 ogrid((uint32_t)(og < 1024 ? og : 1024));
-    if (UNPACK_SPLIT && d_sync) {
-        hipLaunchKernelGGL(unpack_fit_kernel<true>, dim3((uint32_t)blocks), dim3(kThreads),
-                           UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
-                           d_status, d_consumed, d_sync);
-        hipLaunchKernelGGL(unpack_ovf_kernel<true>, ogrid, dim3(kThreads), 0, stream, d_in,
-                           d_in_off, nchunks, tc, d_out, d_out_off, d_status, d_consumed, d_sync,
-                           blocks);
-    } else if (d_sync)
-        hipLaunchKernelGGL(unpack_kernel<true>, dim3((uint32_t)blocks), dim3(kThreads),
-                           UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
-                           d_status, d_consumed, d_sync);
-    else if (UNPACK_SPEC == 2) {
+    if (d_sync) {
+        // fitting tiles and overflow tiles in two kernels (the global path's
+        // registers spilled in the combined kernel)
+        const uint64_t og = (blocks + kThreads - 1) / kThreads;
+        hipLaunchKernelGGL(unpack_fit_kernel<true>, dim3((uint32_t)blocks), dim3(kThreads), 0,
+                           stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off, d_status,
+                           d_consumed, d_sync);
+        hipLaunchKernelGGL(unpack_ovf_kernel<true>, dim3((uint32_t)(og < 1024 ? og : 1024)),
+                           dim3(kThreads), 0, stream, d_in, d_in_off, nchunks, tc, d_out,
+                           d_out_off, d_status, d_consumed, d_sync, blocks);
+    } else {
         // index-free with the segment walk: split as the sync path (the walk's
         // registers and the global path's no longer meet in one kernel)
-        hipLaunchKernelGGL(unpack_fit_kernel<false>, dim3((uint32_t)blocks), dim3(kThreads),
-                           UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
-                           d_status, d_consumed, d_sync);
+        hipLaunchKernelGGL(unpack_fit_kernel<false>, dim3((uint32_t)blocks), dim3(kThreads), 0,
+                           stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off, d_status,
+                           d_consumed, d_sync);
         const uint64_t wg = (blocks + kOvfWindow - 1) / kOvfWindow;
         hipLaunchKernelGGL(unpack_ovf_win_kernel<false>, dim3((uint32_t)(wg < 8192 ? wg : 8192)),
                            dim3(kThreads), 0, stream, d_in, d_in_off, nchunks, tc, d_out,
                            d_out_off, d_status, d_consumed, d_sync, blocks);
-    } else
-        hipLaunchKernelGGL(unpack_kernel<false>, dim3((uint32_t)blocks), dim3(kThreads),
-                           UNPACK_EXTRA_LDS, stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off,
-                           d_status, d_consumed, d_sync);
+    }
     return hipGetLastError();
 }
 
@@ -2648,19 +1852,6 @@ extern "C" size_t capnp_unpack_wt_ws_bytes(uint64_t wlo, uint64_t whi) {
 }
 
 extern "C" uint32_t capnp_unpack_wt_words(void) { return kWtWords; }
-
-extern "C" int capnp_unpack_wt_events(uint32_t* out768) {
-#if UNPACK_WT_DEBUG
-    return hipMemcpyFromSymbol(out768, HIP_SYMBOL(g_wt_ev), sizeof(g_wt_ev)) == hipSuccess ? 0 : -1;
-#else
-    (void)out768;
-    return -1;
-#endif
-}
-
-extern "C" int capnp_unpack_wt_dbg(unsigned long long* out512) {
-    return hipMemcpyFromSymbol(out512, HIP_SYMBOL(g_wt_dbg), sizeof(g_wt_dbg)) == hipSuccess ? 0 : -1;
-}
 
 // Word-tile diagnostics since the last reset: fallback tiles, failed pieces,
 // chunks decoded serially by the finish kernel (tests use them to check that

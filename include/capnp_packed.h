@@ -268,6 +268,20 @@ capnp_status capnp_pack(capnp_ctx* ctx, const uint8_t* in, size_t len,
 capnp_status capnp_unpack(capnp_ctx* ctx, const uint8_t* in, size_t in_len,
                           size_t* consumed, uint8_t* out, size_t out_len);
 
+/* The longest prefix of whole records of the packed bytes in[0, in_len)
+   that decodes to at most max_words words: *bytes its length, *words the
+   words it decodes to, written to out (host, max_words words; NULL: the
+   lengths only).  The primitive of a streaming read over a BufRead: a
+   reader keeps only the incomplete record past *bytes when it must pull the
+   next input buffer, instead of the whole unit seen so far (the records
+   before it are final: PackedRead::read decodes left to right and consumes
+   a buffer before refilling, serialize_packed.rs:59-74, :100-226).  Tags
+   are not validated beyond their record lengths: the exact status comes
+   from capnp_unpack. */
+capnp_status capnp_unpack_prefix(capnp_ctx* ctx, const uint8_t* in, size_t in_len,
+                                 uint64_t max_words, uint64_t* out, size_t* bytes,
+                                 uint64_t* words);
+
 /* ---- host batch API (end-to-end: pinned H2D -> kernel -> D2H) ---------- */
 capnp_status capnp_pack_batch_host(capnp_ctx* ctx, const uint64_t* words,
                                    const uint64_t* chunk_word_off, size_t nchunks,

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-tile phase timeline of pack_cs_kernel from the PACK_PROF=3 build
-(`make -C capnproto-rust_amd prof PROF=3`): start, loads landed, pass 1 +
+(`make -C capnproto-rust_amd variant FILE=pack NAME=prof3 DEFS=-DPACK_PROF=3`): start, loads landed, pass 1 +
 publish, pass 2, look-back, end (s_memrealtime, 100 MHz).  Prints the mean of
 each phase and how many tiles are in each phase on average over the launch
 (the memory-level parallelism of the load phase).  Diagnostic only.

@@ -1,0 +1,127 @@
+#!/usr/bin/env python3
+"""The drop-in at the reference's own call granularity.
+
+`benchmark carsales bytes reuse packed` (benchmark/benchmark.rs:207-259)
+calls serialize_packed::write_message and read_message once per ~12 KB
+request.  Through the C ABI each such call is one host->device->host round
+trip (capnp_packed_write_message, capnp_packed_read_message).  This times:
+
+  * per carsales request: write + read through the library, µs per request
+    pair and requests/s, against the reference's loops on one CPU thread
+    (oracle/refloop_oracle.c, the timed CPU baseline);
+  * a message-size sweep (one segment of 1 KiB .. 64 MiB, config-2 words):
+    the same pair per size, to find where a GPU call starts to win.
+
+Prints one JSON object.  python3 scripts/dropin_bench.py [--reqs N]"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "capnproto-rust_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reqs", type=int, default=2000)
+    ap.add_argument("--max-mib", type=int, default=64)
+    args = ap.parse_args()
+    import torch  # noqa: F401  (device init through the library)
+    import oracle_lib as O
+    from capnp_amd import Context, _lib
+    L = _lib.lib()
+    ctx = Context(0)
+    h = ctx.handle
+    opts = _lib.ReaderOptionsC(0, 0, 64)  # no traversal limit: the sweep goes to 64 MiB
+
+    def gpu_pair(seg, reps):
+        """write_message + read_message of the one-segment message `seg`
+        (np.uint64) through the library -> (seconds per pair, packed bytes)."""
+        nw = len(seg)
+        ptrs = (C.c_void_p * 1)(seg.ctypes.data)
+        lens = (C.c_uint32 * 1)(nw)
+        cap = L.capnp_packed_batch_bound_bytes(nw + 1, 3)
+        out = np.empty(cap, np.uint8)
+        body = np.empty(max(nw, 1), np.uint64)
+        segs = np.empty(512, np.uint32)
+        n, used, nseg = C.c_size_t(0), C.c_size_t(0), C.c_uint32(0)
+        best = None
+        for r in range(reps + 1):
+            t0 = time.perf_counter()
+            st = L.capnp_packed_write_message(h, ptrs, lens, 1, out.ctypes.data, cap, C.byref(n))
+            t1 = time.perf_counter()
+            assert st == 0
+            st = L.capnp_packed_read_message(h, out.ctypes.data, n.value, C.byref(opts), 0,
+                                             body.ctypes.data, nw, segs.ctypes.data,
+                                             C.byref(nseg), C.byref(used))
+            t2 = time.perf_counter()
+            assert st == 0 and used.value == n.value
+            if r and (best is None or t2 - t0 < best[0]):  # (the first pair sizes the buffers)
+                best = (t2 - t0, t1 - t0, t2 - t1)
+        assert np.array_equal(body[:nw], seg)
+        return best, n.value
+
+    def cpu_pair(seg, reps):
+        mo = np.array([0, len(seg)], np.uint64)
+        best = None
+        for _ in range(reps):
+            tw, tr, pb, ok = O.refloop_messages_roundtrip_mt(seg, mo, 1)
+            assert ok
+            best = tw + tr if best is None else min(best, tw + tr)
+        return best
+
+    res = {"what": "write_message + read_message per call through the C ABI "
+                   "(capnp_packed_write_message / capnp_packed_read_message) vs the "
+                   "reference's loops on one CPU thread (oracle/refloop_oracle.c)"}
+    # carsales requests, one per call pair, as the reference benchmark does
+    words, msg_off, _ = O.carsales_stream(args.reqs * 1600)
+    m = min(args.reqs, len(msg_off) - 2)
+    t_gpu, t_cpu, ub = 0.0, 0.0, 0
+    for k in range(m):
+        seg = np.ascontiguousarray(words[int(msg_off[k]):int(msg_off[k + 1])])
+        t_gpu += gpu_pair(seg, 1)[0][0]
+        ub += 8 * len(seg)
+    ww = words[:int(msg_off[m])]
+    tw, tr, _, ok = O.refloop_messages_roundtrip_mt(ww, msg_off[:m + 1], 1)
+    assert ok
+    t_cpu = tw + tr
+    res["carsales"] = {
+        "requests": m, "mean_request_bytes": round(ub / m, 1),
+        "gpu_us_per_request": round(t_gpu / m * 1e6, 2),
+        "gpu_requests_per_s": round(m / t_gpu, 1),
+        "cpu_1thread_us_per_request": round(t_cpu / m * 1e6, 3),
+        "cpu_1thread_requests_per_s": round(m / t_cpu, 1),
+    }
+    print(json.dumps(res["carsales"]), file=sys.stderr, flush=True)
+    # size sweep
+    sweep = []
+    kib = 1
+    while kib <= args.max_mib * 1024:
+        nw = kib * 128
+        offs = np.array([0, nw], np.uint64)
+        seg = np.ascontiguousarray(O.gen_fill(offs, kind0=0, pz=O.PZ30, id0=kib))
+        reps = 5 if kib <= 4096 else 2
+        g, pbytes = gpu_pair(seg, reps)
+        c = cpu_pair(seg, 3 if kib <= 4096 else 1)
+        row = {"kib": kib, "packed_bytes": pbytes, "gpu_us": round(g[0] * 1e6, 1),
+               "gpu_write_us": round(g[1] * 1e6, 1), "gpu_read_us": round(g[2] * 1e6, 1),
+               "cpu_1thread_us": round(c * 1e6, 1), "gpu_GiBps": round(8 * nw / g[0] / 2**30, 3),
+               "cpu_1thread_GiBps": round(8 * nw / c / 2**30, 3), "gpu_faster": g[0] < c}
+        print(json.dumps(row), file=sys.stderr, flush=True)
+        sweep.append(row)
+        kib *= 4
+    res["size_sweep"] = sweep
+    win = [r["kib"] for r in sweep if r["gpu_faster"]]
+    res["gpu_wins_from_kib"] = min(win) if win else None
+    print(json.dumps(res), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Look-back statistics of the pack kernel from the PACK_PROF=1 build
-(`make -C capnproto-rust_amd prof`): spin rounds, fallbacks, group windows
+(`make -C capnproto-rust_amd variant FILE=pack NAME=prof DEFS=-DPACK_PROF=1`): spin rounds, fallbacks, group windows
 scanned and s_memtime cycles spent in the look-back.  Diagnostic only.
 
     python3 scripts/pack_prof.py [--chunks N] [--chunk-words W] [--tc T]
@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--lib", default="")
     ap.add_argument("--phases", action="store_true",
-                    help="PACK_PROF=2 build (make prof PROF=2): prelude / ranges / loads / pass 1")
+                    help="PACK_PROF=2 build (make variant FILE=pack NAME=prof2 DEFS=-DPACK_PROF=2): prelude / ranges / loads / pass 1")
     ap.add_argument("--trace", default="", help="save the per-tile timeline (.npy)")
     a = ap.parse_args()
     import torch

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-tile phase timeline of the resync tile resolution's spec launch
-(k_tile; build: make -C capnproto-rust_amd fvariant NAME=rprof
+(k_tile; build: make -C capnproto-rust_amd variant FILE=resync NAME=rprof
 DEFS=-DRESYNC_PROF=1): staging + chunk search, spec walks, wave 0's rounds,
 the waves in turn, block write-out (s_memrealtime, 100 MHz).  Diagnostic.
 
@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--lib", default=os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_f_rprof.so"))
+    ap.add_argument("--lib", default=os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_rprof.so"))
     ap.add_argument("--workload", default="config4_1GiB")
     a = ap.parse_args()
     os.environ["CAPNP_PACKED_LIB"] = a.lib

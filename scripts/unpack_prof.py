@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Phase breakdown of the unpack kernel from the UNPACK_PROF=1 build
-(`make -C capnproto-rust_amd uprof`): s_memtime cycles of wave 0 per phase
+(`make -C capnproto-rust_amd variant FILE=unpack NAME=uprof DEFS=-DUNPACK_PROF=1`): s_memtime cycles of wave 0 per phase
 (stage bytes, walk, expand) summed over staged tiles.  Diagnostic only.
 
     python3 scripts/unpack_prof.py [--chunks N] [--chunk-words W] [--utc T]

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Interleaved timing of library variants (pack, sync unpack, index-free
-unpack; PACK_WT_ABL builds give wrong output by design) on a bench workload
-(env WL, default config4; env CW = words per chunk for the fixed-size
-workloads, default 128), in one process:
+"""Interleaved A/B timing of library builds (pack, sync unpack, index-free
+unpack) on a bench workload (env WL, default config4; env CW = words per
+chunk for the fixed-size workloads, default 128), in one process; variants
+come from `make -C capnproto-rust_amd variant FILE=... NAME=... DEFS=...`:
     python3 scripts/wt_ablate.py [lib.so ...]"""
 import ctypes as C
 import glob
@@ -34,7 +34,7 @@ def main():
     import torch
     from capnp_amd import Context
     libs = sys.argv[1:] or ([os.path.join(ROOT, "capnproto-rust_amd/capnp_amd/libcapnp_packed.so")]
-                            + sorted(glob.glob(os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_p_*.so"))))
+                            + sorted(glob.glob(os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_*.so"))))
     args = bench.parse(["--workload", os.environ.get("WL", "config4"),
                         "--chunk-words", os.environ.get("CW", "128")])
     ctx = Context(0)
@@ -50,7 +50,13 @@ def main():
     ref_out = torch.empty_like(out)
     ref_oo = torch.empty_like(oo)
     ref_sync = torch.empty_like(sync)
-    ctx.pack_batch_into(words, offs, ref_out, ref_oo, chunks_per_tile=0, sync=ref_sync)
+    from capnp_amd import tile_chunks_for, unpack_tile_chunks_for
+    # explicit tile sizes, as bench.py passes them: no host synchronisation
+    # per call (0 = the long-chunk paths, which size themselves)
+    tc = tile_chunks_for(total, n)
+    utc = unpack_tile_chunks_for(total, n, sync=True)
+    utc_ns = unpack_tile_chunks_for(total, n)
+    ctx.pack_batch_into(words, offs, ref_out, ref_oo, chunks_per_tile=tc, sync=ref_sync)
     stream = torch.cuda.current_stream()
     P = C.c_void_p
     variants = [(os.path.basename(p), *load(p)) for p in libs]
@@ -65,17 +71,17 @@ def main():
                     if kind == "pack":
                         L.capnp_gpu_pack_batch_sync_tuned(h, P(words.data_ptr()), P(offs.data_ptr()), n,
                                                           P(out.data_ptr()), cap, P(oo.data_ptr()),
-                                                          P(sync.data_ptr()), 0, P(stream.cuda_stream))
+                                                          P(sync.data_ptr()), tc, P(stream.cuda_stream))
                     elif kind == "nosync":
                         L.capnp_gpu_unpack_batch_tuned(h, P(ref_out.data_ptr()), P(ref_oo.data_ptr()), n,
                                                        P(back.data_ptr()), P(offs.data_ptr()),
-                                                       P(status.data_ptr()), None, 0,
+                                                       P(status.data_ptr()), None, utc_ns,
                                                        P(stream.cuda_stream))
                     else:
                         L.capnp_gpu_unpack_batch_sync_tuned(h, P(ref_out.data_ptr()), P(ref_oo.data_ptr()), n,
                                                             P(back.data_ptr()), P(offs.data_ptr()),
                                                             P(ref_sync.data_ptr()), P(status.data_ptr()),
-                                                            None, 0, P(stream.cuda_stream))
+                                                            None, utc, P(stream.cuda_stream))
                 e1.record(stream)
                 e1.synchronize()
                 res[name][kind].append(e0.elapsed_time(e1) / 5)

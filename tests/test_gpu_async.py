@@ -306,8 +306,9 @@ def test_bufread_refill_read_exact():
 
 
 class _PlainBufRead:
-    """A BufRead with no look-ahead support (fill_buf / consume only): the
-    per-buffer retry path of _refilling, the reference's stopping points."""
+    """A minimal BufRead (fill_buf / consume only), as a Rust caller's
+    reader: the streamed read units (serialize_packed._read_unit) need
+    nothing more."""
 
     def __init__(self, raw, capacity):
         self.raw, self.capacity, self.buf, self.pos = raw, capacity, b"", 0
@@ -332,9 +333,10 @@ def _drain(r):
 
 
 def test_bufread_lookahead_stops_where_reference_does():
-    """With look-ahead (BufReader.unread) the reader ends each message, and
-    each failure, exactly where the per-buffer retries end it: same
-    messages, same error, same bytes left."""
+    """Over BufReader and a minimal BufRead alike, at buffer sizes from 5
+    bytes to 4 KiB, the reader returns the same messages and error and
+    leaves the same bytes; after each message exactly the bytes the oracle's
+    read_message used are gone."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
@@ -365,11 +367,23 @@ def test_bufread_lookahead_stops_where_reference_does():
                     err = e.status
                 res.append((got, err, _drain(r)))
             assert res[0] == res[1], (cap, len(data))
+            # the messages and where the reader stands after them, against
+            # the oracle's read_message loop
+            pos, ref = 0, []
+            while True:
+                st_, segs_, used_ = O.read_message(data[pos:], try_mode=True)
+                if st_ != 0:
+                    break
+                ref.append([np.asarray(x, np.uint64).tobytes() for x in segs_])
+                pos += used_
+            assert res[0][0] == ref, cap
+            if res[0][1] is None:
+                assert res[0][2] == b"" and pos == len(data), cap
 
 
 def test_bufread_large_message_small_buffer():
-    """An 8 MiB message through 8 KiB buffers (1024 refills): look-ahead
-    retries keep it to a handful of decodes."""
+    """An 8 MiB message through 8 KiB buffers (1024 refills): each buffer
+    is decoded once (the streamed units carry only an incomplete record)."""
     import time
     import torch
     if not torch.cuda.is_available():
