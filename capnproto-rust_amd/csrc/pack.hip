@@ -1953,9 +1953,6 @@ pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ c
 // kCsSteps chunks of its tile.  Tiles with a longer chunk (or more chunks per
 // wave) take the streaming size pass and leave their bytes to
 // pack_ovf_kernel.
-#ifndef PACK_PF
-#define PACK_PF 0  // chunk-step kernel: L2 prefetch distance in tiles (a multiple of 8: same XCD)
-#endif
 constexpr uint32_t kCsSteps = 4;   // chunks (steps) per wave
 constexpr uint32_t kCsWords = 128; // words per step
 
@@ -2117,14 +2114,6 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     const uint64_t TW0 = uniform64(chunk_off[c0]);
     const uint64_t WS0 = uniform64(toff[wc0]);
     const uint64_t TW1 = uniform64(chunk_off[c1]);
-#if PACK_PF
-    // the words of tile + PACK_PF (dealt to this XCD too: blocks go round
-    // robin over the 8 XCDs), touched once per 64 bytes so that its loads
-    // hit L2 when that tile runs
-    const uint64_t pt = tile + PACK_PF < gridDim.x ? tile + PACK_PF : tile;
-    const uint64_t pc0 = pt * tc, pc1 = pc0 + tc < nchunks ? pc0 + tc : nchunks;
-    const uint64_t PW0 = uniform64(chunk_off[pc0]), PW1 = uniform64(chunk_off[pc1]);
-#endif
     const uint32_t tile_bytes = (uint32_t)((TW1 - TW0) * 8);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
@@ -2154,11 +2143,6 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         clo[s] = ((uint64_t)x[1] << 32) | x[0];
         chi[s] = ((uint64_t)y[1] << 32) | y[0];
     }
-#if PACK_PF
-    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint64_t*>(in + PW0), 0, pt == tile ? 0 : (int)((PW1 - PW0) * 8), 0x00020000);
-    const uint32_t pfv = __builtin_amdgcn_raw_buffer_load_b32(prs, (int)(tid * 64u), 0, 0);
-#endif
     const uint32_t onext = (uint32_t)__shfl_down((int)o, 1, 64);
     const uint32_t d_off = lane < nw ? o - (uint32_t)TW0 : 0u;
     const uint32_t d_len = lane < nw ? onext - o : 0u;
@@ -2236,9 +2220,6 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         }
         __syncthreads();
         for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
-#if PACK_PF
-        asm volatile("" ::"v"(pfv));
-#endif
         return;
     }
 
@@ -2331,9 +2312,6 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
         if (tid == 0) ovf[tile] = 1;
     }
-#if PACK_PF
-    asm volatile("" ::"v"(pfv));
-#endif
 }
 
 // Tiles whose staged ranges overflowed (ovf[t] set by pack_kernel, after its

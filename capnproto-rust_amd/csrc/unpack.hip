@@ -1276,9 +1276,6 @@ __device__ __forceinline__ bool tile_fits_lane(const uint8_t* __restrict__ in,
            out_off[cb] - out_off[ca] <= kTileWords;
 }
 
-#ifndef UNPACK_PF
-#define UNPACK_PF 0  // unpack_fit_kernel: L2 prefetch distance in tiles (a multiple of 8)
-#endif
 
 // Split launch: unpack_fit_kernel stages the tiles that fit and returns on
 // the others; unpack_ovf_kernel finds those by the same test (two offsets a
@@ -1300,31 +1297,12 @@ unpack_fit_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
     const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
     uint64_t B0, B1, W0, W1;
     sload4(in_off + ca, in_off + cb, out_off + ca, out_off + cb, B0, B1, W0, W1);
-#if UNPACK_PF
-    // the packed bytes of tile + UNPACK_PF (same XCD: blocks go round robin
-    // over the 8 XCDs), touched once per 64 bytes so that its staging loads
-    // hit L2 when that tile runs
-    const uint64_t pt = (uint64_t)blockIdx.x + UNPACK_PF < gridDim.x ? blockIdx.x + UNPACK_PF
-                                                                      : blockIdx.x;
-    const uint64_t pa = pt * tc, pb = pa + tc < nchunks ? pa + tc : nchunks;
-    uint64_t PB0, PB1, PW0, PW1;
-    sload4(in_off + pa, in_off + pb, out_off + pa, out_off + pb, PB0, PB1, PW0, PW1);
-    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(in + PB0), 0, pt == blockIdx.x ? 0 : (int)(PB1 - PB0), 0x00020000);
-    const uint32_t pfv = __builtin_amdgcn_raw_buffer_load_b32(prs, (int)(tid * 64u), 0, 0);
-#endif
     const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
     if (cb - ca > kStageChunks || B1 - B0 > kTileBytes - off0 || W1 - W0 > kTileWords) {
-#if UNPACK_PF
-        asm volatile("" ::"v"(pfv));
-#endif
         return;
     }
     unpack_staged_at<SYNC, true>(S, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid,
                                  lane, wave, B0, B1, W0, W1);
-#if UNPACK_PF
-    asm volatile("" ::"v"(pfv));
-#endif
 }
 
 template <bool SYNC>
