@@ -31,6 +31,14 @@ from .serialize_packed import OwnedSegments, ReaderOptions, DEFAULT_READER_OPTIO
 SEGMENTS_COUNT_LIMIT = 512
 
 
+def _as_u8(buf):
+    """A uint8 view of a bytes-like object (no copy for contiguous buffers)."""
+    try:
+        return np.frombuffer(memoryview(buf).cast("B"), np.uint8)
+    except (TypeError, ValueError):
+        return np.frombuffer(bytes(buf), np.uint8)
+
+
 def _check(st, ctx):
     if st != _lib.OK:
         raise CapnpError(st, (_lib.lib().capnp_ctx_last_error(ctx.handle) or b"").decode())
@@ -58,11 +66,14 @@ class PackedWrite:
             raise CapnpError(64, "capnp_packed_writer_new")
 
     def write(self, buf):
-        """poll_write: takes every byte of `buf` (packed bytes are queued)."""
-        data = bytes(buf)
-        a = np.frombuffer(data, np.uint8) if data else np.zeros(1, np.uint8)
-        _check(_lib.lib().capnp_packed_writer_write(self._h, a.ctypes.data, len(data)), self.ctx)
-        return len(data)
+        """poll_write: takes every byte of `buf` (packed bytes are queued).
+        `buf` is any bytes-like object; it is read in place (no copy)."""
+        a = _as_u8(buf)
+        n = a.size
+        if n == 0:
+            a = np.zeros(1, np.uint8)
+        _check(_lib.lib().capnp_packed_writer_write(self._h, a.ctypes.data, n), self.ctx)
+        return n
 
     def write_all(self, buf):
         self.write(buf)
@@ -101,10 +112,10 @@ class PackedRead:
         self.inner = inner
         self.ctx = ctx or default_context()
         self._err = None
-        self._extra = b""  # bytes an inner reader returned beyond what was asked
+        self._extra = None  # bytes an inner reader returned beyond what was asked
 
         def read_cb(_user, buf, n):
-            if self._extra:
+            if self._extra is not None and self._extra.size:
                 r = self._extra
             else:
                 try:
@@ -114,11 +125,13 @@ class PackedRead:
                     return -2
                 if r is None:
                     return _lib.IO_PENDING
-                r = bytes(r)
+                r = _as_u8(r)  # (read in place: no copy)
             # never more than n into the adaptor's n-byte staging slot
-            self._extra = r[n:]
-            C.memmove(buf, r, min(len(r), n))
-            return min(len(r), n)
+            k = min(r.size, n)
+            self._extra = r[k:]
+            if k:
+                C.memmove(buf, r.ctypes.data, k)
+            return k
 
         self._cb = _lib.READ_FN(read_cb)
         self._h = _lib.lib().capnp_packed_reader_new(self.ctx.handle, self._cb, None)
@@ -139,6 +152,18 @@ class PackedRead:
         self._raise(_lib.lib().capnp_packed_reader_read(self._h, out.ctypes.data, n,
                                                         C.byref(got)))
         return out[:got.value].tobytes()
+
+    def readinto(self, b):
+        """poll_read into a caller's writable buffer (the reference's
+        `poll_read(buf: &mut [u8])`): the unpacked bytes go straight into
+        `b`; returns how many (1..len(b), 0 at a clean end of the stream)."""
+        out = np.frombuffer(memoryview(b).cast("B"), np.uint8)
+        if out.size == 0:
+            return 0
+        got = C.c_size_t(0)
+        self._raise(_lib.lib().capnp_packed_reader_read(self._h, out.ctypes.data, out.size,
+                                                        C.byref(got)))
+        return got.value
 
     def read_exact(self, n):
         out = np.empty(max(n, 1), np.uint8)

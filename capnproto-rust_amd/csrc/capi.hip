@@ -485,6 +485,9 @@ capnp_ctx* capnp_ctx_create(int device, capnp_status* status) {
     return ctx;
 }
 
+// (internal: stream_io.hip's private contexts)
+int capnp_ctx_device(const capnp_ctx* ctx) { return ctx ? ctx->device : 0; }
+
 void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);

@@ -50,6 +50,29 @@ __device__ __forceinline__ uint32_t mask_rank(uint64_t m) {
 
 __device__ __forceinline__ uint64_t ballot64(bool p) { return __ballot(p); }
 
+// Value of lane i - D of this lane's row of 16 lanes (DPP row_shr:D, a VALU
+// op: no LDS round trip as __shfl_up's ds_bpermute); 0 for the row's first
+// D lanes.  (0 is the identity of the row scans built from it, max and +.)
+template <uint32_t D>
+__device__ __forceinline__ uint32_t row_shr(uint32_t x) {
+    static_assert(D >= 1 && D <= 15, "row_shr:1..15");
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x110 + D, 0xF, 0xF, false);
+}
+
+// Inclusive max / sum over lanes 0..i of this lane's row of 16 lanes.
+__device__ __forceinline__ uint32_t row_max_scan(uint32_t x) {
+    x = max(x, row_shr<1>(x));
+    x = max(x, row_shr<2>(x));
+    x = max(x, row_shr<4>(x));
+    return max(x, row_shr<8>(x));
+}
+__device__ __forceinline__ uint32_t row_sum_scan(uint32_t x) {
+    x += row_shr<1>(x);
+    x += row_shr<2>(x);
+    x += row_shr<4>(x);
+    return x + row_shr<8>(x);
+}
+
 __host__ __device__ __forceinline__ uint64_t low_mask(uint32_t k) {
     return k >= 64 ? ~0ull : ((1ull << k) - 1ull);
 }

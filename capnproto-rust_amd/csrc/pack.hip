@@ -44,6 +44,9 @@
 
 
 
+#ifndef PACK_EARLYPOLL
+#define PACK_EARLYPOLL 0
+#endif
 #ifndef PACK_PROF
 #define PACK_PROF 0  // look-back counters (scripts/pack_prof.py); 0 = product
 #endif
@@ -1166,8 +1169,27 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
 }
 
 // Wave 0: global byte offset of tile t (aggregate already published).
+// Look-back polls issued ahead of the wait (pre_poll, right after the tile
+// publishes its aggregate): the group's earlier tile records and the first
+// window of group records.  Any record read then is final or an aggregate
+// that a later inclusive record only shortcuts, so the look-back may start
+// from them.
+struct PrePoll {
+    uint64_t st, rec;
+};
+__device__ __forceinline__ PrePoll pre_poll(const LookbackArgs& A, uint64_t t, uint32_t lane) {
+    const uint64_t g = t / kGroup;
+    const uint32_t r = (uint32_t)(t % kGroup);
+    const int64_t j = (int64_t)g - 1 - (int64_t)lane;
+    PrePoll pp;
+    pp.st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
+    pp.rec = lane < kGroupWindow ? (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc) : 0;
+    return pp;
+}
+
 [[maybe_unused]] __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, uint32_t lane,
-                                              bool early_group = false) {
+                                              bool early_group = false,
+                                              const PrePoll* pre = nullptr) {
     const uint64_t g = t / kGroup;
     const uint32_t r = (uint32_t)(t % kGroup);
 #if PACK_PROF
@@ -1176,7 +1198,7 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
 #endif
     // aggregates of the group's earlier tiles
     uint64_t within;
-    uint64_t st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
+    uint64_t st = pre ? pre->st : (lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg);
     for (uint32_t spins = 0;;) {
         const uint64_t miss = ballot64((st >> 62) == 0);
         if (!miss) break;
@@ -1207,10 +1229,13 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
     // its inclusive record (and ends the scan), else its aggregate
     uint64_t gexcl = 0;
     int64_t idx = (int64_t)g - 1;
+    bool first = pre != nullptr;
     for (uint32_t spins = 0; idx >= 0;) {
         const int64_t j = idx - (int64_t)lane;
         const bool in_win = lane < kGroupWindow;
-        const uint64_t rec = !in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc);
+        const uint64_t rec =
+            first ? pre->rec : (!in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc));
+        first = false;
         const uint64_t inc = ballot64((rec & kFlagInc) != 0);
         const uint32_t first_inc = ctz64(inc);
         const uint64_t need = first_inc < 64 ? low_mask(first_inc) : low_mask(kGroupWindow);
@@ -1256,8 +1281,9 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
 }
 
 __device__ __forceinline__ uint64_t tile_offset(const LookbackArgs& A, uint64_t t, uint64_t agg,
-                                                uint32_t lane, bool early_group = false) {
-    return lookback(A, t, agg, lane, early_group);
+                                                uint32_t lane, bool early_group = false,
+                                                const PrePoll* pre = nullptr) {
+    return lookback(A, t, agg, lane, early_group, pre);
 }
 
 // The group aggregate, published by the group's last tile from a wave that
@@ -2250,15 +2276,25 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     for (int w = 0; w < kWaves; w++) fits &= sm.wave_bytes[w] <= kStageBytes;
     fits = __builtin_amdgcn_readfirstlane((int)fits) != 0;
     uint64_t agg = 0;
+#if PACK_EARLYPOLL
+    PrePoll pp{};
+#endif
     if (wave == 0) {
         agg = scan_chunks32(sm, nc, lane);
         publish(LA, tile, agg, lane);
+#if PACK_EARLYPOLL
+        pp = pre_poll(LA, tile, lane);
+#endif
 #if PACK_PROF == 3
         if (lane == 0) TRACE(tile, 2, RT());
 #endif
     }
     const bool early_group = (tile % kGroup) == kGroup - 1;
     if (early_group && wave == kWaves - 1) {
+        // (the same sum as wave 0's agg: wave w's local is the sum of the
+        // sizes it stored for its chunks wc0 .. wc0 + nw - 1 (sz = 0 past nw),
+        // and the waves' chunks partition the tile's nc; a mismatch would
+        // shift every later tile's offsets, which the parity tests compare)
         uint32_t a = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; w++) a += (uint32_t)lds_u64(&sm.wave_bytes[w]);
@@ -2288,7 +2324,11 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         wave_lds_sync();
         if (lane == 0) TRACE(tile, 3, RT());
 #endif
+#if PACK_EARLYPOLL
+        const uint64_t excl = tile_offset(LA, tile, agg, lane, early_group, &pp);
+#else
         const uint64_t excl = tile_offset(LA, tile, agg, lane, early_group);
+#endif
 #if PACK_PROF == 3
         if (lane == 0) TRACE(tile, 4, RT());
 #endif

@@ -40,8 +40,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/capnp_packed.h"
@@ -65,6 +70,79 @@ struct Drain {
     size_t pos = 0;
 };
 
+// A background thread that runs one job at a time: the adaptors' device work
+// for the next read unit or the previous write batch, so that it overlaps
+// the caller's copies and the inner stream's calls.  Jobs run on a private
+// context (its own stream and staging buffers, never the caller's).
+class Worker {
+public:
+    Worker() : th_([this] { loop(); }) {}
+    ~Worker() {
+        wait();
+        {
+            std::lock_guard<std::mutex> l(m_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    void run(std::function<void()> f) {
+        std::lock_guard<std::mutex> l(m_);
+        job_ = std::move(f);
+        busy_ = true;
+        cv_.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [this] { return !busy_; });
+    }
+
+private:
+    void loop() {
+        std::unique_lock<std::mutex> l(m_);
+        for (;;) {
+            cv_.wait(l, [this] { return quit_ || busy_; });
+            if (quit_) return;
+            std::function<void()> f = std::move(job_);
+            l.unlock();
+            f();
+            l.lock();
+            busy_ = false;
+            cv_.notify_all();
+        }
+    }
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::function<void()> job_;
+    bool busy_ = false, quit_ = false;
+    std::thread th_;  // (last: starts once the members above exist)
+};
+
+// The private context and worker of one adaptor, created on first use.
+struct Background {
+    capnp_ctx* ctx = nullptr;
+    std::unique_ptr<Worker> wk;
+    ~Background() {
+        wk.reset();  // (joins: no job runs past here)
+        if (ctx) capnp_ctx_destroy(ctx);
+    }
+    capnp_status ensure(int device) {
+        if (wk) return CAPNP_OK;
+        capnp_status st = CAPNP_OK;
+        ctx = capnp_ctx_create(device, &st);
+        if (!ctx) return st == CAPNP_OK ? CAPNP_E_HIP : st;
+        wk.reset(new Worker());
+        return CAPNP_OK;
+    }
+};
+
+}  // namespace
+
+// capi.hip (internal): the device a context was created on.
+extern "C" int capnp_ctx_device(const capnp_ctx* ctx);
+
+namespace {
+
 uint64_t get_u64(const uint8_t* p) {
     uint64_t v;
     memcpy(&v, p, 8);
@@ -82,6 +160,12 @@ struct capnp_packed_writer {
     std::vector<uint64_t> words;        // chunks not yet packed, back to back
     std::vector<uint64_t> off{0};       // their word offsets
     Drain out;                          // packed bytes the inner writer has not taken
+    // the full batch being packed in the background (bw, boff -> bout)
+    Background bg;
+    bool busy = false;
+    std::vector<uint64_t> bw, boff;
+    std::vector<uint8_t> bout;
+    capnp_status bst = CAPNP_OK;
 };
 
 struct capnp_packed_reader {
@@ -94,9 +178,59 @@ struct capnp_packed_reader {
     std::vector<uint8_t> dec;  // decoded bytes not yet handed out
     size_t dp = 0;
     size_t pass_rem = 0;       // raw bytes of a literal run still to pass through
+    capnp_status pull_err = CAPNP_OK;  // a read-ahead pull's error, for the next pull
+    // read-ahead: the next whole-record unit (in[a_ip ..], a_nw words asked),
+    // decoded in the background while the caller drains `dec`
+    Background bg;
+    bool ahead = false;
+    size_t a_ip = 0, a_nw = 0;
+    capnp_status a_st = CAPNP_OK;
+    uint64_t a_pb = 0, a_pw = 0;
+    std::vector<uint8_t> a_out;
 };
 
 namespace {
+
+// The background batch's packed bytes, once packed, go behind the queued
+// ones (batches drain in order).
+capnp_status writer_collect(capnp_packed_writer* w) {
+    if (!w->busy) return CAPNP_OK;
+    w->bg.wk->wait();
+    w->busy = false;
+    if (w->bst != CAPNP_OK) return w->bst;
+    if (w->out.pos == w->out.q.size()) {
+        w->out.q.swap(w->bout);
+        w->out.pos = 0;
+    } else {
+        w->out.q.insert(w->out.q.end(), w->bout.begin(), w->bout.end());
+    }
+    w->bout.clear();
+    return CAPNP_OK;
+}
+
+// Hands the collected chunks to the background (after the previous batch's
+// bytes are queued): the caller's next writes fill a new batch meanwhile.
+capnp_status writer_launch(capnp_packed_writer* w) {
+    capnp_status st = writer_collect(w);
+    if (st != CAPNP_OK) return st;
+    if ((st = w->bg.ensure(capnp_ctx_device(w->ctx))) != CAPNP_OK) return st;
+    w->bw.swap(w->words);
+    w->boff.swap(w->off);
+    w->words.clear();
+    w->off.assign(1, 0);
+    w->busy = true;
+    w->bg.wk->run([w] {
+        const size_t n = w->boff.size() - 1;
+        const uint64_t nw = w->boff[n];
+        const size_t cap = capnp_packed_batch_bound_bytes(nw, n);
+        w->bout.resize(cap);
+        std::vector<uint64_t> oo(n + 1);
+        w->bst = capnp_pack_batch_host(w->bg.ctx, w->bw.data(), w->boff.data(), n, w->bout.data(),
+                                       cap, oo.data());
+        w->bout.resize(w->bst == CAPNP_OK ? oo[n] : 0);
+    });
+    return CAPNP_OK;
+}
 
 capnp_status writer_pack(capnp_packed_writer* w) {
     const size_t n = w->off.size() - 1;
@@ -135,6 +269,11 @@ capnp_status writer_drain(capnp_packed_writer* w) {
 // Pulls more packed input; CAPNP_OK with bytes added, CAPNP_NONE at the end
 // of the stream, CAPNP_PENDING, or an I/O error.
 capnp_status reader_pull(capnp_packed_reader* r, size_t ask = kPull) {
+    if (r->pull_err != CAPNP_OK) {  // (a read-ahead pull failed: the next pull reports it)
+        const capnp_status e = r->pull_err;
+        r->pull_err = CAPNP_OK;
+        return e;
+    }
     if (r->eof) return CAPNP_NONE;
     ask = std::min(std::max(ask, kPull), kPullMax);
     if (r->ip > 0 && r->ip * 2 >= r->in.size()) {  // drop the decoded prefix
@@ -237,8 +376,48 @@ constexpr size_t kWholeUnit = 8192;   // units this long are cut at whole record
 // decode keeps the block walk (a unit with spare input bytes would take the
 // serial walk).  The read returns at most nw words: whole records, at least
 // nw - 255 of them unless the stream pends or ends.
+// Read-ahead after a whole-record unit: stages the input the next unit of
+// nw words consumes (as reader_fill_whole would, at its next call) and
+// decodes it in the background.  Nothing changes what the reads hand out:
+// the unit is the one the next call would decode, and a pull that pends or
+// fails here leaves the next call to meet it.
+void reader_ahead(capnp_packed_reader* r, size_t nw) {
+    for (size_t need = nw * 10 + 16; r->in.size() - r->ip < need;) {
+        const capnp_status p = reader_pull(r, need - (r->in.size() - r->ip));
+        if (p == CAPNP_OK) continue;
+        if (p == CAPNP_NONE) break;      // end of stream: the rest is staged
+        if (p != CAPNP_PENDING) r->pull_err = p;
+        return;
+    }
+    if (r->in.size() == r->ip || r->bg.ensure(capnp_ctx_device(r->ctx)) != CAPNP_OK) return;
+    r->ahead = true;
+    r->a_ip = r->ip;
+    r->a_nw = nw;
+    const uint8_t* src = r->in.data() + r->ip;
+    const size_t n = r->in.size() - r->ip;
+    r->bg.wk->run([r, src, n, nw] {
+        r->a_out.resize(nw * 8);
+        r->a_pb = r->a_pw = 0;
+        r->a_st = capnp_stream_decode_prefix(r->bg.ctx, src, n, nw,
+                                             reinterpret_cast<uint64_t*>(r->a_out.data()),
+                                             &r->a_pb, &r->a_pw);
+        if (r->a_st == CAPNP_OK) r->a_out.resize(r->a_pw * 8);
+    });
+}
+
 capnp_status reader_fill_whole(capnp_packed_reader* r, size_t nw) {
     std::vector<uint8_t> out;
+    if (r->ahead) {  // the unit decoded ahead, if it is this one
+        r->bg.wk->wait();
+        r->ahead = false;
+        if (r->a_st == CAPNP_OK && r->a_pw > 0 && r->a_ip == r->ip && r->a_nw == nw) {
+            r->ip += r->a_pb;
+            r->dec.swap(r->a_out);
+            r->dp = 0;
+            reader_ahead(r, nw);
+            return CAPNP_OK;
+        }
+    }
     for (;;) {
         if (r->ip == r->in.size()) {
             capnp_status p = reader_pull(r);
@@ -261,6 +440,7 @@ capnp_status reader_fill_whole(capnp_packed_reader* r, size_t nw) {
             r->ip += pb;
             r->dec.swap(out);
             r->dp = 0;
+            reader_ahead(r, nw);
             return CAPNP_OK;
         }
         // the first staged record is incomplete: more input, or pending / end
@@ -277,6 +457,11 @@ capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
     want = std::max<size_t>(want, 1);
     size_t nw = std::max(want, kMinUnit);
     std::vector<uint8_t> out;
+    if (r->ahead && (r->pass_rem || nw < kWholeUnit)) {
+        // (not a whole-record unit: the one decoded ahead is not this one)
+        r->bg.wk->wait();
+        r->ahead = false;
+    }
     if (r->pass_rem) return reader_pass(r);
     if (nw >= kWholeUnit) return reader_fill_whole(r, nw);
     for (;;) {
@@ -345,7 +530,10 @@ capnp_packed_writer* capnp_packed_writer_new(capnp_ctx* ctx, capnp_write_fn fn, 
     return w;
 }
 
-void capnp_packed_writer_free(capnp_packed_writer* w) { delete w; }
+void capnp_packed_writer_free(capnp_packed_writer* w) {
+    if (w && w->bg.wk) w->bg.wk->wait();  // (the background batch uses w's buffers)
+    delete w;
+}
 
 capnp_status capnp_packed_writer_write(capnp_packed_writer* w, const uint8_t* buf, size_t len) {
     if (!w || (len && !buf)) return CAPNP_E_INVALID_ARGUMENT;
@@ -374,7 +562,9 @@ capnp_status capnp_packed_writer_write(capnp_packed_writer* w, const uint8_t* bu
     }
     if (w->words.size() > w0) w->off.push_back(w->words.size());  // this call's chunk
     if (w->words.size() >= kBatchWords) {
-        capnp_status st = writer_pack(w);
+        // the previous batch's bytes are queued and drained while this one
+        // packs in the background
+        capnp_status st = writer_launch(w);
         if (st != CAPNP_OK) return st;
         st = writer_drain(w);
         if (st != CAPNP_OK && st != CAPNP_PENDING) return st;
@@ -384,7 +574,9 @@ capnp_status capnp_packed_writer_write(capnp_packed_writer* w, const uint8_t* bu
 
 capnp_status capnp_packed_writer_flush(capnp_packed_writer* w) {
     if (!w) return CAPNP_E_INVALID_ARGUMENT;
-    capnp_status st = writer_pack(w);
+    capnp_status st = writer_collect(w);
+    if (st != CAPNP_OK) return st;
+    st = writer_pack(w);
     if (st != CAPNP_OK) return st;
     return writer_drain(w);
 }
@@ -400,7 +592,10 @@ capnp_packed_reader* capnp_packed_reader_new(capnp_ctx* ctx, capnp_read_fn fn, v
     return r;
 }
 
-void capnp_packed_reader_free(capnp_packed_reader* r) { delete r; }
+void capnp_packed_reader_free(capnp_packed_reader* r) {
+    if (r && r->bg.wk) r->bg.wk->wait();  // (the read-ahead uses r's buffers)
+    delete r;
+}
 
 capnp_status capnp_packed_reader_read(capnp_packed_reader* r, uint8_t* out, size_t len,
                                       size_t* nread) {

@@ -36,6 +36,9 @@
 #ifndef UNPACK_PROF
 #define UNPACK_PROF 0  // phase timers (scripts/unpack_prof.py); 0 = product
 #endif
+#ifndef UNPACK_SEGREC
+#define UNPACK_SEGREC 1
+#endif
 #if UNPACK_PROF
 // per-tile trace (capnp_unpack_trace): s_memrealtime (100 MHz) at
 // [0] start, [1] staged, [2] walked, [3] expanded; [4] 1 = global path
@@ -481,9 +484,17 @@ union USmem {
 __device__ __forceinline__ void rec_bytes(const uint8_t* B, uint32_t q, uint32_t& tag,
                                           uint32_t& b1, uint32_t& b9) {
     const uint32_t p = q - 1u;
+#if UNPACK_TAG8
+    uint32_t p1 = p;
+    asm("" : "+v"(p1));  // (b1's address, opaque: no merge with the tag into a u16 read)
+    tag = B[p];
+    b1 = B[p1 + 1u];
+    asm("" : "+v"(tag));  // (tag's range unknown: no 16-bit arithmetic on it)
+#else
     const uint32_t dw = *reinterpret_cast<const uint32_t*>(B + (p & ~3u));
     tag = __builtin_amdgcn_ubfe(dw, (p & 3u) * 8u, 8u);
     b1 = B[q];
+#endif
     b9 = B[q + 8];
 }
 
@@ -877,10 +888,46 @@ __device__ __forceinline__ void seg_hop(const uint8_t* B, uint32_t& p, uint32_t&
     uint32_t tag, b1, b9;
     rec_bytes(B, p + 1u, tag, b1, b9);
     const bool isz = tag == 0, isf = tag == 0xFF;
+#if UNPACK_TAG8
+    const uint32_t cnt = isf ? b9 : (isz ? b1 : 0u);
+    const uint32_t ext = isf ? 8u * b9 + 1u : (isz ? 1u : 0u);
+    p += __builtin_popcount(tag) + ext + 1u;
+#else
     const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
     p += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) + (isf ? 8u * cnt : 0u);
+#endif
     w += 1u + cnt;
 }
+
+#if UNPACK_SEGREC
+// A segment walk that keeps its first kSegRecs records in registers
+// (position | word offset from the walk start << 16), so that the
+// descriptor pass writes them without walking the chain again; a walk of
+// more records re-walks only the rest, from (qr, wr).
+constexpr uint32_t kSegRecs = 12;
+struct SegRecs {
+    uint32_t r[kSegRecs];
+    uint32_t nr, qr, wr;
+};
+
+// Walks from q (word 0) until q >= se -> exit q, words w.
+__device__ __forceinline__ void seg_walk_rec(const uint8_t* B, uint32_t& q, uint32_t& w,
+                                             uint32_t se, SegRecs& sr) {
+    w = 0;
+    sr.nr = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kSegRecs; k++) {
+        if (q < se) {
+            sr.r[k] = q | (w << 16);
+            sr.nr = k + 1u;
+            seg_hop(B, q, w);
+        }
+    }
+    sr.qr = q;
+    sr.wr = w;
+    while (q < se) seg_hop(B, q, w);
+}
+#endif
 
 template <class SM>
 __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
@@ -906,6 +953,86 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
     const uint32_t s0 = j == 0 ? sb : max(cs, sb >= kSegOverlap ? sb - kSegOverlap : 0u);
     uint32_t p = s0, w = 0;
     while (act && p < sb) seg_hop(S.bytes, p, w);
+#if UNPACK_SEGREC
+    // (inactive threads: sb = se = 0, no hops)
+    const uint32_t f = p;
+    SegRecs sr{};
+    seg_walk_rec(S.bytes, p, w, se, sr);
+    const bool serr = p > pe;
+    const uint32_t xs = serr ? 0u : p, ws = w;
+    uint32_t own = xs, wd = ws;
+    bool err = j == 0 && serr, rep = false;  // rep: sr holds a repair walk's records
+    uint32_t e_used = j == 0 ? sb : ~0u;
+    uint32_t x = row_max_scan(xs);
+    for (;;) {
+        const uint32_t xu = row_shr<1>(x);
+        const uint32_t e = j == 0 ? sb : xu;
+        const bool need = act && e != e_used;
+        if (ballot64(need) == 0) break;
+        if (need) {
+            e_used = e;
+            if (e == f && !rep) {
+                own = xs;
+                wd = ws;
+                err = serr;
+            } else {
+                uint32_t q = e, wt;
+                seg_walk_rec(S.bytes, q, wt, se, sr);
+                rep = true;
+                err = q > pe;
+                own = (err || e >= se) ? 0u : q;
+                wd = wt;
+            }
+        }
+        x = row_max_scan(own);
+    }
+    const uint32_t e = e_used;
+    const uint32_t incl = row_sum_scan(wd);
+    const uint64_t bad_m = ballot64(act && err);
+    const uint32_t gl = lane & ~(nseg - 1u);
+    const uint64_t gm = ((1ull << nseg) - 1ull) << gl;
+    const uint32_t tot = (uint32_t)__shfl((int)incl, (int)(gl + nseg - 1u), 64);
+    const uint32_t xl = (uint32_t)__shfl((int)x, (int)(gl + nseg - 1u), 64);
+    const bool chunk_ok = act && (bad_m & gm) == 0 && tot == n && xl == pe && n > 0 && pe > cs;
+    if (act && j == 0) S.badc[c] = chunk_ok ? 0 : 1;
+    // 3. descriptors of the good chunks: the kept records (independent LDS
+    // accesses, no chain), then a walk over the rest, if any
+    if (chunk_ok) {
+        const uint32_t ww = S.cw[c] + incl - wd;  // word of the entry e
+        uint32_t lit = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kSegRecs; k++) {
+            const uint32_t q = sr.r[k] & 0xFFFFu;
+            if (k < sr.nr) {
+                S.dpos[ww + (sr.r[k] >> 16)] = (uint16_t)q;
+                if (S.bytes[q] == 0xFF) lit |= 1u << k;
+            }
+        }
+        while (lit) {  // literal runs (rare)
+            const uint32_t k = (uint32_t)__builtin_ctz(lit);
+            lit &= lit - 1u;
+            uint32_t rk = sr.r[0];
+#pragma unroll
+            for (uint32_t i = 1; i < kSegRecs; i++)
+                if (i == k) rk = sr.r[i];
+            const uint32_t q = rk & 0xFFFFu;
+            const uint32_t cnt = S.bytes[q + 9];
+            if (cnt) lit_entries(S, ww + (rk >> 16), q, cnt);
+        }
+        uint32_t q = sr.qr, wq = ww + sr.wr;
+        (void)e;
+        while (q < x) {
+            uint32_t tag, b1, b9;
+            rec_bytes(S.bytes, q + 1u, tag, b1, b9);
+            const bool isz = tag == 0, isf = tag == 0xFF;
+            const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+            S.dpos[wq] = (uint16_t)q;
+            if (isf && cnt) lit_entries(S, wq, q, cnt);
+            wq += 1u + cnt;
+            q += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) + (isf ? 8u * cnt : 0u);
+        }
+    }
+#else
     const uint32_t f = p, wf = w;
     while (act && p < se) seg_hop(S.bytes, p, w);
     const bool serr = p > pe;  // (a record past the chunk end: garbage, or j = 0's error)
@@ -991,6 +1118,7 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
             q += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) + (isf ? 8u * cnt : 0u);
         }
     }
+#endif
 #if UNPACK_PROF
     if (tid == 0 && g_utrace) g_utrace[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
 #endif

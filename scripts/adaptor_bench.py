@@ -3,7 +3,9 @@
 PackedWrite equivalents, csrc/stream_io.hip) over an in-memory inner
 stream, in 1 MiB calls: GiB/s of unpacked bytes.  The
 packed stream is config 2's data (30 % zero words), 256 MiB unpacked.
-Prints one JSON line.
+Prints one JSON line.  (Calls pass views of the caller's buffers, as the
+reference's poll_write(&[u8]) / poll_read(&mut [u8]) do: no per-call copy
+in the harness.)
 
     python3 scripts/adaptor_bench.py [--mib 256] [--call-mib 1]
 """
@@ -54,26 +56,31 @@ def main():
     ctx.gen_batch(words, offs, pz_thresh=1288490189)
     raw = words.cpu().numpy().tobytes()
     call = int(a.call_mib * (1 << 20))
-    # write: 1 MiB calls of unpacked bytes, then flush
+    # write: 1 MiB calls of unpacked bytes (views of the caller's buffer, as
+    # a Rust caller passes &[u8]), then flush
+    mv = memoryview(raw)
     sink = MemWrite()
     w = spa.PackedWrite(sink, ctx=ctx)
     t0 = time.perf_counter()
     for i in range(0, len(raw), call):
-        w.write_all(raw[i:i + call])
+        w.write_all(mv[i:i + call])
     w.flush_blocking()
     tw = time.perf_counter() - t0
     packed = b"".join(sink.parts)
-    # read: 1 MiB calls of unpacked bytes until the end
+    # read: calls of up to 1 MiB into the caller's buffer (poll_read(&mut
+    # [u8]) -> readinto) until the end
     r = spa.PackedRead(MemRead(packed), ctx=ctx)
-    got = bytearray()
+    got = bytearray(len(raw) + call)
+    gv = memoryview(got)
+    pos = 0
     t0 = time.perf_counter()
     while True:
-        b = r.read(call)
-        if not b:
+        k = r.readinto(gv[pos:pos + call])
+        if not k:
             break
-        got += b
+        pos += k
     tr = time.perf_counter() - t0
-    ok = bytes(got) == raw
+    ok = pos == len(raw) and gv[:pos] == raw
     GiB = float(1 << 30)
     print(json.dumps({
         "workload": f"config-2 data, {len(raw) / GiB:.3f} GiB unpacked, {len(packed) / GiB:.3f} GiB packed, "

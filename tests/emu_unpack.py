@@ -16,26 +16,43 @@ def record_hop(B, p, pe):
     return q, 1 + cnt, q > pe
 
 
-def seg_walk(B, L, S=16, OV=32):
+def walk_rec(B, q, se, L, K):
+    """Walk from q until q >= se keeping the first K records (position, word
+    offset): -> (exit, words, kept records, state after them)."""
+    w, recs = 0, []
+    while q < se and len(recs) < K:
+        recs.append((q, w))
+        q, dw, _ = record_hop(B, q, L)
+        w += dw
+    qr, wr = q, w
+    while q < se:
+        q, dw, _ = record_hop(B, q, L)
+        w += dw
+    return q, w, recs, (qr, wr)
+
+
+def seg_walk(B, L, S=16, OV=32, K=12, descs=False):
     """Chunk bytes B[0:L] (zero padded past L), S byte segments, spec walks
-    led in by OV bytes: returns (exits, words, err, rounds) as the kernel
-    computes them."""
+    led in by OV bytes, K records kept per walk: returns (exits, words, err,
+    rounds) as the kernel computes them, plus with descs=True the
+    descriptor pass's (word, record start) pairs of the chunk."""
     sb = [(L * j) // S for j in range(S)]
     se = [(L * (j + 1)) // S for j in range(S)]
-    f, xs, ws, serr = [], [], [], []
+    f, xs, ws, serr, recs, rest = [], [], [], [], [], []
     for j in range(S):  # 1. spec walks
         p, w = (sb[j] if j == 0 else max(0, sb[j] - OV)), 0
         while p < sb[j]:
             p, dw, _ = record_hop(B, p, L)
             w += dw
-        fj, wf = p, w
-        while p < se[j]:
-            p, dw, _ = record_hop(B, p, L)
-            w += dw
+        fj = p
+        p, w, rj, sj = walk_rec(B, p, se[j], L, K)
         f.append(fj)
         serr.append(p > L)
         xs.append(0 if p > L else p)
-        ws.append(w - wf)
+        ws.append(w)
+        recs.append(rj)
+        rest.append(sj)
+    rep = [False] * S
     own, x, wd = list(xs), [max(xs[:j + 1]) for j in range(S)], list(ws)
     err = [serr[0]] + [False] * (S - 1)
     used = [sb[0]] + [None] * (S - 1)
@@ -50,13 +67,11 @@ def seg_walk(B, L, S=16, OV=32):
             if not need[j]:
                 continue
             e = used[j] = ent[j]
-            if e == f[j]:
+            if e == f[j] and not rep[j]:
                 own[j], wd[j], err[j] = xs[j], ws[j], serr[j]
             else:
-                q, wt = e, 0
-                while q < se[j]:
-                    q, dw, _ = record_hop(B, q, L)
-                    wt += dw
+                q, wt, recs[j], rest[j] = walk_rec(B, e, se[j], L, K)
+                rep[j] = True
                 err[j] = q > L
                 own[j] = 0 if (err[j] or e >= se[j]) else q
                 wd[j] = wt
@@ -64,7 +79,31 @@ def seg_walk(B, L, S=16, OV=32):
         for v in own:
             m = max(m, v)
             x.append(m)
-    return x, wd, err, rounds
+    if not descs:
+        return x, wd, err, rounds
+    # 3. descriptors: word base of each segment's entry by a scan of wd, the
+    # kept records, then a walk from the state after them to the exit
+    out, base = [], 0
+    for j in range(S):
+        out += [(base + w, q) for q, w in recs[j]]
+        q, w = rest[j]
+        w += base
+        while q < x[j]:
+            out.append((w, q))
+            q, dw, _ = record_hop(B, q, L)
+            w += dw
+        base += wd[j]
+    return x, wd, err, rounds, out
+
+
+def true_records(B, L):
+    """The exact chain's (word, record start) pairs."""
+    out, p, w = [], 0, 0
+    while p < L:
+        out.append((w, p))
+        p, dw, _ = record_hop(B, p, L)
+        w += dw
+    return out
 
 
 def true_exits(B, L, S=16):
