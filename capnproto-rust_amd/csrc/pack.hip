@@ -44,6 +44,12 @@
 
 
 
+#ifndef PACK_ASMOR
+#define PACK_ASMOR 0
+#endif
+#ifndef PACK_SELPRE
+#define PACK_SELPRE 0
+#endif
 #ifndef PACK_EARLYPOLL
 #define PACK_EARLYPOLL 0
 #endif
@@ -2072,14 +2078,13 @@ __device__ __forceinline__ uint32_t cs_size_step(uint64_t wlo, uint64_t whi, uin
 // after it (d = the distance to the next sync point, shared by both words of
 // a lane; b = the entry's byte offset in the tile's index window).
 template <bool SYNC>
-__device__ __forceinline__ void cs_emit_word(uint64_t w, uint32_t info, uint8_t* region_m1,
-                                             const Sel8* sel, __amdgpu_buffer_rsrc_t srs,
-                                             uint32_t oc, uint32_t d, uint32_t b) {
+__device__ __forceinline__ void cs_emit_word_sel(uint64_t w, uint32_t info, uint8_t* region_m1,
+                                                 Sel8 se, __amdgpu_buffer_rsrc_t srs,
+                                                 uint32_t oc, uint32_t d, uint32_t b) {
     if (info >= kCsSkip) return;  // (the skip flag is the top field)
     const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
     const uint32_t idx = __builtin_amdgcn_ubfe(info, kInfoPosBits, 9);
     const uint32_t cnt = info >> 22;
-    const Sel8 se = sel[idx];
     const uint32_t hdr = idx == 0 ? (cnt << 8) : (idx & 0xFFu);  // (copy words: 256 & 0xFF)
     const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, se.s0) | hdr;
     const uint32_t r1 = __builtin_amdgcn_perm(hi, lo, se.s1);
@@ -2091,10 +2096,24 @@ __device__ __forceinline__ void cs_emit_word(uint64_t w, uint32_t info, uint8_t*
     const uint32_t e3 = __builtin_amdgcn_alignbyte(0u, r2, s);
     const uint32_t pos = info & ((1u << kInfoPosBits) - 1u);
     uint32_t* b32 = reinterpret_cast<uint32_t*>(__builtin_align_down(region_m1 + pos, 4));
+#if PACK_ASMOR
+    // (ds_or_b32 as asm: the compiler's atomics were each followed by a full
+    // LGKM wait before the next LDS access; LDS ops of a wave complete in
+    // order, and the barrier before the copy-out waits for all of them)
+    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)b32;
+    asm volatile("ds_or_b32 %0, %1\n\t"
+                 "ds_or_b32 %0, %2 offset:4\n\t"
+                 "ds_or_b32 %0, %3 offset:8\n\t"
+                 "ds_or_b32 %0, %4 offset:12"
+                 :
+                 : "v"(a), "v"(e0), "v"(e1), "v"(e2), "v"(e3)
+                 : "memory");
+#else
     __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#endif
     if constexpr (SYNC) {
         if (idx < kSelCopy && d <= cnt) {
             const uint32_t rel = pos - oc;
@@ -2104,6 +2123,20 @@ __device__ __forceinline__ void cs_emit_word(uint64_t w, uint32_t info, uint8_t*
                 __builtin_amdgcn_raw_buffer_store_b32(rel | (dd << 24), srs, (int)bb, 0, 0);
         }
     }
+}
+
+// The selector of a word's record (pass 2 reads a step's selectors before
+// its emission's LDS atomics).
+__device__ __forceinline__ Sel8 cs_sel(const Sel8* sel, uint32_t info) {
+    return sel[__builtin_amdgcn_ubfe(info, kInfoPosBits, 9)];
+}
+
+template <bool SYNC>
+__device__ __forceinline__ void cs_emit_word(uint64_t w, uint32_t info, uint8_t* region_m1,
+                                             const Sel8* sel, __amdgpu_buffer_rsrc_t srs,
+                                             uint32_t oc, uint32_t d, uint32_t b) {
+    if (info >= kCsSkip) return;  // (the skip flag is the top field)
+    cs_emit_word_sel<SYNC>(w, info, region_m1, cs_sel(sel, info), srs, oc, d, b);
 }
 
 template <bool SYNC>
@@ -2313,9 +2346,16 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             const uint32_t c = t0 - g;
             const uint32_t d = (c - lane) & (kSyncWords - 1);
             const uint32_t b = (lane + d - c) / (kSyncWords / 4u);
+#if PACK_SELPRE
+            const Sel8 sa = cs_sel(sm.sel, ilo[s]), sb2 = cs_sel(sm.sel, ihi[s]);
+            cs_emit_word_sel<SYNC>(clo[s], ilo[s], region_m1, sa, srs, oc, d, b);
+            cs_emit_word_sel<SYNC>(chi[s], ihi[s], region_m1, sb2, srs, oc, d,
+                                   b + 64u / (kSyncWords / 4u));
+#else
             cs_emit_word<SYNC>(clo[s], ilo[s], region_m1, sm.sel, srs, oc, d, b);
             cs_emit_word<SYNC>(chi[s], ihi[s], region_m1, sm.sel, srs, oc, d,
                                b + 64u / (kSyncWords / 4u));
+#endif
             __builtin_amdgcn_sched_barrier(0);
         }
     }
