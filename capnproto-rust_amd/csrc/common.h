@@ -59,6 +59,24 @@ __device__ __forceinline__ uint32_t row_shr(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x110 + D, 0xF, 0xF, false);
 }
 
+// Inclusive max over lanes 0..i of the wave (DPP: row_shr within each row of
+// 16 lanes, then row_bcast:15 / row_bcast:31 carry the row maxima on; all
+// VALU, no LDS round trip).
+__device__ __forceinline__ uint32_t wave_max_scan(uint32_t x) {
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+    x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+    return x;
+}
+
+// The value of lane i - 1 (DPP wave_shr:1); 0 in lane 0.
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);
+}
+
 // Inclusive max / sum over lanes 0..i of this lane's row of 16 lanes.
 __device__ __forceinline__ uint32_t row_max_scan(uint32_t x) {
     x = max(x, row_shr<1>(x));

@@ -2458,6 +2458,8 @@ struct WtSmem {
     uint64_t wave_bytes[kWaves];
     uint32_t lastcs[kWaves];               // region position of the last chunk start
     uint64_t excl;
+    uint32_t wcarry[kWaves];               // run state entering range w (w >= 1): type | rem << 2
+    uint32_t wext[kWaves];                 // words from range w's start its open run absorbs
     alignas(16) uint32_t pad[4];           // (emit_step ORs a zero before a region)
     alignas(16) uint8_t stage[kWaves][kRegion];
     uint16_t wpos[kWaves][kWtRange];       // region position of chunk-start words
@@ -2548,13 +2550,15 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     // bits are one vector load; guarded loads had each waited at its join)
     const uint64_t r = tile * kWaves + wave;
     const uint64_t cAr = uniform64(map[r]);
-    const uint32_t pinr = uniform(plan[r]), poutr = uniform(plan[r + 1]);
+    // the run states at the tile's ends (pack_wt_plan plans tile starts
+    // only); between the tile's ranges they come from the neighbouring
+    // waves' words (below), which this workgroup holds anyway
+    const uint32_t pin0 = uniform(plan[tile * kWaves]), pnext = uniform(plan[(tile + 1) * kWaves]);
     const uint64_t q0 = have ? 1 + (R0 >> 6) - b64 : 0;
     const uint64_t cbv = cbits[q0 + (lane < kStageSteps ? lane : kStageSteps)];
     const uint64_t cA = have ? cAr : nchunks;
-    // the run states at both ends (pack_wt_plan)
-    const uint32_t pin = have ? pinr : 0u;
-    const uint32_t pout = (have && !lastr) ? poutr : 0u;
+    // a full range followed by another range of this tile
+    const bool succ = have && wave + 1 < (uint32_t)kWaves && R1 < Tb;
     const uint64_t stv = chunk_off[cA + lane < nchunks ? cA + lane : nchunks];
     const uint64_t st0 = cA + lane < nchunks ? stv : ~0ull;
     // chunk starts (forced heads) of the steps
@@ -2567,15 +2571,40 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         const uint64_t bits = rr ? (lo >> rr) | (hi << (64 - rr)) : lo;
         smk[s] = nv ? bits & low_mask(nv) : 0ull;
     }
+    // the run state entering the next range (R1), from this range's last 64
+    // words (pack_wt_plan's carry_in_b over the same window)
+    if (succ) {
+        uint32_t rec = 0;
+        if (((readlane64(cbv, kStageSteps) >> rr) & 1) == 0) {  // R1 inside a chunk
+            const Carry c = carry_in_b<64>(in, cbits, b64, wlo, R1, lane, cache[kStageSteps - 1],
+                                           readlane64(cache[kStageSteps - 2], 63),
+                                           smk[kStageSteps - 1]);
+            rec = c.type | (c.rem << 2);
+        }
+        if (lane == 0) wm.wcarry[wave + 1] = rec;
+    }
     for (uint32_t o = 16 * lane; o < kRegion; o += 16 * CAPNP_WAVE)
         *reinterpret_cast<uint4*>(region + o) = make_uint4(0, 0, 0, 0);
     wave_lds_sync();
-    const Carry cin{pin & 3u, (pin >> 2) & 0xFFu};
     // (pin the words here: nothing of pass 1 is computed ahead of the carry,
     // which would keep eight steps' worth of values live through it)
 #pragma unroll
     for (uint32_t s = 0; s < kStageSteps; s++) asm volatile("" : "+v"(cache[s]));
     __syncthreads();
+    const uint32_t pin = !have ? 0u : (wave == 0 ? pin0 : uniform(wm.wcarry[wave]));
+    const Carry cin{pin & 3u, (pin >> 2) & 0xFFu};
+    if (have && wave > 0) {
+        // the words from R0 on that the run open at R0 absorbs: the previous
+        // range's last record (its pass 2 needs them)
+        uint32_t ext = 0;
+        if (cin.type != 0 && cin.rem != 0) {
+            const uint64_t w0 = nw >= 64u ? cache[0] : (R0 + lane < whi ? in[R0 + lane] : 0ull);
+            ext = run_ext_b(in, cbits, b64, whi, R0, cin, lane, w0,
+                            rr ? (readlane64(cbv, 0) >> rr) | (readlane64(cbv, 1) << (64 - rr))
+                               : readlane64(cbv, 0));
+        }
+        if (lane == 0) wm.wext[wave] = ext;
+    }
     // pass 1: sizes and positions
     StepInfo si[kStageSteps];
     StageState pk;
@@ -2591,12 +2620,13 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             lastcs = (uint32_t)__builtin_amdgcn_readlane((int)si[s].pos,
                                                          63 - __builtin_clzll(smk[s]));
     }
-    const uint32_t rext = pout >> 10;  // (the run open at R1 is the next range's carry)
     if (lane == 0) {
         sm.wave_bytes[wave] = pk.total;
         wm.lastcs[wave] = lastcs;
     }
     __syncthreads();
+    // (the run open at R1 is the next range's carry: the words it absorbs)
+    const uint32_t rext = (!have || lastr) ? 0u : (succ ? uniform(wm.wext[wave + 1]) : pnext >> 10);
     uint32_t woff = 0, agg = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; w++) {
@@ -2700,16 +2730,22 @@ pack_wt_bits(const uint64_t* __restrict__ chunk_off, uint64_t nchunks, uint64_t 
 // words before a range examined first (16: 254 vs 190 us, more deep searches)
 constexpr uint32_t kPlanWin = 64;
 static_assert(kPlanWin >= 2 && kPlanWin <= 64, "plan window");
-// Run state at every wave range's first word, one wave per range: plan[r] =
+// Run state at a wave range's first word, one wave per range: plan[r] =
 // type | rem << 2 | ext << 10, ext = the words from R0 on that the run open
-// there absorbs (run_ext_b).  The pack kernel reads its own entry and the
-// next range's, so no range waits on the words around its ends.
+// there absorbs (run_ext_b).  Launched for the tiles' first ranges only
+// (rstride = kWaves): inside a tile, range w's state comes from range w - 1's
+// last 64 words and the ext from range w's first words, both held by the
+// tile's own waves (round 4; planning every range read ~2 KiB around each
+// 4 KiB range, 519 MB of config 4's 1 GiB).  The pack kernel
+// reads its tile's entry and the next tile's.
 __global__ void __launch_bounds__(256)
 pack_wt_plan(const uint64_t* __restrict__ in, const uint64_t* __restrict__ cbits, uint64_t wlo,
-             uint64_t whi, uint64_t g0, uint64_t nranges, uint32_t* __restrict__ plan) {
+             uint64_t whi, uint64_t g0, uint64_t nranges, uint32_t rstride,
+             uint32_t* __restrict__ plan) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (r >= nranges) return;
+    const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (i >= nranges) return;
+    const uint64_t r = i * rstride;  // (rstride kWaves: the tiles' first ranges only)
     const uint64_t g = g0 + r / kWaves;
     const uint64_t Ta = g * kWtTile > wlo ? g * kWtTile : wlo;
     const uint64_t R = uniform64(Ta + (r % kWaves) * kWtRange);
@@ -2940,8 +2976,10 @@ extern "C" hipError_t capnp_launch_pack_wt(const uint64_t* d_in, const uint64_t*
     const uint64_t nr = ntiles * kWaves;
     hipLaunchKernelGGL(pack_wt_map, dim3((uint32_t)((nr + 255) / 256)), dim3(256), 0, stream,
                        d_chunk_off, nchunks, wlo, whi, g0, nr, map);
-    hipLaunchKernelGGL(pack_wt_plan, dim3((uint32_t)((nr + 3) / 4)), dim3(256), 0, stream, d_in,
-                       cbits, wlo, whi, g0, nr, plan);
+    // run states at the tiles' first ranges (and past the last tile); the
+    // kernel derives the others from the words it holds
+    hipLaunchKernelGGL(pack_wt_plan, dim3((uint32_t)((ntiles + 1 + 3) / 4)), dim3(256), 0, stream,
+                       d_in, cbits, wlo, whi, g0, ntiles + 1, (uint32_t)kWaves, plan);
     if (d_sync) {
         hipLaunchKernelGGL(pack_wt_kernel<true>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
                            d_in, d_chunk_off, nchunks, d_out, out_cap, d_out_off, d_state,

@@ -121,6 +121,9 @@ __global__ void __launch_bounds__(kThreads) k_count(const uint64_t* __restrict__
     nblk[c] = len == 0 ? (out_off[c + 1] != out_off[c] ? 1 : 0) : (len + kBlock - 1) / kBlock;
 }
 
+#ifndef RESYNC_DPP
+#define RESYNC_DPP 1  // the rounds' wave scans by DPP (0: ds_bpermute shuffles, A/B)
+#endif
 #ifndef RESYNC_PROF
 #define RESYNC_PROF 0  // diagnostic: per-tile phase timestamps of the spec launch (scripts/resync_prof.py)
 #endif
@@ -238,6 +241,11 @@ __device__ __forceinline__ bool seg_rounds(const uint8_t* buf, SegState& S, bool
         }
         uint32_t v = S.own > in_j ? S.own : in_j;
         if (!valid) v = 0;
+#if RESYNC_DPP
+        const uint32_t x = wave_max_scan(v);  // (DPP: no LDS round trips)
+        if (lane == CAPNP_WAVE - 1) wmax[wave] = x;
+        uint32_t pm = wave_shr1(x);
+#else
         uint32_t x = v;
 #pragma unroll
         for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
@@ -247,6 +255,7 @@ __device__ __forceinline__ bool seg_rounds(const uint8_t* buf, SegState& S, bool
         if (lane == CAPNP_WAVE - 1) wmax[wave] = x;
         uint32_t pm = (uint32_t)__shfl_up((int)x, 1);
         if (lane == 0) pm = 0;
+#endif
         __syncthreads();
         for (uint32_t w2 = 0; w2 < wave; w2++) pm = wmax[w2] > pm ? wmax[w2] : pm;
         const uint32_t ent = fixed_j ? in_j : pm;

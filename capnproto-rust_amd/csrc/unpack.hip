@@ -36,6 +36,9 @@
 #ifndef UNPACK_PROF
 #define UNPACK_PROF 0  // phase timers (scripts/unpack_prof.py); 0 = product
 #endif
+#ifndef UNPACK_LEANHOP
+#define UNPACK_LEANHOP 0
+#endif
 #ifndef UNPACK_SEGREC
 #define UNPACK_SEGREC 1
 #endif
@@ -489,7 +492,6 @@ __device__ __forceinline__ void rec_bytes(const uint8_t* B, uint32_t q, uint32_t
     asm("" : "+v"(p1));  // (b1's address, opaque: no merge with the tag into a u16 read)
     tag = B[p];
     b1 = B[p1 + 1u];
-    asm("" : "+v"(tag));  // (tag's range unknown: no 16-bit arithmetic on it)
 #else
     const uint32_t dw = *reinterpret_cast<const uint32_t*>(B + (p & ~3u));
     tag = __builtin_amdgcn_ubfe(dw, (p & 3u) * 8u, 8u);
@@ -726,7 +728,13 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     // (the hop runs under the exec mask of the lanes still
     // below stopw, so the state updates need no selects and the record
     // checks collect in a wave mask)
+#if UNPACK_LEANHOP
+    // (the record checks as running maxima: cpe1 and cwe are fixed in phase
+    // A, and a record past either bound is an error wherever it occurs)
+    uint32_t qmx = 0, wmx = 0;
+#else
     uint64_t errm = 0;
+#endif
 #pragma unroll 1  // (x2 / x4 / x8 measured within noise)
     for (uint32_t it = 0; it < kSyncWords; it++) {
         if (w < stopw) {
@@ -738,12 +746,22 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
             rec_bytes(B, qn, ntag, nb1, nb9);
             const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
             const uint32_t wn0 = w + 1u + cnt;
+#if UNPACK_LEANHOP
+            qmx = max(qmx, qe);
+            wmx = max(wmx, wn0);
+#else
             errm |= ballot64(qe > cpe1 || wn0 > cwe);
+#endif
             const uint32_t wn = wn0 < cwe ? wn0 : cwe;
             S.dpos[w] = (uint16_t)(q - 1u);
+#if UNPACK_LEANHOP
+            if (isf && wn > w + 1)  // literal-run words (rare)
+                lit_entries(S, w, q - 1u, (WT && wn > wlim ? wlim : wn) - w - 1);
+#else
             if (ballot64(isf && wn > w + 1)) {  // literal-run words (rare)
                 if (isf) lit_entries(S, w, q - 1u, (WT && wn > wlim ? wlim : wn) - w - 1);
             }
+#endif
             q = qn;
             w = wn;
             tag = ntag;
@@ -751,7 +769,11 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
             b9 = nb9;
         }
     }
+#if UNPACK_LEANHOP
+    err = qmx > cpe1 || wmx > cwe;
+#else
     err = (errm >> lane_id()) & 1;
+#endif
 #if UNPACK_PROF
     const uint64_t lt1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -887,6 +909,9 @@ constexpr uint32_t kSegChunks = 16;  // tiles of at most this many chunks take t
 __device__ __forceinline__ void seg_hop(const uint8_t* B, uint32_t& p, uint32_t& w) {
     uint32_t tag, b1, b9;
     rec_bytes(B, p + 1u, tag, b1, b9);
+#if UNPACK_TAG8
+    asm("" : "+v"(tag));  // (tag's range unknown: no 16-bit arithmetic on it)
+#endif
     const bool isz = tag == 0, isf = tag == 0xFF;
 #if UNPACK_TAG8
     const uint32_t cnt = isf ? b9 : (isz ? b1 : 0u);

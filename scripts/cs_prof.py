@@ -100,11 +100,27 @@ def main():
         print("   phase us : " + "  ".join(f"{p} {m:.2f}" for p, m in zip(ph, means)))
         print("   in flight: " + "  ".join(f"{p} {x:.0f}" for p, x in zip(ph, inflight))
               + f"  (total {sum(inflight):.0f})")
-        if not a.pipe and (T[:, 7] > 0).all():  # look-back split: own group, then groups
-            w = (T[:, 7] - T[:, 3]) / 100.0
-            g = (T[:, 4] - T[:, 7]) / 100.0
+        ok7 = (T[:, 7] >= T[:, 3]) & (T[:, 7] <= T[:, 4]) & (T[:, 7] > 0)
+        if not a.pipe and ok7.mean() > 0.9:  # look-back split: own group, then groups
+            w = (T[ok7, 7] - T[ok7, 3]) / 100.0
+            g = (T[ok7, 4] - T[ok7, 7]) / 100.0
             print(f"   lookback: own group {w.mean():.2f} (p90 {np.percentile(w, 90):.2f})  "
-                  f"group records {g.mean():.2f} (p90 {np.percentile(g, 90):.2f}) us")
+                  f"group records {g.mean():.2f} (p90 {np.percentile(g, 90):.2f}) us "
+                  f"({ok7.sum()} tiles)")
+            lb = (T[:, 4] - T[:, 3]) / 100.0
+            r = np.arange(ntiles) % 64
+            print("   lookback by tile in group (r 0, 1-15, 16-47, 48-62, 63): " + "  ".join(
+                f"{lb[m].mean():.2f}" for m in (r == 0, (r >= 1) & (r < 16), (r >= 16) & (r < 48),
+                                                (r >= 48) & (r < 63), r == 63)))
+        if not a.pipe:
+            xcc = (T[:, 6] >> 32) & 0xF
+            same = (xcc[1:] == xcc[:-1]).mean()
+            b8 = (xcc == (np.arange(ntiles) % 8)).mean()
+            print(f"   XCD: tile t and t+1 on the same XCD {same:.3f}; XCD == t % 8 for {b8:.3f}")
+            # how far a tile's start trails its predecessor's publish (pass 1 done)
+            gap = (T[1:, 2] - T[:-1, 2]) / 100.0
+            print(f"   publish(t) - publish(t-1): mean {gap.mean():.2f} p10/p90 "
+                  f"{np.percentile(gap, 10):.2f}/{np.percentile(gap, 90):.2f} us")
         q = np.percentile(T[:, 5] - T[:, order[0]], [10, 50, 90]) / 100.0
         print(f"   lifetime p10/p50/p90 {q[0]:.2f}/{q[1]:.2f}/{q[2]:.2f} us; "
               f"first start->last start {starts[-1] - starts[0]:.1f} us")

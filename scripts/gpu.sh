@@ -20,6 +20,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 O=gpurun_out/$TAG
 fail() { echo "STEP FAILED: $1"; tail -40 "$2"; exit 1; }
+k=0
 for step in "$@"; do
   name=${step%%=*}
   arg=
@@ -53,9 +54,10 @@ for step in "$@"; do
       python scripts/bench_summary.py prof ${O}_trace_${arg}.json ;;
     py)
       IFS=',' read -r -a pa <<< "$arg"
-      timeout -k 10 600 python -u scripts/${pa[0]} "${pa[@]:1}" > ${O}_py_${pa[0]%.py}.txt 2>&1 \
-        || fail "$step" ${O}_py_${pa[0]%.py}.txt
-      grep -v amdgpu.ids ${O}_py_${pa[0]%.py}.txt | tail -40 ;;
+      k=$((k + 1))
+      f=${O}_py${k}_${pa[0]%.py}.txt
+      timeout -k 10 600 python -u scripts/${pa[0]} "${pa[@]:1}" > $f 2>&1 || fail "$step" $f
+      grep -v amdgpu.ids $f | tail -40 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

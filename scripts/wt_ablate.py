@@ -3,7 +3,7 @@
 unpack) on a bench workload (env WL, default config4; env CW = words per
 chunk for the fixed-size workloads, default 128), in one process; variants
 come from `make -C capnproto-rust_amd variant FILE=... NAME=... DEFS=...`:
-    python3 scripts/wt_ablate.py [lib.so ...]"""
+    python3 scripts/wt_ablate.py [--wl=WORKLOAD] [lib.so ...]"""
 import ctypes as C
 import glob
 import os
@@ -33,9 +33,14 @@ def main():
     import bench
     import torch
     from capnp_amd import Context
-    libs = sys.argv[1:] or ([os.path.join(ROOT, "capnproto-rust_amd/capnp_amd/libcapnp_packed.so")]
-                            + sorted(glob.glob(os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_*.so"))))
-    args = bench.parse(["--workload", os.environ.get("WL", "config4"),
+    argv = sys.argv[1:]
+    wl = os.environ.get("WL", "config4")
+    if argv and argv[0].startswith("--wl="):  # (gpu.sh py= steps pass arguments, not env)
+        wl = argv.pop(0)[5:]
+    libs = argv or ([os.path.join(ROOT, "capnproto-rust_amd/capnp_amd/libcapnp_packed.so")]
+                    + sorted(glob.glob(os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_*.so"))))
+    print(f"workload {wl}", flush=True)
+    args = bench.parse(["--workload", wl,
                         "--chunk-words", os.environ.get("CW", "128")])
     ctx = Context(0)
     dev = torch.device("cuda", 0)
