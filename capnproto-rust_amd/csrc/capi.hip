@@ -156,8 +156,17 @@ struct capnp_ctx {
     int resync_passes = 0, resync_serial = 0;  // last capnp_gpu_unpack_batch_resync
     uint32_t* d_bad = nullptr;  // offset validation flag (check_offsets)
     uint32_t* h_bad = nullptr;  // pinned copy
+    uint8_t* h_pin = nullptr;   // pinned staging of the small host calls (kPinnedCall)
+    size_t pin_cap = 0;
     std::string err;
 };
+
+// Host calls whose staging fits this many bytes go through a pinned buffer:
+// one copy in and one copy out, each a plain DMA (a pageable copy is staged
+// by the runtime in pieces, and each costs a synchronisation).  That is the
+// drop-in's per-message cost (write_message / read_message at the
+// reference's call granularity).
+constexpr size_t kPinnedCall = size_t(4) << 20;
 
 namespace {
 
@@ -236,6 +245,21 @@ capnp_status ensure_buf(capnp_ctx* ctx, uint8_t** buf, size_t* cap_io, size_t by
 
 capnp_status ensure_stage(capnp_ctx* ctx, size_t bytes) {
     return ensure_buf(ctx, &ctx->d_stage, &ctx->stage_cap, bytes);
+}
+
+capnp_status ensure_pin(capnp_ctx* ctx, size_t bytes) {
+    if (bytes <= ctx->pin_cap) return CAPNP_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    if (ctx->h_pin) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        HIP_TRY(hipHostFree(ctx->h_pin));
+        ctx->h_pin = nullptr;
+        ctx->pin_cap = 0;
+    }
+    const size_t cap = std::max<size_t>(round16(bytes) + 64, 1 << 16);
+    HIP_TRY(hipHostMalloc(&ctx->h_pin, cap, 0));
+    ctx->pin_cap = cap;
+    return CAPNP_OK;
 }
 
 // Enqueues the checks of `arrays` (device offset arrays of n + 1 entries with
@@ -361,12 +385,34 @@ capnp_status pack_host(capnp_ctx* ctx, const uint64_t* words, const uint64_t* of
     if (st != CAPNP_OK) return st;
     uint8_t* d = ctx->d_stage;
     hipStream_t s = ctx->stream;
+    const uint32_t tc = (n && nw / n >= kWordTileMean) ? 0u : tile_chunks_for(nw, n);
+    if (o_out + bound <= kPinnedCall) {
+        // small call: words and offsets in, offsets and the bound's bytes
+        // out, through the pinned buffer: one copy each way, one wait
+        st = ensure_pin(ctx, o_out + bound + 16);
+        if (st != CAPNP_OK) return st;
+        uint8_t* h = ctx->h_pin;
+        if (nw) memcpy(h + o_words, words + base, nw * 8);
+        memcpy(h + o_off, rel.data(), (n + 1) * 8);
+        HIP_TRY(hipMemcpyAsync(d, h, o_oo, hipMemcpyHostToDevice, s));
+        st = pack_batch_dev(ctx, reinterpret_cast<uint64_t*>(d + o_words),
+                            reinterpret_cast<uint64_t*>(d + o_off), n, d + o_out, bound,
+                            reinterpret_cast<uint64_t*>(d + o_oo), tc, s);
+        if (st != CAPNP_OK) return st;
+        HIP_TRY(hipMemcpyAsync(h + o_oo, d + o_oo, o_out - o_oo + bound, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        const uint64_t* oo = reinterpret_cast<const uint64_t*>(h + o_oo);
+        *total = oo[n];
+        const size_t ncopy = std::min<uint64_t>(oo[n], out_cap);
+        if (ncopy) memcpy(out, h + o_out, ncopy);
+        if (out_off_host) memcpy(out_off_host, oo, (n + 1) * 8);
+        return oo[n] > out_cap ? CAPNP_E_BUFFER_NOT_LARGE_ENOUGH : CAPNP_OK;
+    }
     if (nw) HIP_TRY(hipMemcpyAsync(d + o_words, words + base, nw * 8, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(d + o_off, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
     st = pack_batch_dev(ctx, reinterpret_cast<uint64_t*>(d + o_words),
                         reinterpret_cast<uint64_t*>(d + o_off), n, d + o_out, bound,
-                        reinterpret_cast<uint64_t*>(d + o_oo),
-                        (n && nw / n >= kWordTileMean) ? 0u : tile_chunks_for(nw, n), s);
+                        reinterpret_cast<uint64_t*>(d + o_oo), tc, s);
     if (st != CAPNP_OK) return st;
     std::vector<uint64_t> oo(n + 1);
     HIP_TRY(hipMemcpyAsync(oo.data(), d + o_oo, (n + 1) * 8, hipMemcpyDeviceToHost, s));
@@ -499,6 +545,7 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (ctx->h_frame) (void)hipHostFree(ctx->h_frame);
     if (ctx->d_bad) (void)hipFree(ctx->d_bad);
     if (ctx->h_bad) (void)hipHostFree(ctx->h_bad);
+    if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
     if (ctx->d_msg) (void)hipFree(ctx->d_msg);
     if (ctx->d_resync) (void)hipFree(ctx->d_resync);
     if (ctx->d_wt) (void)hipFree(ctx->d_wt);
@@ -1434,10 +1481,14 @@ static capnp_status read_message_impl(capnp_ctx* ctx, const uint8_t* in, size_t 
     // O(message), not O(remaining stream).
     const size_t pre = std::min<size_t>(in_len, kTablePrefixBytes);
     capnp_status st = ensure_stage(ctx, round16(pre + 16) + 64);
+    if (st == CAPNP_OK) st = ensure_pin(ctx, pre + 16);
     if (st != CAPNP_OK) return st;
     uint8_t* d = ctx->d_stage;
     hipStream_t s = ctx->stream;
-    if (pre) HIP_TRY(hipMemcpyAsync(d + o_in, in, pre, hipMemcpyHostToDevice, s));
+    if (pre) {
+        memcpy(ctx->h_pin, in, pre);
+        HIP_TRY(hipMemcpyAsync(d + o_in, ctx->h_pin, pre, hipMemcpyHostToDevice, s));
+    }
     HIP_TRY(capnp_launch_frame(d + o_in, pre, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
                                o.traversal_limit_in_words, (uint32_t)(o.has_traversal_limit != 0),
                                buffer_len, ctx->d_frame, s));
@@ -1468,6 +1519,31 @@ static capnp_status read_body(capnp_ctx* ctx, const FrameResult& fr, const uint8
     uint8_t* d = ctx->d_body;
     hipStream_t s = ctx->stream;
     const uint64_t offs[4] = {0, take, 0, fr.total_words};
+    // a small body: staged bytes and their unit offsets in, status and words
+    // out, through the pinned buffer (one copy each way)
+    const bool pinned = fr.total_words < kParallelBodyWords && o_res + o_st + 64 <= kPinnedCall;
+    if (pinned) {
+        st = ensure_pin(ctx, std::max<size_t>(o_res, o_st + 32) + 64);
+        if (st != CAPNP_OK) return st;
+        uint8_t* h = ctx->h_pin;
+        if (take) memcpy(h + o_in, in + fr.table_consumed, take);
+        memcpy(h + o_off, offs, sizeof(offs));
+        HIP_TRY(hipMemcpyAsync(di, h, o_off + sizeof(offs), hipMemcpyHostToDevice, s));
+        HIP_TRY(capnp_launch_unpack(di + o_in, reinterpret_cast<uint64_t*>(di + o_off), 1, 0,
+                                    reinterpret_cast<uint64_t*>(d),
+                                    reinterpret_cast<uint64_t*>(di + o_off + 16),
+                                    reinterpret_cast<int32_t*>(d + o_st),
+                                    reinterpret_cast<uint64_t*>(d + o_st + 16), nullptr, s));
+        HIP_TRY(hipMemcpyAsync(h, d, o_st + 24, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        uint64_t res[3];
+        memcpy(res, h + o_st, 24);  // status (low 32 bits), pad, consumed
+        memcpy(host_out, h, fr.total_words * 8);  // (as below: the words even on an error)
+        const int32_t status = (int32_t)(uint32_t)res[0];
+        if (status != CAPNP_OK) return (capnp_status)status;
+        *body_consumed = res[2];
+        return CAPNP_OK;
+    }
     if (take) HIP_TRY(hipMemcpyAsync(di + o_in, in + fr.table_consumed, take,
                                      hipMemcpyHostToDevice, s));
     if (fr.total_words >= kParallelBodyWords && take) {
