@@ -44,14 +44,8 @@
 
 
 
-#ifndef PACK_ASMOR
-#define PACK_ASMOR 0
-#endif
-#ifndef PACK_SELPRE
-#define PACK_SELPRE 0
-#endif
-#ifndef PACK_EARLYPOLL
-#define PACK_EARLYPOLL 0
+#ifndef PACK_LB1RT
+#define PACK_LB1RT 0  // look-back: the group's tile records and the first group window in one round trip
 #endif
 #ifndef PACK_PROF
 #define PACK_PROF 0  // look-back counters (scripts/pack_prof.py); 0 = product
@@ -1143,7 +1137,10 @@ __device__ uint64_t tile_aggregate(const LookbackArgs& A, uint64_t j, uint32_t l
 // Every wait is bounded: on timeout the waiter computes the missing aggregate
 // itself from the input (records are idempotent), so the kernel finishes with
 // the right answer under any workgroup dispatch order.
-constexpr uint32_t kGroup = 64;  // tiles per look-back group (<= 64: one lane per tile)
+#ifndef PACK_GROUP
+#define PACK_GROUP 63
+#endif
+constexpr uint32_t kGroup = PACK_GROUP;  // tiles per look-back group (<= 64: one lane per tile)
 constexpr int kSleep = 2;        // s_sleep between look-back polls (x 64 cycles)
 // group records per poll; measured: 64 -> 564 us, 16 -> 552, 4 -> 555, 1 -> 603
 constexpr uint32_t kGroupWindow = 16;
@@ -1183,7 +1180,7 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
 struct PrePoll {
     uint64_t st, rec;
 };
-__device__ __forceinline__ PrePoll pre_poll(const LookbackArgs& A, uint64_t t, uint32_t lane) {
+[[maybe_unused]] __device__ __forceinline__ PrePoll pre_poll(const LookbackArgs& A, uint64_t t, uint32_t lane) {
     const uint64_t g = t / kGroup;
     const uint32_t r = (uint32_t)(t % kGroup);
     const int64_t j = (int64_t)g - 1 - (int64_t)lane;
@@ -1205,27 +1202,57 @@ __device__ __forceinline__ PrePoll pre_poll(const LookbackArgs& A, uint64_t t, u
     // aggregates of the group's earlier tiles
     uint64_t within;
     uint64_t st = pre ? pre->st : (lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg);
+#if PACK_LB1RT == 2
+    // ... and of the previous group's tiles, polled in the same round trip
+    // (the previous group's record trails its last tile by a poll and a
+    // store); the group scan then starts two groups back
+    const uint64_t gp = g ? g - 1 : 0;
+    const uint32_t np = g ? kGroup : 0u;
+    uint64_t sp = lane < np ? poll_agent(&A.ts[gp * kGroup + lane]) : kFlagAgg;
+    const int64_t j0 = (int64_t)g - 2 - (int64_t)lane;
+    const uint64_t rec0 = lane < kGroupWindow ? (j0 >= 0 ? poll_agent(&A.gs[j0]) : kFlagInc) : 0;
+#endif
     for (uint32_t spins = 0;;) {
         const uint64_t miss = ballot64((st >> 62) == 0);
+#if PACK_LB1RT == 2
+        const uint64_t missp = ballot64((sp >> 62) == 0);
+        if (!miss && !missp) break;
+#else
         if (!miss) break;
+#endif
 #if PACK_PROF
         n_ws++;
 #endif
         if (++spins >= kSpinLimit) {
             if (lane == 0) PROF_ADD(2, 1);
+#if PACK_LB1RT == 2
+            const uint64_t j = miss ? g * kGroup + ctz64(miss) : gp * kGroup + ctz64(missp);
+#else
             const uint64_t j = g * kGroup + ctz64(miss);
+#endif
             const uint64_t a = tile_aggregate(A, j, lane);
             if (lane == 0) publish_agent(&A.ts[j], kFlagAgg | a);
         } else {
             __builtin_amdgcn_s_sleep(kSleep);
         }
         st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
+#if PACK_LB1RT == 2
+        sp = lane < np ? poll_agent(&A.ts[gp * kGroup + lane]) : kFlagAgg;
+#endif
     }
     {
         uint64_t v = st & kValMask;
         for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
         within = v;
     }
+#if PACK_LB1RT == 2
+    uint64_t prev;
+    {
+        uint64_t v = sp & kValMask;
+        for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+        prev = v;
+    }
+#endif
 #if PACK_PROF == 3
     if (lane == 0) TRACE(t, 7, RT());  // (the group's earlier tiles are summed)
 #endif
@@ -1233,14 +1260,25 @@ __device__ __forceinline__ PrePoll pre_poll(const LookbackArgs& A, uint64_t t, u
     if (group_last && !early_group && lane == 0) publish_agent(&A.gs[g], kFlagAgg | (within + agg));
     // exclusive prefix of the group: 64 groups per round; a group contributes
     // its inclusive record (and ends the scan), else its aggregate
+#if PACK_LB1RT == 2
+    uint64_t gexcl = prev;
+    int64_t idx = (int64_t)g - 2;
+    bool first = true;
+#else
     uint64_t gexcl = 0;
     int64_t idx = (int64_t)g - 1;
     bool first = pre != nullptr;
+#endif
     for (uint32_t spins = 0; idx >= 0;) {
         const int64_t j = idx - (int64_t)lane;
         const bool in_win = lane < kGroupWindow;
+#if PACK_LB1RT == 2
+        const uint64_t rec =
+            first ? rec0 : (!in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc));
+#else
         const uint64_t rec =
             first ? pre->rec : (!in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc));
+#endif
         first = false;
         const uint64_t inc = ballot64((rec & kFlagInc) != 0);
         const uint32_t first_inc = ctz64(inc);
@@ -2096,24 +2134,10 @@ __device__ __forceinline__ void cs_emit_word_sel(uint64_t w, uint32_t info, uint
     const uint32_t e3 = __builtin_amdgcn_alignbyte(0u, r2, s);
     const uint32_t pos = info & ((1u << kInfoPosBits) - 1u);
     uint32_t* b32 = reinterpret_cast<uint32_t*>(__builtin_align_down(region_m1 + pos, 4));
-#if PACK_ASMOR
-    // (ds_or_b32 as asm: the compiler's atomics were each followed by a full
-    // LGKM wait before the next LDS access; LDS ops of a wave complete in
-    // order, and the barrier before the copy-out waits for all of them)
-    const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)b32;
-    asm volatile("ds_or_b32 %0, %1\n\t"
-                 "ds_or_b32 %0, %2 offset:4\n\t"
-                 "ds_or_b32 %0, %3 offset:8\n\t"
-                 "ds_or_b32 %0, %4 offset:12"
-                 :
-                 : "v"(a), "v"(e0), "v"(e1), "v"(e2), "v"(e3)
-                 : "memory");
-#else
     __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-#endif
     if constexpr (SYNC) {
         if (idx < kSelCopy && d <= cnt) {
             const uint32_t rel = pos - oc;
@@ -2309,15 +2333,9 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     for (int w = 0; w < kWaves; w++) fits &= sm.wave_bytes[w] <= kStageBytes;
     fits = __builtin_amdgcn_readfirstlane((int)fits) != 0;
     uint64_t agg = 0;
-#if PACK_EARLYPOLL
-    PrePoll pp{};
-#endif
     if (wave == 0) {
         agg = scan_chunks32(sm, nc, lane);
         publish(LA, tile, agg, lane);
-#if PACK_EARLYPOLL
-        pp = pre_poll(LA, tile, lane);
-#endif
 #if PACK_PROF == 3
         if (lane == 0) TRACE(tile, 2, RT());
 #endif
@@ -2346,16 +2364,9 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             const uint32_t c = t0 - g;
             const uint32_t d = (c - lane) & (kSyncWords - 1);
             const uint32_t b = (lane + d - c) / (kSyncWords / 4u);
-#if PACK_SELPRE
-            const Sel8 sa = cs_sel(sm.sel, ilo[s]), sb2 = cs_sel(sm.sel, ihi[s]);
-            cs_emit_word_sel<SYNC>(clo[s], ilo[s], region_m1, sa, srs, oc, d, b);
-            cs_emit_word_sel<SYNC>(chi[s], ihi[s], region_m1, sb2, srs, oc, d,
-                                   b + 64u / (kSyncWords / 4u));
-#else
             cs_emit_word<SYNC>(clo[s], ilo[s], region_m1, sm.sel, srs, oc, d, b);
             cs_emit_word<SYNC>(chi[s], ihi[s], region_m1, sm.sel, srs, oc, d,
                                b + 64u / (kSyncWords / 4u));
-#endif
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -2364,7 +2375,8 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         wave_lds_sync();
         if (lane == 0) TRACE(tile, 3, RT());
 #endif
-#if PACK_EARLYPOLL
+#if PACK_LB1RT == 1
+        const PrePoll pp = pre_poll(LA, tile, lane);
         const uint64_t excl = tile_offset(LA, tile, agg, lane, early_group, &pp);
 #else
         const uint64_t excl = tile_offset(LA, tile, agg, lane, early_group);

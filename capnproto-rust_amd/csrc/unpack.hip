@@ -36,9 +36,6 @@
 #ifndef UNPACK_PROF
 #define UNPACK_PROF 0  // phase timers (scripts/unpack_prof.py); 0 = product
 #endif
-#ifndef UNPACK_LEANHOP
-#define UNPACK_LEANHOP 0
-#endif
 #ifndef UNPACK_SEGREC
 #define UNPACK_SEGREC 1
 #endif
@@ -479,24 +476,20 @@ union USmem {
 // run count) and q+8 (literal run count).  Left alone, the compiler merges
 // the adjacent tag and count reads into one ds_read_u16, which at an odd
 // address is a misaligned LDS access: replayed, and SQ_LDS_UNALIGNED_STALL
-// was half of this kernel's LDS cycles.  The tag is extracted from its
-// aligned dword instead (32-bit reads are never misaligned).
-// (Three ds_read_u8 kept apart by volatile -- a byte read is never
-// misaligned, and all three share q's address register -- measured slower:
-// 427 vs 403 us; volatile pins the reads' order.)
+// was half of this kernel's LDS cycles.  b1's address goes through an opaque
+// copy, so the three reads stay ds_read_u8 (never misaligned).  Round 4
+// (interleaved A/B, config 2, settled clocks): byte reads 445 vs 490 us for
+// the index-free decode and 297 vs 302 with the index, against the earlier
+// form (the tag extracted from its aligned dword, which costs a dependent
+// bit-field extract on every hop; round 1 measured that form faster, 403
+// vs 427 us, on a walk with more VALU per hop).
 __device__ __forceinline__ void rec_bytes(const uint8_t* B, uint32_t q, uint32_t& tag,
                                           uint32_t& b1, uint32_t& b9) {
     const uint32_t p = q - 1u;
-#if UNPACK_TAG8
     uint32_t p1 = p;
     asm("" : "+v"(p1));  // (b1's address, opaque: no merge with the tag into a u16 read)
     tag = B[p];
     b1 = B[p1 + 1u];
-#else
-    const uint32_t dw = *reinterpret_cast<const uint32_t*>(B + (p & ~3u));
-    tag = __builtin_amdgcn_ubfe(dw, (p & 3u) * 8u, 8u);
-    b1 = B[q];
-#endif
     b9 = B[q + 8];
 }
 
@@ -728,13 +721,9 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
     // (the hop runs under the exec mask of the lanes still
     // below stopw, so the state updates need no selects and the record
     // checks collect in a wave mask)
-#if UNPACK_LEANHOP
     // (the record checks as running maxima: cpe1 and cwe are fixed in phase
     // A, and a record past either bound is an error wherever it occurs)
     uint32_t qmx = 0, wmx = 0;
-#else
-    uint64_t errm = 0;
-#endif
 #pragma unroll 1  // (x2 / x4 / x8 measured within noise)
     for (uint32_t it = 0; it < kSyncWords; it++) {
         if (w < stopw) {
@@ -746,22 +735,12 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
             rec_bytes(B, qn, ntag, nb1, nb9);
             const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
             const uint32_t wn0 = w + 1u + cnt;
-#if UNPACK_LEANHOP
             qmx = max(qmx, qe);
             wmx = max(wmx, wn0);
-#else
-            errm |= ballot64(qe > cpe1 || wn0 > cwe);
-#endif
             const uint32_t wn = wn0 < cwe ? wn0 : cwe;
             S.dpos[w] = (uint16_t)(q - 1u);
-#if UNPACK_LEANHOP
             if (isf && wn > w + 1)  // literal-run words (rare)
                 lit_entries(S, w, q - 1u, (WT && wn > wlim ? wlim : wn) - w - 1);
-#else
-            if (ballot64(isf && wn > w + 1)) {  // literal-run words (rare)
-                if (isf) lit_entries(S, w, q - 1u, (WT && wn > wlim ? wlim : wn) - w - 1);
-            }
-#endif
             q = qn;
             w = wn;
             tag = ntag;
@@ -769,11 +748,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
             b9 = nb9;
         }
     }
-#if UNPACK_LEANHOP
     err = qmx > cpe1 || wmx > cwe;
-#else
-    err = (errm >> lane_id()) & 1;
-#endif
 #if UNPACK_PROF
     const uint64_t lt1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -909,18 +884,11 @@ constexpr uint32_t kSegChunks = 16;  // tiles of at most this many chunks take t
 __device__ __forceinline__ void seg_hop(const uint8_t* B, uint32_t& p, uint32_t& w) {
     uint32_t tag, b1, b9;
     rec_bytes(B, p + 1u, tag, b1, b9);
-#if UNPACK_TAG8
     asm("" : "+v"(tag));  // (tag's range unknown: no 16-bit arithmetic on it)
-#endif
     const bool isz = tag == 0, isf = tag == 0xFF;
-#if UNPACK_TAG8
     const uint32_t cnt = isf ? b9 : (isz ? b1 : 0u);
     const uint32_t ext = isf ? 8u * b9 + 1u : (isz ? 1u : 0u);
     p += __builtin_popcount(tag) + ext + 1u;
-#else
-    const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
-    p += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) + (isf ? 8u * cnt : 0u);
-#endif
     w += 1u + cnt;
 }
 

@@ -121,6 +121,27 @@ def main():
             gap = (T[1:, 2] - T[:-1, 2]) / 100.0
             print(f"   publish(t) - publish(t-1): mean {gap.mean():.2f} p10/p90 "
                   f"{np.percentile(gap, 10):.2f}/{np.percentile(gap, 90):.2f} us")
+            # the earliest a tile's offset can be known: every earlier tile has
+            # published its aggregate (cummax of the publish times before t);
+            # what the look-back waits beyond that is the chain's own latency
+            ready = np.maximum.accumulate(T[:, 2])
+            ready = np.concatenate([[T[0, 2]], ready[:-1]])
+            inh = np.maximum(0, ready - T[:, 3]) / 100.0
+            lb = (T[:, 4] - T[:, 3]) / 100.0
+            extra = (T[:, 4] - np.maximum(ready, T[:, 3])) / 100.0
+            print(f"   lookback {lb.mean():.2f}: predecessors unpublished at its start {inh.mean():.2f} "
+                  f"(p90 {np.percentile(inh, 90):.2f}; {(inh > 0).mean():.3f} of tiles), "
+                  f"beyond the last publish {extra.mean():.2f} (p90 {np.percentile(extra, 90):.2f}) us")
+            # dispatch skew by XCD: mean start time of each XCD's tiles relative
+            # to the tile-index order (start - the linear fit of start vs t)
+            st = (T[:, 0] - t0) / 100.0
+            fit = np.polyval(np.polyfit(np.arange(ntiles), st, 1), np.arange(ntiles))
+            print("   start - fit by XCD: " + " ".join(
+                f"{(st - fit)[xcc == x].mean():+.2f}" for x in range(8)))
+            pub = (T[:, 2] - t0) / 100.0
+            late = pub - np.minimum.accumulate(pub[::-1])[::-1]
+            print(f"   publish later than some later tile's: mean {late.mean():.2f} "
+                  f"p90 {np.percentile(late, 90):.2f} us")
         q = np.percentile(T[:, 5] - T[:, order[0]], [10, 50, 90]) / 100.0
         print(f"   lifetime p10/p50/p90 {q[0]:.2f}/{q[1]:.2f}/{q[2]:.2f} us; "
               f"first start->last start {starts[-1] - starts[0]:.1f} us")

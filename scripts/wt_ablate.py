@@ -38,7 +38,8 @@ def main():
     if argv and argv[0].startswith("--wl="):  # (gpu.sh py= steps pass arguments, not env)
         wl = argv.pop(0)[5:]
     libs = argv or ([os.path.join(ROOT, "capnproto-rust_amd/capnp_amd/libcapnp_packed.so")]
-                    + sorted(glob.glob(os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_*.so"))))
+                    + sorted(p for p in glob.glob(os.path.join(ROOT, "capnproto-rust_amd/build/abl/libcapnp_packed_*.so"))
+                           if "prof" not in os.path.basename(p)))
     print(f"workload {wl}", flush=True)
     args = bench.parse(["--workload", wl,
                         "--chunk-words", os.environ.get("CW", "128")])
@@ -65,8 +66,14 @@ def main():
     stream = torch.cuda.current_stream()
     P = C.c_void_p
     variants = [(os.path.basename(p), *load(p)) for p in libs]
+    # settle the GPU's clocks first (after idle the per-call times run ~10 %
+    # slow for ~30 ms of load: scripts/clock_curve.py)
+    for _ in range(60):
+        ctx.pack_batch_into(words, offs, out, oo, chunks_per_tile=tc, sync=sync)
+        ctx.unpack_batch_into(ref_out, ref_oo, offs, back, status, chunks_per_tile=utc, sync=ref_sync)
+    torch.cuda.synchronize()
     res = {v[0]: {"pack": [], "unpack": [], "nosync": []} for v in variants}
-    for r in range(5):
+    for r in range(int(os.environ.get("ROUNDS", "7"))):
         for name, L, h in variants:
             for kind in ("pack", "unpack", "nosync"):
                 e0 = torch.cuda.Event(enable_timing=True)
@@ -90,6 +97,15 @@ def main():
                 e1.record(stream)
                 e1.synchronize()
                 res[name][kind].append(e0.elapsed_time(e1) / 5)
+                if r == 0:  # each variant's output checked once against the product's
+                    if kind == "pack":
+                        ok = (torch.equal(oo, ref_oo) and torch.equal(sync, ref_sync)
+                              and torch.equal(out[:int(ref_oo[-1])], ref_out[:int(ref_oo[-1])]))
+                    else:
+                        ok = torch.equal(back, words) and bool((status == 0).all())
+                    if not ok:
+                        print(f"MISMATCH {name} {kind}", flush=True)
+                    back.zero_()
     U = total * 8
     for name, d in res.items():
         pm, um, nm = (statistics.median(d[k]) for k in ("pack", "unpack", "nosync"))
