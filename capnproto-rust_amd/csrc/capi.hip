@@ -109,7 +109,7 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
                                           uint64_t* d_consumed, void* d_ws, size_t ws_bytes,
                                           hipStream_t s, int* passes, int* serial);
 extern "C" hipError_t capnp_launch_frame(const uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t,
-                                         uint32_t, uint64_t, FrameResult*, hipStream_t);
+                                         uint32_t, uint64_t, uint64_t, FrameResult*, hipStream_t);
 
 namespace {
 
@@ -329,20 +329,28 @@ constexpr uint64_t kWordTileMean = 512;
 // synchronisation to read it): word tiles (capnp_launch_pack_wt: chunks of
 // any length) for a mean chunk of at least kWordTileMean words, else chunk
 // tiles of about capnp_pack_tile_words() words.
+// host_wr: the batch's word range when the caller already knows it (and has
+// validated the offsets on the host): no synchronisation at all.
 capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint64_t* d_off,
                             size_t n, uint8_t* d_out, size_t cap, uint64_t* d_out_off,
-                            uint32_t tc, hipStream_t s, uint32_t* d_sync = nullptr) {
+                            uint32_t tc, hipStream_t s, uint32_t* d_sync = nullptr,
+                            const uint64_t* host_wr = nullptr) {
     if (n > 0 && !d_off) return CAPNP_E_INVALID_ARGUMENT;
     if (!d_out_off) return CAPNP_E_INVALID_ARGUMENT;
     if (tc == 0 && n > 0) {
         uint64_t wr[2];
-        capnp_status vst = check_offsets(ctx, s, {{d_off, n, ~0ull}}, false);
-        if (vst != CAPNP_OK) return vst;
-        HIP_TRY(hipMemcpyAsync(&wr[0], d_off, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(&wr[1], d_off + n, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        vst = offsets_verdict(ctx);
-        if (vst != CAPNP_OK) return vst;
+        if (host_wr) {
+            wr[0] = host_wr[0];
+            wr[1] = host_wr[1];
+        } else {
+            capnp_status vst = check_offsets(ctx, s, {{d_off, n, ~0ull}}, false);
+            if (vst != CAPNP_OK) return vst;
+            HIP_TRY(hipMemcpyAsync(&wr[0], d_off, 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipMemcpyAsync(&wr[1], d_off + n, 8, hipMemcpyDeviceToHost, s));
+            HIP_TRY(hipStreamSynchronize(s));
+            vst = offsets_verdict(ctx);
+            if (vst != CAPNP_OK) return vst;
+        }
         if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
         const uint64_t words = wr[1] - wr[0];
         if (words && (words / n >= kWordTileMean || force_word_tiles())) {
@@ -375,7 +383,11 @@ capnp_status pack_host(capnp_ctx* ctx, const uint64_t* words, const uint64_t* of
     const uint64_t base = n ? off[0] : 0;
     const uint64_t nw = n ? off[n] - base : 0;
     std::vector<uint64_t> rel(n + 1);
-    for (size_t i = 0; i <= n; i++) rel[i] = n ? off[i] - base : 0;
+    for (size_t i = 0; i <= n; i++) {
+        rel[i] = n ? off[i] - base : 0;
+        if (i && off[i] < off[i - 1]) return CAPNP_E_INVALID_ARGUMENT;  // (checked here, on the host)
+    }
+    const uint64_t wr[2] = {0, nw};
     const size_t bound = capnp_packed_batch_bound_bytes(nw, n);
     const size_t o_words = 0;
     const size_t o_off = round16(nw * 8);
@@ -397,7 +409,7 @@ capnp_status pack_host(capnp_ctx* ctx, const uint64_t* words, const uint64_t* of
         HIP_TRY(hipMemcpyAsync(d, h, o_oo, hipMemcpyHostToDevice, s));
         st = pack_batch_dev(ctx, reinterpret_cast<uint64_t*>(d + o_words),
                             reinterpret_cast<uint64_t*>(d + o_off), n, d + o_out, bound,
-                            reinterpret_cast<uint64_t*>(d + o_oo), tc, s);
+                            reinterpret_cast<uint64_t*>(d + o_oo), tc, s, nullptr, wr);
         if (st != CAPNP_OK) return st;
         HIP_TRY(hipMemcpyAsync(h + o_oo, d + o_oo, o_out - o_oo + bound, hipMemcpyDeviceToHost, s));
         HIP_TRY(hipStreamSynchronize(s));
@@ -412,7 +424,7 @@ capnp_status pack_host(capnp_ctx* ctx, const uint64_t* words, const uint64_t* of
     HIP_TRY(hipMemcpyAsync(d + o_off, rel.data(), (n + 1) * 8, hipMemcpyHostToDevice, s));
     st = pack_batch_dev(ctx, reinterpret_cast<uint64_t*>(d + o_words),
                         reinterpret_cast<uint64_t*>(d + o_off), n, d + o_out, bound,
-                        reinterpret_cast<uint64_t*>(d + o_oo), tc, s);
+                        reinterpret_cast<uint64_t*>(d + o_oo), tc, s, nullptr, wr);
     if (st != CAPNP_OK) return st;
     std::vector<uint64_t> oo(n + 1);
     HIP_TRY(hipMemcpyAsync(oo.data(), d + o_oo, (n + 1) * 8, hipMemcpyDeviceToHost, s));
@@ -1468,34 +1480,63 @@ capnp_status capnp_packed_write_message(capnp_ctx* ctx, const uint64_t* const* s
     return st;
 }
 
-static capnp_status read_message_impl(capnp_ctx* ctx, const uint8_t* in, size_t in_len,
+// A message whose body is short (< kParallelBodyWords words, and within the
+// caller's capacity) in ONE round trip: the input prefix that can hold the
+// table and such a body (<= 10 bytes per word) goes in through the pinned
+// buffer, the frame kernel reads the table and leaves the body's unit in
+// device memory, the batch unpack decodes it from there (a body too long,
+// or a failed table, is an empty unit), and the frame result, the body's
+// status and consumed bytes and its words come back together.  *done =
+// false when the body still has to be read the long way (read_body): it is
+// longer than that, or its unit ran past the staged prefix of a longer
+// input.  The reference's per-message cost (serialize_packed::read_message
+// once per request, benchmark.rs:207-259) is this call.
+static capnp_status read_message_fast(capnp_ctx* ctx, const uint8_t* in, size_t in_len,
                                       const capnp_reader_options* opts, int try_mode,
-                                      int no_alloc, uint64_t buffer_len, FrameResult* fr,
-                                      uint8_t** d_body_out) {
+                                      int no_alloc, uint64_t buffer_len, uint64_t cap_words,
+                                      FrameResult* fr, const uint8_t** words,
+                                      uint64_t* body_consumed, bool* done) {
     capnp_reader_options o = opts ? *opts : capnp_default_reader_options();
-    const size_t o_in = 0;
-    // Only the table's read units go to the device here: a table of <= 511
-    // segments is <= 257 words, which decode from at most 10 bytes each, so
-    // a 4 KiB prefix holds it whatever the stream (the body is staged by
-    // read_body from the table's end, bounded the same way).  A call costs
-    // O(message), not O(remaining stream).
-    const size_t pre = std::min<size_t>(in_len, kTablePrefixBytes);
-    capnp_status st = ensure_stage(ctx, round16(pre + 16) + 64);
-    if (st == CAPNP_OK) st = ensure_pin(ctx, pre + 16);
+    *done = false;
+    *body_consumed = 0;
+    const uint64_t cap = std::min<uint64_t>(cap_words, kParallelBodyWords - 1);
+    const size_t stage = std::min<size_t>(in_len, kTablePrefixBytes + cap * 10 + 16);
+    const size_t o_st = round16(cap * 8);  // body words, then status, pad, consumed
+    const size_t h_out = round16(stage + 16);
+    capnp_status st = ensure_stage(ctx, round16(stage + 16) + 64);
+    if (st == CAPNP_OK) st = ensure_buf(ctx, &ctx->d_body, &ctx->body_cap, o_st + 64);
+    if (st == CAPNP_OK) st = ensure_pin(ctx, h_out + o_st + 64);
     if (st != CAPNP_OK) return st;
     uint8_t* d = ctx->d_stage;
+    uint8_t* db = ctx->d_body;
+    uint8_t* h = ctx->h_pin;
     hipStream_t s = ctx->stream;
-    if (pre) {
-        memcpy(ctx->h_pin, in, pre);
-        HIP_TRY(hipMemcpyAsync(d + o_in, ctx->h_pin, pre, hipMemcpyHostToDevice, s));
+    if (stage) {
+        memcpy(h, in, stage);
+        HIP_TRY(hipMemcpyAsync(d, h, stage, hipMemcpyHostToDevice, s));
     }
-    HIP_TRY(capnp_launch_frame(d + o_in, pre, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
+    FrameResult* df = ctx->d_frame;
+    HIP_TRY(capnp_launch_frame(d, stage, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
                                o.traversal_limit_in_words, (uint32_t)(o.has_traversal_limit != 0),
-                               buffer_len, ctx->d_frame, s));
-    HIP_TRY(hipMemcpyAsync(ctx->h_frame, ctx->d_frame, sizeof(FrameResult), hipMemcpyDeviceToHost, s));
+                               buffer_len, cap, df, s));
+    HIP_TRY(capnp_launch_unpack(d, df->body_in_off, 1, 0, reinterpret_cast<uint64_t*>(db),
+                                df->body_out_off, reinterpret_cast<int32_t*>(db + o_st),
+                                reinterpret_cast<uint64_t*>(db + o_st + 16), nullptr, s));
+    HIP_TRY(hipMemcpyAsync(ctx->h_frame, df, sizeof(FrameResult), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(h + h_out, db, o_st + 24, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     *fr = *ctx->h_frame;
-    (void)d_body_out;
+    if (fr->status != CAPNP_OK || fr->total_words > cap) return CAPNP_OK;  // (the caller decides)
+    uint64_t res[3];
+    memcpy(res, h + h_out + o_st, 24);  // status (low 32 bits), pad, consumed
+    const int32_t bst = (int32_t)(uint32_t)res[0];
+    if ((bst == CAPNP_E_PREMATURE_END_OF_PACKED_INPUT || bst == CAPNP_E_FAILED_TO_FILL_WHOLE_BUFFER) &&
+        stage < in_len)
+        return CAPNP_OK;  // the unit ran past the staged prefix: the long way
+    *done = true;
+    *words = h + h_out;  // (the caller copies them out, even on an error, as read_body does)
+    if (bst != CAPNP_OK) return (capnp_status)bst;
+    *body_consumed = res[2];
     return CAPNP_OK;
 }
 
@@ -1593,7 +1634,12 @@ capnp_status capnp_packed_read_message(capnp_ctx* ctx, const uint8_t* in, size_t
     *consumed = 0;
     *nseg_out = 0;
     FrameResult fr;
-    capnp_status st = read_message_impl(ctx, in, in_len, opts, try_mode, 0, 0, &fr, nullptr);
+    uint64_t used = 0;
+    bool done = false;
+    const uint8_t* fw = nullptr;
+    capnp_status st = read_message_fast(ctx, in, in_len, opts, try_mode, 0, 0, body_cap_words, &fr,
+                                        &fw, &used, &done);
+    if (done && fr.total_words) memcpy(body, fw, fr.total_words * 8);
     if (st != CAPNP_OK) return st;
     if (fr.status != CAPNP_OK) return (capnp_status)fr.status;
     if (fr.total_words > body_cap_words) {
@@ -1602,8 +1648,7 @@ capnp_status capnp_packed_read_message(capnp_ctx* ctx, const uint8_t* in, size_t
         *nseg_out = fr.nseg;
         return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;
     }
-    uint64_t used = 0;
-    st = read_body(ctx, fr, in, in_len, reinterpret_cast<uint8_t*>(body), &used);
+    if (!done) st = read_body(ctx, fr, in, in_len, reinterpret_cast<uint8_t*>(body), &used);
     if (st != CAPNP_OK) return st;
     memcpy(seg_words_out, fr.seg_words, fr.nseg * sizeof(uint32_t));
     *nseg_out = fr.nseg;
@@ -1623,13 +1668,23 @@ capnp_status capnp_packed_read_message_no_alloc(capnp_ctx* ctx, const uint8_t* i
     if (((uintptr_t)buffer) % 8 != 0) return CAPNP_E_UNALIGNED_SEGMENT;  // serialize.rs:341-343
     if (buffer_len < 8) return CAPNP_E_BUFFER_NOT_LARGE_ENOUGH;          // :345-347
     FrameResult fr;
-    capnp_status st = read_message_impl(ctx, in, in_len, opts, try_mode, 1, buffer_len, &fr, nullptr);
-    if (st != CAPNP_OK) return st;
+    uint64_t used = 0;
+    bool done = false;
+    // (the frame kernel checks the table plus body against buffer_len, so a
+    // body it passes fits after the table)
+    const uint64_t cap_words = buffer_len / 8;
+    const uint8_t* fw = nullptr;
+    capnp_status st = read_message_fast(ctx, in, in_len, opts, try_mode, 1, buffer_len, cap_words,
+                                        &fr, &fw, &used, &done);
+    if (st != CAPNP_OK && !done) return st;
     // the table bytes land in the caller's buffer as the reference reads them
     if (fr.status == CAPNP_OK) memcpy(buffer, fr.table, fr.table_bytes);
     if (fr.status != CAPNP_OK) return (capnp_status)fr.status;
-    uint64_t used = 0;
-    st = read_body(ctx, fr, in, in_len, buffer + fr.table_bytes, &used);
+    if (done) {  // (the words came back with the table)
+        if (fr.total_words) memcpy(buffer + fr.table_bytes, fw, fr.total_words * 8);
+    } else {
+        st = read_body(ctx, fr, in, in_len, buffer + fr.table_bytes, &used);
+    }
     if (st != CAPNP_OK) return st;
     *nseg_out = fr.nseg;
     *table_bytes_out = fr.table_bytes;

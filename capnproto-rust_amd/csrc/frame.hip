@@ -72,9 +72,14 @@ __device__ __forceinline__ uint32_t le32(const uint8_t* p) {
 
 __global__ void frame_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_alloc,
                              uint32_t try_mode, uint64_t limit, uint32_t has_limit,
-                             uint64_t buffer_len, FrameResult* __restrict__ r) {
+                             uint64_t buffer_len, uint64_t body_cap,
+                             FrameResult* __restrict__ r) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     uint8_t* t = r->table;
+    // (a chained body unpack reads these: an empty unit unless the table is
+    // read and its body fits body_cap words)
+    r->body_in_off[0] = r->body_in_off[1] = 0;
+    r->body_out_off[0] = r->body_out_off[1] = 0;
     uint64_t used = 0, nread = 0, pos = 0;
     r->nseg = 0;
     r->total_words = 0;
@@ -129,7 +134,7 @@ __global__ void frame_kernel(const uint8_t* __restrict__ in, uint64_t in_len, ui
     r->body_in_off[0] = pos;
     r->body_in_off[1] = in_len;
     r->body_out_off[0] = 0;
-    r->body_out_off[1] = total;
+    r->body_out_off[1] = total <= body_cap ? total : 0;
     r->status = ST_OK;
 }
 
@@ -137,9 +142,9 @@ __global__ void frame_kernel(const uint8_t* __restrict__ in, uint64_t in_len, ui
 
 extern "C" hipError_t capnp_launch_frame(const uint8_t* d_in, uint64_t in_len, uint32_t no_alloc,
                                          uint32_t try_mode, uint64_t limit, uint32_t has_limit,
-                                         uint64_t buffer_len, FrameResult* d_result,
-                                         hipStream_t stream) {
+                                         uint64_t buffer_len, uint64_t body_cap,
+                                         FrameResult* d_result, hipStream_t stream) {
     hipLaunchKernelGGL(frame_kernel, dim3(1), dim3(64), 0, stream, d_in, in_len, no_alloc,
-                       try_mode, limit, has_limit, buffer_len, d_result);
+                       try_mode, limit, has_limit, buffer_len, body_cap, d_result);
     return hipGetLastError();
 }

@@ -79,22 +79,48 @@ def main():
     res = {"what": "write_message + read_message per call through the C ABI "
                    "(capnp_packed_write_message / capnp_packed_read_message) vs the "
                    "reference's loops on one CPU thread (oracle/refloop_oracle.c)"}
-    # carsales requests, one per call pair, as the reference benchmark does
+    # carsales requests, one per call pair, as the reference benchmark does:
+    # the whole request loop timed as one block (after one untimed pass),
+    # buffers allocated once
     words, msg_off, _ = O.carsales_stream(args.reqs * 1600)
     m = min(args.reqs, len(msg_off) - 2)
-    t_gpu, t_cpu, ub = 0.0, 0.0, 0
-    for k in range(m):
-        seg = np.ascontiguousarray(words[int(msg_off[k]):int(msg_off[k + 1])])
-        t_gpu += gpu_pair(seg, 1)[0][0]
-        ub += 8 * len(seg)
+    segs_l = [np.ascontiguousarray(words[int(msg_off[k]):int(msg_off[k + 1])]) for k in range(m)]
+    maxw = max(len(x) for x in segs_l)
+    cap = L.capnp_packed_batch_bound_bytes(maxw + 1, 3)
+    out = np.empty(cap, np.uint8)
+    body = np.empty(maxw, np.uint64)
+    segs = np.empty(512, np.uint32)
+    n, used, nseg = C.c_size_t(0), C.c_size_t(0), C.c_uint32(0)
+    ptrs = [(C.c_void_p * 1)(x.ctypes.data) for x in segs_l]
+    lens = [(C.c_uint32 * 1)(len(x)) for x in segs_l]
+    ub = sum(8 * len(x) for x in segs_l)
+    t_gpu = None
+    for rep in range(3):
+        tw = tr = 0.0
+        t0 = time.perf_counter()
+        for k in range(m):
+            ta = time.perf_counter()
+            st = L.capnp_packed_write_message(h, ptrs[k], lens[k], 1, out.ctypes.data, cap, C.byref(n))
+            tb = time.perf_counter()
+            st2 = L.capnp_packed_read_message(h, out.ctypes.data, n.value, C.byref(opts), 0,
+                                              body.ctypes.data, maxw, segs.ctypes.data,
+                                              C.byref(nseg), C.byref(used))
+            tw += tb - ta
+            tr += time.perf_counter() - tb
+            assert st == 0 and st2 == 0 and used.value == n.value
+        t = time.perf_counter() - t0
+        assert np.array_equal(body[:len(segs_l[-1])], segs_l[-1])
+        if rep and (t_gpu is None or t < t_gpu[0]):
+            t_gpu = (t, tw, tr)
     ww = words[:int(msg_off[m])]
-    tw, tr, _, ok = O.refloop_messages_roundtrip_mt(ww, msg_off[:m + 1], 1)
+    tw_c, tr_c, _, ok = O.refloop_messages_roundtrip_mt(ww, msg_off[:m + 1], 1)
     assert ok
-    t_cpu = tw + tr
+    t_cpu = tw_c + tr_c
     res["carsales"] = {
         "requests": m, "mean_request_bytes": round(ub / m, 1),
-        "gpu_us_per_request": round(t_gpu / m * 1e6, 2),
-        "gpu_requests_per_s": round(m / t_gpu, 1),
+        "gpu_us_per_request": round(t_gpu[0] / m * 1e6, 2),
+        "gpu_write_us": round(t_gpu[1] / m * 1e6, 2), "gpu_read_us": round(t_gpu[2] / m * 1e6, 2),
+        "gpu_requests_per_s": round(m / t_gpu[0], 1),
         "cpu_1thread_us_per_request": round(t_cpu / m * 1e6, 3),
         "cpu_1thread_requests_per_s": round(m / t_cpu, 1),
     }
