@@ -2498,6 +2498,118 @@ __device__ __forceinline__ void size_step_s(StageState& pk, uint64_t w, uint32_t
     pk.total += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
 }
 
+// The run state at the end R1 = R0 + nw of a wave's range, from the range's
+// own words (w[s] = word R0 + 64 s + lane, sb[s] = their chunk-start bits):
+// the last sure head or chunk start in the range (word R0 itself counts
+// only as a chunk start: its sureness needs word R0 - 1), then heads every
+// 256 words through an all-zero / all-0xFF stretch, or the steps resolved
+// forward from it.  homog = 1 / 2 when the range has none and is one
+// all-zero / all-0xFF stretch (the state at R1 then follows from the state
+// at R0: wt_compose), 3 when it has none and is neither (pop-7/8 words:
+// the caller searches before R0).  No memory access: the in-kernel
+// derivation's global searches (carry_in_b's deep windows, run_ext_b's
+// forward loop) had made pack_wt_kernel 1194 us at config 4 (640 with a
+// planned entry per range), its long zero / literal stretches sending most
+// waves to them.
+struct RangeExit {
+    Carry c;
+    uint32_t homog;
+};
+__device__ __forceinline__ RangeExit range_exit(const uint64_t (&w)[kStageSteps],
+                                                const uint64_t (&sb)[kStageSteps], uint32_t nw,
+                                                uint32_t lane) {
+    uint32_t t[kStageSteps];
+#pragma unroll
+    for (uint32_t s = 0; s < kStageSteps; s++) t[s] = tag_of(w[s]);
+    int ks = -1;
+    uint32_t js = 0;
+    bool allz = true, allf = true;  // over the words from the head found (or all)
+#pragma unroll
+    for (int s = kStageSteps - 1; s >= 0; s--) {
+        const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
+        const bool v = lane < nv;
+        const uint32_t up = (uint32_t)__shfl_up((int)t[s], 1, 64);
+        // (lane 63 of the step below by readlane, outside the select: a
+        // shuffle under it would run with lane 63 masked off and read 0)
+        const uint32_t below = s ? (uint32_t)__builtin_amdgcn_readlane((int)t[s > 0 ? s - 1 : 0], 63) : 0u;
+        const uint32_t pt = lane ? up : below;
+        const bool sure = v && (((sb[s] >> lane) & 1) || ((lane || s) && sure_head(t[s], pt)));
+        if (ks < 0) {
+            const uint64_t G = ballot64(sure);
+            const uint32_t j = G ? 63u - (uint32_t)__builtin_clzll(G) : 0u;
+            const bool mine = v && (!G || lane >= j);
+            allz = allz && ballot64(mine && t[s] != 0) == 0;
+            allf = allf && ballot64(mine && t[s] != 0xFF) == 0;
+            if (G) {
+                ks = s;
+                js = j;
+            }
+        }
+    }
+    RangeExit r{{0u, 0u}, 0u};
+    if (ks < 0) {
+        r.homog = allz ? 1u : (allf ? 2u : 3u);
+        return r;
+    }
+    const uint32_t sp = 64u * (uint32_t)ks + js;  // the last sure head, range-relative
+    if (allz || allf) {
+        r.c = Carry{allz ? 1u : 2u, 255u - (nw - 1u - sp) % 256u};
+        return r;
+    }
+    Carry c{0, 0};  // resolve forward from the head (no sure head after it)
+#pragma unroll
+    for (int s = 0; s < kStageSteps; s++) {
+        if (s < ks) continue;
+        const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
+        const uint64_t V = low_mask(nv) & (s == ks ? ~low_mask(js) : ~0ull);
+        const uint32_t pop = __builtin_popcount(t[s]);
+        c = resolve_step_s(ballot64(t[s] == 0) & V, ballot64(pop >= 7) & V,
+                           ballot64(t[s] == 0xFF) & V, s == ks ? 1ull << js : 0ull,
+                           s == ks ? 64u : nv, c)
+                .next;
+    }
+    r.c = c;
+    return r;
+}
+
+// The state after n words of one all-zero (T = 1) / all-0xFF (T = 2)
+// stretch entered in state c: the open run of the same kind absorbs up to
+// its remaining words, then a head every 256 words.
+__device__ __forceinline__ Carry wt_compose(Carry c, uint32_t T, uint32_t n) {
+    const uint32_t a = c.type == T ? c.rem : 0u;
+    if (a >= n) return Carry{T, a - n};
+    return Carry{T, 255u - (n - a - 1u) % 256u};
+}
+
+// Words from R0 on that the run open there (c) absorbs, from the range's
+// own words: the leading words of its class (zero / at most one zero byte)
+// before a chunk start, capped by the run's room.  *beyond = true when the
+// whole range is such words and the run has room past it (the caller asks
+// run_ext_b).
+__device__ __forceinline__ uint32_t range_ext(const uint64_t (&w)[kStageSteps],
+                                              const uint64_t (&sb)[kStageSteps], uint32_t nw,
+                                              Carry c, uint32_t lane, bool& beyond) {
+    beyond = false;
+    if (c.type == 0 || c.rem == 0) return 0;
+    uint32_t lead = 0;
+    bool open = true;
+#pragma unroll
+    for (uint32_t s = 0; s < kStageSteps; s++) {
+        const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
+        const uint32_t tag = tag_of(w[s]);
+        const bool cls = c.type == 1 ? tag == 0 : __builtin_popcount(tag) >= 7;
+        const uint32_t cut = ctz64(sb[s]);
+        const uint32_t lim = cut < nv ? cut : nv;
+        const uint32_t l = ctz64(~ballot64(lane < lim && cls));
+        if (open) {
+            lead += l < lim ? l : lim;
+            open = l >= lim && lim == 64u;
+        }
+    }
+    beyond = open && lead < c.rem;
+    return lead < c.rem ? lead : c.rem;
+}
+
 // (6 waves per SIMD: the LDS, 24.3 KB, allows 6 workgroups per CU)
 template <bool SYNC>
 __global__ void __launch_bounds__(kThreads, 6)
@@ -2583,15 +2695,20 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         const uint64_t bits = rr ? (lo >> rr) | (hi << (64 - rr)) : lo;
         smk[s] = nv ? bits & low_mask(nv) : 0ull;
     }
-    // the run state entering the next range (R1), from this range's last 64
-    // words (pack_wt_plan's carry_in_b over the same window)
+    // the run state entering the next range (R1), from this range's own
+    // words (range_exit): wcarry = type | rem << 2 | homog << 10
     if (succ) {
         uint32_t rec = 0;
         if (((readlane64(cbv, kStageSteps) >> rr) & 1) == 0) {  // R1 inside a chunk
-            const Carry c = carry_in_b<64>(in, cbits, b64, wlo, R1, lane, cache[kStageSteps - 1],
-                                           readlane64(cache[kStageSteps - 2], 63),
-                                           smk[kStageSteps - 1]);
-            rec = c.type | (c.rem << 2);
+            const RangeExit ex = range_exit(cache, smk, nw, lane);
+            Carry c = ex.c;
+            uint32_t hg = ex.homog;
+            if (hg == 3) {  // no sure head, pop-7/8 words: search before R0 (rare)
+                c = carry_in_b<64>(in, cbits, b64, wlo, R1, lane, cache[kStageSteps - 1],
+                                   readlane64(cache[kStageSteps - 2], 63), smk[kStageSteps - 1]);
+                hg = 0;
+            }
+            rec = c.type | (c.rem << 2) | (hg << 10);
         }
         if (lane == 0) wm.wcarry[wave + 1] = rec;
     }
@@ -2603,18 +2720,43 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
 #pragma unroll
     for (uint32_t s = 0; s < kStageSteps; s++) asm volatile("" : "+v"(cache[s]));
     __syncthreads();
-    const uint32_t pin = !have ? 0u : (wave == 0 ? pin0 : uniform(wm.wcarry[wave]));
-    const Carry cin{pin & 3u, (pin >> 2) & 0xFFu};
+    // the state entering this range: the tile's planned entry, carried
+    // through the earlier ranges (a homogeneous range composes: wt_compose)
+    Carry cin{pin0 & 3u, (pin0 >> 2) & 0xFFu};
+    for (uint32_t v = 1; v <= wave; v++) {
+        const uint32_t e = uniform(wm.wcarry[v]);
+        const uint32_t hg = e >> 10;
+        cin = hg ? wt_compose(cin, hg, kWtRange) : Carry{e & 3u, (e >> 2) & 0xFFu};
+    }
+    if (!have) cin = Carry{0, 0};
+#ifdef WT_CHECK
+    if (have && wave > 0) {  // (diagnostic: the global search's state at R0)
+        const uint64_t wq = in[R0 - 64 + lane];
+        const uint64_t wpq = in[R0 - 65];
+        const uint64_t bq = start_bits(cbits, b64, R0 - 64);
+        const bool cs0 = (smk[0] & 1) != 0;
+        const Carry oc = cs0 ? Carry{0, 0} : carry_in_b<64>(in, cbits, b64, wlo, R0, lane, wq, wpq, bq);
+        if ((oc.type != cin.type || oc.rem != cin.rem) && lane == 0) {
+            static __device__ unsigned int nprint;
+            if (atomicAdd(&nprint, 1u) < 24u) {
+                uint32_t es[4];
+                for (uint32_t v = 0; v < 4; v++) es[v] = v ? wm.wcarry[v] : pin0;
+                printf("WTCHK tile %lu wave %u R0 %lu old {%u,%u} new {%u,%u} tag0 %02x e %x %x %x %x\n",
+                       (unsigned long)tile, wave, (unsigned long)R0, oc.type, oc.rem, cin.type, cin.rem,
+                       tag_of(cache[0]), es[0], es[1], es[2], es[3]);
+            }
+        }
+    }
+#endif
     if (have && wave > 0) {
         // the words from R0 on that the run open at R0 absorbs: the previous
         // range's last record (its pass 2 needs them)
-        uint32_t ext = 0;
-        if (cin.type != 0 && cin.rem != 0) {
-            const uint64_t w0 = nw >= 64u ? cache[0] : (R0 + lane < whi ? in[R0 + lane] : 0ull);
-            ext = run_ext_b(in, cbits, b64, whi, R0, cin, lane, w0,
+        bool beyond = false;
+        uint32_t ext = range_ext(cache, smk, nw, cin, lane, beyond);
+        if (beyond)  // (the run reaches past this range: only a short last range)
+            ext = run_ext_b(in, cbits, b64, whi, R0, cin, lane, cache[0],
                             rr ? (readlane64(cbv, 0) >> rr) | (readlane64(cbv, 1) << (64 - rr))
                                : readlane64(cbv, 0));
-        }
         if (lane == 0) wm.wext[wave] = ext;
     }
     // pass 1: sizes and positions
