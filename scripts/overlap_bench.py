@@ -45,9 +45,9 @@ def main():
         s = torch.cuda.current_stream()
         for _ in range(k):
             ctx.pack_batch_into(words, offs, packed[0], poffs[0], chunks_per_tile=tc, sync=sync[0],
-                                stream=s)
+                                stream=s.cuda_stream)
             ctx.unpack_batch_into(packed[0], poffs[0], offs, back, status, chunks_per_tile=utc,
-                                  sync=sync[0], stream=s)
+                                  sync=sync[0], stream=s.cuda_stream)
 
     def ovl(k):
         packed_ev = [torch.cuda.Event() for _ in range(k)]
@@ -57,11 +57,11 @@ def main():
             if i >= 2:
                 sA.wait_event(used_ev[i - 2])
             ctx.pack_batch_into(words, offs, packed[b], poffs[b], chunks_per_tile=tc, sync=sync[b],
-                                stream=sA)
+                                stream=sA.cuda_stream)
             packed_ev[i].record(sA)
             sB.wait_event(packed_ev[i])
             ctx.unpack_batch_into(packed[b], poffs[b], offs, back, status, chunks_per_tile=utc,
-                                  sync=sync[b], stream=sB)
+                                  sync=sync[b], stream=sB.cuda_stream)
             used_ev[i].record(sB)
 
     def timed(f, k):
