@@ -61,6 +61,39 @@ extern "C" capnp_status capnp_stream_complete_prefix(capnp_ctx* ctx, const uint8
 
 namespace {
 
+// The adaptors' bulk buffers live in pinned host memory, so the device
+// copies of a unit or batch are direct DMAs (a copy from pageable memory is
+// staged by the runtime through its own pinned buffers, and blocks), and
+// resize() does not zero what the next copy overwrites anyway.
+template <class T>
+struct PinnedAlloc {
+    using value_type = T;
+    PinnedAlloc() = default;
+    template <class U>
+    PinnedAlloc(const PinnedAlloc<U>&) {}
+    T* allocate(size_t n) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, n * sizeof(T), hipHostMallocPortable) != hipSuccess || !p)
+            throw std::bad_alloc();
+        return static_cast<T*>(p);
+    }
+    void deallocate(T* p, size_t) { (void)hipHostFree(p); }
+    template <class U>
+    void construct(U* p) noexcept {
+        ::new (static_cast<void*>(p)) U;  // default-init: no zero fill
+    }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) {
+        ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+    }
+    template <class U>
+    bool operator==(const PinnedAlloc<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const PinnedAlloc<U>&) const { return false; }
+};
+using PBytes = std::vector<uint8_t, PinnedAlloc<uint8_t>>;
+using PWords = std::vector<uint64_t, PinnedAlloc<uint64_t>>;
+
 // writer: pack every 8 MiB of input (one device batch of many write_all
 // chunks; 1 MiB batches measured 4.1 GiB/s at 1 MiB calls, each batch paying
 // the launches and waits of one device call)
@@ -69,7 +102,7 @@ constexpr size_t kPull = size_t(1) << 16;        // reader: bytes asked of the i
 constexpr size_t kPullMax = size_t(1) << 24;     // ... at most, when a unit needs more
 
 struct Drain {
-    std::vector<uint8_t> q;
+    PBytes q;
     size_t pos = 0;
 };
 
@@ -160,14 +193,15 @@ struct capnp_packed_writer {
     void* user;
     uint8_t part[8];
     size_t npart = 0;                   // carried bytes of an incomplete word
-    std::vector<uint64_t> words;        // chunks not yet packed, back to back
+    PWords words;                       // chunks not yet packed, back to back
     std::vector<uint64_t> off{0};       // their word offsets
     Drain out;                          // packed bytes the inner writer has not taken
     // the full batch being packed in the background (bw, boff -> bout)
     Background bg;
     bool busy = false;
-    std::vector<uint64_t> bw, boff;
-    std::vector<uint8_t> bout;
+    PWords bw;
+    std::vector<uint64_t> boff;
+    PBytes bout;
     capnp_status bst = CAPNP_OK;
 };
 
@@ -175,10 +209,11 @@ struct capnp_packed_reader {
     capnp_ctx* ctx;
     capnp_read_fn fn;
     void* user;
-    std::vector<uint8_t> in;  // staged packed input
+    PBytes in;                // staged packed input
     size_t ip = 0;            // bytes of `in` already decoded
     bool eof = false;
-    std::vector<uint8_t> dec;  // decoded bytes not yet handed out
+    PBytes dec;                // decoded bytes not yet handed out
+    PBytes spare;              // the next decode's buffer (swapped with dec)
     size_t dp = 0;
     size_t pass_rem = 0;       // raw bytes of a literal run still to pass through
     capnp_status pull_err = CAPNP_OK;  // a read-ahead pull's error, for the next pull
@@ -189,7 +224,7 @@ struct capnp_packed_reader {
     size_t a_ip = 0, a_nw = 0;
     capnp_status a_st = CAPNP_OK;
     uint64_t a_pb = 0, a_pw = 0;
-    std::vector<uint8_t> a_out;
+    PBytes a_out;
 };
 
 namespace {
@@ -305,7 +340,7 @@ capnp_status reader_pull(capnp_packed_reader* r, size_t ask = kPull) {
 // One PackedRead::read of `nw` words at the current position, on the GPU.
 // A stream decodes at most 10 input bytes per output word (tag, 8 bytes,
 // count), so only that much of the staged input is handed to the kernel.
-capnp_status reader_unit(capnp_packed_reader* r, size_t nw, std::vector<uint8_t>& out,
+capnp_status reader_unit(capnp_packed_reader* r, size_t nw, PBytes& out,
                          size_t* used, int32_t* status, size_t max_bytes = ~size_t(0)) {
     const size_t avail = std::min(r->in.size() - r->ip, max_bytes);
     const size_t take = std::min(avail, nw * 10 + 16);
@@ -414,7 +449,7 @@ void reader_ahead(capnp_packed_reader* r, size_t nw) {
 }
 
 capnp_status reader_fill_whole(capnp_packed_reader* r, size_t nw) {
-    std::vector<uint8_t> out;
+    PBytes& out = r->spare;
     if (r->ahead) {  // the unit decoded ahead, if it is this one
         r->bg.wk->wait();
         r->ahead = false;
@@ -464,7 +499,7 @@ capnp_status reader_fill_whole(capnp_packed_reader* r, size_t nw) {
 capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
     want = std::max<size_t>(want, 1);
     size_t nw = std::max(want, kMinUnit);
-    std::vector<uint8_t> out;
+    PBytes& out = r->spare;
     if (r->ahead && (r->pass_rem || nw < kWholeUnit)) {
         // (not a whole-record unit: the one decoded ahead is not this one)
         r->bg.wk->wait();
