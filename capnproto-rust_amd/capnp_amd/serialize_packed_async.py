@@ -54,7 +54,11 @@ class PackedWrite:
 
         def write_cb(_user, buf, n):
             try:
-                r = self.inner.write(C.string_at(buf, n))
+                # (a view of the adaptor's queue, valid during the call, as
+                # the reference's poll_write(&[u8]): the inner writer copies
+                # what it keeps)
+                addr = C.cast(buf, C.c_void_p).value
+                r = self.inner.write(memoryview((C.c_ubyte * n).from_address(addr)).cast("B"))
             except Exception as e:  # surfaced as CAPNP_E_IO
                 self._err = e
                 return -2

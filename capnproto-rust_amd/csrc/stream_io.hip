@@ -222,6 +222,7 @@ struct capnp_packed_reader {
     Background bg;
     bool ahead = false;
     size_t a_ip = 0, a_nw = 0;
+    double bpw = 10.0;  // packed bytes per word of the last whole-record unit
     capnp_status a_st = CAPNP_OK;
     uint64_t a_pb = 0, a_pw = 0;
     PBytes a_out;
@@ -314,7 +315,9 @@ capnp_status reader_pull(capnp_packed_reader* r, size_t ask = kPull) {
     }
     if (r->eof) return CAPNP_NONE;
     ask = std::min(std::max(ask, kPull), kPullMax);
-    if (r->ip > 0 && r->ip * 2 >= r->in.size()) {  // drop the decoded prefix
+    // drop the decoded prefix when the pull would otherwise grow the buffer
+    // (a compaction moves what is staged ahead: only as often as needed)
+    if (r->ip > 0 && r->in.size() + ask > r->in.capacity()) {
         r->in.erase(r->in.begin(), r->in.begin() + (ptrdiff_t)r->ip);
         r->ip = 0;
     }
@@ -437,7 +440,12 @@ void reader_ahead(capnp_packed_reader* r, size_t nw) {
     r->a_ip = r->ip;
     r->a_nw = nw;
     const uint8_t* src = r->in.data() + r->ip;
-    const size_t n = r->in.size() - r->ip;
+    // the unit resolves only what it may consume: the last unit's bytes per
+    // word with a margin (its records past nw words are resolved for
+    // nothing); a unit that finds no complete record in that is decoded
+    // again from everything staged by the next read (reader_fill_whole)
+    const size_t est = (size_t)(r->bpw * 1.25 * 8.0 * (double)nw / 8.0) + (size_t(64) << 10);
+    const size_t n = std::min(r->in.size() - r->ip, est);
     r->bg.wk->run([r, src, n, nw] {
         r->a_out.resize(nw * 8);
         r->a_pb = r->a_pw = 0;
@@ -454,6 +462,7 @@ capnp_status reader_fill_whole(capnp_packed_reader* r, size_t nw) {
         r->bg.wk->wait();
         r->ahead = false;
         if (r->a_st == CAPNP_OK && r->a_pw > 0 && r->a_ip == r->ip && r->a_nw == nw) {
+            r->bpw = (double)r->a_pb / (double)r->a_pw;
             r->ip += r->a_pb;
             r->dec.swap(r->a_out);
             r->dp = 0;
@@ -480,6 +489,7 @@ capnp_status reader_fill_whole(capnp_packed_reader* r, size_t nw) {
         if (e != CAPNP_OK) return e;
         if (pw > 0) {
             out.resize(pw * 8);
+            r->bpw = (double)pb / (double)pw;
             r->ip += pb;
             r->dec.swap(out);
             r->dp = 0;

@@ -56,23 +56,34 @@ def main():
     ctx.gen_batch(words, offs, pz_thresh=1288490189)
     raw = words.cpu().numpy().tobytes()
     call = int(a.call_mib * (1 << 20))
+    warm = min(len(raw) // 8, 16 << 20) // call * call  # untimed lead-in of each adaptor
     # write: 1 MiB calls of unpacked bytes (views of the caller's buffer, as
-    # a Rust caller passes &[u8]), then flush
+    # a Rust caller passes &[u8]), then flush.  The first `warm` bytes go
+    # untimed: an adaptor's first calls create its background context and
+    # staging buffers (the reader's first unit took 26 ms on the box).
     mv = memoryview(raw)
     sink = MemWrite()
     w = spa.PackedWrite(sink, ctx=ctx)
+    for i in range(0, warm, call):
+        w.write_all(mv[i:i + call])
     t0 = time.perf_counter()
-    for i in range(0, len(raw), call):
+    for i in range(warm, len(raw), call):
         w.write_all(mv[i:i + call])
     w.flush_blocking()
     tw = time.perf_counter() - t0
     packed = b"".join(sink.parts)
     # read: calls of up to 1 MiB into the caller's buffer (poll_read(&mut
-    # [u8]) -> readinto) until the end
+    # [u8]) -> readinto) until the end, the first `warm` bytes untimed
     r = spa.PackedRead(MemRead(packed), ctx=ctx)
     got = bytearray(len(raw) + call)
     gv = memoryview(got)
     pos = 0
+    while pos < warm:
+        k = r.readinto(gv[pos:pos + min(call, warm - pos)])
+        if not k:
+            break
+        pos += k
+    p0 = pos
     t0 = time.perf_counter()
     while True:
         k = r.readinto(gv[pos:pos + call])
@@ -85,7 +96,8 @@ def main():
     print(json.dumps({
         "workload": f"config-2 data, {len(raw) / GiB:.3f} GiB unpacked, {len(packed) / GiB:.3f} GiB packed, "
                     f"{call} B calls, in-memory inner stream",
-        "write_GiBps": round(len(raw) / GiB / tw, 3), "read_GiBps": round(len(raw) / GiB / tr, 3),
+        "timed_bytes": {"write": len(raw) - warm, "read": len(raw) - p0, "untimed_lead_in": warm},
+        "write_GiBps": round((len(raw) - warm) / GiB / tw, 3), "read_GiBps": round((len(raw) - p0) / GiB / tr, 3),
         "write_s": round(tw, 4), "read_s": round(tr, 4), "ok": ok}), flush=True)
 
 
