@@ -44,9 +44,6 @@
 
 
 
-#ifndef PACK_LB1RT
-#define PACK_LB1RT 0  // look-back: the group's tile records and the first group window in one round trip
-#endif
 #ifndef PACK_PROF
 #define PACK_PROF 0  // look-back counters (scripts/pack_prof.py); 0 = product
 #endif
@@ -678,56 +675,6 @@ __device__ __forceinline__ void copy_out(const uint8_t* region, uint8_t* __restr
     if (lane < hi - b) out[b + lane] = region[(b - D0) + lane];
 }
 
-// copy_out for a region of at most 1024 MAXIT bytes: every LDS read of the
-// wave first, then the stores (the passes' registers are dead by the
-// copy-out, so the reads need no extra occupancy), instead of one LDS round
-// trip per 1 KiB store.
-template <int MAXIT>
-__device__ __forceinline__ void copy_out_pre(const uint8_t* region, uint8_t* __restrict__ out,
-                                             uint64_t D0, uint64_t len, uint64_t cap,
-                                             uint32_t lane) {
-    const uint64_t lo = D0;
-    const uint64_t hi = (D0 + len < cap) ? D0 + len : cap;
-    if (hi <= lo) return;
-    const uint64_t a = (lo + 15) & ~15ull, b = hi & ~15ull;
-    if (a > b) {
-        if (lane < hi - lo) out[lo + lane] = region[lane];
-        return;
-    }
-    if (lane < a - lo) out[lo + lane] = region[lane];
-    const uint32_t m = (uint32_t)((a - D0) & 15);  // source misalignment (uniform)
-    const uint32_t q = m >> 2, sb = m & 3;
-    uint4 A[MAXIT], B[MAXIT];
-#pragma unroll
-    for (int it = 0; it < MAXIT; it++) {
-        const uint64_t blk = a + 16ull * lane + 1024ull * it;
-        const uint32_t s = (uint32_t)(blk - D0) & ~15u;
-        if (blk < b) {
-            A[it] = *reinterpret_cast<const uint4*>(region + s);
-            B[it] = *reinterpret_cast<const uint4*>(region + s + 16);
-        }
-    }
-#pragma unroll
-    for (int it = 0; it < MAXIT; it++) {
-        const uint64_t blk = a + 16ull * lane + 1024ull * it;
-        if (blk < b) {
-            const uint32_t w[8] = {A[it].x, A[it].y, A[it].z, A[it].w,
-                                   B[it].x, B[it].y, B[it].z, B[it].w};
-            const uint32_t w0 = q == 0 ? w[0] : q == 1 ? w[1] : q == 2 ? w[2] : w[3];
-            const uint32_t w1 = q == 0 ? w[1] : q == 1 ? w[2] : q == 2 ? w[3] : w[4];
-            const uint32_t w2 = q == 0 ? w[2] : q == 1 ? w[3] : q == 2 ? w[4] : w[5];
-            const uint32_t w3 = q == 0 ? w[3] : q == 1 ? w[4] : q == 2 ? w[5] : w[6];
-            const uint32_t w4 = q == 0 ? w[4] : q == 1 ? w[5] : q == 2 ? w[6] : w[7];
-            const uint4 o = make_uint4(__builtin_amdgcn_alignbyte(w1, w0, sb),
-                                       __builtin_amdgcn_alignbyte(w2, w1, sb),
-                                       __builtin_amdgcn_alignbyte(w3, w2, sb),
-                                       __builtin_amdgcn_alignbyte(w4, w3, sb));
-            *reinterpret_cast<uint4*>(out + blk) = o;
-        }
-    }
-    if (lane < hi - b) out[b + lane] = region[(b - D0) + lane];
-}
-
 // Streaming path: wave w owns chunks w, w+4, ...  MODE_SIZE fills
 // chunk_size; MODE_RING re-reads and writes at chunk_pos.
 template <int MODE>
@@ -1172,27 +1119,8 @@ __device__ __forceinline__ void publish(const LookbackArgs& A, uint64_t t, uint6
 }
 
 // Wave 0: global byte offset of tile t (aggregate already published).
-// Look-back polls issued ahead of the wait (pre_poll, right after the tile
-// publishes its aggregate): the group's earlier tile records and the first
-// window of group records.  Any record read then is final or an aggregate
-// that a later inclusive record only shortcuts, so the look-back may start
-// from them.
-struct PrePoll {
-    uint64_t st, rec;
-};
-[[maybe_unused]] __device__ __forceinline__ PrePoll pre_poll(const LookbackArgs& A, uint64_t t, uint32_t lane) {
-    const uint64_t g = t / kGroup;
-    const uint32_t r = (uint32_t)(t % kGroup);
-    const int64_t j = (int64_t)g - 1 - (int64_t)lane;
-    PrePoll pp;
-    pp.st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
-    pp.rec = lane < kGroupWindow ? (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc) : 0;
-    return pp;
-}
-
-[[maybe_unused]] __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, uint32_t lane,
-                                              bool early_group = false,
-                                              const PrePoll* pre = nullptr) {
+__device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, uint32_t lane,
+                             bool early_group = false) {
     const uint64_t g = t / kGroup;
     const uint32_t r = (uint32_t)(t % kGroup);
 #if PACK_PROF
@@ -1201,58 +1129,28 @@ struct PrePoll {
 #endif
     // aggregates of the group's earlier tiles
     uint64_t within;
-    uint64_t st = pre ? pre->st : (lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg);
-#if PACK_LB1RT == 2
-    // ... and of the previous group's tiles, polled in the same round trip
-    // (the previous group's record trails its last tile by a poll and a
-    // store); the group scan then starts two groups back
-    const uint64_t gp = g ? g - 1 : 0;
-    const uint32_t np = g ? kGroup : 0u;
-    uint64_t sp = lane < np ? poll_agent(&A.ts[gp * kGroup + lane]) : kFlagAgg;
-    const int64_t j0 = (int64_t)g - 2 - (int64_t)lane;
-    const uint64_t rec0 = lane < kGroupWindow ? (j0 >= 0 ? poll_agent(&A.gs[j0]) : kFlagInc) : 0;
-#endif
+    uint64_t st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
     for (uint32_t spins = 0;;) {
         const uint64_t miss = ballot64((st >> 62) == 0);
-#if PACK_LB1RT == 2
-        const uint64_t missp = ballot64((sp >> 62) == 0);
-        if (!miss && !missp) break;
-#else
         if (!miss) break;
-#endif
 #if PACK_PROF
         n_ws++;
 #endif
         if (++spins >= kSpinLimit) {
             if (lane == 0) PROF_ADD(2, 1);
-#if PACK_LB1RT == 2
-            const uint64_t j = miss ? g * kGroup + ctz64(miss) : gp * kGroup + ctz64(missp);
-#else
             const uint64_t j = g * kGroup + ctz64(miss);
-#endif
             const uint64_t a = tile_aggregate(A, j, lane);
             if (lane == 0) publish_agent(&A.ts[j], kFlagAgg | a);
         } else {
             __builtin_amdgcn_s_sleep(kSleep);
         }
         st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
-#if PACK_LB1RT == 2
-        sp = lane < np ? poll_agent(&A.ts[gp * kGroup + lane]) : kFlagAgg;
-#endif
     }
     {
         uint64_t v = st & kValMask;
         for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
         within = v;
     }
-#if PACK_LB1RT == 2
-    uint64_t prev;
-    {
-        uint64_t v = sp & kValMask;
-        for (uint32_t d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-        prev = v;
-    }
-#endif
 #if PACK_PROF == 3
     if (lane == 0) TRACE(t, 7, RT());  // (the group's earlier tiles are summed)
 #endif
@@ -1260,26 +1158,13 @@ struct PrePoll {
     if (group_last && !early_group && lane == 0) publish_agent(&A.gs[g], kFlagAgg | (within + agg));
     // exclusive prefix of the group: 64 groups per round; a group contributes
     // its inclusive record (and ends the scan), else its aggregate
-#if PACK_LB1RT == 2
-    uint64_t gexcl = prev;
-    int64_t idx = (int64_t)g - 2;
-    bool first = true;
-#else
     uint64_t gexcl = 0;
     int64_t idx = (int64_t)g - 1;
-    bool first = pre != nullptr;
-#endif
     for (uint32_t spins = 0; idx >= 0;) {
         const int64_t j = idx - (int64_t)lane;
         const bool in_win = lane < kGroupWindow;
-#if PACK_LB1RT == 2
         const uint64_t rec =
-            first ? rec0 : (!in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc));
-#else
-        const uint64_t rec =
-            first ? pre->rec : (!in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc));
-#endif
-        first = false;
+            !in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc);
         const uint64_t inc = ballot64((rec & kFlagInc) != 0);
         const uint32_t first_inc = ctz64(inc);
         const uint64_t need = first_inc < 64 ? low_mask(first_inc) : low_mask(kGroupWindow);
@@ -1325,9 +1210,8 @@ struct PrePoll {
 }
 
 __device__ __forceinline__ uint64_t tile_offset(const LookbackArgs& A, uint64_t t, uint64_t agg,
-                                                uint32_t lane, bool early_group = false,
-                                                const PrePoll* pre = nullptr) {
-    return lookback(A, t, agg, lane, early_group, pre);
+                                                uint32_t lane, bool early_group = false) {
+    return lookback(A, t, agg, lane, early_group);
 }
 
 // The group aggregate, published by the group's last tile from a wave that
@@ -2375,12 +2259,7 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         wave_lds_sync();
         if (lane == 0) TRACE(tile, 3, RT());
 #endif
-#if PACK_LB1RT == 1
-        const PrePoll pp = pre_poll(LA, tile, lane);
-        const uint64_t excl = tile_offset(LA, tile, agg, lane, early_group, &pp);
-#else
         const uint64_t excl = tile_offset(LA, tile, agg, lane, early_group);
-#endif
 #if PACK_PROF == 3
         if (lane == 0) TRACE(tile, 4, RT());
 #endif
