@@ -107,7 +107,8 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
                                           uint64_t total_bytes, uint64_t* d_out,
                                           const uint64_t* d_out_off, int32_t* d_status,
                                           uint64_t* d_consumed, void* d_ws, size_t ws_bytes,
-                                          hipStream_t s, int* passes, int* serial);
+                                          hipStream_t s, int* passes, int* serial,
+                                          const int32_t** failed_flag);
 extern "C" hipError_t capnp_launch_frame(const uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t,
                                          uint32_t, uint64_t, uint64_t, FrameResult*, hipStream_t);
 
@@ -154,6 +155,8 @@ struct capnp_ctx {
     uint8_t* d_stream_words = nullptr;  // message discovery: the stream decoded to words
     size_t stream_words_cap = 0;
     int resync_passes = 0, resync_serial = 0;  // last capnp_gpu_unpack_batch_resync
+    const int32_t* resync_failed = nullptr;     // its device "a chunk failed" flag (read on demand)
+    hipStream_t resync_stream = nullptr;
     uint32_t* d_bad = nullptr;  // offset validation flag (check_offsets)
     uint32_t* h_bad = nullptr;  // pinned copy
     uint8_t* h_pin = nullptr;   // pinned staging of the small host calls (kPinnedCall)
@@ -228,7 +231,24 @@ capnp_status ensure_state(capnp_ctx* ctx, size_t bytes) {
     return CAPNP_OK;
 }
 
+// The last index-free decode's "a chunk failed its check" flag lives in the
+// resync workspace and is read on demand (capnp_resync_stats), or here before
+// the workspace is reused or reallocated.
+capnp_status settle_resync(capnp_ctx* ctx) {
+    if (!ctx->resync_failed) return CAPNP_OK;
+    int32_t f = 0;
+    HIP_TRY(hipStreamSynchronize(ctx->resync_stream));
+    HIP_TRY(hipMemcpy(&f, ctx->resync_failed, 4, hipMemcpyDeviceToHost));
+    if (f) ctx->resync_serial = 3;
+    ctx->resync_failed = nullptr;
+    return CAPNP_OK;
+}
+
 capnp_status ensure_buf(capnp_ctx* ctx, uint8_t** buf, size_t* cap_io, size_t bytes) {
+    if (buf == &ctx->d_resync) {
+        const capnp_status st = settle_resync(ctx);
+        if (st != CAPNP_OK) return st;
+    }
     if (bytes <= *cap_io) return CAPNP_OK;
     HIP_TRY(hipSetDevice(ctx->device));
     if (*buf) {
@@ -737,6 +757,7 @@ static capnp_status unpack_resync_dev(capnp_ctx* ctx, const uint8_t* d_packed,
                                       const uint64_t* d_in_byte_off, size_t nchunks,
                                       uint64_t* d_words, const uint64_t* d_out_word_off,
                                       int32_t* d_status, uint64_t* d_consumed, hipStream_t s) {
+    ctx->resync_failed = nullptr;  // (a new call: the previous call's flag is moot)
     ctx->resync_passes = ctx->resync_serial = 0;
     if (nchunks == 0) return CAPNP_OK;
     uint64_t ends[2];
@@ -754,12 +775,16 @@ static capnp_status unpack_resync_dev(capnp_ctx* ctx, const uint8_t* d_packed,
     if (st != CAPNP_OK) return st;
     HIP_TRY(capnp_resync_unpack(d_packed, d_in_byte_off, nchunks, ends[1] - ends[0], d_words,
                                 d_out_word_off, d_status, d_consumed, ctx->d_resync,
-                                ctx->resync_cap, s, &ctx->resync_passes, &ctx->resync_serial));
+                                ctx->resync_cap, s, &ctx->resync_passes, &ctx->resync_serial,
+                                &ctx->resync_failed));
+    ctx->resync_stream = s;
     return CAPNP_OK;
 }
 
 capnp_status capnp_resync_stats(capnp_ctx* ctx, int* passes, int* serial) {
     if (!ctx) return CAPNP_E_INVALID_ARGUMENT;
+    const capnp_status st = settle_resync(ctx);  // (the decode did not wait for its flag)
+    if (st != CAPNP_OK) return st;
     if (passes) *passes = ctx->resync_passes;
     if (serial) *serial = ctx->resync_serial;
     return CAPNP_OK;

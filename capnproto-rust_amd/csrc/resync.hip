@@ -50,11 +50,6 @@ namespace {
 
 constexpr uint64_t kBlock = 512;  // packed bytes per block
 constexpr uint32_t kThreads = 256;
-constexpr int kMaxPasses = 512;  // fix passes before giving up to the serial path
-int g_max_passes = kMaxPasses;   // (capnp_resync_max_passes: tests drive the fallbacks)
-constexpr int kPassBatch = 8;    // fix passes enqueued per flag read-back
-// (a first read-back after 1 or 2 passes, then 8: config 4 index-free 2253 /
-// 2165 vs 2207 us, round 4: not kept)
 constexpr uint64_t kShortChunk = 2 * kBlock;  // mean packed bytes per chunk below which
                                               // the batch goes straight to the batch unpack
 
@@ -102,8 +97,9 @@ struct Ws {
     uint64_t* words;       // [nbb]
     uint64_t* wbase;       // [nbb] exclusive scan of words
     int32_t* ok;           // [n]
-    int32_t* flags;        // [0] a tile hit the round cap, [1] chunk failed,
-                           // [2 + i] fix pass i changed an exit
+    int32_t* flags;        // [0] a tile hit the round cap, [1] chunk failed
+    uint64_t* trec;        // [ntiles] look-back records of k_tile ({final, last exit})
+    uint32_t* ticket;      // k_tile's tile counter (zeroed with trec)
     void* tmp;
     size_t tmp_bytes;
 };
@@ -131,7 +127,7 @@ __global__ void __launch_bounds__(kThreads) k_count(const uint64_t* __restrict__
 #endif
 #if RESYNC_PROF
 __device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave 0), waves, end
-#define RTRACE(k) do { if (fix == 0 && tid == 0 && g_rtrace) g_rtrace[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define RTRACE(k) do { if (tid == 0 && g_rtrace) g_rtrace[t * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define RTRACE(k) ((void)0)
 #endif
@@ -167,12 +163,22 @@ __device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave
 // walks its whole segment; with one lane per 512-byte block that was the
 // critical path, ~100 hops, and four waves share the tile's LDS).  Positions
 // inside the tile are 32-bit offsets from the staged base.
-// The tile's own entry is the previous tile's last exit: the spec launch
-// assumes its first lane's f; fix passes (k_tile with fix = 1) re-resolve a
-// tile whose stored entry differs from the predecessor's exit, and flag a
-// pass whose last exit moved.  A region no walk couples with costs one tile
-// at most one tile per pass (32 KiB); tiles later in a pass often read an
-// exit their predecessor wrote in the same pass.
+// The tile's own entry is the previous tile's last exit, handed over by a
+// look-back record (round 4; it replaces the host-driven fix passes): tiles
+// take their index from a ticket in start order, and a tile whose first
+// block continues a chunk from the previous tile polls that tile's record
+// once before its rounds (taking the true entry if it is there, else
+// assuming its first lane's f), and after them waits for it if needed and
+// re-runs the rounds from the true entry when it differs (the lanes' states
+// stay in registers, so only the cascade the new entry causes walks again).
+// A tile that starts a chunk at its first block needs no predecessor, so the
+// waits chain only within one chunk (<= 3 tiles for 64 KiB segments; a
+// longer unit chains tile by tile, each waiting on one predecessor that has
+// already started).  Then every tile publishes its last block's exit.  The
+// record is one 8-byte granule {bit 63: final, exit}, stored and polled with
+// agent-scope atomics (memory-side, so no XCD's L2 serves a stale copy).
+// Round 3/4's fix passes cost config 4 302 + 78 us for the two that moved
+// exits, 6 x 7 us for no-op passes and two host read-backs per call.
 // Segments per block re-checked in round 3 (2 / 4 / 8: 2574 / 2367 / 2497 us,
 // config 4 index-free): 4.
 constexpr uint32_t kSegs = 4;                               // segments per block
@@ -191,7 +197,15 @@ constexpr uint32_t kRelCap = 0xF0000000u;  // chunk ends past this are "far" (ti
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
 static_assert(kBlock % kSegs == 0, "segments tile the block");
 
-// hop() on the staged bytes, positions relative to the staged base.
+// hop() on the staged bytes, positions relative to the staged base.  The tag
+// and both possible count bytes (p+1 for 0x00, p+9 for 0xFF) are read
+// together, as unpack.hip's seg_hop does: one LDS latency per hop instead of
+// two dependent ones (the staged range has slack past every segment end, so
+// p+9 stays inside the buffer; a count byte past the chunk end is never used).
+// hop() on the staged bytes, positions relative to the staged base.  (The
+// tag and both possible count bytes read together, as unpack.hip's seg_hop
+// does, measured slower here: config 4 index-free 2967 vs 2717 us, round 4;
+// three byte reads per hop load the LDS more than the dependent read costs.)
 __device__ __forceinline__ void hop32(const uint8_t* buf, uint32_t& p, uint32_t& w, uint32_t b) {
     const uint32_t tag = buf[p];
     uint32_t q = p + 1 + __builtin_popcount(tag);
@@ -232,11 +246,13 @@ struct SegState {
 // false, and the caller flags the resolution as unreliable (the batch then
 // takes the serial decode).
 constexpr uint32_t kMaxRounds = kTileThreads + 2;
+uint32_t g_max_rounds = kMaxRounds;  // (capnp_resync_max_passes: tests drive the fallbacks)
 __device__ __forceinline__ bool seg_rounds(const uint8_t* buf, SegState& S, bool valid,
                                            uint32_t in_j, bool fixed_j, uint32_t lane,
-                                           uint32_t wave, uint32_t* wmax, uint32_t* wneed) {
+                                           uint32_t wave, uint32_t* wmax, uint32_t* wneed,
+                                           uint32_t max_rounds) {
     for (uint32_t round = 0;; round++) {
-        if (round == kMaxRounds) {  // (uniform: every wave counts the same rounds)
+        if (round == max_rounds) {  // (uniform: every wave counts the same rounds)
             S.ex = S.b + 1;
             S.wd = 0;
             return false;
@@ -322,35 +338,26 @@ __device__ __forceinline__ bool seg_rounds(const uint8_t* buf, SegState& S, bool
 
 __global__ void __launch_bounds__(kTileThreads)
 k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
-       const uint64_t* __restrict__ bstart, uint64_t* exit, uint64_t* __restrict__ entry,
-       uint64_t* __restrict__ words, uint64_t* __restrict__ blk_c, int32_t* flags, int pass,
-       int fix) {
+       const uint64_t* __restrict__ bstart, uint64_t* __restrict__ exit,
+       uint64_t* __restrict__ entry, uint64_t* __restrict__ words, uint64_t* __restrict__ blk_c,
+       int32_t* flags, uint64_t* trec, uint32_t* ticket, uint32_t max_rounds) {
     extern __shared__ __align__(16) uint8_t tbuf[];
     __shared__ uint32_t wmax[kTileWaves], wneed[kTileWaves];
+    __shared__ uint64_t s_t, s_e0;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & (CAPNP_WAVE - 1);
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid / CAPNP_WAVE));
+    // the tile index: a ticket in start order (a tile's predecessor has
+    // started before it, so waiting on it cannot deadlock)
+    if (tid == 0)
+        s_t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t nb = uniform64(bstart[n]);
-    const uint64_t k0 = (uint64_t)blockIdx.x * kTileBlocks;
+    __syncthreads();
+    const uint64_t t = uniform64(s_t);
+    const uint64_t k0 = t * kTileBlocks;
     if (k0 >= nb) return;
-    if (fix && pass > 0 && __atomic_load_n(&flags[2 + pass - 1], __ATOMIC_RELAXED) == 0) return;
     RTRACE(0);
     const uint64_t kn = nb - k0 < kTileBlocks ? nb - k0 : kTileBlocks;
-    uint64_t e0 = 0;  // the tile's entry (fix passes)
-    if (fix) {
-        if (k0 == 0) return;  // (block 0 starts chunk 0: exact since the spec launch)
-        // One read of the predecessor's exit for the whole workgroup.  The
-        // predecessor tile may rewrite exit[k0 - 1] during this same pass; when
-        // each wave read it for itself, waves that read it before and after
-        // the write disagreed on returning here, and the waves left in
-        // seg_rounds polled round flags (wneed) that the returned waves never
-        // wrote -- the timing-dependent hang of two resync tests in round 3.
-        __shared__ uint64_t s_e0;
-        if (tid == 0) s_e0 = __atomic_load_n(&exit[k0 - 1], __ATOMIC_RELAXED);
-        __syncthreads();
-        e0 = uniform64(s_e0);
-        if (e0 == uniform64(entry[k0])) return;  // consistent (entry[k0] is this tile's own)
-    }
     // c0 = the last chunk with bstart[c0] <= k0: a 64-way search (3 probes
     // deep for 10^5 chunks, where one lane's binary search was 17 dependent
     // loads)
@@ -366,7 +373,12 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     }
     const uint64_t c0 = clo;
     const uint64_t bs0 = uniform64(bstart[c0]), a0 = uniform64(in_off[c0]);
-    if (fix && bs0 == k0) return;  // a tile that starts a chunk is exact since the spec launch
+    // dep: the tile's first block continues a chunk from the previous tile
+    const bool dep = bs0 != k0;
+    if (tid == 0)  // one poll of the predecessor's record (0: not final yet)
+        s_e0 = dep ? __hip_atomic_fetch_add(&trec[t - 1], 0ull, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)
+                   : 0ull;
     // stage [s0 - kLead, s0 + 32 KiB + 16) (clamped to the batch: the tile's
     // blocks are contiguous bytes, at most kBlock each) by LDS DMA, 16 bytes a
     // lane, every load in flight at once
@@ -451,39 +463,76 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
         S.own = S.serr ? 0 : S.sx;
     }
     RTRACE(2);
-    // the tile's entry (lane 0 of wave 0): the previous tile's last exit in a
-    // fix pass, else its own f
-    uint32_t E0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(S.f == kNone32 ? S.ss : S.f));
-    if (fix) {
+    // the tile's entry (lane 0 of wave 0): the previous tile's last exit if
+    // its record is final already, else this lane's own f
+    constexpr uint64_t kFinal = 1ull << 63;
+    auto rel_entry = [&](uint64_t rec) -> uint32_t {
+        const uint64_t e0 = rec & ~kFinal;
         const uint64_t r = e0 - base;
-        E0 = e0 < base ? 0 : (r < kRelCap ? (uint32_t)r : kRelCap + 1);
-    }
+        return e0 < base ? 0u : (r < kRelCap ? (uint32_t)r : kRelCap + 1);
+    };
+    uint64_t rec = uniform64(s_e0);  // (written before the staging barrier)
+    uint32_t E0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(S.f == kNone32 ? S.ss : S.f));
+    if (rec & kFinal) E0 = rel_entry(rec);
     const bool tile_lane0 = wave == 0 && lane == 0;
     const bool fixed_j = cfirst || tile_lane0;
-    const uint32_t in_j = cfirst ? S.ss : (tile_lane0 ? E0 : 0u);
-    if (!seg_rounds(tbuf, S, valid, in_j, fixed_j, lane, wave, wmax, wneed) && tid == 0)
-        flags[0] = 1;  // resolution unreliable: the caller decodes serially
-    RTRACE(3);
-    RTRACE(4);
+    bool settled = seg_rounds(tbuf, S, valid, cfirst ? S.ss : (tile_lane0 ? E0 : 0u), fixed_j,
+                              lane, wave, wmax, wneed, max_rounds);
     // blocks: entry of segment 0, exit of segment 3, words summed
     // (a segment left with an error exit -- its walk ran past the chunk, or
     // no entry reached it -- marks the whole block, so the chunk fails its check)
-    uint32_t wsum = S.wd, berr = S.ex > S.b ? 1u : 0u;
+    uint32_t wsum, berr, bx;
+    auto block_result = [&]() {
+        wsum = S.wd;
+        berr = S.ex > S.b ? 1u : 0u;
 #pragma unroll
-    for (uint32_t m = 1; m < kSegs; m <<= 1) {
-        wsum += (uint32_t)__shfl_xor((int)wsum, (int)m);
-        berr |= (uint32_t)__shfl_xor((int)berr, (int)m);
+        for (uint32_t m = 1; m < kSegs; m <<= 1) {
+            wsum += (uint32_t)__shfl_xor((int)wsum, (int)m);
+            berr |= (uint32_t)__shfl_xor((int)berr, (int)m);
+        }
+        bx = (uint32_t)__shfl((int)S.ex, (int)(lane | (kSegs - 1)));
+    };
+    auto block_exit = [&]() -> uint64_t { return (berr || bx > S.b) ? b + 1 : base + bx; };
+    // the tile's last block: its exit is final already unless its chunk began
+    // before this tile and the tile's entry is still a guess, so it goes to
+    // the next tile now (only the waits within one chunk chain)
+    const bool last = valid && q == 0 && (uint64_t)jb == kn - 1;
+    const bool guess = dep && !(rec & kFinal);
+    block_result();
+    if (last && (!guess || bsc >= k0))
+        __hip_atomic_exchange(&trec[t], kFinal | block_exit(), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+    if (guess) {
+        // wait for the predecessor's last exit (it started before this tile
+        // and waits, if at all, only on an earlier tile of the same chunk),
+        // then re-run the rounds from it if the assumed entry was wrong
+        if (tid == 0) {
+            uint64_t v;
+            while (!((v = __hip_atomic_fetch_add(&trec[t - 1], 0ull, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) & kFinal))
+                __builtin_amdgcn_s_sleep(2);
+            s_e0 = v;
+        }
+        __syncthreads();
+        rec = uniform64(s_e0);
+        const uint32_t E1 = rel_entry(rec);
+        if (E1 != E0 && settled) {
+            settled = seg_rounds(tbuf, S, valid, cfirst ? S.ss : (tile_lane0 ? E1 : 0u), fixed_j,
+                                 lane, wave, wmax, wneed, max_rounds);
+            block_result();
+        }
+        if (last && bsc < k0)
+            __hip_atomic_exchange(&trec[t], kFinal | block_exit(), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
     }
-    const uint32_t bx = (uint32_t)__shfl((int)S.ex, (int)(lane | (kSegs - 1)));
+    if (!settled && tid == 0) flags[0] = 1;  // round cap: the segments carry error exits
+    RTRACE(3);
+    RTRACE(4);
     if (valid && q == 0) {
-        const uint64_t xa = (berr || bx > S.b) ? b + 1 : base + bx;
-        const uint64_t ea = S.used > S.b ? b + 1 : base + S.used;
-        const uint64_t old = fix ? exit[k] : 0;
-        exit[k] = xa;
-        entry[k] = ea;
+        exit[k] = block_exit();
+        entry[k] = S.used > S.b ? b + 1 : base + S.used;
         words[k] = wsum;
-        if (!fix) blk_c[k] = c;
-        if (fix && (uint64_t)jb == kn - 1 && old != xa) flags[2 + pass] = 1;
+        blk_c[k] = c;
     }
     RTRACE(5);
 }
@@ -544,11 +593,11 @@ __global__ void __launch_bounds__(kThreads)
 k_blocks(const uint64_t* __restrict__ in_off, uint64_t n, const uint64_t* __restrict__ out_off,
          const uint64_t* __restrict__ bstart, const uint64_t* __restrict__ exit,
          const uint64_t* __restrict__ wbase, const int32_t* __restrict__ ok,
-         uint64_t* __restrict__ blk_in, uint64_t* __restrict__ blk_out) {
+         uint64_t* __restrict__ blk_in, uint64_t* __restrict__ blk_out, uint64_t nbb) {
     const uint64_t k = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     const uint64_t nb = bstart[n];
-    if (k > nb) return;
-    if (k == nb) {
+    if (k > nbb) return;
+    if (k >= nb) {  // (units nb .. nbb - 1: empty, past the batch end)
         blk_in[k] = in_off[n];
         blk_out[k] = out_off[n];
         return;
@@ -586,14 +635,16 @@ size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes) {
     };
     w->nblk = (uint64_t*)take(8 * (n + 1));
     w->bstart = (uint64_t*)take(8 * (n + 1));
-    w->spec_exit = (uint64_t*)take(8 * nbb);
+    w->spec_exit = (uint64_t*)take(8 * (nbb + 1));  // (then the decode units' starts: nbb + 1)
     w->spec_words = (uint32_t*)take(4 * nbb);
     w->exit = (uint64_t*)take(8 * nbb);
-    w->entry = (uint64_t*)take(8 * nbb);
+    w->entry = (uint64_t*)take(8 * (nbb + 1));
     w->words = (uint64_t*)take(8 * nbb);
     w->wbase = (uint64_t*)take(8 * nbb);
     w->ok = (int32_t*)take(4 * n + 4);
-    w->flags = (int32_t*)take(4 * (2 + kMaxPasses));
+    w->flags = (int32_t*)take(4 * 2);
+    w->trec = (uint64_t*)take(8 * (nbb / kTileBlocks + 2));  // (ticket right after)
+    w->ticket = (uint32_t*)(w->trec ? w->trec + nbb / kTileBlocks + 1 : nullptr);
     w->tmp = take(tmp_bytes);
     w->tmp_bytes = tmp_bytes;
     return off;
@@ -610,40 +661,26 @@ uint64_t blocks_bound(uint64_t n, uint64_t total_bytes) { return total_bytes / k
 
 unsigned grid(uint64_t items) { return (unsigned)((items + kThreads - 1) / kThreads); }
 
-// Spec walks, then fix passes to the fixed point (kPassBatch per flag
-// read-back).  *converged = false after kMaxPasses passes.  Blocking.
+// Tile resolution: one k_tile launch (the tiles hand their exits on by
+// look-back).  check_cap: read back whether a tile hit the round cap
+// (*converged = false; blocking); otherwise the capped tiles' error exits
+// fail their chunks, which the block decode then walks serially.
 hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, const Ws& w,
-                   uint64_t nbb, hipStream_t s, int* passes, bool* converged) {
+                   uint64_t nbb, hipStream_t s, bool check_cap, bool* converged) {
     hipError_t e;
-    *passes = 0;
     *converged = true;
-    const unsigned tgrid = (unsigned)((nbb + kTileBlocks - 1) / kTileBlocks);
-    k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
-                                                w.words, w.spec_exit, w.flags, 0, 0);
-    int pass = 0;
-    for (;;) {
-        if (pass >= g_max_passes) {
-            *converged = false;
-            break;
-        }
-        for (int i = 0; i < kPassBatch && pass < g_max_passes; i++, pass++)
-            k_tile<<<tgrid, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
-                                                        w.entry, w.words, w.spec_exit, w.flags,
-                                                        pass, 1);
-        int32_t last = 0, capped = 0;
-        if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
-            hipSuccess)
-            return e;
+    const uint64_t ntiles = (nbb + kTileBlocks - 1) / kTileBlocks;
+    if ((e = hipMemsetAsync(w.trec, 0, 8 * (ntiles + 1), s)) != hipSuccess) return e;
+    k_tile<<<(unsigned)ntiles, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
+                                                           w.entry, w.words, w.spec_exit, w.flags,
+                                                           w.trec, w.ticket, g_max_rounds);
+    if (check_cap) {
+        int32_t capped = 0;
         if ((e = hipMemcpyAsync(&capped, w.flags, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
             return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        if (capped) {  // a tile hit the round cap (never, by seg_rounds' argument)
-            *converged = false;
-            break;
-        }
-        if (!last) break;
+        *converged = capped == 0;
     }
-    *passes = pass;
     return hipGetLastError();
 }
 
@@ -651,10 +688,13 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
 
 extern "C" uint32_t capnp_resync_block_bytes(void) { return (uint32_t)kBlock; }
 
-extern "C" int capnp_resync_max_passes(int passes) {
-    const int old = g_max_passes;
-    g_max_passes = passes <= 0 ? kMaxPasses : (passes > kMaxPasses ? kMaxPasses : passes);
-    return old;
+// Test hook (the name predates the look-back): caps the rounds a tile may run
+// (1 .. kMaxRounds; 0 restores the default), so tests reach the fallbacks.
+extern "C" int capnp_resync_max_passes(int rounds) {
+    const int old = (int)g_max_rounds;
+    g_max_rounds = rounds <= 0 ? kMaxRounds
+                               : ((uint32_t)rounds > kMaxRounds ? kMaxRounds : (uint32_t)rounds);
+    return old == (int)kMaxRounds ? 0 : old;
 }
 
 // RESYNC_PROF builds: the per-tile trace buffer (8 words per tile), or null.
@@ -675,18 +715,21 @@ extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes) {
     return carve(&w, nullptr, n, nbb, scan_tmp_bytes(m)) + 256;
 }
 
-// Blocking (the fix passes read a flag back).  On return, *passes = fix passes
-// run and *serial = 1 if the batch was re-decoded by the serial batch unpack
-// (the fix passes did not converge), 2 if its chunks were short enough to go
-// there directly, 3 if some chunks failed their check (those alone were
-// decoded serially, each as one unit of the block decode).
+// Asynchronous after its first launches (no host read-back once the block
+// counts are scanned).  On return, *passes = resolution launches (1), *serial
+// = 2 if the chunks were short enough to go straight to the batch unpack;
+// *failed_flag (device) turns nonzero if some chunks failed their check
+// (those alone were decoded serially, each as one unit of the block decode:
+// the caller reports serial = 3 from it, on demand).
 extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d_in_off, uint64_t n,
                                           uint64_t total_bytes, uint64_t* d_out,
                                           const uint64_t* d_out_off, int32_t* d_status,
                                           uint64_t* d_consumed, void* d_ws, size_t ws_bytes,
-                                          hipStream_t s, int* passes, int* serial) {
+                                          hipStream_t s, int* passes, int* serial,
+                                          const int32_t** failed_flag) {
     if (passes) *passes = 0;
     if (serial) *serial = 0;
+    if (failed_flag) *failed_flag = nullptr;
     if (n == 0) return hipSuccess;
     hipError_t e;
     if (total_bytes < n * kShortChunk) {
@@ -705,59 +748,46 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
     if (carve(&w, base, n, nbb, scan_tmp_bytes(m)) + (base - (uint8_t*)d_ws) >
         ws_bytes)
         return hipErrorInvalidValue;
-    int32_t hflags[2] = {0, 0};
-    if ((e = hipMemsetAsync(w.flags, 0, 4 * (2 + kMaxPasses), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.flags, 0, 4 * 2, s)) != hipSuccess) return e;
     k_count<<<grid(n + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.nblk);
     size_t tb = w.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
         return e;
-    int pass = 0;
-    bool conv = true;
-    if ((e = resolve(d_in, d_in_off, n, w, nbb, s, &pass, &conv)) != hipSuccess) return e;
-    if (!conv) hflags[1] = 1;  // not converged: let the serial walk decide
-    if (passes) *passes = pass;
-    if (!hflags[1]) {
-        tb = w.tmp_bytes;
-        if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.words, w.wbase, (int)nbb, s)) !=
-            hipSuccess)
-            return e;
-        // (blk_c in spec_exit, bad in spec_words: both dead until k_blocks)
-        int32_t* bad = reinterpret_cast<int32_t*>(w.spec_words);
-        if ((e = hipMemsetAsync(bad, 0, 4 * n, s)) != hipSuccess) return e;
-        k_mark<<<grid(nbb), kThreads, 0, s>>>(w.exit, w.spec_exit, d_in_off, w.bstart, n, bad);
-        k_check<<<grid(n), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit, w.words,
-                                             w.wbase, bad, w.ok, d_status, d_consumed, w.flags);
-        uint64_t nb = 0;
-        if ((e = hipMemcpyAsync(hflags, w.flags, 8, hipMemcpyDeviceToHost, s)) != hipSuccess)
-            return e;
-        if ((e = hipMemcpyAsync(&nb, w.bstart + n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess)
-            return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        // decode the blocks as independent read units with the batch unpack
-        // (staged LDS tiles, coalesced stores); a chunk that failed its check
-        // is one unit of its own, decoded serially in the same launch
-        uint64_t* blk_in = w.spec_exit;  // (spec state is dead by now)
-        uint64_t* blk_out = w.entry;
-        int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
-        uint64_t* blk_consumed = w.words;  // (dead after the wbase scan and the check)
-        k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit,
-                                                   w.wbase, w.ok, blk_in, blk_out);
-        if ((e = capnp_launch_unpack(d_in, blk_in, nb, 0, d_out, blk_out, blk_status,
-                                     hflags[1] ? blk_consumed : nullptr, nullptr, s)) != hipSuccess)
-            return e;
-        if (hflags[1]) {
-            if (serial) *serial = 3;
-            k_fail<<<grid(n), kThreads, 0, s>>>(n, w.bstart, w.ok, blk_status, blk_consumed,
-                                                d_status, d_consumed);
-        }
-    } else {
-        if (serial) *serial = 1;
-        if ((e = capnp_launch_unpack(d_in, d_in_off, n, 0, d_out, d_out_off, d_status, d_consumed,
-                                     nullptr, s)) != hipSuccess)
-            return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    }
+    bool conv = true;  // (not read back: a tile that hits the round cap fails its
+                       // chunks, which the block decode below walks serially)
+    if ((e = resolve(d_in, d_in_off, n, w, nbb, s, false, &conv)) != hipSuccess) return e;
+    if (passes) *passes = 1;
+    tb = w.tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.words, w.wbase, (int)nbb, s)) !=
+        hipSuccess)
+        return e;
+    // (blk_c in spec_exit, bad in spec_words: both dead until k_blocks)
+    int32_t* bad = reinterpret_cast<int32_t*>(w.spec_words);
+    if ((e = hipMemsetAsync(bad, 0, 4 * n, s)) != hipSuccess) return e;
+    k_mark<<<grid(nbb), kThreads, 0, s>>>(w.exit, w.spec_exit, d_in_off, w.bstart, n, bad);
+    k_check<<<grid(n), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit, w.words,
+                                         w.wbase, bad, w.ok, d_status, d_consumed, w.flags);
+    // decode the blocks as independent read units with the batch unpack
+    // (staged LDS tiles, coalesced stores); a chunk that failed its check
+    // is one unit of its own, decoded serially in the same launch.  No
+    // host read-back here: the decode runs over the nbb-unit bound (k_blocks
+    // makes the units past the last block empty) and always returns the
+    // units' consumed counts for k_fail, which only touches failed chunks
+    // (one host round trip fewer per call; *failed_flag lets the caller
+    // learn serial = 3 later, on demand).
+    uint64_t* blk_in = w.spec_exit;  // (spec state is dead by now)
+    uint64_t* blk_out = w.entry;
+    int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
+    uint64_t* blk_consumed = w.words;  // (dead after the wbase scan and the check)
+    k_blocks<<<grid(nbb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit,
+                                                w.wbase, w.ok, blk_in, blk_out, nbb);
+    if ((e = capnp_launch_unpack(d_in, blk_in, nbb, 0, d_out, blk_out, blk_status,
+                                 blk_consumed, nullptr, s)) != hipSuccess)
+        return e;
+    k_fail<<<grid(n), kThreads, 0, s>>>(n, w.bstart, w.ok, blk_status, blk_consumed,
+                                        d_status, d_consumed);
+    if (failed_flag) *failed_flag = w.flags + 1;
     return hipGetLastError();
 }
 
@@ -1314,15 +1344,14 @@ extern "C" hipError_t capnp_resync_decode_prefix(const uint8_t* d_in, uint64_t n
     uint64_t* cutk = aux + 10;    // [1]
     const uint64_t h_in_off[2] = {0, nbytes};
     if ((e = hipMemcpyAsync(in_off, h_in_off, 16, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(w.flags, 0, 4 * (2 + kMaxPasses), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.flags, 0, 4 * 2, s)) != hipSuccess) return e;
     k_count<<<grid(n + 1), kThreads, 0, s>>>(in_off, n, in_off, w.nblk);
     size_t tb = w.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
         return e;
-    int pass = 0;
     bool conv = true;
-    if ((e = resolve(d_in, in_off, n, w, nbb, s, &pass, &conv)) != hipSuccess) return e;
+    if ((e = resolve(d_in, in_off, n, w, nbb, s, true, &conv)) != hipSuccess) return e;
     if (!conv) {  // exact serial walk for the cut, one unit for the decode
         k_cut_serial<<<1, 1, 0, s>>>(d_in, nbytes, max_words, cut);
         uint64_t hc[2] = {0, 0};
@@ -1364,7 +1393,7 @@ extern "C" hipError_t capnp_resync_decode_prefix(const uint8_t* d_in, uint64_t n
     uint64_t* blk_out = w.entry;
     int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
     k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(in_off, n, out_off, w.bstart, w.exit, w.wbase,
-                                               nullptr, blk_in, blk_out);
+                                               nullptr, blk_in, blk_out, nb);
     k_set_cut<<<1, 64, 0, s>>>(blk_in, blk_out, nu, cut, cutk);
     if ((e = capnp_launch_unpack(d_in, blk_in, nu, 0, d_out, blk_out, blk_status, nullptr, nullptr,
                                  s)) != hipSuccess)
@@ -1422,16 +1451,15 @@ static hipError_t find_messages_impl(const uint8_t* d_in, uint64_t nbytes, uint6
     if ((size_t)(chain + chain_bytes - (uint8_t*)d_ws) > ws_bytes) return hipErrorInvalidValue;
     const uint64_t h_in_off[2] = {0, nbytes};
     if ((e = hipMemcpyAsync(in_off, h_in_off, 16, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(w.flags, 0, 4 * (2 + kMaxPasses), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.flags, 0, 4 * 2, s)) != hipSuccess) return e;
     // (one chunk of nbytes > 0 bytes: k_count never reads its word offsets)
     k_count<<<grid(n + 1), kThreads, 0, s>>>(in_off, n, in_off, w.nblk);
     size_t tb = w.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
         return e;
-    int pass = 0;
-    bool conv = true;  // (not converged: k_consistent bounds the walk to the exact prefix)
-    if ((e = resolve(d_in, in_off, n, w, nbb, s, &pass, &conv)) != hipSuccess) return e;
+    bool conv = true;  // (a capped tile: k_consistent bounds the walk to the exact prefix)
+    if ((e = resolve(d_in, in_off, n, w, nbb, s, false, &conv)) != hipSuccess) return e;
     uint64_t nb = 0;
     if ((e = hipMemcpyAsync(&nb, w.bstart + n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
@@ -1466,7 +1494,7 @@ static hipError_t find_messages_impl(const uint8_t* d_in, uint64_t nbytes, uint6
     uint64_t* blk_out = w.entry;
     int32_t* blk_status = reinterpret_cast<int32_t*>(w.spec_words);
     k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(in_off, n, out_off, w.bstart, w.exit, w.wbase,
-                                               nullptr, blk_in, blk_out);
+                                               nullptr, blk_in, blk_out, nb);
     k_set_cut<<<grid(nb + 1), kThreads, 0, s>>>(blk_in, blk_out, nb, tail, cutk);
     if ((e = capnp_launch_unpack(d_in, blk_in, nb, 0, d_words, blk_out, blk_status, nullptr,
                                  nullptr, s)) != hipSuccess)

@@ -59,11 +59,13 @@ capnp_status capnp_resync_stats(capnp_ctx* ctx, int* passes, int* serial);
 /* Packed bytes per lane of the index-free decode. */
 uint32_t capnp_resync_block_bytes(void);
 
-/* Diagnostic: the fix passes the index-free decode runs before it gives up
- * to its serial fallbacks (process-wide; 1 .. 512, 0 restores the default
- * 512).  Returns the previous cap.  Lets the tests drive the non-converging
- * paths (capnp_gpu_unpack_batch_resync's serial batch decode, the stream
- * reader's serial whole-record cut) without a 16 MiB adversarial stream. */
+/* Diagnostic: caps the rounds a tile of the index-free decode's resolution
+ * may run before it gives up to the serial fallbacks (process-wide; 1 .. 258,
+ * 0 restores the default 258, which the rounds' termination bound never
+ * reaches; the name predates the round-4 look-back, which replaced the fix
+ * passes).  Returns the previous cap (0 = default).  Lets the tests drive the
+ * fallback paths (capnp_gpu_unpack_batch_resync's per-chunk serial decode,
+ * the stream reader's serial whole-record cut) without adversarial input. */
 int capnp_resync_max_passes(int passes);
 
 /* Pre-sizes the context workspace for batches of up to max_chunks chunks so

@@ -1,13 +1,14 @@
 """Termination and fallback of the index-free decode (csrc/resync.hip) on
 streams where the speculative chains never couple: in a literal-run region
 (serialize_packed.rs:394-433 packs incompressible words as 0xFF records of
-255 raw words) only the true chain settles a tile, so the fix passes carry
-it tile by tile, and a long enough region can reach kMaxPasses (512) (the
-tests cap the passes through capnp_resync_max_passes to get there).  The
-decode must still terminate and return the reference's bytes:
+255 raw words) only the true chain settles a tile, so the tiles hand their
+exits on one by one (look-back) and each needs several rounds.  The tests
+cap the rounds per tile through capnp_resync_max_passes (the hook's name
+predates the look-back) to reach the fallbacks.  The decode must still
+terminate and return the reference's bytes:
 
-* capnp_gpu_unpack_batch_resync sends such a batch to the serial batch
-  unpack (serial = 1);
+* capnp_gpu_unpack_batch_resync fails the capped tiles' chunks, which its
+  block decode then walks serially, each as one unit (serial = 3);
 * the stream reader's whole-record cut (capnp_resync_decode_prefix, reads
   of 64 KiB and more) falls back to an exact serial walk for the cut.
 
@@ -43,7 +44,7 @@ def _literal_words(n, seed):
 
 @pytest.fixture
 def pass_cap():
-    """Fix passes capped at 1 (capnp_resync_max_passes), restored after."""
+    """Rounds per tile capped at 1 (capnp_resync_max_passes), restored after."""
     from capnp_amd import _lib
     old = _lib.lib().capnp_resync_max_passes(1)
     yield
@@ -51,7 +52,7 @@ def pass_cap():
 
 
 def test_resync_batch_literal_region_past_pass_cap(ctx, pass_cap):
-    n = (4 << 20) // 8  # 4 MiB of literal words: 128 tiles, more than one fix pass
+    n = (4 << 20) // 8  # 4 MiB of literal words: 128 tiles, each past the round cap
     w = _literal_words(n, 3)
     st, p = O.pack(w.tobytes())
     assert st == 0
@@ -63,13 +64,13 @@ def test_resync_batch_literal_region_past_pass_cap(ctx, pass_cap):
     consumed = torch.zeros(1, dtype=torch.int64, device="cuda")
     passes, serial = ctx.unpack_batch_resync_into(packed, in_off, out_off, words, status,
                                                   consumed)
-    assert serial == 1 and passes == 1, (passes, serial)
+    assert serial == 3 and passes == 1, (passes, serial)
     assert int(status[0]) == 0 and int(consumed[0]) == len(p)
     assert np.array_equal(words.cpu().numpy().view(np.uint64), w)
 
 
 def test_reader_large_read_literal_region_past_pass_cap(ctx, pass_cap):
-    """Large reads of a 4 MiB literal stream with the fix passes capped: the
+    """Large reads of a 4 MiB literal stream with the rounds capped: the
     reader's whole-record cut (capnp_resync_decode_prefix) does not converge
     and takes the serial cut, with the same bytes (the reader
     used to fail with CAPNP_E_HIP there)."""
@@ -102,9 +103,9 @@ def test_reader_large_read_literal_region_past_pass_cap(ctx, pass_cap):
 
 
 def test_literal_region_converges_uncapped(ctx):
-    """The same 20 MiB literal region with the default cap: the fix passes
-    converge (tiles later in a pass read exits their predecessors wrote in
-    that pass) and the block decode is exact."""
+    """A 20 MiB literal region with the default cap: the tiles' look-back
+    carries the true chain through all 640 tiles and the block decode is
+    exact."""
     n = (20 << 20) // 8
     w = _literal_words(n, 5)
     st, p = O.pack(w.tobytes())
@@ -115,15 +116,15 @@ def test_literal_region_converges_uncapped(ctx):
     words = torch.zeros(n, dtype=torch.int64, device="cuda")
     status = torch.full((1,), -1, dtype=torch.int32, device="cuda")
     passes, serial = ctx.unpack_batch_resync_into(packed, in_off, out_off, words, status)
-    assert serial == 0 and passes < 512, (passes, serial)
+    assert serial == 0 and passes == 1, (passes, serial)
     assert int(status[0]) == 0
     assert np.array_equal(words.cpu().numpy().view(np.uint64), w)
 
 
 def test_resync_hang_inputs_repeat(ctx):
     """The round-3 hang inputs (test_batch_long_runs' chunks, _mixed_words'
-    stream), each decoded several times: the fix passes' tiles now read
-    their predecessor's exit once per workgroup."""
+    stream), each decoded several times (round 3's fix passes raced on the
+    predecessor's exit; the look-back reads it once per workgroup)."""
     chunks = []
     for n in (255, 256, 257, 300, 511, 512, 513, 1023, 1500):
         for lead in (0, 1, 63):
