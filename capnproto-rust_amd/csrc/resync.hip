@@ -126,7 +126,7 @@ __global__ void __launch_bounds__(kThreads) k_count(const uint64_t* __restrict__
 #define RESYNC_PROF 0  // diagnostic: per-tile phase timestamps of the spec launch (scripts/resync_prof.py)
 #endif
 #if RESYNC_PROF
-__device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave 0), waves, end
+__device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds, look-back wait + re-run, end
 #define RTRACE(k) do { if (tid == 0 && g_rtrace) g_rtrace[t * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
 #define RTRACE(k) ((void)0)
@@ -134,9 +134,9 @@ __device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave
 
 // ---- tile resolution (k_tile) ----
 // A 256-thread workgroup takes a tile of kTileBlocks consecutive blocks
-// (contiguous packed bytes, <= 32 KiB), stages them in LDS by DMA, and each
-// wave resolves 16 blocks cut into kSegs segments of kSegBytes, one lane
-// each:
+// (contiguous packed bytes, <= 26 KiB), stages them in LDS by DMA, and each
+// wave resolves kWaveBlocks blocks cut into kSegs segments of kSegBytes, one
+// lane each:
 //   spec   lane j walks from kLead bytes before its segment (or from its
 //          chunk's start) to its first record start f >= s, then on to its
 //          exit; the lead-in lets chains from different starts couple before
@@ -172,7 +172,7 @@ __device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave
 // re-runs the rounds from the true entry when it differs (the lanes' states
 // stay in registers, so only the cascade the new entry causes walks again).
 // A tile that starts a chunk at its first block needs no predecessor, so the
-// waits chain only within one chunk (<= 3 tiles for 64 KiB segments; a
+// waits chain only within one chunk (<= 4 tiles for 64 KiB segments; a
 // longer unit chains tile by tile, each waiting on one predecessor that has
 // already started).  Then every tile publishes its last block's exit.  The
 // record is one 8-byte granule {bit 63: final, exit}, stored and polled with
@@ -183,9 +183,19 @@ __device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds (wave
 // config 4 index-free): 4.
 constexpr uint32_t kSegs = 4;                               // segments per block
 constexpr uint32_t kSegBytes = (uint32_t)kBlock / kSegs;    // 128
-constexpr uint32_t kTileWaves = kSegs;                      // (so a tile stays 64 blocks)
-constexpr uint32_t kWaveBlocks = CAPNP_WAVE / kSegs;        // 16
-constexpr uint32_t kTileBlocks = kTileWaves * kWaveBlocks;  // 64
+constexpr uint32_t kTileWaves = kSegs;                      // (a wave per 128-byte column)
+// Blocks per wave (<= CAPNP_WAVE / kSegs): 13 leaves 12 of a wave's 64 lanes
+// idle, but the tile's LDS (26.7 KB) lets 6 tiles share a CU instead of 4
+// (73 VGPRs allow 6 waves per SIMD).  Round 4, config 4 index-free,
+// interleaved: 16 / 15 / 13 / 12 blocks 1938 / 1788 / 1762 / 1798 us; 10 and
+// 9 blocks at 8 waves per SIMD (57 VGPRs) 1816 / 1780; 11 at 7 (12 B spill)
+// 1774.
+#ifndef RESYNC_WAVE_BLOCKS
+#define RESYNC_WAVE_BLOCKS 13
+#endif
+constexpr uint32_t kWaveBlocks = RESYNC_WAVE_BLOCKS;
+static_assert(kWaveBlocks * kSegs <= CAPNP_WAVE, "a wave's segments fit its lanes");
+constexpr uint32_t kTileBlocks = kTileWaves * kWaveBlocks;  // 52
 constexpr uint32_t kTileThreads = kTileWaves * CAPNP_WAVE;
 // spec walk lead-in (bytes); 48 -> 64: config 4 index-free -2.7 % on two
 // boxes (32 / 80 / 96: 2478 / 2340 / 2295 us against 2311-2329)
@@ -379,7 +389,7 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
         s_e0 = dep ? __hip_atomic_fetch_add(&trec[t - 1], 0ull, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT)
                    : 0ull;
-    // stage [s0 - kLead, s0 + 32 KiB + 16) (clamped to the batch: the tile's
+    // stage [s0 - kLead, s0 + kTileBlocks * kBlock + 16) (clamped to the batch: the tile's
     // blocks are contiguous bytes, at most kBlock each) by LDS DMA, 16 bytes a
     // lane, every load in flight at once
     const uint64_t A = uniform64(in_off[0]), Z = uniform64(in_off[n]);
@@ -402,7 +412,7 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     // the chunk starts in (k0, k0 + jb], counted over batches of 64 starts (a
     // lane's binary search over the batch by shuffles)
     const uint32_t jb = wave * kWaveBlocks + lane / kSegs, q = lane % kSegs;
-    const bool valid = jb < kn;
+    const bool valid = lane / kSegs < kWaveBlocks && jb < kn;
     const uint32_t jj = valid ? jb : (uint32_t)(kn - 1);
     const uint64_t k = k0 + jj;
     uint64_t c = c0;
@@ -478,6 +488,7 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     const bool fixed_j = cfirst || tile_lane0;
     bool settled = seg_rounds(tbuf, S, valid, cfirst ? S.ss : (tile_lane0 ? E0 : 0u), fixed_j,
                               lane, wave, wmax, wneed, max_rounds);
+    RTRACE(3);
     // blocks: entry of segment 0, exit of segment 3, words summed
     // (a segment left with an error exit -- its walk ran past the chunk, or
     // no entry reached it -- marks the whole block, so the chunk fails its check)
@@ -526,7 +537,6 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
                                   __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!settled && tid == 0) flags[0] = 1;  // round cap: the segments carry error exits
-    RTRACE(3);
     RTRACE(4);
     if (valid && q == 0) {
         exit[k] = block_exit();
@@ -626,6 +636,10 @@ k_fail(uint64_t n, const uint64_t* __restrict__ bstart, const int32_t* __restric
     if (consumed) consumed[c] = blk_consumed[l];
 }
 
+// k_tile's look-back records: one per tile (<= nbb / kTileBlocks + 1 tiles),
+// then the ticket; resolve() zeroes all of them before each launch.
+uint64_t trec_words(uint64_t nbb) { return nbb / kTileBlocks + 2; }
+
 size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes) {
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -643,8 +657,8 @@ size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes) {
     w->wbase = (uint64_t*)take(8 * nbb);
     w->ok = (int32_t*)take(4 * n + 4);
     w->flags = (int32_t*)take(4 * 2);
-    w->trec = (uint64_t*)take(8 * (nbb / kTileBlocks + 2));  // (ticket right after)
-    w->ticket = (uint32_t*)(w->trec ? w->trec + nbb / kTileBlocks + 1 : nullptr);
+    w->trec = (uint64_t*)take(8 * trec_words(nbb));  // (the ticket in its last word)
+    w->ticket = (uint32_t*)(w->trec ? w->trec + trec_words(nbb) - 1 : nullptr);
     w->tmp = take(tmp_bytes);
     w->tmp_bytes = tmp_bytes;
     return off;
@@ -670,7 +684,7 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
     hipError_t e;
     *converged = true;
     const uint64_t ntiles = (nbb + kTileBlocks - 1) / kTileBlocks;
-    if ((e = hipMemsetAsync(w.trec, 0, 8 * (ntiles + 1), s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(w.trec, 0, 8 * trec_words(nbb), s)) != hipSuccess) return e;
     k_tile<<<(unsigned)ntiles, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
                                                            w.entry, w.words, w.spec_exit, w.flags,
                                                            w.trec, w.ticket, g_max_rounds);
@@ -782,6 +796,8 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
     uint64_t* blk_consumed = w.words;  // (dead after the wbase scan and the check)
     k_blocks<<<grid(nbb + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.bstart, w.exit,
                                                 w.wbase, w.ok, blk_in, blk_out, nbb);
+    // (block units per tile: the unpack's 16; 4 / 8 / 32 measured 2576 / 2079
+    // / 2618 vs 1906 us for config 4, round 4)
     if ((e = capnp_launch_unpack(d_in, blk_in, nbb, 0, d_out, blk_out, blk_status,
                                  blk_consumed, nullptr, s)) != hipSuccess)
         return e;

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Per-tile phase timeline of the resync tile resolution's spec launch
 (k_tile; build: make -C capnproto-rust_amd variant FILE=resync NAME=rprof
-DEFS=-DRESYNC_PROF=1): staging + chunk search, spec walks, wave 0's rounds,
-the waves in turn, block write-out (s_memrealtime, 100 MHz).  Diagnostic.
+DEFS=-DRESYNC_PROF=1): staging + chunk search, spec walks, the rounds,
+the look-back wait and re-run, block write-out (s_memrealtime, 100 MHz).  Diagnostic.
 
     python3 scripts/resync_prof.py [--lib path] [--workload config4_1GiB]
 """
@@ -44,7 +44,7 @@ def main():
     assert torch.equal(out, words) and int(st.abs().sum()) == 0
     T = trace.view(ntiles, 8).cpu().numpy().astype(np.int64)
     T = T[T[:, 5] > 0]
-    names = ["stage+search", "spec", "rounds(w0)", "waves", "write"]
+    names = ["stage+search", "spec", "rounds", "wait+rerun", "write"]
     d = [(T[:, k + 1] - T[:, k]) / 100.0 for k in range(5)]
     span = (T[:, 5].max() - T[:, 0].min()) / 100.0
     life = (T[:, 5] - T[:, 0]) / 100.0

@@ -150,3 +150,23 @@ def test_resync_hang_inputs_repeat(ctx):
         ctx.unpack_batch_resync_into(dp, di, do, out, status)
         assert (status.cpu().numpy() == 0).all()
         assert np.array_equal(out.cpu().numpy().view(np.uint64), words)
+
+
+def test_lookback_ticket_reset_at_whole_tile_bound(ctx):
+    """A unit whose block bound (packed bytes / 512 + chunks + 1) is a whole
+    number of 64-block tiles, decoded twice on one context: k_tile's ticket
+    sits in the record array's last word and must be zeroed before every
+    launch (a stale ticket would hand every tile an index past the batch)."""
+    n = 4000  # 0xFF records: 32032 packed bytes -> 62 + 2 = 64 blocks
+    w = _literal_words(n, 6)
+    st, p = O.pack(w.tobytes())
+    assert st == 0 and len(p) // 512 + 2 == 64, len(p)
+    packed = torch.from_numpy(np.frombuffer(p, np.uint8).copy()).cuda()
+    in_off = torch.tensor([0, len(p)], dtype=torch.int64, device="cuda")
+    out_off = torch.tensor([0, n], dtype=torch.int64, device="cuda")
+    for _ in range(3):
+        words = torch.zeros(n, dtype=torch.int64, device="cuda")
+        status = torch.full((1,), -1, dtype=torch.int32, device="cuda")
+        passes, serial = ctx.unpack_batch_resync_into(packed, in_off, out_off, words, status)
+        assert serial == 0 and int(status[0]) == 0, (passes, serial, int(status[0]))
+        assert np.array_equal(words.cpu().numpy().view(np.uint64), w)
