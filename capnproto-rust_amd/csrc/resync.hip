@@ -50,6 +50,8 @@ namespace {
 
 constexpr uint64_t kBlock = 512;  // packed bytes per block
 constexpr uint32_t kThreads = 256;
+constexpr int kMaxPasses = 512;  // fix passes before giving up to the serial path
+constexpr int kPassBatch = 8;    // fix passes enqueued per flag read-back (after the first)
 constexpr uint64_t kShortChunk = 2 * kBlock;  // mean packed bytes per chunk below which
                                               // the batch goes straight to the batch unpack
 
@@ -97,7 +99,8 @@ struct Ws {
     uint64_t* words;       // [nbb]
     uint64_t* wbase;       // [nbb] exclusive scan of words
     int32_t* ok;           // [n]
-    int32_t* flags;        // [0] a tile hit the round cap, [1] chunk failed
+    int32_t* flags;        // [0] a tile hit the round cap, [1] chunk failed,
+                           // [2 + i] fix pass i changed a tile's last exit
     uint64_t* trec;        // [ntiles] look-back records of k_tile ({final, last exit})
     uint32_t* ticket;      // k_tile's tile counter (zeroed with trec)
     void* tmp;
@@ -163,22 +166,28 @@ __device__ uint64_t* g_rtrace;  // 8 per tile: start, staged, spec, rounds, look
 // walks its whole segment; with one lane per 512-byte block that was the
 // critical path, ~100 hops, and four waves share the tile's LDS).  Positions
 // inside the tile are 32-bit offsets from the staged base.
-// The tile's own entry is the previous tile's last exit, handed over by a
-// look-back record (round 4; it replaces the host-driven fix passes): tiles
-// take their index from a ticket in start order, and a tile whose first
-// block continues a chunk from the previous tile polls that tile's record
-// once before its rounds (taking the true entry if it is there, else
-// assuming its first lane's f), and after them waits for it if needed and
-// re-runs the rounds from the true entry when it differs (the lanes' states
-// stay in registers, so only the cascade the new entry causes walks again).
-// A tile that starts a chunk at its first block needs no predecessor, so the
-// waits chain only within one chunk (<= 4 tiles for 64 KiB segments; a
-// longer unit chains tile by tile, each waiting on one predecessor that has
-// already started).  Then every tile publishes its last block's exit.  The
-// record is one 8-byte granule {bit 63: final, exit}, stored and polled with
-// agent-scope atomics (memory-side, so no XCD's L2 serves a stale copy).
-// Round 3/4's fix passes cost config 4 302 + 78 us for the two that moved
-// exits, 6 x 7 us for no-op passes and two host read-backs per call.
+// The tile's own entry is the previous tile's last exit.  Round 4 hands it
+// over by look-back where that is cheap: tiles take their index from a
+// ticket in start order; a tile whose last block's chunk starts inside it
+// has a last exit that does not depend on its own entry, and publishes it
+// right after its first rounds (one 8-byte granule {bit 63: final, exit},
+// stored and polled with agent-scope atomics: memory-side, so no XCD's L2
+// serves a stale copy).  A "near" tile -- its first block continues a chunk
+// that starts at most kNearTiles tiles back -- polls that record once before its
+// rounds (taking the true entry if it is there, else assuming its first
+// lane's f), and after them waits for it if needed and re-runs the rounds
+// from the true entry when it differs (the lanes' states stay in registers:
+// only the cascade walks again), then publishes its own last exit: waits
+// chain at most kNearTiles deep.  Deeper tiles of long units (more than
+// kNearTiles tiles into a unit) keep their guess, and fix
+// passes (fix = 1, host-driven) re-resolve
+// the tiles whose stored entry is not their predecessor's exit, until no
+// last exit moves; tiles later in a pass often read an exit their
+// predecessor wrote in the same pass.  (Waiting in every tile chained the
+// hand-offs through a long unit: one 256 MiB unit 8.1 ms against 0.5 with
+// fix passes.)  Config 4 (segments <= 64 KiB): round 3's fix passes cost 302
+// + 78 us for the two that moved exits, 6 x 7 us of no-op passes and two host
+// read-backs per call.
 // Segments per block re-checked in round 3 (2 / 4 / 8: 2574 / 2367 / 2497 us,
 // config 4 index-free): 4.
 constexpr uint32_t kSegs = 4;                               // segments per block
@@ -203,6 +212,10 @@ constexpr uint64_t kLead = 64;
 // hops a re-walk lets its spec chain catch up per step (32: 2439 us, slower)
 constexpr uint32_t kCatchUp = 16;
 constexpr uint32_t kTileLds = (uint32_t)(kTileBlocks * kBlock + kLead + 64);
+// look-back waits chain at most this many tiles from a chunk's first tile
+// (config 4's 64 KiB segments span <= 3 tiles; 1: its third tiles went to a
+// fix pass that moved exits, 9 passes a call, 1984 vs 1790 us)
+constexpr uint64_t kNearTiles = 4;
 constexpr uint32_t kRelCap = 0xF0000000u;  // chunk ends past this are "far" (tile offsets are < 40 K)
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
 static_assert(kBlock % kSegs == 0, "segments tile the block");
@@ -350,22 +363,37 @@ __global__ void __launch_bounds__(kTileThreads)
 k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint64_t n,
        const uint64_t* __restrict__ bstart, uint64_t* __restrict__ exit,
        uint64_t* __restrict__ entry, uint64_t* __restrict__ words, uint64_t* __restrict__ blk_c,
-       int32_t* flags, uint64_t* trec, uint32_t* ticket, uint32_t max_rounds) {
+       int32_t* flags, uint64_t* trec, uint32_t* ticket, uint32_t max_rounds, int fix, int pass) {
     extern __shared__ __align__(16) uint8_t tbuf[];
     __shared__ uint32_t wmax[kTileWaves], wneed[kTileWaves];
     __shared__ uint64_t s_t, s_e0;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & (CAPNP_WAVE - 1);
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid / CAPNP_WAVE));
-    // the tile index: a ticket in start order (a tile's predecessor has
-    // started before it, so waiting on it cannot deadlock)
-    if (tid == 0)
-        s_t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the tile index: in the first launch a ticket in start order (a tile's
+    // predecessor has started before it, so waiting on it cannot deadlock);
+    // in a fix pass the block index (fix passes never wait)
+    if (fix && pass > 0 && __atomic_load_n(&flags[2 + pass - 1], __ATOMIC_RELAXED) == 0) return;
+    if (tid == 0) {
+        s_t = fix ? blockIdx.x
+                  : __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_e0 = 0;
+    }
     const uint64_t nb = uniform64(bstart[n]);
     __syncthreads();
     const uint64_t t = uniform64(s_t);
     const uint64_t k0 = t * kTileBlocks;
     if (k0 >= nb) return;
+    if (fix) {
+        if (k0 == 0) return;  // (block 0 starts chunk 0: exact since the first launch)
+        // One read of the predecessor's exit for the whole workgroup (the
+        // predecessor may rewrite it during this same pass: waves that read it
+        // before and after the write disagreed on returning here and hung in
+        // seg_rounds' barriers -- round 3).
+        if (tid == 0) s_e0 = __atomic_load_n(&exit[k0 - 1], __ATOMIC_RELAXED);
+        __syncthreads();
+        if (uniform64(s_e0) == uniform64(entry[k0])) return;  // consistent
+    }
     RTRACE(0);
     const uint64_t kn = nb - k0 < kTileBlocks ? nb - k0 : kTileBlocks;
     // c0 = the last chunk with bstart[c0] <= k0: a 64-way search (3 probes
@@ -383,12 +411,17 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     }
     const uint64_t c0 = clo;
     const uint64_t bs0 = uniform64(bstart[c0]), a0 = uniform64(in_off[c0]);
-    // dep: the tile's first block continues a chunk from the previous tile
+    // dep: the tile's first block continues a chunk from the previous tile;
+    // near: that chunk starts at most kNearTiles tiles back, so the waits
+    // chain at most that deep (the tile that holds the chunk start publishes
+    // right after its first rounds, each near tile after its wait); a deeper
+    // tile keeps its guess (fix passes follow)
     const bool dep = bs0 != k0;
-    if (tid == 0)  // one poll of the predecessor's record (0: not final yet)
-        s_e0 = dep ? __hip_atomic_fetch_add(&trec[t - 1], 0ull, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT)
-                   : 0ull;
+    if (fix && !dep) return;  // a tile that starts a chunk is exact since the first launch
+    const bool near = !fix && dep && bs0 + kNearTiles * kTileBlocks >= k0;
+    if (near && tid == 0)  // one poll of the predecessor's record (0: not final yet)
+        s_e0 = __hip_atomic_fetch_add(&trec[t - 1], 0ull, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
     // stage [s0 - kLead, s0 + kTileBlocks * kBlock + 16) (clamped to the batch: the tile's
     // blocks are contiguous bytes, at most kBlock each) by LDS DMA, 16 bytes a
     // lane, every load in flight at once
@@ -482,6 +515,7 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
         return e0 < base ? 0u : (r < kRelCap ? (uint32_t)r : kRelCap + 1);
     };
     uint64_t rec = uniform64(s_e0);  // (written before the staging barrier)
+    if (fix) rec |= kFinal;           // (a fix pass's entry: the predecessor's exit)
     uint32_t E0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(S.f == kNone32 ? S.ss : S.f));
     if (rec & kFinal) E0 = rel_entry(rec);
     const bool tile_lane0 = wave == 0 && lane == 0;
@@ -510,10 +544,10 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
     const bool last = valid && q == 0 && (uint64_t)jb == kn - 1;
     const bool guess = dep && !(rec & kFinal);
     block_result();
-    if (last && (!guess || bsc >= k0))
+    if (!fix && last && (!guess || bsc >= k0))
         __hip_atomic_exchange(&trec[t], kFinal | block_exit(), __ATOMIC_RELAXED,
                               __HIP_MEMORY_SCOPE_AGENT);
-    if (guess) {
+    if (guess && near) {
         // wait for the predecessor's last exit (it started before this tile
         // and waits, if at all, only on an earlier tile of the same chunk),
         // then re-run the rounds from it if the assumed entry was wrong
@@ -532,17 +566,20 @@ k_tile(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off, uint
                                  lane, wave, wmax, wneed, max_rounds);
             block_result();
         }
-        if (last && bsc < k0)
+        if (last && bsc < k0)  // (for a near successor)
             __hip_atomic_exchange(&trec[t], kFinal | block_exit(), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
     }
     if (!settled && tid == 0) flags[0] = 1;  // round cap: the segments carry error exits
     RTRACE(4);
     if (valid && q == 0) {
-        exit[k] = block_exit();
+        const uint64_t xa = block_exit();
+        const uint64_t old = fix ? exit[k] : 0;
+        exit[k] = xa;
         entry[k] = S.used > S.b ? b + 1 : base + S.used;
         words[k] = wsum;
-        blk_c[k] = c;
+        if (!fix) blk_c[k] = c;
+        if (fix && last && old != xa) flags[2 + pass] = 1;  // the next tile must look again
     }
     RTRACE(5);
 }
@@ -656,7 +693,7 @@ size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes) {
     w->words = (uint64_t*)take(8 * nbb);
     w->wbase = (uint64_t*)take(8 * nbb);
     w->ok = (int32_t*)take(4 * n + 4);
-    w->flags = (int32_t*)take(4 * 2);
+    w->flags = (int32_t*)take(4 * (2 + kMaxPasses));
     w->trec = (uint64_t*)take(8 * trec_words(nbb));  // (the ticket in its last word)
     w->ticket = (uint32_t*)(w->trec ? w->trec + trec_words(nbb) - 1 : nullptr);
     w->tmp = take(tmp_bytes);
@@ -675,26 +712,44 @@ uint64_t blocks_bound(uint64_t n, uint64_t total_bytes) { return total_bytes / k
 
 unsigned grid(uint64_t items) { return (unsigned)((items + kThreads - 1) / kThreads); }
 
-// Tile resolution: one k_tile launch (the tiles hand their exits on by
-// look-back).  check_cap: read back whether a tile hit the round cap
-// (*converged = false; blocking); otherwise the capped tiles' error exits
-// fail their chunks, which the block decode then walks serially.
+// Tile resolution: the first k_tile launch (near tiles settled by
+// look-back), then fix passes over the tiles whose entry is not their
+// predecessor's exit (deep tiles of long units whose guess was wrong): one
+// pass before the first flag read-back, then kPassBatch per read-back.
+// *converged = false if the passes reach kMaxPasses; *capped = true if a
+// tile hit the round cap (its segments carry error exits).  Blocking.
 hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, const Ws& w,
-                   uint64_t nbb, hipStream_t s, bool check_cap, bool* converged) {
+                   uint64_t nbb, hipStream_t s, bool* converged, bool* capped, int* passes) {
     hipError_t e;
     *converged = true;
-    const uint64_t ntiles = (nbb + kTileBlocks - 1) / kTileBlocks;
+    *capped = false;
+    const unsigned ntiles = (unsigned)((nbb + kTileBlocks - 1) / kTileBlocks);
     if ((e = hipMemsetAsync(w.trec, 0, 8 * trec_words(nbb), s)) != hipSuccess) return e;
-    k_tile<<<(unsigned)ntiles, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
-                                                           w.entry, w.words, w.spec_exit, w.flags,
-                                                           w.trec, w.ticket, g_max_rounds);
-    if (check_cap) {
-        int32_t capped = 0;
-        if ((e = hipMemcpyAsync(&capped, w.flags, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+    if ((e = hipMemsetAsync(w.flags + 2, 0, 4 * kMaxPasses, s)) != hipSuccess) return e;
+    k_tile<<<ntiles, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
+                                                 w.words, w.spec_exit, w.flags, w.trec, w.ticket,
+                                                 g_max_rounds, 0, 0);
+    int pass = 0;
+    for (int batch = 1;; batch = kPassBatch) {
+        if (pass >= kMaxPasses) {
+            *converged = false;
+            break;
+        }
+        for (int i = 0; i < batch && pass < kMaxPasses; i++, pass++)
+            k_tile<<<ntiles, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit,
+                                                         w.entry, w.words, w.spec_exit, w.flags,
+                                                         w.trec, w.ticket, g_max_rounds, 1, pass);
+        int32_t last = 0, cap = 0;
+        if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
+            hipSuccess)
+            return e;
+        if ((e = hipMemcpyAsync(&cap, w.flags, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
             return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        *converged = capped == 0;
+        if (cap) *capped = true;
+        if (!last) break;
     }
+    *passes = pass;
     return hipGetLastError();
 }
 
@@ -729,12 +784,13 @@ extern "C" size_t capnp_resync_ws_bytes(uint64_t n, uint64_t total_bytes) {
     return carve(&w, nullptr, n, nbb, scan_tmp_bytes(m)) + 256;
 }
 
-// Asynchronous after its first launches (no host read-back once the block
-// counts are scanned).  On return, *passes = resolution launches (1), *serial
-// = 2 if the chunks were short enough to go straight to the batch unpack;
-// *failed_flag (device) turns nonzero if some chunks failed their check
-// (those alone were decoded serially, each as one unit of the block decode:
-// the caller reports serial = 3 from it, on demand).
+// Blocking until the resolution's fix passes settle (one flag read-back when
+// none moves an exit), asynchronous after that.  On return, *passes = fix
+// passes run, *serial = 1 if they did not converge (the batch went to the
+// serial batch unpack), 2 if the chunks were short enough to go straight
+// there; *failed_flag (device) turns nonzero if some chunks failed their
+// check (those alone were decoded serially, each as one unit of the block
+// decode: the caller reports serial = 3 from it, on demand).
 extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d_in_off, uint64_t n,
                                           uint64_t total_bytes, uint64_t* d_out,
                                           const uint64_t* d_out_off, int32_t* d_status,
@@ -768,10 +824,20 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
         return e;
-    bool conv = true;  // (not read back: a tile that hits the round cap fails its
-                       // chunks, which the block decode below walks serially)
-    if ((e = resolve(d_in, d_in_off, n, w, nbb, s, false, &conv)) != hipSuccess) return e;
-    if (passes) *passes = 1;
+    // (a tile that hits the round cap fails its chunks, which the block
+    // decode below walks serially; fix passes that do not converge send the
+    // batch to the serial batch unpack)
+    bool conv = true, capped = false;
+    int pass = 0;
+    if ((e = resolve(d_in, d_in_off, n, w, nbb, s, &conv, &capped, &pass)) != hipSuccess) return e;
+    if (passes) *passes = pass;
+    if (!conv) {
+        if (serial) *serial = 1;
+        if ((e = capnp_launch_unpack(d_in, d_in_off, n, 0, d_out, d_out_off, d_status, d_consumed,
+                                     nullptr, s)) != hipSuccess)
+            return e;
+        return hipStreamSynchronize(s);
+    }
     tb = w.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.words, w.wbase, (int)nbb, s)) !=
         hipSuccess)
@@ -1366,9 +1432,10 @@ extern "C" hipError_t capnp_resync_decode_prefix(const uint8_t* d_in, uint64_t n
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
         return e;
-    bool conv = true;
-    if ((e = resolve(d_in, in_off, n, w, nbb, s, true, &conv)) != hipSuccess) return e;
-    if (!conv) {  // exact serial walk for the cut, one unit for the decode
+    bool conv = true, capped = false;
+    int pass = 0;
+    if ((e = resolve(d_in, in_off, n, w, nbb, s, &conv, &capped, &pass)) != hipSuccess) return e;
+    if (!conv || capped) {  // exact serial walk for the cut, one unit for the decode
         k_cut_serial<<<1, 1, 0, s>>>(d_in, nbytes, max_words, cut);
         uint64_t hc[2] = {0, 0};
         if ((e = hipMemcpyAsync(hc, cut, 16, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
@@ -1474,8 +1541,11 @@ static hipError_t find_messages_impl(const uint8_t* d_in, uint64_t nbytes, uint6
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
         hipSuccess)
         return e;
-    bool conv = true;  // (a capped tile: k_consistent bounds the walk to the exact prefix)
-    if ((e = resolve(d_in, in_off, n, w, nbb, s, false, &conv)) != hipSuccess) return e;
+    // (not converged, or a capped tile: k_consistent bounds the walk to the
+    // exact prefix)
+    bool conv = true, capped = false;
+    int pass = 0;
+    if ((e = resolve(d_in, in_off, n, w, nbb, s, &conv, &capped, &pass)) != hipSuccess) return e;
     uint64_t nb = 0;
     if ((e = hipMemcpyAsync(&nb, w.bstart + n, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;

@@ -52,7 +52,7 @@ def pass_cap():
 
 
 def test_resync_batch_literal_region_past_pass_cap(ctx, pass_cap):
-    n = (4 << 20) // 8  # 4 MiB of literal words: 128 tiles, each past the round cap
+    n = (4 << 20) // 8  # 4 MiB of literal words: ~160 tiles, each past the round cap
     w = _literal_words(n, 3)
     st, p = O.pack(w.tobytes())
     assert st == 0
@@ -64,7 +64,7 @@ def test_resync_batch_literal_region_past_pass_cap(ctx, pass_cap):
     consumed = torch.zeros(1, dtype=torch.int64, device="cuda")
     passes, serial = ctx.unpack_batch_resync_into(packed, in_off, out_off, words, status,
                                                   consumed)
-    assert serial == 3 and passes == 1, (passes, serial)
+    assert serial == 3 and passes >= 1, (passes, serial)
     assert int(status[0]) == 0 and int(consumed[0]) == len(p)
     assert np.array_equal(words.cpu().numpy().view(np.uint64), w)
 
@@ -103,9 +103,9 @@ def test_reader_large_read_literal_region_past_pass_cap(ctx, pass_cap):
 
 
 def test_literal_region_converges_uncapped(ctx):
-    """A 20 MiB literal region with the default cap: the tiles' look-back
-    carries the true chain through all 640 tiles and the block decode is
-    exact."""
+    """A 20 MiB literal region with the default cap: the fix passes carry the
+    true chain through all ~800 tiles (tiles later in a pass read exits their
+    predecessors wrote in that pass) and the block decode is exact."""
     n = (20 << 20) // 8
     w = _literal_words(n, 5)
     st, p = O.pack(w.tobytes())
@@ -116,7 +116,7 @@ def test_literal_region_converges_uncapped(ctx):
     words = torch.zeros(n, dtype=torch.int64, device="cuda")
     status = torch.full((1,), -1, dtype=torch.int32, device="cuda")
     passes, serial = ctx.unpack_batch_resync_into(packed, in_off, out_off, words, status)
-    assert serial == 0 and passes == 1, (passes, serial)
+    assert serial == 0 and passes < 512, (passes, serial)
     assert int(status[0]) == 0
     assert np.array_equal(words.cpu().numpy().view(np.uint64), w)
 
