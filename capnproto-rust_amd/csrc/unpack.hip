@@ -222,12 +222,15 @@ __device__ void unpack_global(const uint8_t* __restrict__ in, const uint64_t* __
 }
 
 // Global path for one chunk too large for the tile tables (unpack_tile_rest):
-// one wave, windows of kG1Words output words, the descriptor table as one flat
-// array.  Lane 0 walks the records from global memory, writing a descriptor at
-// each record's first word and a continuation at each 64-word group a run
-// enters (positions are 12-bit offsets from the group's first source byte,
-// gpb[g]); then the wave expands the window group by group with coalesced
-// 512-byte stores.  unpack_global's 64-word windows cost a walk round, an
+// the workgroup, windows of kG1Words output words, the descriptor table as one
+// flat array.  Lane 0 of wave 0 walks the records from global memory, writing
+// a descriptor at each record's first word and a continuation at each 64-word
+// group a run enters (positions are 12-bit offsets from the group's first
+// source byte, gpb[g]); then all waves expand the window's groups in turn
+// with coalesced 512-byte stores.  (Round 4: wave 0 alone expanded, at ~370
+// cycles a 512-byte store -- one wave's store throughput: a zero-run chunk of
+// 8192 words took ~52 us, scripts/ovf_probe.py; config 4's index-free block
+// decode and the drop-in read of long message bodies take this path.)  unpack_global's 64-word windows cost a walk round, an
 // 8 KiB table clear and two waits per 64 words: a 512-byte block of zero runs
 // (config 4's index-free block decode, ~600-word runs) spent ~1 us per 64 words.
 // Statuses, consumed bytes and the words written before an error are
@@ -238,8 +241,27 @@ __device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* _
                                uint64_t c, uint64_t* __restrict__ out,
                                const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
                                uint64_t* __restrict__ consumed, uint16_t* desc, uint32_t* gpb,
-                               uint32_t lane) {
+                               uint64_t* shared3, uint8_t* bcache, uint32_t lane,
+                               uint32_t wave) {
     const uint64_t p_start = uniform64(in_off[c]), in_end = uniform64(in_off[c + 1]);
+    // wave 0 walks with every lane in step (the same state on each), reading
+    // tag and count bytes from a 1 KiB window of the packed bytes in LDS that
+    // the wave refills with one coalesced load when a byte falls outside (a
+    // lane-0 walk on global memory waited for two dependent loads a record)
+    constexpr uint32_t kCache = 16 * CAPNP_WAVE;
+    uint64_t cb0 = ~0ull;  // bcache holds bytes [cb0, cb0 + kCache) (16-byte aligned in memory)
+    auto byte_at = [&](uint64_t x) -> uint32_t {  // (x < in_end; uniform in wave 0)
+        if (x < cb0 || x - cb0 >= kCache) {  // (cb0 = ~0: empty)
+            cb0 = x - (reinterpret_cast<uintptr_t>(in + x) & 15u);
+            const uint64_t v = cb0 + 16u * lane;
+            // (an aligned vector starting before in_end stays in mapped memory)
+            const uint4 d = v < in_end ? *reinterpret_cast<const uint4*>(in + v)
+                                       : make_uint4(0, 0, 0, 0);
+            reinterpret_cast<uint4*>(bcache)[lane] = d;
+            wave_lds_sync();
+        }
+        return bcache[x - cb0];
+    };
     const uint64_t obase = uniform64(out_off[c]), n = uniform64(out_off[c + 1]) - obase;
     uint64_t p = p_start, w = 0;
     int32_t st = ST_OK;
@@ -251,83 +273,96 @@ __device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* _
     uint32_t pend_kind = KIND_NONE;
     uint64_t pend_rem = 0, pend_src = 0;
     for (uint64_t wbeg = 0; active; wbeg += kG1Words) {
-        {
-            uint4* d4 = reinterpret_cast<uint4*>(desc);
+        __syncthreads();  // (the previous window's expansion is done with the tables)
+        if (wave == 0) {
+            {
+                uint4* d4 = reinterpret_cast<uint4*>(desc);
 #pragma unroll
-            for (uint32_t k = 0; k < kG1Words / 8 / CAPNP_WAVE; k++)
-                d4[k * CAPNP_WAVE + lane] = make_uint4(0, 0, 0, 0);
-        }
-        wave_lds_sync();
-        uint64_t pbw = 0;
-        uint32_t cnt_round = 0;
-        if (lane == 0) {
-            const uint64_t wend = (wbeg + kG1Words < n) ? wbeg + kG1Words : n;
-            pbw = pend_kind == KIND_LIT_CONT ? pend_src : p;
-            int32_t gcur = -1;
-            auto put = [&](uint64_t wi, uint32_t kind, uint64_t pos) {
-                const uint32_t i = (uint32_t)(wi - wbeg), g = i / CAPNP_WAVE;
-                if ((int32_t)g != gcur) {
-                    gpb[g] = (uint32_t)(pos - pbw);
-                    gcur = (int32_t)g;
-                }
-                desc[i] = (uint16_t)((kind << 12) | (uint32_t)(pos - pbw - gpb[g]));
-            };
-            // run words [from, from + take): a continuation at each group start among them
-            auto cont = [&](uint64_t from, uint64_t take, uint32_t kind, uint64_t src,
-                            uint64_t after) {
-                const uint64_t r = (from - wbeg) % CAPNP_WAVE;
-                for (uint64_t gs = r ? from + (CAPNP_WAVE - r) : from; gs < from + take;
-                     gs += CAPNP_WAVE)
-                    put(gs, kind, kind == KIND_LIT_CONT ? src + 8 * (gs - from) : after);
-            };
-            if (pend_kind != KIND_NONE) {  // the run carried in from the previous window
-                const uint64_t take = pend_rem < wend - w ? pend_rem : wend - w;
-                cont(w, take, pend_kind, pend_src, p);
-                w += take;
-                pend_rem -= take;
-                if (pend_kind == KIND_LIT_CONT) pend_src += 8 * take;
-                if (pend_rem == 0) pend_kind = KIND_NONE;
+                for (uint32_t k = 0; k < kG1Words / 8 / CAPNP_WAVE; k++)
+                    d4[k * CAPNP_WAVE + lane] = make_uint4(0, 0, 0, 0);
             }
-            while (w < wend) {
-                if (p >= in_end) { st = ST_PREMATURE; break; }
-                const uint32_t tag = in[p];
-                const uint32_t pop = __builtin_popcount(tag);
-                if (p + 1 + pop > in_end) { st = ST_PREMATURE; break; }
-                const uint32_t kind = tag == 0 ? KIND_ZERO : (tag == 0xFF ? KIND_LIT : KIND_NORMAL);
-                put(w, kind, p);
-                uint64_t q = p + 1 + pop;
-                w += 1;
-                if (kind != KIND_NORMAL) {
-                    if (q >= in_end) { st = ST_PREMATURE; break; }
-                    const uint64_t cnt = in[q];
-                    q += 1;
-                    if (cnt > n - w) { st = ST_NOT_CLEAN; break; }
-                    const uint64_t src = q;
-                    if (kind == KIND_LIT) {
-                        if (in_end - q < 8 * cnt) { st = ST_FAILED_FILL; break; }
-                        q += 8 * cnt;
+            wave_lds_sync();
+            {
+                const uint64_t wend = (wbeg + kG1Words < n) ? wbeg + kG1Words : n;
+                const uint64_t pbw = pend_kind == KIND_LIT_CONT ? pend_src : p;
+                int32_t gcur = -1;
+                uint32_t gbase = 0;  // gpb[gcur] (the table writes go from lane 0 only:
+                                     // 64 lanes storing to one LDS address serialise)
+                auto put = [&](uint64_t wi, uint32_t kind, uint64_t pos) {
+                    const uint32_t i = (uint32_t)(wi - wbeg), g = i / CAPNP_WAVE;
+                    if ((int32_t)g != gcur) {
+                        gbase = (uint32_t)(pos - pbw);
+                        if (lane == 0) gpb[g] = gbase;
+                        gcur = (int32_t)g;
                     }
-                    const uint64_t take = cnt < wend - w ? cnt : wend - w;
-                    const uint32_t ck = kind == KIND_LIT ? KIND_LIT_CONT : KIND_ZERO_CONT;
-                    cont(w, take, ck, src, q);
+                    if (lane == 0)
+                        desc[i] = (uint16_t)((kind << 12) | (uint32_t)(pos - pbw - gbase));
+                };
+                // run words [from, from + take): a continuation at each group start among them
+                auto cont = [&](uint64_t from, uint64_t take, uint32_t kind, uint64_t src,
+                                uint64_t after) {
+                    const uint64_t r = (from - wbeg) % CAPNP_WAVE;
+                    for (uint64_t gs = r ? from + (CAPNP_WAVE - r) : from; gs < from + take;
+                         gs += CAPNP_WAVE)
+                        put(gs, kind, kind == KIND_LIT_CONT ? src + 8 * (gs - from) : after);
+                };
+                if (pend_kind != KIND_NONE) {  // the run carried in from the previous window
+                    const uint64_t take = pend_rem < wend - w ? pend_rem : wend - w;
+                    cont(w, take, pend_kind, pend_src, p);
                     w += take;
-                    if (cnt > take) {
-                        pend_kind = ck;
-                        pend_rem = cnt - take;
-                        pend_src = src + 8 * take;
-                    }
+                    pend_rem -= take;
+                    if (pend_kind == KIND_LIT_CONT) pend_src += 8 * take;
+                    if (pend_rem == 0) pend_kind = KIND_NONE;
                 }
-                p = q;
+                while (w < wend) {
+                    if (p >= in_end) { st = ST_PREMATURE; break; }
+                    const uint32_t tag = byte_at(p);
+                    const uint32_t pop = __builtin_popcount(tag);
+                    if (p + 1 + pop > in_end) { st = ST_PREMATURE; break; }
+                    const uint32_t kind =
+                        tag == 0 ? KIND_ZERO : (tag == 0xFF ? KIND_LIT : KIND_NORMAL);
+                    put(w, kind, p);
+                    uint64_t q = p + 1 + pop;
+                    w += 1;
+                    if (kind != KIND_NORMAL) {
+                        if (q >= in_end) { st = ST_PREMATURE; break; }
+                        const uint64_t cnt = byte_at(q);
+                        q += 1;
+                        if (cnt > n - w) { st = ST_NOT_CLEAN; break; }
+                        const uint64_t src = q;
+                        if (kind == KIND_LIT) {
+                            if (in_end - q < 8 * cnt) { st = ST_FAILED_FILL; break; }
+                            q += 8 * cnt;
+                        }
+                        const uint64_t take = cnt < wend - w ? cnt : wend - w;
+                        const uint32_t ck = kind == KIND_LIT ? KIND_LIT_CONT : KIND_ZERO_CONT;
+                        cont(w, take, ck, src, q);
+                        w += take;
+                        if (cnt > take) {
+                            pend_kind = ck;
+                            pend_rem = cnt - take;
+                            pend_src = src + 8 * take;
+                        }
+                    }
+                    p = q;
+                }
+                uint32_t cnt_round = (uint32_t)(w - wbeg);
+                bool more = true;
+                if (st != ST_OK) { more = false; cnt_round = 0; }
+                else if (w == n) more = false;
+                // the window for every wave: {more, words, the window's base byte}
+                if (lane == 0) {
+                    shared3[0] = more;
+                    shared3[1] = cnt_round;
+                    shared3[2] = pbw;
+                }
             }
-            cnt_round = (uint32_t)(w - wbeg);
-            if (st != ST_OK) { active = false; cnt_round = 0; }
-            else if (w == n) active = false;
         }
-        active = __builtin_amdgcn_readfirstlane((int)active) != 0;
-        cnt_round = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt_round);
-        pbw = readlane64(pbw, 0);
-        wave_lds_sync();
-        for (uint32_t g = 0; g * CAPNP_WAVE < cnt_round; g++) {
+        __syncthreads();
+        active = uniform64(shared3[0]) != 0;
+        const uint32_t cnt_round = (uint32_t)uniform64(shared3[1]);
+        const uint64_t pbw = uniform64(shared3[2]);
+        for (uint32_t g = wave; g * CAPNP_WAVE < cnt_round; g += kWaves) {
             const uint32_t i = g * CAPNP_WAVE + lane;
             const bool valid = i < cnt_round;
             const uint32_t d = valid ? desc[i] : 0u;
@@ -351,9 +386,8 @@ __device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* _
                 out[obase + wbeg + i] = word;
             }
         }
-        wave_lds_sync();
     }
-    if (lane == 0) {
+    if (wave == 0 && lane == 0) {
         status[c] = st;
         if (consumed)
             consumed[c] = st == ST_OK ? p - p_start : (st == ST_NOT_CLEAN ? 0 : in_end - p_start);
@@ -1363,14 +1397,14 @@ __device__ void unpack_tile_rest(USmem& sm, const uint8_t* __restrict__ in,
 #if UNPACK_PROF
             if (tid == 0 && g_utrace) g_utrace[blockIdx.x * 8 + 4] = 1;
 #endif
-            if (wave == 0) {
-                if (G1)  // (the split overflow kernels; the combined kernels keep their registers)
-                    unpack_global1(in, in_off, lo, out, out_off, status, consumed, &sm.desc[0][0][0],
-                                   reinterpret_cast<uint32_t*>(&sm.desc[1][0][0]), lane);
-                else
-                    unpack_global<CAPNP_WAVE>(in, in_off, lo, lo + 1, out, out_off, status,
-                                              consumed, sm.desc[0], lane);
-            }
+            if (G1)  // (the split overflow kernels; the combined kernels keep their registers)
+                unpack_global1(in, in_off, lo, out, out_off, status, consumed, &sm.desc[0][0][0],
+                               reinterpret_cast<uint32_t*>(&sm.desc[1][0][0]),
+                               reinterpret_cast<uint64_t*>(&sm.desc[1][8][0]),
+                               reinterpret_cast<uint8_t*>(&sm.desc[1][16][0]), lane, wave);
+            else if (wave == 0)
+                unpack_global<CAPNP_WAVE>(in, in_off, lo, lo + 1, out, out_off, status,
+                                          consumed, sm.desc[0], lane);
             resel = true;
             lo += 1;
             continue;
