@@ -237,33 +237,47 @@ __device__ void unpack_global(const uint8_t* __restrict__ in, const uint64_t* __
 // unpack_global's rules (a window that fails writes nothing).
 constexpr uint32_t kG1Words = CAPNP_WAVE * CAPNP_WAVE;
 
-__device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+template <typename T>
+__device__ void unpack_global1_t(const uint8_t* __restrict__ in_abs,
+                               const uint64_t* __restrict__ in_off,
                                uint64_t c, uint64_t* __restrict__ out,
                                const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
                                uint64_t* __restrict__ consumed, uint16_t* desc, uint32_t* gpb,
                                uint64_t* shared3, uint8_t* bcache, uint32_t lane,
                                uint32_t wave) {
-    const uint64_t p_start = uniform64(in_off[c]), in_end = uniform64(in_off[c + 1]);
+    // positions relative to the chunk start and words in T (32 bits where the
+    // chunk allows: the walk's compares then stay scalar -- the SALU has no
+    // 64-bit less-than, and each 64-bit compare went through a VALU compare
+    // and a VCC branch)
+    const uint64_t P0 = uniform64(in_off[c]);
+    const uint8_t* __restrict__ in = in_abs + P0;
+    const T p_start = 0, in_end = (T)(uniform64(in_off[c + 1]) - P0);
     // wave 0 walks with every lane in step (the same state on each), reading
     // tag and count bytes from a 1 KiB window of the packed bytes in LDS that
     // the wave refills with one coalesced load when a byte falls outside (a
     // lane-0 walk on global memory waited for two dependent loads a record)
     constexpr uint32_t kCache = 16 * CAPNP_WAVE;
-    uint64_t cb0 = ~0ull;  // bcache holds bytes [cb0, cb0 + kCache) (16-byte aligned in memory)
-    auto byte_at = [&](uint64_t x) -> uint32_t {  // (x < in_end; uniform in wave 0)
-        if (x < cb0 || x - cb0 >= kCache) {  // (cb0 = ~0: empty)
-            cb0 = x - (reinterpret_cast<uintptr_t>(in + x) & 15u);
-            const uint64_t v = cb0 + 16u * lane;
-            // (an aligned vector starting before in_end stays in mapped memory)
-            const uint4 d = v < in_end ? *reinterpret_cast<const uint4*>(in + v)
-                                       : make_uint4(0, 0, 0, 0);
+    // (positions shifted by the chunk start's misalignment, so that the
+    // window bases are aligned and never below the chunk's first vector)
+    const uint32_t mis0 = (uint32_t)(reinterpret_cast<uintptr_t>(in) & 15u);
+    const uint8_t* __restrict__ in16 = in - mis0;
+    T cb0 = (T)~0ull;  // bcache holds shifted bytes [cb0, cb0 + kCache)
+    auto byte_at = [&](T x) -> uint32_t {  // (x < in_end; uniform in wave 0)
+        const T xs = x + mis0;
+        if (xs < cb0 || xs - cb0 >= kCache) {  // (cb0 = ~0: empty)
+            cb0 = xs & ~(T)15;
+            const T v = cb0 + 16u * lane;
+            // (an aligned vector starting before the chunk end stays in mapped memory)
+            const uint4 d = v < in_end + mis0 ? *reinterpret_cast<const uint4*>(in16 + v)
+                                              : make_uint4(0, 0, 0, 0);
             reinterpret_cast<uint4*>(bcache)[lane] = d;
             wave_lds_sync();
         }
-        return bcache[x - cb0];
+        return bcache[xs - cb0];
     };
-    const uint64_t obase = uniform64(out_off[c]), n = uniform64(out_off[c + 1]) - obase;
-    uint64_t p = p_start, w = 0;
+    const uint64_t obase = uniform64(out_off[c]);
+    const T n = (T)(uniform64(out_off[c + 1]) - obase);
+    T p = p_start, w = 0;
     int32_t st = ST_OK;
     bool active = n > 0;
     if (active && p == in_end) {  // read() returns Ok(0): read_exact fails
@@ -271,9 +285,17 @@ __device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* _
         active = false;
     }
     uint32_t pend_kind = KIND_NONE;
-    uint64_t pend_rem = 0, pend_src = 0;
-    for (uint64_t wbeg = 0; active; wbeg += kG1Words) {
+    T pend_rem = 0, pend_src = 0;
+#if UNPACK_PROF
+    const uint64_t gt0 = __builtin_amdgcn_s_memtime();
+    uint64_t gwalk = 0, gexp = 0, gwin = 0;
+#endif
+    for (T wbeg = 0; active; wbeg += kG1Words) {
         __syncthreads();  // (the previous window's expansion is done with the tables)
+#if UNPACK_PROF
+        const uint64_t gw0 = __builtin_amdgcn_s_memtime();
+        gwin++;
+#endif
         if (wave == 0) {
             {
                 uint4* d4 = reinterpret_cast<uint4*>(desc);
@@ -283,12 +305,12 @@ __device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* _
             }
             wave_lds_sync();
             {
-                const uint64_t wend = (wbeg + kG1Words < n) ? wbeg + kG1Words : n;
-                const uint64_t pbw = pend_kind == KIND_LIT_CONT ? pend_src : p;
+                const T wend = (wbeg + kG1Words < n) ? wbeg + kG1Words : n;
+                const T pbw = pend_kind == KIND_LIT_CONT ? pend_src : p;
                 int32_t gcur = -1;
                 uint32_t gbase = 0;  // gpb[gcur] (the table writes go from lane 0 only:
                                      // 64 lanes storing to one LDS address serialise)
-                auto put = [&](uint64_t wi, uint32_t kind, uint64_t pos) {
+                auto put = [&](T wi, uint32_t kind, T pos) {
                     const uint32_t i = (uint32_t)(wi - wbeg), g = i / CAPNP_WAVE;
                     if ((int32_t)g != gcur) {
                         gbase = (uint32_t)(pos - pbw);
@@ -299,15 +321,14 @@ __device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* _
                         desc[i] = (uint16_t)((kind << 12) | (uint32_t)(pos - pbw - gbase));
                 };
                 // run words [from, from + take): a continuation at each group start among them
-                auto cont = [&](uint64_t from, uint64_t take, uint32_t kind, uint64_t src,
-                                uint64_t after) {
-                    const uint64_t r = (from - wbeg) % CAPNP_WAVE;
-                    for (uint64_t gs = r ? from + (CAPNP_WAVE - r) : from; gs < from + take;
+                auto cont = [&](T from, T take, uint32_t kind, T src, T after) {
+                    const T r = (from - wbeg) % CAPNP_WAVE;
+                    for (T gs = r ? from + (CAPNP_WAVE - r) : from; gs < from + take;
                          gs += CAPNP_WAVE)
                         put(gs, kind, kind == KIND_LIT_CONT ? src + 8 * (gs - from) : after);
                 };
                 if (pend_kind != KIND_NONE) {  // the run carried in from the previous window
-                    const uint64_t take = pend_rem < wend - w ? pend_rem : wend - w;
+                    const T take = pend_rem < wend - w ? pend_rem : wend - w;
                     cont(w, take, pend_kind, pend_src, p);
                     w += take;
                     pend_rem -= take;
@@ -322,19 +343,19 @@ __device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* _
                     const uint32_t kind =
                         tag == 0 ? KIND_ZERO : (tag == 0xFF ? KIND_LIT : KIND_NORMAL);
                     put(w, kind, p);
-                    uint64_t q = p + 1 + pop;
+                    T q = p + 1 + pop;
                     w += 1;
                     if (kind != KIND_NORMAL) {
                         if (q >= in_end) { st = ST_PREMATURE; break; }
-                        const uint64_t cnt = byte_at(q);
+                        const T cnt = byte_at(q);
                         q += 1;
                         if (cnt > n - w) { st = ST_NOT_CLEAN; break; }
-                        const uint64_t src = q;
+                        const T src = q;
                         if (kind == KIND_LIT) {
                             if (in_end - q < 8 * cnt) { st = ST_FAILED_FILL; break; }
                             q += 8 * cnt;
                         }
-                        const uint64_t take = cnt < wend - w ? cnt : wend - w;
+                        const T take = cnt < wend - w ? cnt : wend - w;
                         const uint32_t ck = kind == KIND_LIT ? KIND_LIT_CONT : KIND_ZERO_CONT;
                         cont(w, take, ck, src, q);
                         w += take;
@@ -354,11 +375,15 @@ __device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* _
                 if (lane == 0) {
                     shared3[0] = more;
                     shared3[1] = cnt_round;
-                    shared3[2] = pbw;
+                    shared3[2] = P0 + pbw;  // (absolute: the expansion reads in_abs)
                 }
             }
         }
         __syncthreads();
+#if UNPACK_PROF
+        const uint64_t gw1 = __builtin_amdgcn_s_memtime();
+        gwalk += gw1 - gw0;
+#endif
         active = uniform64(shared3[0]) != 0;
         const uint32_t cnt_round = (uint32_t)uniform64(shared3[1]);
         const uint64_t pbw = uniform64(shared3[2]);
@@ -371,27 +396,54 @@ __device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* _
             const uint32_t h = hm ? 63u - (uint32_t)__builtin_clzll(hm) : 0u;
             const uint32_t dh = (h == lane) ? d : (uint32_t)desc[g * CAPNP_WAVE + h];
             const uint32_t kind = dh >> 12;
-            const uint64_t pos = pbw + gpb[g] + (dh & 0xFFFu);
+            const uint64_t pos = pbw + gpb[g] + (dh & 0xFFFu);  // (absolute)
             uint64_t word = 0;
             if (valid) {
                 if (kind == KIND_NORMAL) {
-                    const uint32_t tag = in[pos];
-                    word = expand_word(tag, load_bytes(in, pos + 1, __builtin_popcount(tag)));
+                    const uint32_t tag = in_abs[pos];
+                    word = expand_word(tag, load_bytes(in_abs, pos + 1, __builtin_popcount(tag)));
                 } else if (kind == KIND_LIT) {
                     const uint64_t src = (h == lane) ? pos + 1 : pos + 10 + 8ull * (lane - h - 1);
-                    word = load_bytes(in, src, 8);
+                    word = load_bytes(in_abs, src, 8);
                 } else if (kind == KIND_LIT_CONT) {
-                    word = load_bytes(in, pos + 8ull * (lane - h), 8);
+                    word = load_bytes(in_abs, pos + 8ull * (lane - h), 8);
                 }
                 out[obase + wbeg + i] = word;
             }
         }
+#if UNPACK_PROF
+        gexp += __builtin_amdgcn_s_memtime() - gw1;
+#endif
     }
+#if UNPACK_PROF
+    if (wave == 0 && lane == 0 && g_utrace) {
+        g_utrace[4 * c + 0] = __builtin_amdgcn_s_memtime() - gt0;
+        g_utrace[4 * c + 1] = gwalk;
+        g_utrace[4 * c + 2] = gexp;
+        g_utrace[4 * c + 3] = gwin;
+    }
+#endif
     if (wave == 0 && lane == 0) {
         status[c] = st;
         if (consumed)
             consumed[c] = st == ST_OK ? p - p_start : (st == ST_NOT_CLEAN ? 0 : in_end - p_start);
     }
+}
+
+__device__ void unpack_global1(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
+                               uint64_t c, uint64_t* __restrict__ out,
+                               const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
+                               uint64_t* __restrict__ consumed, uint16_t* desc, uint32_t* gpb,
+                               uint64_t* shared3, uint8_t* bcache, uint32_t lane,
+                               uint32_t wave) {
+    const uint64_t nb = uniform64(in_off[c + 1]) - uniform64(in_off[c]);
+    const uint64_t nw = uniform64(out_off[c + 1]) - uniform64(out_off[c]);
+    if (nb < (1ull << 31) && nw < (1ull << 31))
+        unpack_global1_t<uint32_t>(in, in_off, c, out, out_off, status, consumed, desc, gpb,
+                                   shared3, bcache, lane, wave);
+    else
+        unpack_global1_t<uint64_t>(in, in_off, c, out, out_off, status, consumed, desc, gpb,
+                                   shared3, bcache, lane, wave);
 }
 
 
