@@ -97,7 +97,10 @@ using PWords = std::vector<uint64_t, PinnedAlloc<uint64_t>>;
 // writer: pack every 8 MiB of input (one device batch of many write_all
 // chunks; 1 MiB batches measured 4.1 GiB/s at 1 MiB calls, each batch paying
 // the launches and waits of one device call)
-constexpr size_t kBatchWords = size_t(1) << 20;
+#ifndef STREAM_BATCH_LG
+#define STREAM_BATCH_LG 20
+#endif
+constexpr size_t kBatchWords = size_t(1) << STREAM_BATCH_LG;
 constexpr size_t kPull = size_t(1) << 16;        // reader: bytes asked of the inner reader
 constexpr size_t kPullMax = size_t(1) << 24;     // ... at most, when a unit needs more
 
@@ -410,11 +413,16 @@ capnp_status reader_lit_head(capnp_packed_reader* r) {
 // those decoded rather than a pending answer.
 constexpr size_t kMinUnit = 256;      // (>= the words of any one record: a run is 1 + 255)
 constexpr size_t kWholeUnit = 8192;   // units this long are cut at whole records on the device
-// a read of a whole-record unit decodes at least this many words (4 MiB):
+// a read of a whole-record unit decodes at least this many words (8 MiB):
 // the surplus serves the next reads from `dec` while the unit after it
 // decodes in the background (a 1 MiB unit paid ~18 launches and a few waits
-// of the resync decode per 1 MiB read: 2.1 GiB/s)
-constexpr size_t kBigUnit = size_t(1) << 19;
+// of the resync decode per 1 MiB read: 2.1 GiB/s; round 4, interleaved on
+// one box, 1 MiB reads: 8 MiB units 8.1 / 8.3 / 8.6 GiB/s against 4 MiB
+// units 5.6 / 6.7 / 6.4, profiles/r04af_adaptor_unit_ab.txt)
+#ifndef STREAM_BIGUNIT_LG
+#define STREAM_BIGUNIT_LG 20
+#endif
+constexpr size_t kBigUnit = size_t(1) << STREAM_BIGUNIT_LG;
 
 // A long unit: the staged input is resolved on the device and cut after the
 // last complete record that fits nw words (capnp_stream_decode_prefix), so

@@ -7,7 +7,7 @@ Prints one JSON line.  (Calls pass views of the caller's buffers, as the
 reference's poll_write(&[u8]) / poll_read(&mut [u8]) do: no per-call copy
 in the harness.)
 
-    python3 scripts/adaptor_bench.py [--mib 256] [--call-mib 1]
+    python3 scripts/adaptor_bench.py [--mib 256] [--call-mib 1] [--lib path]
 """
 import argparse
 import json
@@ -45,7 +45,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=int, default=256)
     ap.add_argument("--call-mib", type=float, default=1.0)
+    ap.add_argument("--lib", default="", help="another build of the library (A/B)")
     a = ap.parse_args()
+    if a.lib:
+        os.environ["CAPNP_PACKED_LIB"] = a.lib
     import torch
     from capnp_amd import Context, serialize_packed_async as spa
     ctx = Context(0)
