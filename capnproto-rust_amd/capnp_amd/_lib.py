@@ -51,7 +51,7 @@ EXPORTS = [
     "capnp_gpu_read_message_stream", "capnp_abi_version", "capnp_resync_max_passes",
     "capnp_unpack_prefix",
 ]
-ABI_VERSION = 4  # include/capnp_packed.h CAPNP_ABI_VERSION
+ABI_VERSION = 5  # include/capnp_packed.h CAPNP_ABI_VERSION
 
 
 class ReaderOptionsC(C.Structure):

@@ -132,11 +132,13 @@ class Context:
         _check(st, self._h)
 
     def unpack_batch_resync_into(self, packed, in_byte_off, out_word_off, words, status,
-                                 consumed=None, stream=None):
+                                 consumed=None, stream=None, stats=True):
         """Index-free UNPACK of chunks of any length (capnp_gpu_unpack_batch_resync):
-        results identical to unpack_batch_into; blocks until done.  Returns
-        (fix passes; serial: 1 the batch went to the serial batch unpack, 2 short chunks went
-        there directly, 3 only the chunks that failed their check were decoded serially)."""
+        results identical to unpack_batch_into.  With stats (the default) it
+        blocks until done and returns (fix passes; serial: 1 the batch went to
+        the serial batch unpack, 2 short chunks went there directly, 3 only the
+        chunks that failed their check were decoded serially); stats=False
+        returns None with the decode only enqueued (ordered on the stream)."""
         import ctypes as C
         n = in_byte_off.numel() - 1
         L = _lib.lib()
@@ -144,6 +146,8 @@ class Context:
             self._h, _ptr(packed), _ptr(in_byte_off), n, _ptr(words), _ptr(out_word_off),
             _ptr(status), _ptr(consumed), self._stream(stream))
         _check(st, self._h)
+        if not stats:
+            return None
         passes, serial = C.c_int(0), C.c_int(0)
         _check(L.capnp_resync_stats(self._h, C.byref(passes), C.byref(serial)), self._h)
         return passes.value, serial.value

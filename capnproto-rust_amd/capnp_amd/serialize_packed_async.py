@@ -20,6 +20,8 @@ functions retry until the inner stream moves, as a future driven by
 block_on does.
 """
 import ctypes as C
+import io
+import socket
 
 import numpy as np
 
@@ -47,21 +49,36 @@ def _check(st, ctx):
 class PackedWrite:
     """An AsyncWrite wrapper that packs any data passed into it."""
 
-    def __init__(self, inner, ctx=None):
+    def __init__(self, inner, ctx=None, inner_copies=None):
+        """`inner_copies`: whether `inner.write(b)` copies the bytes of `b`
+        before it returns (io objects and sockets do).  Such a writer is
+        handed a view of the adaptor's queue, valid during the call only, as
+        the reference's poll_write(&[u8]) hands a borrow; the view is
+        released afterwards, so a writer that kept it gets an error on use
+        instead of bytes the queue has since overwritten.  Any other writer
+        (a list sink that keeps what it is given, a buffered transport) gets
+        a bytes copy.  None = decide by type."""
         self.inner = inner
         self.ctx = ctx or default_context()
         self._err = None
+        if inner_copies is None:
+            inner_copies = isinstance(inner, (io.IOBase, socket.socket))
+        self._view = bool(inner_copies)
 
         def write_cb(_user, buf, n):
+            addr = C.cast(buf, C.c_void_p).value
+            mv = memoryview((C.c_ubyte * n).from_address(addr)).cast("B")
             try:
-                # (a view of the adaptor's queue, valid during the call, as
-                # the reference's poll_write(&[u8]): the inner writer copies
-                # what it keeps)
-                addr = C.cast(buf, C.c_void_p).value
-                r = self.inner.write(memoryview((C.c_ubyte * n).from_address(addr)).cast("B"))
+                r = self.inner.write(mv if self._view else bytes(mv))
             except Exception as e:  # surfaced as CAPNP_E_IO
                 self._err = e
                 return -2
+            finally:
+                try:
+                    mv.release()
+                except BufferError as e:  # the writer exported the view and kept it
+                    self._err = e
+                    return -2
             return _lib.IO_PENDING if r is None else int(r)
 
         self._cb = _lib.WRITE_FN(write_cb)
@@ -129,7 +146,13 @@ class PackedRead:
                     return -2
                 if r is None:
                     return _lib.IO_PENDING
-                r = _as_u8(r)  # (read in place: no copy)
+                # (read in place: no copy; but an object the reader may reuse
+                # -- a bytearray, a view of its buffer -- is copied before any
+                # of it is carried to the next call)
+                keep = isinstance(r, bytes) or (isinstance(r, memoryview) and r.readonly)
+                r = _as_u8(r)
+                if not keep and r.size > n:
+                    r = r.copy()
             # never more than n into the adaptor's n-byte staging slot
             k = min(r.size, n)
             self._extra = r[k:]

@@ -157,6 +157,7 @@ struct capnp_ctx {
     int resync_passes = 0, resync_serial = 0;  // last capnp_gpu_unpack_batch_resync
     const int32_t* resync_failed = nullptr;     // its device "a chunk failed" flag (read on demand)
     hipStream_t resync_stream = nullptr;
+    hipEvent_t ev_resync = nullptr;  // orders a resync decode after the previous one
     uint32_t* d_bad = nullptr;  // offset validation flag (check_offsets)
     uint32_t* h_bad = nullptr;  // pinned copy
     uint8_t* h_pin = nullptr;   // pinned staging of the small host calls (kPinnedCall)
@@ -252,7 +253,9 @@ capnp_status ensure_buf(capnp_ctx* ctx, uint8_t** buf, size_t* cap_io, size_t by
     if (bytes <= *cap_io) return CAPNP_OK;
     HIP_TRY(hipSetDevice(ctx->device));
     if (*buf) {
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        // (work queued on a caller's stream, not only ctx->stream, may still
+        // use the buffer: the device batch calls run on the caller's stream)
+        HIP_TRY(hipDeviceSynchronize());
         HIP_TRY(hipFree(*buf));
         *buf = nullptr;
         *cap_io = 0;
@@ -570,6 +573,7 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->resync_failed) (void)hipStreamSynchronize(ctx->resync_stream);  // (still decoding)
     if (ctx->d_state) (void)hipFree(ctx->d_state);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_body) (void)hipFree(ctx->d_body);
@@ -582,6 +586,7 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (ctx->d_resync) (void)hipFree(ctx->d_resync);
     if (ctx->d_wt) (void)hipFree(ctx->d_wt);
     if (ctx->d_pwt) (void)hipFree(ctx->d_pwt);
+    if (ctx->ev_resync) (void)hipEventDestroy(ctx->ev_resync);
     for (int k = 0; k < 3; k++)
         if (ctx->sstream[k]) {
             (void)hipStreamSynchronize(ctx->sstream[k]);
@@ -757,6 +762,16 @@ static capnp_status unpack_resync_dev(capnp_ctx* ctx, const uint8_t* d_packed,
                                       const uint64_t* d_in_byte_off, size_t nchunks,
                                       uint64_t* d_words, const uint64_t* d_out_word_off,
                                       int32_t* d_status, uint64_t* d_consumed, hipStream_t s) {
+    // The previous index-free decode returned with its kernels still queued on
+    // its own stream, and they read and write the workspace this call is about
+    // to reset: a call on another stream waits for them first (an event, no
+    // host synchronisation); on the same stream, stream order already does.
+    if (ctx->resync_failed && ctx->resync_stream != s) {
+        if (!ctx->ev_resync)
+            HIP_TRY(hipEventCreateWithFlags(&ctx->ev_resync, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(ctx->ev_resync, ctx->resync_stream));
+        HIP_TRY(hipStreamWaitEvent(s, ctx->ev_resync, 0));
+    }
     ctx->resync_failed = nullptr;  // (a new call: the previous call's flag is moot)
     ctx->resync_passes = ctx->resync_serial = 0;
     if (nchunks == 0) return CAPNP_OK;

@@ -215,6 +215,10 @@ struct capnp_packed_reader {
     PBytes in;                // staged packed input
     size_t ip = 0;            // bytes of `in` already decoded
     bool eof = false;
+    // the last pull got every byte it asked for: the inner reader had more
+    // ready than that, so pulling ahead of need is safe (a short read means
+    // the source is drained for now, and a blocking reader would block)
+    bool last_full = false;
     PBytes dec;                // decoded bytes not yet handed out
     PBytes spare;              // the next decode's buffer (swapped with dec)
     size_t dp = 0;
@@ -336,11 +340,23 @@ capnp_status reader_pull(capnp_packed_reader* r, size_t ask = kPull) {
         return CAPNP_E_IO;
     }
     r->in.resize(base + (size_t)got);
+    r->last_full = (size_t)got == ask;
     if (got == 0) {
         r->eof = true;
         return CAPNP_NONE;
     }
     return CAPNP_OK;
+}
+
+// Whether a pull ahead of need may be made: nothing is staged, or the last
+// pull was full.  The reference pulls only what the caller's words need
+// (poll_read asks for a tag, a word, a run), so a reader over a blocking
+// pipe or socket never waits for input beyond the current request; the
+// adaptors pull in bulk (one decode per MiBs, not per record) but stop at the
+// first short read, so with a blocking inner reader the same holds: every
+// further pull is one the decode of the staged bytes showed it needs.
+bool may_pull_ahead(const capnp_packed_reader* r) {
+    return r->in.size() == r->ip || r->last_full;
 }
 
 // One PackedRead::read of `nw` words at the current position, on the GPU.
@@ -437,6 +453,7 @@ constexpr size_t kBigUnit = size_t(1) << STREAM_BIGUNIT_LG;
 // fails here leaves the next call to meet it.
 void reader_ahead(capnp_packed_reader* r, size_t nw) {
     for (size_t need = nw * 10 + 16; r->in.size() - r->ip < need;) {
+        if (!r->last_full) break;  // (never a pull the caller's request does not need)
         const capnp_status p = reader_pull(r, need - (r->in.size() - r->ip));
         if (p == CAPNP_OK) continue;
         if (p == CAPNP_NONE) break;      // end of stream: the rest is staged
@@ -486,7 +503,7 @@ capnp_status reader_fill_whole(capnp_packed_reader* r, size_t nw) {
             continue;
         }
         capnp_status p = CAPNP_OK;
-        for (size_t need = nw * 10 + 16; r->in.size() - r->ip < need;)
+        for (size_t need = nw * 10 + 16; r->in.size() - r->ip < need && may_pull_ahead(r);)
             if ((p = reader_pull(r, need - (r->in.size() - r->ip))) != CAPNP_OK) break;
         out.resize(nw * 8);
         uint64_t pb = 0, pw = 0;
@@ -535,7 +552,7 @@ capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
         // stage what the unit can consume (<= 10 bytes a word) before the
         // decode, so one read costs one launch rather than one per pull; a
         // pull that stops short (pending, end, error) is met again below
-        for (size_t need = nw * 10 + 16; r->in.size() - r->ip < need;)
+        for (size_t need = nw * 10 + 16; r->in.size() - r->ip < need && may_pull_ahead(r);)
             if (reader_pull(r, need - (r->in.size() - r->ip)) != CAPNP_OK) break;
         size_t used = 0;
         int32_t st = 0;
@@ -551,10 +568,17 @@ capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
             nw = nw * 2 + 256;
             continue;
         }
-        // PrematureEnd / FailedToFill: the unit needs more input
-        capnp_status p = reader_pull(r);
-        if (p == CAPNP_OK) continue;
-        if (p != CAPNP_NONE && p != CAPNP_PENDING) return p;
+        // PrematureEnd / FailedToFill: the unit needs more input.  A bulk
+        // source is pulled at once; from a drained one (the last pull was
+        // short) the complete records already staged go out first, as the
+        // reference's read returns what it has decoded, and a pull is made
+        // only when there is none.
+        capnp_status p = r->eof ? CAPNP_NONE : CAPNP_PENDING;
+        if (r->last_full) {
+            p = reader_pull(r);
+            if (p == CAPNP_OK) continue;
+            if (p != CAPNP_NONE && p != CAPNP_PENDING) return p;
+        }
         // nothing more now (pending) or ever (end of stream): every complete
         // record staged (the device resolves where the last one ends), then
         // a literal run's head, else pending / a partial record
@@ -571,6 +595,11 @@ capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
             r->dec.swap(out);
             r->dp = 0;
             return CAPNP_OK;
+        }
+        if (!r->last_full && !r->eof) {  // nothing complete staged: the request needs input
+            p = reader_pull(r);
+            if (p == CAPNP_OK) continue;
+            if (p != CAPNP_NONE && p != CAPNP_PENDING) return p;
         }
         e = reader_lit_head(r);
         if (e != CAPNP_NONE) return e;

@@ -552,9 +552,32 @@ struct StageSmemT {
 };
 using StageSmem = StageSmemT<kTileWords, kTileBytes>;
 
+// Long-unit decode (unpack_long): one chunk too large for the tile tables,
+// decoded by the whole workgroup in windows of packed bytes.  Each window
+// stages kLuWinBytes of record starts plus the tail of a record that starts
+// in them (a literal run: <= 2050 bytes), cut into one kLuSeg-byte segment
+// per thread; the decoded words leave in descriptor windows of kLuWords.
+constexpr uint32_t kLuSeg = 64;
+constexpr uint32_t kLuSegMin = 8;  // (a short last window: segments of at least this many bytes)
+constexpr uint32_t kLuWinBytes = kLuSeg * kThreads;     // 16 KiB of record starts
+constexpr uint32_t kLuLead = 48;                         // spec lead-in (as kSegOverlap)
+constexpr uint32_t kLuAvail = kLuWinBytes + 2080;        // bytes staged past the window start
+constexpr uint32_t kLuStage = kLuAvail + 32;             // (+ misalignment and a hop's read-ahead)
+constexpr uint32_t kLuWords = 4096;                      // descriptor window (output words)
+constexpr uint32_t kLuMaxRounds = 64;                    // then the exact serial walk
+static_assert(kLuStage + 16 < 0x8000, "LDS positions fit the descriptors' 15 bits");
+struct LongSmem {
+    uint64_t sel[256];  // (at the offset of StageSmem::sel: the copy serves both)
+    alignas(16) uint8_t bytes[kLuStage];
+    alignas(16) uint16_t dpos[kLuWords];
+    uint32_t wsum[kWaves];
+    uint32_t misc[4];
+};
+
 union USmem {
     StageSmem st;
     uint16_t desc[kGlobalWaves][CAPNP_WAVE][CAPNP_WAVE];  // global path
+    LongSmem lu;                                          // long-unit path
 };
 
 
@@ -1412,6 +1435,315 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
                                  uniform64(out_off[ca]), uniform64(out_off[cb]));
 }
 
+// ---------------------------------------------------------------------------
+// Long units: one chunk too large for the tile tables, decoded by the whole
+// workgroup (round 5; it replaces the single-wave serial walk of
+// unpack_global1, ~1000 cycles a record, as the overflow kernels' path).
+
+// A segment walk from q (word 0) until q >= se -> exit q, words w, keeping
+// its first kLuRecs records (position | word offset << 15) so that the
+// descriptor pass writes them without walking the chain again.
+constexpr uint32_t kLuRecs = 12;
+struct LuRecs {
+    uint32_t r[kLuRecs];
+    uint32_t nr, from;
+    bool full;  // every record of the walk is kept
+};
+__device__ __forceinline__ void lu_walk(const uint8_t* B, uint32_t& q, uint32_t se, uint32_t& w,
+                                        LuRecs& rc) {
+    rc.from = q;
+    rc.nr = 0;
+    w = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kLuRecs; k++) {
+        if (q < se) {
+            rc.r[k] = q | (w << 15);
+            rc.nr = k + 1u;
+            seg_hop(B, q, w);
+        }
+    }
+    rc.full = q >= se;
+    while (q < se) seg_hop(B, q, w);
+}
+
+// Inclusive sum over lanes 0..i of the wave (the DPP pattern of wave_max_scan).
+__device__ __forceinline__ uint32_t wave_sum_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+    return x;
+}
+
+// Exclusive max (MAX) or sum over the workgroup's threads in order; *total
+// = the value over all of them.  One barrier inside; two uses of wsum need a
+// barrier between them (the caller's).
+template <bool MAX>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* wsum, uint32_t wave,
+                                                    uint32_t lane, uint32_t& total) {
+    const uint32_t inc = MAX ? wave_max_scan(x) : wave_sum_scan(x);
+    if (lane == CAPNP_WAVE - 1) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t carry = 0, all = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)kWaves; k++) {
+        const uint32_t v = wsum[k];
+        if (k < wave) carry = MAX ? max(carry, v) : carry + v;
+        all = MAX ? max(all, v) : all + v;
+    }
+    total = all;
+    const uint32_t prev = wave_shr1(inc);
+    return MAX ? max(prev, carry) : prev + carry;
+}
+
+// PackedRead::read_exact of chunk c (serialize_packed.rs:80-228, io.rs:16-31)
+// by the whole workgroup, window by window.  A window starts at a record of
+// the true chain (P) and stages kLuAvail packed bytes; its first kLuWinBytes
+// are cut into one kLuSeg-byte segment per thread, and:
+//   spec    each thread walks from kLuLead bytes before its segment (the tag
+//           chains from different starts couple on the way in) to its first
+//           record start f at or past the segment and on to its exit, the
+//           first record start at or past the segment end, counting words;
+//   rounds  a segment's entry is the previous segments' exit (an exclusive
+//           max over the workgroup); a thread whose entry is not f walks
+//           again from it, until no entry changes (spec_seg_tile's rounds,
+//           across four waves; a segment inside a longer record owns no
+//           exit and passes its entry on);
+//   words   an exclusive sum of the segments' words places each segment's
+//           records; where the chunk's words end inside the window, the
+//           segment holding its last word walks to it with every check (the
+//           decode stops right after the record that fills the buffer,
+//           :222-225; a run past it is DidNotEndCleanly);
+//   expand  in descriptor windows of kLuWords output words: each thread whose
+//           words meet the window writes its records' descriptors, then every
+//           thread expands words from LDS (expand_desc) in coalesced stores.
+// The next window starts at the exit of the last segment.  Anything that is
+// not a clean chain -- a record past the chunk's bytes, bytes that end before
+// its words, a run past its words, rounds that do not settle -- sends the
+// chunk to the exact serial walk (unpack_global1), which gives the status,
+// the consumed count and the words written before the error; speculation
+// changes the speed only.
+__device__ __forceinline__ void unpack_long(USmem& sm, const uint8_t* __restrict__ in,
+                            const uint64_t* __restrict__ in_off, uint64_t c,
+                            uint64_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                            int32_t* __restrict__ status, uint64_t* __restrict__ consumed,
+                            uint32_t tid, uint32_t lane, uint32_t wave) {
+    LongSmem& S = sm.lu;
+    const uint64_t P0 = uniform64(in_off[c]);
+    const uint64_t E = uniform64(in_off[c + 1]) - P0;  // the chunk's packed bytes
+    const uint64_t obase = uniform64(out_off[c]);
+    const uint64_t n = uniform64(out_off[c + 1]) - obase;
+    const uint8_t* __restrict__ u = in + P0;
+    bool bad = n == 0 || E == 0;  // (empty units: the serial walk's rules)
+    uint64_t P = 0, W = 0;        // the window's first byte (a true record start), words so far
+    S.sel[tid] = kExpandTable.s[tid];
+    while (!bad && W < n) {
+        const uint64_t rem = E - P;
+        const bool tail = rem <= kLuWinBytes;  // every remaining record start is in a segment
+        const uint32_t L = rem < kLuAvail ? (uint32_t)rem : kLuAvail;  // bytes staged
+        const uint32_t Lc = L < kLuWinBytes ? L : kLuWinBytes;        // record starts cut
+        // ---- stage [P, P + L) (16-byte loads from the aligned base below P)
+        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(u + P) & 15u);
+        const uint4* src = reinterpret_cast<const uint4*>(u + P - mis);
+        const uint32_t nblk = (mis + L + 15) / 16;
+        __syncthreads();  // (the previous window is done with the LDS)
+        {
+            // LDS DMA, 16 bytes a lane, every load in flight at once (no
+            // registers held); the vectors past the chunk's bytes are zeroed
+            constexpr uint32_t kVec = kLuStage / 16;
+            for (uint32_t i0 = wave * CAPNP_WAVE; i0 < kVec; i0 += kThreads) {
+                const uint32_t i = i0 + lane;
+                if (i0 + CAPNP_WAVE <= nblk) {
+                    __builtin_amdgcn_global_load_lds(
+                        (const __attribute__((address_space(1))) void*)(src + i),
+                        (__attribute__((address_space(3))) void*)(S.bytes + 16u * i0), 16, 0, 0);
+                } else if (i < kVec) {
+                    reinterpret_cast<uint4*>(S.bytes)[i] =
+                        i < nblk ? src[i] : make_uint4(0, 0, 0, 0);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's bytes are in
+        }
+        __syncthreads();
+        const uint8_t* B = S.bytes + mis;  // B[x] = the chunk's byte P + x
+        // ---- spec walk (segments of kLuSeg bytes; a last window of fewer
+        // bytes cuts shorter ones, down to kLuSegMin, so its walks are short)
+        const uint32_t segb = Lc > kLuSegMin * kThreads ? (Lc + kThreads - 1) / kThreads : kLuSegMin;
+        const uint32_t sb = tid * segb;
+        const bool act = sb < Lc;
+        const uint32_t se = act ? (sb + segb < Lc ? sb + segb : Lc) : 0u;
+        uint32_t p = (tid == 0 || !act) ? sb : (sb > kLuLead ? sb - kLuLead : 0u);
+        uint32_t w = 0;
+        while (act && p < sb) seg_hop(B, p, w);
+        const uint32_t f = p;
+        LuRecs rc;
+        lu_walk(B, p, se, w, rc);
+        const bool serr = p > L;  // (a record past the staged bytes: past the chunk end)
+        const uint32_t xs = serr ? 0u : p, ws = w;
+        uint32_t own = act ? xs : 0u, wd = act ? ws : 0u;
+        bool err = act && serr;
+        uint32_t e_used = tid == 0 ? 0u : ~0u, e = 0, xall = 0;
+        // ---- rounds
+        for (uint32_t round = 0;; round++) {
+            e = block_excl_scan<true>(own, S.wsum, wave, lane, xall);
+            const bool need = act && e != e_used;
+            if (!__syncthreads_or(need)) break;
+            if (round == kLuMaxRounds) {
+                bad = true;
+                break;
+            }
+            if (need) {
+                e_used = e;
+                if (e == f) {
+                    own = xs;
+                    wd = ws;
+                    err = serr;
+                } else {
+                    uint32_t q = e, wt = 0;
+                    lu_walk(B, q, se, wt, rc);
+                    err = q > L;
+                    own = (err || e >= se) ? 0u : q;
+                    wd = wt;
+                }
+            }
+        }
+        if (bad) break;
+        // ---- words
+        uint32_t wtot;
+        const uint32_t base = block_excl_scan<false>(wd, S.wsum, wave, lane, wtot);
+        const uint64_t nrem = n - W;
+        const bool fin = (uint64_t)wtot >= nrem;
+        uint32_t Wc, adv;
+        if (!fin) {
+            // the chunk's words go on past the window: its bytes must too
+            if (__syncthreads_or(err) || tail || xall > L || xall < Lc) {
+                bad = true;
+                break;
+            }
+            Wc = wtot;
+            adv = xall;
+        } else {
+            // the segment holding the last word walks to it with every check
+            if (tid == 0) S.misc[0] = kThreads;
+            __syncthreads();
+            const uint32_t lim = (uint32_t)nrem;
+            if (act && base < lim && lim <= base + wd) S.misc[0] = tid;
+            __syncthreads();
+            const uint32_t ts = S.misc[0];
+            const bool errb = __syncthreads_or(err && tid < ts);
+            if (tid == ts) {
+                uint32_t q = e, wq = base;
+                bool ok = true;
+                while (wq < lim) {
+                    uint32_t tag, b1, b9;
+                    rec_bytes(B, q + 1u, tag, b1, b9);
+                    const bool isz = tag == 0, isf = tag == 0xFF;
+                    const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+                    const uint32_t qe = q + 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) +
+                                        (isf ? 8u * cnt : 0u);
+                    const uint32_t wn = wq + 1u + cnt;
+                    if (qe > L || wn > lim) {
+                        ok = false;
+                        break;
+                    }
+                    q = qe;
+                    wq = wn;
+                }
+                S.misc[1] = q;
+                S.misc[2] = ok ? 1u : 0u;
+            }
+            __syncthreads();
+            if (ts >= kThreads || errb || S.misc[2] == 0) {
+                bad = true;
+                break;
+            }
+            Wc = lim;
+            adv = S.misc[1];
+        }
+        // ---- descriptors and expansion, kLuWords output words at a time
+        for (uint32_t sw = 0; sw < Wc; sw += kLuWords) {
+            const uint32_t swe = Wc - sw < kLuWords ? Wc : sw + kLuWords;
+            __syncthreads();  // (the previous descriptor window is expanded)
+            {
+                uint4* d4 = reinterpret_cast<uint4*>(S.dpos);
+                const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+                for (uint32_t k = 0; k < kLuWords / 8 / kThreads; k++) d4[tid + k * kThreads] = none;
+            }
+            __syncthreads();
+            if (act && wd > 0 && base < swe && base + wd > sw) {
+                const uint32_t wlim = base + wd < swe ? base + wd : swe;
+                if (rc.from == e && rc.full) {
+                    // the records of the walk from the entry, kept in registers:
+                    // independent LDS accesses, no chain; literal runs after
+                    uint32_t lit = 0;
+#pragma unroll
+                    for (uint32_t k = 0; k < kLuRecs; k++) {
+                        const uint32_t q = rc.r[k] & 0x7FFFu, wq = base + (rc.r[k] >> 15);
+                        if (k < rc.nr && wq < wlim) {
+                            if (wq >= sw) S.dpos[wq - sw] = (uint16_t)(q + mis);
+                            if (B[q] == 0xFF) lit |= 1u << k;
+                        }
+                    }
+                    while (lit) {  // literal runs (rare)
+                        const uint32_t k = (uint32_t)__builtin_ctz(lit);
+                        lit &= lit - 1u;
+                        uint32_t rk = rc.r[0];
+#pragma unroll
+                        for (uint32_t i = 1; i < kLuRecs; i++)
+                            if (i == k) rk = rc.r[i];
+                        const uint32_t q = rk & 0x7FFFu, wq = base + (rk >> 15);
+                        const uint32_t lp = q + mis, cnt = B[q + 9u];
+                        const uint32_t lo = wq + 1u > sw ? wq + 1u : sw;
+                        const uint32_t hi = wq + 1u + cnt < swe ? wq + 1u + cnt : swe;
+                        for (uint32_t i = lo; i < hi; i++)
+                            S.dpos[i - sw] = (uint16_t)(kRaw | (lp + 10u + 8u * (i - wq - 1u)));
+                    }
+                } else {
+                uint32_t q = e, wq = base;
+                while (wq < wlim) {
+                    uint32_t tag, b1, b9;
+                    rec_bytes(B, q + 1u, tag, b1, b9);
+                    const bool isz = tag == 0, isf = tag == 0xFF;
+                    const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+                    const uint32_t lp = q + mis;  // (LDS position of the tag)
+                    if (wq >= sw) S.dpos[wq - sw] = (uint16_t)lp;
+                    if (isf && cnt) {  // literal-run words (raw, 8 bytes each after the count)
+                        const uint32_t lo = wq + 1u > sw ? wq + 1u : sw;
+                        const uint32_t hi = wq + 1u + cnt < swe ? wq + 1u + cnt : swe;
+                        for (uint32_t i = lo; i < hi; i++)
+                            S.dpos[i - sw] = (uint16_t)(kRaw | (lp + 10u + 8u * (i - wq - 1u)));
+                    }
+                    wq += 1u + cnt;
+                    q += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) +
+                         (isf ? 8u * cnt : 0u);
+                }
+                }
+            }
+            __syncthreads();
+            uint64_t* o = out + obase + W + sw;
+            for (uint32_t i = tid; i < swe - sw; i += kThreads)
+                o[i] = expand_desc(S.bytes, S.sel, S.dpos[i]);
+        }
+        W += Wc;
+        P += adv;
+    }
+    if (bad) {  // the exact serial walk, from the chunk start
+        __syncthreads();
+        unpack_global1(in, in_off, c, out, out_off, status, consumed, &sm.desc[0][0][0],
+                       reinterpret_cast<uint32_t*>(&sm.desc[1][0][0]),
+                       reinterpret_cast<uint64_t*>(&sm.desc[1][8][0]),
+                       reinterpret_cast<uint8_t*>(&sm.desc[1][16][0]), lane, wave);
+        return;
+    }
+    if (tid == 0) {
+        status[c] = ST_OK;
+        if (consumed) consumed[c] = P;
+    }
+}
+
 // One workgroup per tile of `tc` chunks.  The tile is cut into sub-tiles
 // that fit the LDS tables (normally one: the whole tile), each staged,
 // walked and expanded in turn; a single chunk too large for the tables
@@ -1450,10 +1782,8 @@ __device__ void unpack_tile_rest(USmem& sm, const uint8_t* __restrict__ in,
             if (tid == 0 && g_utrace) g_utrace[blockIdx.x * 8 + 4] = 1;
 #endif
             if (G1)  // (the split overflow kernels; the combined kernels keep their registers)
-                unpack_global1(in, in_off, lo, out, out_off, status, consumed, &sm.desc[0][0][0],
-                               reinterpret_cast<uint32_t*>(&sm.desc[1][0][0]),
-                               reinterpret_cast<uint64_t*>(&sm.desc[1][8][0]),
-                               reinterpret_cast<uint8_t*>(&sm.desc[1][16][0]), lane, wave);
+                unpack_long(sm, in, in_off, lo, out, out_off, status, consumed,
+                            lane + wave * CAPNP_WAVE, lane, wave);
             else if (wave == 0)
                 unpack_global<CAPNP_WAVE>(in, in_off, lo, lo + 1, out, out_off, status,
                                           consumed, sm.desc[0], lane);
@@ -1513,7 +1843,7 @@ unpack_fit_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
 }
 
 template <bool SYNC>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, 4)
 unpack_ovf_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                   uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
                   const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
@@ -1558,10 +1888,11 @@ unpack_ovf_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
 // (config 4 index-free: 4.3 ms in the overflow kernel; one workgroup per
 // tile instead cost config 2 0.13 ms of empty workgroups).
 constexpr uint32_t kOvfWindow = 16;  // (64: config 4 index-free overflow 1.86 ms on 1155 workgroups)
+constexpr uint64_t kOvfGrid = 4096;  // (config 2's 65536 tiles: 16 per workgroup, as in round 4)
 static_assert(kOvfWindow <= CAPNP_WAVE, "one lane per tile of the window");
 
 template <bool SYNC>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kThreads, 4)
 unpack_ovf_win_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                       uint64_t nchunks, uint32_t tc, uint64_t* __restrict__ out,
                       const uint64_t* __restrict__ out_off, int32_t* __restrict__ status,
@@ -1573,10 +1904,14 @@ unpack_ovf_win_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict
     const uint32_t lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     bool sel_ok = false;
-    for (uint64_t base = (uint64_t)blockIdx.x * kOvfWindow; base < ntiles;
-         base += (uint64_t)gridDim.x * kOvfWindow) {
+    // (tiles dealt round robin: workgroup g checks tiles g, g + G, g + 2G, ...
+    // kOvfWindow at a time, so a batch whose tiles all overflow -- long
+    // chunks one per tile -- spreads them over the whole grid instead of
+    // kOvfWindow consecutive ones per workgroup)
+    const uint64_t G = gridDim.x;
+    for (uint64_t base = blockIdx.x; base < ntiles; base += G * kOvfWindow) {
         if (wave == 0) {
-            const uint64_t t = base + lane;
+            const uint64_t t = base + lane * G;
             bool o = false;
             if (lane < kOvfWindow && t < ntiles) {
                 const uint64_t ca = t * tc;
@@ -1589,7 +1924,7 @@ unpack_ovf_win_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict
         __syncthreads();
         uint64_t m = ovf_mask;
         while (m) {
-            const uint64_t t = base + ctz64(m);
+            const uint64_t t = base + ctz64(m) * G;
             m &= m - 1;
             const uint64_t ca = t * tc;
             const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
@@ -2020,8 +2355,10 @@ extern "C" hipError_t capnp_launch_unpack(const uint8_t* d_in, const uint64_t* d
         hipLaunchKernelGGL(unpack_fit_kernel<false>, dim3((uint32_t)blocks), dim3(kThreads), 0,
                            stream, d_in, d_in_off, nchunks, tc, d_out, d_out_off, d_status,
                            d_consumed, d_sync);
-        const uint64_t wg = (blocks + kOvfWindow - 1) / kOvfWindow;
-        hipLaunchKernelGGL(unpack_ovf_win_kernel<false>, dim3((uint32_t)(wg < 8192 ? wg : 8192)),
+        // (one workgroup per tile up to kOvfGrid, tiles dealt round robin: a
+        // batch of long chunks, one per tile, decodes them all at once)
+        const uint64_t wg = blocks < kOvfGrid ? blocks : kOvfGrid;
+        hipLaunchKernelGGL(unpack_ovf_win_kernel<false>, dim3((uint32_t)wg),
                            dim3(kThreads), 0, stream, d_in, d_in_off, nchunks, tc, d_out,
                            d_out_off, d_status, d_consumed, d_sync, blocks);
     }

@@ -119,7 +119,7 @@ const char* capnp_version(void);
    signature changes in place (round 3 inserted buf_len into
    capnp_gpu_read_flat_messages under the same name); a binding checks
    capnp_abi_version() == CAPNP_ABI_VERSION once, before any other call. */
-#define CAPNP_ABI_VERSION 4u
+#define CAPNP_ABI_VERSION 5u
 uint32_t capnp_abi_version(void);
 /* Default ReaderOptions (message.rs:117-120). */
 capnp_reader_options capnp_default_reader_options(void);
@@ -163,8 +163,12 @@ capnp_status capnp_gpu_pack_batch(capnp_ctx* ctx, const uint64_t* d_words,
    nothing launched, otherwise).  Synchronises `stream` once (the check, and
    d_out_word_off[0] and [nchunks] to size the launch); a batch whose mean
    chunk is >= 512 words then takes the index-free block decode of
-   capnp_gpu_unpack_batch_resync, which synchronises again.
-   capnp_gpu_unpack_batch_tuned below does neither. */
+   capnp_gpu_unpack_batch_resync (one more synchronisation, before its
+   decode).  The decode itself is only enqueued: d_words, d_status and
+   d_consumed are ordered on `stream` (read them after a synchronisation of
+   `stream`, or from work queued on it) -- never with a plain hipMemcpy or
+   from another stream without an event.
+   capnp_gpu_unpack_batch_tuned below does neither synchronisation. */
 capnp_status capnp_gpu_unpack_batch(capnp_ctx* ctx, const uint8_t* d_packed,
                                     const uint64_t* d_in_byte_off, size_t nchunks,
                                     uint64_t* d_words, const uint64_t* d_out_word_off,
@@ -250,8 +254,13 @@ capnp_status capnp_gpu_unpack_batch_sync_tuned(capnp_ctx* ctx, const uint8_t* d_
    serially on its own (in the same launch as the resolved blocks), so its
    status, consumed count and partial output are exactly what
    capnp_gpu_unpack_batch gives it.  The offset arrays are checked first as
-   for capnp_gpu_unpack_batch.  Blocking: synchronises `stream` (typically
-   twice). */
+   for capnp_gpu_unpack_batch: that check synchronises `stream` once, before
+   any decode work.  The decode is then enqueued on `stream` and the call
+   returns without waiting for it (so documented from ABI 5; the ABI-4 header
+   said it waited): the results are
+   ordered on `stream` only.  A later resync call on the same context but
+   another stream waits for this one's kernels by an event (they share the
+   context's workspace); capnp_resync_stats synchronises `stream`. */
 capnp_status capnp_gpu_unpack_batch_resync(capnp_ctx* ctx, const uint8_t* d_packed,
                                            const uint64_t* d_in_byte_off, size_t nchunks,
                                            uint64_t* d_words, const uint64_t* d_out_word_off,

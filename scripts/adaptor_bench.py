@@ -66,7 +66,7 @@ def main():
     # staging buffers (the reader's first unit took 26 ms on the box).
     mv = memoryview(raw)
     sink = MemWrite()
-    w = spa.PackedWrite(sink, ctx=ctx)
+    w = spa.PackedWrite(sink, ctx=ctx, inner_copies=True)  # (MemWrite keeps bytes(b))
     for i in range(0, warm, call):
         w.write_all(mv[i:i + call])
     t0 = time.perf_counter()

@@ -647,3 +647,92 @@ def test_large_reads_truncated_stream(A):
             got += b
         assert got == ref, (cut, len(got), len(ref))
         assert (err == "PrematureEndOfFile") == (end == "EOF"), (cut, err, end)
+
+
+class _Pipe:
+    """A blocking pipe after the peer wrote `data` and waits for an answer:
+    a read returns what is buffered (short reads, POSIX read(2)), and a read
+    with nothing buffered would block forever -- here it fails the test."""
+
+    def __init__(self, data, piece=None):
+        self.data, self.pos, self.piece = bytes(data), 0, piece
+        self.reads = 0
+
+    def read(self, n):
+        if self.pos == len(self.data):
+            raise AssertionError("read() on an empty blocking pipe: would hang")
+        k = min(n, len(self.data) - self.pos, self.piece or n)
+        self.reads += 1
+        b = self.data[self.pos:self.pos + k]
+        self.pos += k
+        return b
+
+
+@pytest.mark.parametrize("body_words,piece", [(200, None), (20_000, None), (300_000, None),
+                                              (300_000, 65_536 + 24)])
+def test_reader_stops_at_request_over_blocking_pipe(A, body_words, piece):
+    """read_message over a blocking inner reader that has exactly one message
+    buffered returns that message without another read (the reference's
+    PackedRead pulls only what the caller's words need): no read-ahead of MiBs
+    on the caller's thread (stream_io.hip reader_ahead)."""
+    rng = np.random.default_rng(body_words)
+    seg = rng.integers(0, 1 << 63, body_words, dtype=np.uint64)
+    seg[rng.random(body_words) < 0.3] = 0
+    st, msg = O.write_message([seg])
+    assert st == 0
+    pipe = _Pipe(msg, piece)
+    pr = A.PackedRead(pipe)
+    m = A.read_message(pr)
+    assert np.array_equal(np.asarray(m.segments()[0]).view(np.uint64), seg)
+    assert pipe.pos == len(msg)
+
+
+def test_writer_list_sink_keeps_its_bytes(A):
+    """An inner writer that keeps what it is given (no copy) sees bytes that
+    stay valid after the adaptor reuses its queue."""
+    class Keep:
+        def __init__(self):
+            self.parts = []
+
+        def write(self, b):
+            self.parts.append(b)  # (keeps the object itself)
+            return len(b)
+
+    w = _mixed_words(11, 150_000)
+    u = w.tobytes()
+    sink = Keep()
+    pw = A.PackedWrite(sink)
+    for i in range(0, len(u), 1 << 18):
+        pw.write_all(u[i:i + (1 << 18)])
+        pw.flush_blocking()
+    ref = b""
+    for i in range(0, len(u), 1 << 18):
+        ref += O.pack(u[i:i + (1 << 18)])[1]
+    assert b"".join(bytes(x) for x in sink.parts) == ref
+
+
+def test_reader_reused_bytearray(A):
+    """An inner reader that returns its own reused bytearray: the bytes the
+    adaptor carries past one call are its own copy."""
+    w = _mixed_words(12, 60_000)
+    u = w.tobytes()
+    st, p = O.pack(u)
+
+    class Reuse:
+        def __init__(self, data):
+            self.data, self.pos, self.buf = data, 0, bytearray(100_003)
+
+        def read(self, n):
+            k = min(len(self.buf), len(self.data) - self.pos)
+            self.buf[:k] = self.data[self.pos:self.pos + k]
+            self.pos += k
+            return memoryview(self.buf)[:k]
+
+    pr = A.PackedRead(Reuse(p))
+    got = bytearray()
+    while True:
+        b = pr.read(4096)
+        if not b:
+            break
+        got += b
+    assert bytes(got) == u

@@ -213,3 +213,30 @@ def test_resync_short_chunks_dispatch(ctx):
     assert serial == 2 and passes == 0
     assert (st == 0).all() and np.array_equal(used, np.diff(poffs))
     assert np.array_equal(g, words)
+
+
+def test_resync_two_streams_one_ctx(ctx):
+    """Two index-free decodes queued back to back on different streams of one
+    context (the second call must not reset the shared workspace under the
+    first one's kernels: it waits for them by an event)."""
+    w1, o1, p1, po1 = packed_batch([1 << 16] * 4, [0, 1, 0, 2], id0=77)
+    w2, o2, p2, po2 = packed_batch([1 << 15] * 6, [1, 0, 2, 0, 0, 0], pz=O.PZ80, id0=78)
+    args = []
+    for (w, o, p, po) in ((w1, o1, p1, po1), (w2, o2, p2, po2)):
+        n = len(o) - 1
+        args.append((dev(p), dev(po), dev(o), torch.zeros(int(o[-1]), dtype=torch.int64, device="cuda"),
+                     torch.full((n,), -1, dtype=torch.int32, device="cuda"),
+                     torch.zeros(n, dtype=torch.int64, device="cuda")))
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    for rep in range(3):
+        for a in args:
+            a[3].zero_()
+        torch.cuda.synchronize()
+        ctx.unpack_batch_resync_into(*args[0], stream=s1.cuda_stream, stats=False)
+        ctx.unpack_batch_resync_into(*args[1], stream=s2.cuda_stream, stats=False)
+        torch.cuda.synchronize()
+        for (w, o, p, po), a in zip(((w1, o1, p1, po1), (w2, o2, p2, po2)), args):
+            assert (a[4].cpu().numpy() == 0).all(), rep
+            assert np.array_equal(a[5].cpu().numpy().view(np.uint64), np.diff(po)), rep
+            assert np.array_equal(a[3].cpu().numpy().view(np.uint64), w), rep
