@@ -13,6 +13,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <cmath>
 #include <vector>
@@ -109,6 +110,13 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
                                           uint64_t* d_consumed, void* d_ws, size_t ws_bytes,
                                           hipStream_t s, int* passes, int* serial,
                                           const int32_t** failed_flag);
+extern "C" hipError_t capnp_launch_msg_read(const uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t,
+                                            uint32_t, uint64_t, uint64_t, FrameResult*, uint64_t*,
+                                            uint64_t*, uint32_t*, uint32_t, hipStream_t);
+extern "C" uint32_t capnp_msg_pack_words(void);
+extern "C" hipError_t capnp_launch_msg_pack(const uint64_t*, const uint64_t*, uint32_t, uint32_t,
+                                            uint8_t*, uint64_t, uint64_t*, uint32_t*, uint32_t,
+                                            hipStream_t);
 extern "C" hipError_t capnp_launch_frame(const uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t,
                                          uint32_t, uint64_t, uint64_t, FrameResult*, hipStream_t);
 
@@ -123,7 +131,7 @@ size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
 
 constexpr size_t kTablePrefixBytes = 4096;  // >= 10 bytes x (1 + 256) table words
 // message bodies of at least this many words decode in parallel (read_body)
-constexpr uint64_t kParallelBodyWords = 4096;
+constexpr uint64_t kParallelBodyWords = 32768;
 
 struct capnp_ctx {
     int device = 0;
@@ -161,7 +169,12 @@ struct capnp_ctx {
     uint32_t* d_bad = nullptr;  // offset validation flag (check_offsets)
     uint32_t* h_bad = nullptr;  // pinned copy
     uint8_t* h_pin = nullptr;   // pinned staging of the small host calls (kPinnedCall)
+    uint8_t* d_pin = nullptr;   // ... its device address (the one-launch calls read and write it)
     size_t pin_cap = 0;
+    FrameResult* d_hframe = nullptr;  // h_frame's device address
+    uint32_t* h_flag = nullptr;  // pinned: the one-launch calls' completion flag
+    uint32_t* d_flag = nullptr;  // ... its device address
+    uint32_t call_seq = 0;
     std::string err;
 };
 
@@ -282,6 +295,32 @@ capnp_status ensure_pin(capnp_ctx* ctx, size_t bytes) {
     const size_t cap = std::max<size_t>(round16(bytes) + 64, 1 << 16);
     HIP_TRY(hipHostMalloc(&ctx->h_pin, cap, 0));
     ctx->pin_cap = cap;
+    void* dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, ctx->h_pin, 0));
+    ctx->d_pin = static_cast<uint8_t*>(dp);
+    return CAPNP_OK;
+}
+
+// Waits for a one-launch call (msg_read_kernel / msg_pack_kernel) by its
+// completion flag in pinned memory: the kernel stores `seq` there after its
+// results, and polling the flag returns a few microseconds sooner than the
+// runtime's stream wait (the per-message calls are latency-bound).  A call
+// that has not finished within ~5 ms, or failed, falls to that wait, which
+// reports the error.
+capnp_status wait_call(capnp_ctx* ctx, uint32_t seq, hipStream_t s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; i++) {
+        if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) == seq) return CAPNP_OK;
+        __builtin_ia32_pause();
+        if ((i & 1023) == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5))
+            break;
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) != seq) {
+        ctx->err = "one-launch call finished without its completion flag";
+        return CAPNP_E_HIP;
+    }
     return CAPNP_OK;
 }
 
@@ -555,6 +594,18 @@ capnp_ctx* capnp_ctx_create(int device, capnp_status* status) {
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&ctx->d_frame, sizeof(FrameResult));
     if (e == hipSuccess) e = hipHostMalloc(&ctx->h_frame, sizeof(FrameResult), 0);
+    if (e == hipSuccess) {
+        void* dp = nullptr;
+        e = hipHostGetDevicePointer(&dp, ctx->h_frame, 0);
+        ctx->d_hframe = static_cast<FrameResult*>(dp);
+    }
+    if (e == hipSuccess) e = hipHostMalloc(&ctx->h_flag, 64, 0);
+    if (e == hipSuccess) {
+        *ctx->h_flag = 0;
+        void* dp = nullptr;
+        e = hipHostGetDevicePointer(&dp, ctx->h_flag, 0);
+        ctx->d_flag = static_cast<uint32_t*>(dp);
+    }
     if (e == hipSuccess) e = hipMalloc(&ctx->d_bad, 4);
     if (e == hipSuccess) e = hipHostMalloc(&ctx->h_bad, 4, 0);
     if (e != hipSuccess) {
@@ -582,6 +633,7 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (ctx->d_bad) (void)hipFree(ctx->d_bad);
     if (ctx->h_bad) (void)hipHostFree(ctx->h_bad);
     if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+    if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
     if (ctx->d_msg) (void)hipFree(ctx->d_msg);
     if (ctx->d_resync) (void)hipFree(ctx->d_resync);
     if (ctx->d_wt) (void)hipFree(ctx->d_wt);
@@ -1492,45 +1544,110 @@ capnp_status capnp_packed_write_message(capnp_ctx* ctx, const uint64_t* const* s
     *written = 0;
     // chunks: word 0, the rest of the table, then one per segment
     // (serialize.rs:605-679)
-    std::vector<uint64_t> off;
-    std::vector<uint64_t> words;
-    off.push_back(0);
-    words.push_back((uint64_t)(nseg - 1) | ((uint64_t)seg_words[0] << 32));
-    off.push_back(words.size());
-    if (nseg > 1) {
-        const size_t rest = nseg < 4 ? 8 : (size_t)(nseg & ~1u) * 4;
-        std::vector<uint32_t> t(rest / 4, 0u);
-        for (uint32_t i = 1; i < nseg; i++) t[i - 1] = seg_words[i];
-        const size_t w0 = words.size();
-        words.resize(w0 + rest / 8);
-        memcpy(words.data() + w0, t.data(), rest);
-        off.push_back(words.size());
-    }
+    const size_t rest = nseg == 1 ? 0 : (nseg < 4 ? 8 : (size_t)(nseg & ~1u) * 4);
+    const size_t tw = 1 + rest / 8;  // table words
+    const size_t nch = 1 + (nseg > 1 ? 1 : 0) + nseg;
+    uint64_t nw = tw;
     for (uint32_t i = 0; i < nseg; i++) {
         if (seg_words[i] && !segs[i]) return CAPNP_E_INVALID_ARGUMENT;
-        const size_t w0 = words.size();
-        words.resize(w0 + seg_words[i]);
-        if (seg_words[i]) memcpy(words.data() + w0, segs[i], (size_t)seg_words[i] * 8);
-        off.push_back(words.size());
+        nw += seg_words[i];
     }
+    const size_t bound = capnp_packed_batch_bound_bytes(nw, nch);
+    const size_t o_off = round16(nw * 8), o_tot = o_off + round16((nch + 1) * 8);
+    const size_t o_out = o_tot + 16;
+    hipStream_t s = ctx->stream;
+    // the table words and the chunk offsets, written where `base` points
+    auto lay_out = [&](uint64_t* w, uint64_t* off) {
+        w[0] = (uint64_t)(nseg - 1) | ((uint64_t)seg_words[0] << 32);
+        if (rest) {
+            uint32_t* t = reinterpret_cast<uint32_t*>(w + 1);
+            memset(t, 0, rest);
+            for (uint32_t i = 1; i < nseg; i++) t[i - 1] = seg_words[i];
+        }
+        size_t k = 0;
+        off[k++] = 0;
+        off[k++] = 1;
+        if (rest) off[k++] = tw;
+        uint64_t o = tw;
+        for (uint32_t i = 0; i < nseg; i++) off[k++] = (o += seg_words[i]);
+    };
+    if (nw <= capnp_msg_pack_words() && nch <= 515 && o_out + bound + 64 <= kPinnedCall) {
+        // one launch (msg_pack_kernel): chunks and offsets laid out in pinned
+        // memory, the kernel writes the packed bytes and their total there
+        capnp_status st = ensure_pin(ctx, o_out + bound + 64);
+        if (st != CAPNP_OK) return st;
+        uint8_t* h = ctx->h_pin;
+        uint8_t* dh = ctx->d_pin;
+        uint64_t* w = reinterpret_cast<uint64_t*>(h);
+        lay_out(w, reinterpret_cast<uint64_t*>(h + o_off));
+        uint64_t o = tw;
+        for (uint32_t i = 0; i < nseg; i++) {
+            if (seg_words[i]) memcpy(w + o, segs[i], (size_t)seg_words[i] * 8);
+            o += seg_words[i];
+        }
+        HIP_TRY(capnp_launch_msg_pack(reinterpret_cast<uint64_t*>(dh),
+                                      reinterpret_cast<uint64_t*>(dh + o_off), (uint32_t)nch,
+                                      (uint32_t)nw, dh + o_out, bound,
+                                      reinterpret_cast<uint64_t*>(dh + o_tot), ctx->d_flag,
+                                      ++ctx->call_seq, s));
+        st = wait_call(ctx, ctx->call_seq, s);
+        if (st != CAPNP_OK) return st;
+        const uint64_t total = *reinterpret_cast<volatile uint64_t*>(h + o_tot);
+        const size_t ncopy = std::min<uint64_t>(total, cap);
+        if (ncopy) memcpy(out, h + o_out, ncopy);
+        *written = ncopy;
+        return total > cap ? CAPNP_E_BUFFER_NOT_LARGE_ENOUGH : CAPNP_OK;
+    }
+    // a long message: each segment goes to the device staging buffer straight
+    // from the caller's memory (no host gather), the table and offsets from a
+    // small host array; the batch pack; the bytes straight back into `out`
+    const size_t o_oo = o_tot;  // (device layout: words, offsets, out offsets, out)
+    const size_t o_dout = o_oo + round16((nch + 1) * 8);
+    capnp_status st = ensure_stage(ctx, o_dout + bound + 16);
+    if (st != CAPNP_OK) return st;
+    uint8_t* d = ctx->d_stage;
+    std::vector<uint64_t> small(tw);
+    std::vector<uint64_t> off(nch + 1);
+    lay_out(small.data(), off.data());
+    HIP_TRY(hipMemcpyAsync(d, small.data(), tw * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(d + o_off, off.data(), (nch + 1) * 8, hipMemcpyHostToDevice, s));
+    uint64_t o = tw;
+    for (uint32_t i = 0; i < nseg; i++) {
+        if (seg_words[i])
+            HIP_TRY(hipMemcpyAsync(d + o * 8, segs[i], (size_t)seg_words[i] * 8,
+                                   hipMemcpyHostToDevice, s));
+        o += seg_words[i];
+    }
+    const uint64_t wr[2] = {0, nw};
+    const uint32_t tc = nw / nch >= kWordTileMean ? 0u : tile_chunks_for(nw, nch);
+    st = pack_batch_dev(ctx, reinterpret_cast<uint64_t*>(d), reinterpret_cast<uint64_t*>(d + o_off),
+                        nch, d + o_dout, bound, reinterpret_cast<uint64_t*>(d + o_oo), tc, s,
+                        nullptr, wr);
+    if (st != CAPNP_OK) return st;
     uint64_t total = 0;
-    capnp_status st = pack_host(ctx, words.data(), off.data(), off.size() - 1, out, cap, nullptr,
-                                &total);
-    *written = std::min<uint64_t>(total, cap);
-    return st;
+    HIP_TRY(hipMemcpyAsync(&total, d + o_oo + nch * 8, 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const size_t ncopy = std::min<uint64_t>(total, cap);
+    if (ncopy) {
+        HIP_TRY(hipMemcpyAsync(out, d + o_dout, ncopy, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    *written = ncopy;
+    return total > cap ? CAPNP_E_BUFFER_NOT_LARGE_ENOUGH : CAPNP_OK;
 }
 
 // A message whose body is short (< kParallelBodyWords words, and within the
-// caller's capacity) in ONE round trip: the input prefix that can hold the
-// table and such a body (<= 10 bytes per word) goes in through the pinned
-// buffer, the frame kernel reads the table and leaves the body's unit in
-// device memory, the batch unpack decodes it from there (a body too long,
-// or a failed table, is an empty unit), and the frame result, the body's
-// status and consumed bytes and its words come back together.  *done =
-// false when the body still has to be read the long way (read_body): it is
-// longer than that, or its unit ran past the staged prefix of a longer
-// input.  The reference's per-message cost (serialize_packed::read_message
-// once per request, benchmark.rs:207-259) is this call.
+// caller's capacity) in ONE launch: the input prefix that can hold the table
+// and such a body (<= 10 bytes per word) is copied into the pinned buffer,
+// and msg_read_kernel (unpack.hip) reads it there, checks the table, decodes
+// the body with the workgroup's long-unit decode and writes the frame
+// result, the body's status and consumed bytes and its words back into
+// pinned memory (a body too long, or a failed table, is an empty unit): one
+// launch and one wait.  *done = false when the body still has to be read the
+// long way (read_body): it is longer than that, or its unit ran past the
+// staged prefix of a longer input.  The reference's per-message cost
+// (serialize_packed::read_message once per request, benchmark.rs:207-259) is
+// this call.
 static capnp_status read_message_fast(capnp_ctx* ctx, const uint8_t* in, size_t in_len,
                                       const capnp_reader_options* opts, int try_mode,
                                       int no_alloc, uint64_t buffer_len, uint64_t cap_words,
@@ -1543,28 +1660,22 @@ static capnp_status read_message_fast(capnp_ctx* ctx, const uint8_t* in, size_t 
     const size_t stage = std::min<size_t>(in_len, kTablePrefixBytes + cap * 10 + 16);
     const size_t o_st = round16(cap * 8);  // body words, then status, pad, consumed
     const size_t h_out = round16(stage + 16);
-    capnp_status st = ensure_stage(ctx, round16(stage + 16) + 64);
-    if (st == CAPNP_OK) st = ensure_buf(ctx, &ctx->d_body, &ctx->body_cap, o_st + 64);
-    if (st == CAPNP_OK) st = ensure_pin(ctx, h_out + o_st + 64);
+    capnp_status st = ensure_pin(ctx, h_out + o_st + 64);
     if (st != CAPNP_OK) return st;
-    uint8_t* d = ctx->d_stage;
-    uint8_t* db = ctx->d_body;
     uint8_t* h = ctx->h_pin;
+    uint8_t* dh = ctx->d_pin;
     hipStream_t s = ctx->stream;
-    if (stage) {
-        memcpy(h, in, stage);
-        HIP_TRY(hipMemcpyAsync(d, h, stage, hipMemcpyHostToDevice, s));
-    }
-    FrameResult* df = ctx->d_frame;
-    HIP_TRY(capnp_launch_frame(d, stage, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
-                               o.traversal_limit_in_words, (uint32_t)(o.has_traversal_limit != 0),
-                               buffer_len, cap, df, s));
-    HIP_TRY(capnp_launch_unpack(d, df->body_in_off, 1, 0, reinterpret_cast<uint64_t*>(db),
-                                df->body_out_off, reinterpret_cast<int32_t*>(db + o_st),
-                                reinterpret_cast<uint64_t*>(db + o_st + 16), nullptr, s));
-    HIP_TRY(hipMemcpyAsync(ctx->h_frame, df, sizeof(FrameResult), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(h + h_out, db, o_st + 24, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    if (stage) memcpy(h, in, stage);
+    // one launch: the kernel reads the staged bytes and writes the frame
+    // record, the body's status and its words in pinned memory
+    HIP_TRY(capnp_launch_msg_read(dh, stage, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
+                                  o.traversal_limit_in_words,
+                                  (uint32_t)(o.has_traversal_limit != 0), buffer_len, cap,
+                                  ctx->d_hframe, reinterpret_cast<uint64_t*>(dh + h_out),
+                                  reinterpret_cast<uint64_t*>(dh + h_out + o_st), ctx->d_flag,
+                                  ++ctx->call_seq, s));
+    st = wait_call(ctx, ctx->call_seq, s);
+    if (st != CAPNP_OK) return st;
     *fr = *ctx->h_frame;
     if (fr->status != CAPNP_OK || fr->total_words > cap) return CAPNP_OK;  // (the caller decides)
     uint64_t res[3];

@@ -682,7 +682,7 @@ __device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* o
                               uint64_t* chunk_size, const uint64_t* chunk_pos, uint32_t nc,
                               uint32_t wave, uint32_t lane, uint8_t* ring, const Sel8* sel,
                               uint8_t* out, uint32_t mis, uint64_t out_cap,
-                              const uint32_t* cgap) {
+                              const uint32_t* cgap, uint64_t* last_size = nullptr) {
     Packer pk;
     for (uint32_t ci = wave; ci < nc; ci += kWaves) {
         const uint64_t woff = uniform64(off[ci]);
@@ -710,6 +710,8 @@ __device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* o
             if (last) break;
         }
         if (MODE == MODE_SIZE && lane == 0) chunk_size[ci] = pk.total + g;
+        // (RING: the size of the last chunk, which its caller did not size)
+        if (MODE == MODE_RING && last_size && ci + 1 == nc && lane == 0) *last_size = pk.total + g;
     }
 }
 
@@ -2867,6 +2869,98 @@ pack_wt_fix_sync(const uint64_t* __restrict__ chunk_off, const uint64_t* __restr
     }
 }
 
+// ---------------------------------------------------------------------------
+// One write_message call in one launch (the drop-in at the reference's call
+// granularity: serialize_packed::write_message once per message,
+// serialize_packed.rs:446-453 -> serialize.rs:574-679, benchmark.rs:207-259).
+// The host lays the message's write_all chunks out in pinned memory (word 0
+// of the table, the rest of the table, each segment) with their word
+// offsets; one workgroup stages the words into LDS in one round trip, sizes
+// every chunk with the streaming path's pass A (wave w: chunks w, w + 4, ...),
+// places them by a scan and writes their bytes with pass B into the pinned
+// output.  No look-back state, no second launch, one wait on the host.
+constexpr uint32_t kMsgWords = 4096;   // words staged in LDS (table + segments)
+constexpr uint32_t kMsgChunks = 516;   // word 0, the table rest, <= 511 segments (+ pad)
+
+struct MsgPackSmem {
+    Sel8 sel[kSelCopy + 1];
+    uint64_t off[kMsgChunks + 1];
+    uint64_t chunk_size[kMsgChunks];
+    uint64_t chunk_pos[kMsgChunks];
+    uint32_t wsum[kWaves];
+    alignas(16) uint32_t pad[4];  // (emit ORs a zero into the dword before a region)
+    alignas(16) uint8_t ring[kWaves][kRing];
+    alignas(16) uint64_t words[kMsgWords];
+};
+
+__global__ void __launch_bounds__(kThreads)
+msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__ off,
+                uint32_t nchunks, uint32_t nwords, uint8_t* __restrict__ out, uint64_t out_cap,
+                uint64_t* __restrict__ total, uint32_t* __restrict__ flag, uint32_t seq) {
+    __shared__ MsgPackSmem S;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    // stage: every load in flight at once (one round trip to host memory)
+    for (uint32_t i = tid; i <= nchunks; i += kThreads) S.off[i] = off[i];
+    {
+        const uint4* w4 = reinterpret_cast<const uint4*>(words);
+        uint4* s4 = reinterpret_cast<uint4*>(S.words);
+        for (uint32_t i = tid; i < nwords / 2; i += kThreads) s4[i] = w4[i];
+        if ((nwords & 1) && tid == 0) S.words[nwords - 1] = words[nwords - 1];
+    }
+    for (uint32_t i = tid; i <= kSelCopy; i += kThreads) S.sel[i] = kSel8Table.e[i];
+    __syncthreads();
+    uint8_t* ring = S.ring[wave];
+    // (the last chunk -- a message's one segment, usually the longest -- is
+    // placed without its size: pass B measures it)
+    if (tid == 0) S.chunk_size[nchunks - 1] = 0;
+    run_streaming<MODE_SIZE>(S.words, S.off, S.chunk_size, S.chunk_pos, nchunks - 1, wave, lane,
+                             ring, S.sel, nullptr, 0, 0, nullptr);
+    __syncthreads();
+    // chunk positions: exclusive scan of the sizes, up to 3 chunks per thread
+    {
+        constexpr uint32_t kPer = (kMsgChunks + kThreads - 1) / kThreads;
+        uint32_t v[kPer], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++) {
+            const uint32_t i = tid * kPer + k;
+            v[k] = i < nchunks ? (uint32_t)S.chunk_size[i] : 0u;
+            sum += v[k];
+        }
+        const uint32_t inc = wave_incl_scan(sum);
+        if (lane == CAPNP_WAVE - 1) S.wsum[wave] = inc;
+        __syncthreads();
+        uint32_t run = inc - sum, all = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)kWaves; k++) {
+            if (k < wave) run += S.wsum[k];
+            all += S.wsum[k];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; k++) {
+            const uint32_t i = tid * kPer + k;
+            if (i < nchunks) S.chunk_pos[i] = run;
+            run += v[k];
+        }
+        if (tid == 0) S.wsum[0] = all;  // (the chunks before the last)
+    }
+    __syncthreads();
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
+    uint64_t* last = reinterpret_cast<uint64_t*>(S.chunk_size + nchunks - 1);
+    run_streaming<MODE_RING>(S.words, S.off, S.chunk_size, S.chunk_pos, nchunks, wave, lane, ring,
+                             S.sel, out - mis, mis, out_cap, nullptr, last);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's stores have landed)
+    __syncthreads();
+    if (tid == 0) {
+        total[0] = S.chunk_pos[nchunks - 1] + S.chunk_size[nchunks - 1];
+        if (flag) {  // (the host waits on this flag: everything above is visible first)
+            __threadfence_system();
+            __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 }  // namespace
 
 // Words per tile the staged path is sized for (kWaves waves x kStageSteps
@@ -3041,3 +3135,19 @@ extern "C" hipError_t capnp_pack_prof(unsigned long long* host8, int reset) {
     return e;
 }
 #endif
+
+// One write_message call in one launch (msg_pack_kernel): the message's
+// chunks (nwords <= capnp_msg_pack_words(), nchunks <= 515) and offsets, the
+// output and *total may be pinned host memory.  Bytes at or past out_cap are
+// not written; *total is the size needed.
+extern "C" uint32_t capnp_msg_pack_words(void) { return kMsgWords; }
+extern "C" hipError_t capnp_launch_msg_pack(const uint64_t* words, const uint64_t* off,
+                                            uint32_t nchunks, uint32_t nwords, uint8_t* out,
+                                            uint64_t out_cap, uint64_t* total, uint32_t* flag,
+                                            uint32_t seq, hipStream_t stream) {
+    if (nwords > kMsgWords || nchunks + 1 > kMsgChunks || nchunks == 0)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(msg_pack_kernel, dim3(1), dim3(kThreads), 0, stream, words, off, nchunks,
+                       nwords, out, out_cap, total, flag, seq);
+    return hipGetLastError();
+}

@@ -32,6 +32,7 @@
 #include "common.h"
 #include <stdlib.h>
 #include "../../include/capnp_packed.h"
+#include "frame.h"
 
 #ifndef UNPACK_PROF
 #define UNPACK_PROF 0  // phase timers (scripts/unpack_prof.py); 0 = product
@@ -45,8 +46,15 @@
 __device__ uint64_t* g_utrace;
 __device__ unsigned long long g_uprof[8];
 #define UPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
+// long-unit phases (unpack_long): g_uprof[1] windows, [2] rounds, [3..7]
+// s_memrealtime ticks (10 ns) in stage, spec, rounds, words (+ the last
+// segment's walk), descriptors + expansion; thread 0 of each workgroup adds
+#define LUPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
+#define LUPROF_ADD(i, x) do { if (tid == 0) atomicAdd(&g_uprof[i], (unsigned long long)(x)); } while (0)
 #else
 #define UPROF_T(v)
+#define LUPROF_T(v)
+#define LUPROF_ADD(i, x)
 #endif
 
 namespace {
@@ -560,7 +568,7 @@ using StageSmem = StageSmemT<kTileWords, kTileBytes>;
 constexpr uint32_t kLuSeg = 64;
 constexpr uint32_t kLuSegMin = 8;  // (a short last window: segments of at least this many bytes)
 constexpr uint32_t kLuWinBytes = kLuSeg * kThreads;     // 16 KiB of record starts
-constexpr uint32_t kLuLead = 48;                         // spec lead-in (as kSegOverlap)
+constexpr uint32_t kLuLead = 64;                         // spec lead-in (tests/emu_long.py: 64 > 48)
 constexpr uint32_t kLuAvail = kLuWinBytes + 2080;        // bytes staged past the window start
 constexpr uint32_t kLuStage = kLuAvail + 32;             // (+ misalignment and a hop's read-ahead)
 constexpr uint32_t kLuWords = 4096;                      // descriptor window (output words)
@@ -1549,6 +1557,7 @@ __device__ __forceinline__ void unpack_long(USmem& sm, const uint8_t* __restrict
         const uint4* src = reinterpret_cast<const uint4*>(u + P - mis);
         const uint32_t nblk = (mis + L + 15) / 16;
         __syncthreads();  // (the previous window is done with the LDS)
+        LUPROF_T(lt0);
         {
             // LDS DMA, 16 bytes a lane, every load in flight at once (no
             // registers held); the vectors past the chunk's bytes are zeroed
@@ -1568,6 +1577,7 @@ __device__ __forceinline__ void unpack_long(USmem& sm, const uint8_t* __restrict
         }
         __syncthreads();
         const uint8_t* B = S.bytes + mis;  // B[x] = the chunk's byte P + x
+        LUPROF_T(lt1);
         // ---- spec walk (segments of kLuSeg bytes; a last window of fewer
         // bytes cuts shorter ones, down to kLuSegMin, so its walks are short)
         const uint32_t segb = Lc > kLuSegMin * kThreads ? (Lc + kThreads - 1) / kThreads : kLuSegMin;
@@ -1582,34 +1592,80 @@ __device__ __forceinline__ void unpack_long(USmem& sm, const uint8_t* __restrict
         lu_walk(B, p, se, w, rc);
         const bool serr = p > L;  // (a record past the staged bytes: past the chunk end)
         const uint32_t xs = serr ? 0u : p, ws = w;
-        uint32_t own = act ? xs : 0u, wd = act ? ws : 0u;
+        // (a spec walk that found no record start in its segment says "passes
+        // through": it owns no exit; one past the staged bytes owns none)
+        const uint32_t xsp = (serr || f >= se) ? 0u : xs;
+        uint32_t own = act ? xsp : 0u, wd = act ? ws : 0u;
         bool err = act && serr;
         uint32_t e_used = tid == 0 ? 0u : ~0u, e = 0, xall = 0;
-        // ---- rounds
+#if UNPACK_PROF
+        __syncthreads();  // (the spec walks are done)
+#endif
+        LUPROF_T(lt2);
+        // ---- rounds (resync.hip seg_rounds' rules).  At the fixed point
+        // every entry is at or past its segment start: lane 0 walks from the
+        // window start, and each later segment's entry is an earlier one's
+        // exit (>= that segment's end) or a pass-through's entry -- unless a
+        // walk ran past the staged bytes (err), which sends the chunk to the
+        // exact walk.  So the rule for an entry below the segment (the spec
+        // walk stands in, no walk) acts only on the way there: it keeps a
+        // pass-through on a missed spec walk's far garbage exit from erasing
+        // its successors' exits, which would send them walking from far back.
         for (uint32_t round = 0;; round++) {
             e = block_excl_scan<true>(own, S.wsum, wave, lane, xall);
             const bool need = act && e != e_used;
-            if (!__syncthreads_or(need)) break;
+            if (!__syncthreads_or(need)) {
+                LUPROF_ADD(2, round);
+                break;
+            }
             if (round == kLuMaxRounds) {
                 bad = true;
                 break;
             }
             if (need) {
                 e_used = e;
-                if (e == f) {
-                    own = xs;
+                if (e < sb || e == f) {  // (below the segment: the spec walk stands in)
+                    own = xsp;
                     wd = ws;
                     err = serr;
+                } else if (e >= se) {  // a record covers the segment: pass through
+                    own = 0;
+                    wd = 0;
+                    err = false;
                 } else {
-                    uint32_t q = e, wt = 0;
-                    lu_walk(B, q, se, wt, rc);
-                    err = q > L;
-                    own = (err || e >= se) ? 0u : q;
-                    wd = wt;
+                    // from the entry, with the spec chain kept in step: where
+                    // they meet the rest of the walk is the spec walk's
+                    uint32_t pt = e, wt = 0, ps = f, wsp = 0;
+                    bool met = false;
+#if UNPACK_PROF == 2
+                    atomicAdd(&g_uprof[3], 1ull);
+#endif
+                    while (pt < se) {
+                        while (ps < pt && ps < se) seg_hop(B, ps, wsp);
+                        if (ps == pt) {
+                            met = true;
+                            break;
+                        }
+                        seg_hop(B, pt, wt);
+#if UNPACK_PROF == 2
+                        atomicAdd(&g_uprof[4], 1ull);
+#endif
+                    }
+                    rc.from = ~0u;  // (the descriptor pass walks from the entry)
+                    if (met) {
+                        own = xsp;
+                        wd = wt + ws - wsp;
+                        err = serr;
+                    } else {
+                        err = pt > L;
+                        own = err ? 0u : pt;
+                        wd = wt;
+                    }
                 }
             }
         }
         if (bad) break;
+        LUPROF_T(lt3);
         // ---- words
         uint32_t wtot;
         const uint32_t base = block_excl_scan<false>(wd, S.wsum, wave, lane, wtot);
@@ -1662,6 +1718,7 @@ __device__ __forceinline__ void unpack_long(USmem& sm, const uint8_t* __restrict
             Wc = lim;
             adv = S.misc[1];
         }
+        LUPROF_T(lt4);
         // ---- descriptors and expansion, kLuWords output words at a time
         for (uint32_t sw = 0; sw < Wc; sw += kLuWords) {
             const uint32_t swe = Wc - sw < kLuWords ? Wc : sw + kLuWords;
@@ -1729,6 +1786,18 @@ __device__ __forceinline__ void unpack_long(USmem& sm, const uint8_t* __restrict
         }
         W += Wc;
         P += adv;
+#if UNPACK_PROF
+        __syncthreads();
+        LUPROF_T(lt5);
+        LUPROF_ADD(1, 1);
+#if UNPACK_PROF != 2
+        LUPROF_ADD(3, lt1 - lt0);
+        LUPROF_ADD(4, lt2 - lt1);
+#endif
+        LUPROF_ADD(5, lt3 - lt2);
+        LUPROF_ADD(6, lt4 - lt3);
+        LUPROF_ADD(7, lt5 - lt4);
+#endif
     }
     if (bad) {  // the exact serial walk, from the chunk start
         __syncthreads();
@@ -2320,6 +2389,88 @@ unpack_wt_finish(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
     }
 }
 
+// ---------------------------------------------------------------------------
+// One read_message call in one launch (the drop-in at the reference's call
+// granularity: serialize_packed::read_message / try_read_message /
+// read_message_no_alloc once per message, serialize_packed.rs:233-291,
+// benchmark.rs:207-259).  The input prefix sits in pinned host memory and the
+// kernel reads it there: the first kMsgPre bytes (more than any segment
+// table's read units take, <= 10 bytes x 257 words) come into LDS in one
+// round trip, lane 0 reads and checks the table from them (frame.h, the
+// frame kernel's code), and the workgroup decodes the body unit with the
+// long-unit decode (unpack_long) straight from the host bytes into the
+// caller's pinned words.  The frame result and the body's status and
+// consumed count are written to pinned memory too: the host waits once.
+constexpr uint32_t kMsgPre = 4096;
+static_assert(kMsgPre == 16 * kThreads, "one 16-byte load per thread");
+
+struct MsgReadSmem {
+    alignas(16) uint8_t pre[kMsgPre];
+    alignas(16) FrameResult fr;
+    uint64_t offs[4];  // the body unit: packed range, words
+    int32_t st;
+    uint64_t used;
+};
+
+__global__ void __launch_bounds__(kThreads, 4)
+msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_alloc,
+                uint32_t try_mode, uint64_t limit, uint32_t has_limit, uint64_t buffer_len,
+                uint64_t body_cap, FrameResult* __restrict__ fr_out, uint64_t* __restrict__ words,
+                uint64_t* __restrict__ res, uint32_t* __restrict__ flag, uint32_t seq) {
+    __shared__ USmem sm;
+    __shared__ MsgReadSmem M;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    const uint64_t npre = in_len < kMsgPre ? in_len : kMsgPre;
+    {
+        // (16-byte loads of whole vectors; the host buffer is 16-byte aligned
+        // and padded, so the last vector stays inside it)
+        const uint4* src = reinterpret_cast<const uint4*>(in);
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (16ull * tid < npre) v = src[tid];
+        reinterpret_cast<uint4*>(M.pre)[tid] = v;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        // (the table's read units end within kMsgPre bytes whenever the input
+        // is longer: the staged prefix gives the same results as the input)
+        capnp_frame::frame_table(M.pre, npre, no_alloc, try_mode, limit, has_limit, buffer_len,
+                                 body_cap, &M.fr);
+        if (M.fr.status == 0) M.fr.body_in_off[1] = in_len;  // (the unit runs to the input end)
+        M.offs[0] = M.fr.body_in_off[0];
+        M.offs[1] = M.fr.body_in_off[1];
+        M.offs[2] = 0;
+        M.offs[3] = M.fr.body_out_off[1];
+        M.st = 0;
+        M.used = 0;
+    }
+    __syncthreads();
+    if (M.fr.status == 0 && M.offs[3] > 0)  // (uniform: LDS after the barrier)
+        unpack_long(sm, in, M.offs, 0, words, M.offs + 2, &M.st, &M.used, tid, lane, wave);
+    __syncthreads();
+    // results out: the frame record (whole 16-byte vectors) and {status, 0, consumed}
+    {
+        constexpr uint32_t kV = (uint32_t)(sizeof(FrameResult) / 16);
+        const uint4* f4 = reinterpret_cast<const uint4*>(&M.fr);
+        uint4* o4 = reinterpret_cast<uint4*>(fr_out);
+        for (uint32_t i = tid; i < kV; i += kThreads) o4[i] = f4[i];
+        if (tid == 0) {
+            res[0] = (uint64_t)(uint32_t)M.st;
+            res[1] = 0;
+            res[2] = M.used;
+        }
+    }
+    if (flag) {  // (the host waits on this flag: everything above is visible first)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __threadfence_system();
+            __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 }  // namespace
 
 // Output words per unpack tile the staged path is sized for; the host picks
@@ -2425,3 +2576,17 @@ extern "C" hipError_t capnp_unpack_prof(unsigned long long* host8, int reset) {
     return e;
 }
 #endif
+
+// One read_message call in one launch (msg_read_kernel): `in` (in_len bytes,
+// 16-byte aligned, readable to the next multiple of 16) and the three outputs
+// may be pinned host memory.  res = {status of the body, 0, consumed bytes}.
+extern "C" hipError_t capnp_launch_msg_read(const uint8_t* in, uint64_t in_len, uint32_t no_alloc,
+                                            uint32_t try_mode, uint64_t limit, uint32_t has_limit,
+                                            uint64_t buffer_len, uint64_t body_cap,
+                                            FrameResult* fr_out, uint64_t* words, uint64_t* res,
+                                            uint32_t* flag, uint32_t seq, hipStream_t stream) {
+    hipLaunchKernelGGL(msg_read_kernel, dim3(1), dim3(kThreads), 0, stream, in, in_len, no_alloc,
+                       try_mode, limit, has_limit, buffer_len, body_cap, fr_out, words, res, flag,
+                       seq);
+    return hipGetLastError();
+}

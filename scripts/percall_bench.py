@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Per-call latency of the drop-in message calls (capnp_packed_write_message /
+capnp_packed_read_message, one message per call as the reference's
+`benchmark carsales bytes reuse packed` makes them, benchmark.rs:207-259):
+median and 10th percentile over many calls, write and read separately, for
+one-segment messages of config-2 words of several sizes.
+
+    python3 scripts/percall_bench.py [--reps N]
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "capnproto-rust_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=400)
+    a = ap.parse_args()
+    import torch  # noqa: F401
+    import oracle_lib as O
+    from capnp_amd import Context, _lib
+    L = _lib.lib()
+    ctx = Context(0)
+    h = ctx.handle
+    opts = _lib.ReaderOptionsC(0, 0, 64)
+    rows = []
+    for words in (128, 512, 1500, 2048, 8192, 32768):
+        offs = np.array([0, words], np.uint64)
+        seg = O.gen_fill(offs, kind0=0, pz=O.PZ30)
+        ptrs = (C.c_void_p * 1)(seg.ctypes.data)
+        lens = (C.c_uint32 * 1)(words)
+        cap = L.capnp_packed_batch_bound_bytes(words + 1, 3)
+        out = np.empty(cap, np.uint8)
+        body = np.empty(words, np.uint64)
+        segs = np.empty(512, np.uint32)
+        n, used, nseg = C.c_size_t(0), C.c_size_t(0), C.c_uint32(0)
+        tw, tr = [], []
+        for r in range(a.reps + 10):
+            t0 = time.perf_counter()
+            st = L.capnp_packed_write_message(h, ptrs, lens, 1, out.ctypes.data, cap, C.byref(n))
+            t1 = time.perf_counter()
+            st2 = L.capnp_packed_read_message(h, out.ctypes.data, n.value, C.byref(opts), 0,
+                                              body.ctypes.data, words, segs.ctypes.data,
+                                              C.byref(nseg), C.byref(used))
+            t2 = time.perf_counter()
+            assert st == 0 and st2 == 0 and used.value == n.value
+            if r >= 10:
+                tw.append(t1 - t0)
+                tr.append(t2 - t1)
+        assert np.array_equal(body, seg)
+        st, ref = O.write_message([seg])
+        assert bytes(out[:n.value]) == ref
+        tw, tr = np.array(tw) * 1e6, np.array(tr) * 1e6
+        r = {"words": words, "kib": words * 8 / 1024, "packed_bytes": n.value,
+             "write_us_median": round(float(np.median(tw)), 1),
+             "write_us_p10": round(float(np.percentile(tw, 10)), 1),
+             "read_us_median": round(float(np.median(tr)), 1),
+             "read_us_p10": round(float(np.percentile(tr, 10)), 1)}
+        rows.append(r)
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
