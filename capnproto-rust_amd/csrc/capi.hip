@@ -116,7 +116,7 @@ extern "C" hipError_t capnp_launch_msg_read(const uint8_t*, uint64_t, uint32_t, 
 extern "C" uint32_t capnp_msg_pack_words(void);
 extern "C" hipError_t capnp_launch_msg_pack(const uint64_t*, const uint64_t*, uint32_t, uint32_t,
                                             uint8_t*, uint64_t, uint64_t*, uint32_t*, uint32_t,
-                                            hipStream_t);
+                                            uint8_t*, hipStream_t);
 extern "C" hipError_t capnp_launch_frame(const uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t,
                                          uint32_t, uint64_t, uint64_t, FrameResult*, hipStream_t);
 
@@ -1575,6 +1575,7 @@ capnp_status capnp_packed_write_message(capnp_ctx* ctx, const uint64_t* const* s
         // one launch (msg_pack_kernel): chunks and offsets laid out in pinned
         // memory, the kernel writes the packed bytes and their total there
         capnp_status st = ensure_pin(ctx, o_out + bound + 64);
+        if (st == CAPNP_OK) st = ensure_stage(ctx, bound + 64);
         if (st != CAPNP_OK) return st;
         uint8_t* h = ctx->h_pin;
         uint8_t* dh = ctx->d_pin;
@@ -1589,7 +1590,7 @@ capnp_status capnp_packed_write_message(capnp_ctx* ctx, const uint64_t* const* s
                                       reinterpret_cast<uint64_t*>(dh + o_off), (uint32_t)nch,
                                       (uint32_t)nw, dh + o_out, bound,
                                       reinterpret_cast<uint64_t*>(dh + o_tot), ctx->d_flag,
-                                      ++ctx->call_seq, s));
+                                      ++ctx->call_seq, ctx->d_stage, s));
         st = wait_call(ctx, ctx->call_seq, s);
         if (st != CAPNP_OK) return st;
         const uint64_t total = *reinterpret_cast<volatile uint64_t*>(h + o_tot);

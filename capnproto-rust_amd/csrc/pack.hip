@@ -2397,8 +2397,7 @@ struct RangeExit {
     uint32_t homog;
 };
 __device__ __forceinline__ RangeExit range_exit(const uint64_t (&w)[kStageSteps],
-                                                const uint64_t (&sb)[kStageSteps], uint32_t nw,
-                                                uint32_t lane) {
+                                                uint32_t sbits, uint32_t nw, uint32_t lane) {
     uint32_t t[kStageSteps];
 #pragma unroll
     for (uint32_t s = 0; s < kStageSteps; s++) t[s] = tag_of(w[s]);
@@ -2414,7 +2413,7 @@ __device__ __forceinline__ RangeExit range_exit(const uint64_t (&w)[kStageSteps]
         // shuffle under it would run with lane 63 masked off and read 0)
         const uint32_t below = s ? (uint32_t)__builtin_amdgcn_readlane((int)t[s > 0 ? s - 1 : 0], 63) : 0u;
         const uint32_t pt = lane ? up : below;
-        const bool sure = v && (((sb[s] >> lane) & 1) || ((lane || s) && sure_head(t[s], pt)));
+        const bool sure = v && (((sbits >> s) & 1u) || ((lane || s) && sure_head(t[s], pt)));
         if (ks < 0) {
             const uint64_t G = ballot64(sure);
             const uint32_t j = G ? 63u - (uint32_t)__builtin_clzll(G) : 0u;
@@ -2467,9 +2466,8 @@ __device__ __forceinline__ Carry wt_compose(Carry c, uint32_t T, uint32_t n) {
 // before a chunk start, capped by the run's room.  *beyond = true when the
 // whole range is such words and the run has room past it (the caller asks
 // run_ext_b).
-__device__ __forceinline__ uint32_t range_ext(const uint64_t (&w)[kStageSteps],
-                                              const uint64_t (&sb)[kStageSteps], uint32_t nw,
-                                              Carry c, uint32_t lane, bool& beyond) {
+__device__ __forceinline__ uint32_t range_ext(const uint64_t (&w)[kStageSteps], uint32_t sbits,
+                                              uint32_t nw, Carry c, uint32_t lane, bool& beyond) {
     beyond = false;
     if (c.type == 0 || c.rem == 0) return 0;
     uint32_t lead = 0;
@@ -2479,7 +2477,7 @@ __device__ __forceinline__ uint32_t range_ext(const uint64_t (&w)[kStageSteps],
         const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
         const uint32_t tag = tag_of(w[s]);
         const bool cls = c.type == 1 ? tag == 0 : __builtin_popcount(tag) >= 7;
-        const uint32_t cut = ctz64(sb[s]);
+        const uint32_t cut = ctz64(ballot64(((sbits >> s) & 1u) != 0));
         const uint32_t lim = cut < nv ? cut : nv;
         const uint32_t l = ctz64(~ballot64(lane < lim && cls));
         if (open) {
@@ -2576,17 +2574,26 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         const uint64_t bits = rr ? (lo >> rr) | (hi << (64 - rr)) : lo;
         smk[s] = nv ? bits & low_mask(nv) : 0ull;
     }
+    // (per-lane bits from here on: bit s = this lane's word of step s starts
+    // a chunk; each use rebuilds the step's mask with one compare, so no
+    // 64-bit mask stays live in SGPRs across the kernel -- with the eight
+    // masks and the eight steps' head masks live, it spilled 162 SGPRs to
+    // VGPR lanes, a v_writelane / v_readlane pair per use)
+    uint32_t sbits = 0;
+#pragma unroll
+    for (uint32_t s = 0; s < kStageSteps; s++) sbits |= mask_sel(smk[s], 1u << s, 0u);
     // the run state entering the next range (R1), from this range's own
     // words (range_exit): wcarry = type | rem << 2 | homog << 10
     if (succ) {
         uint32_t rec = 0;
         if (((readlane64(cbv, kStageSteps) >> rr) & 1) == 0) {  // R1 inside a chunk
-            const RangeExit ex = range_exit(cache, smk, nw, lane);
+            const RangeExit ex = range_exit(cache, sbits, nw, lane);
             Carry c = ex.c;
             uint32_t hg = ex.homog;
             if (hg == 3) {  // no sure head, pop-7/8 words: search before R0 (rare)
                 c = carry_in_b<64>(in, cbits, b64, wlo, R1, lane, cache[kStageSteps - 1],
-                                   readlane64(cache[kStageSteps - 2], 63), smk[kStageSteps - 1]);
+                                   readlane64(cache[kStageSteps - 2], 63),
+                                   ballot64(((sbits >> (kStageSteps - 1)) & 1u) != 0));
                 hg = 0;
             }
             rec = c.type | (c.rem << 2) | (hg << 10);
@@ -2615,7 +2622,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         const uint64_t wq = in[R0 - 64 + lane];
         const uint64_t wpq = in[R0 - 65];
         const uint64_t bq = start_bits(cbits, b64, R0 - 64);
-        const bool cs0 = (smk[0] & 1) != 0;
+        const bool cs0 = (ballot64((sbits & 1u) != 0) & 1ull) != 0;
         const Carry oc = cs0 ? Carry{0, 0} : carry_in_b<64>(in, cbits, b64, wlo, R0, lane, wq, wpq, bq);
         if ((oc.type != cin.type || oc.rem != cin.rem) && lane == 0) {
             static __device__ unsigned int nprint;
@@ -2633,7 +2640,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         // the words from R0 on that the run open at R0 absorbs: the previous
         // range's last record (its pass 2 needs them)
         bool beyond = false;
-        uint32_t ext = range_ext(cache, smk, nw, cin, lane, beyond);
+        uint32_t ext = range_ext(cache, sbits, nw, cin, lane, beyond);
         if (beyond)  // (the run reaches past this range: only a short last range)
             ext = run_ext_b(in, cbits, b64, whi, R0, cin, lane, cache[0],
                             rr ? (readlane64(cbv, 0) >> rr) | (readlane64(cbv, 1) << (64 - rr))
@@ -2646,14 +2653,18 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     pk.begin(0);
     pk.carry = cin;
     uint32_t lastcs = ~0u;
+    uint32_t hbits = 0;  // bit s = this lane heads a record in step s
+    uint32_t metav = 0;  // lane s = step s's meta (nvalid | absorbed << 16)
 #pragma unroll
     for (uint32_t s = 0; s < kStageSteps; s++) {
         const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
-        size_step_s(pk, cache[s], nv, smk[s], lane, si[s]);
-        if ((smk[s] >> lane) & 1) wm.wpos[wave][64u * s + lane] = (uint16_t)si[s].pos;
-        if (smk[s])
-            lastcs = (uint32_t)__builtin_amdgcn_readlane((int)si[s].pos,
-                                                         63 - __builtin_clzll(smk[s]));
+        const uint64_t Sm = ballot64(((sbits >> s) & 1u) != 0);
+        size_step_s(pk, cache[s], nv, Sm, lane, si[s]);
+        hbits |= mask_sel(si[s].H, 1u << s, 0u);
+        metav = lane == s ? si[s].meta : metav;
+        if ((sbits >> s) & 1u) wm.wpos[wave][64u * s + lane] = (uint16_t)si[s].pos;
+        if (Sm)
+            lastcs = (uint32_t)__builtin_amdgcn_readlane((int)si[s].pos, 63 - __builtin_clzll(Sm));
     }
     if (lane == 0) {
         sm.wave_bytes[wave] = pk.total;
@@ -2678,8 +2689,11 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
 #pragma unroll
         for (int s = (int)kStageSteps - 1; s >= 0; s--) {
             const uint32_t e = ext;
-            emit_step<false>(cache[s], si[s], e, lane, region_m1, sm.sel, nullptr, 0, 0, 0);
-            ext = (si[s].meta >> 16) + (si[s].H == 0 ? e : 0u);
+            StepInfo sj = si[s];
+            sj.H = ballot64(((hbits >> s) & 1u) != 0);
+            sj.meta = (uint32_t)__builtin_amdgcn_readlane((int)metav, s);
+            emit_step<false>(cache[s], sj, e, lane, region_m1, sm.sel, nullptr, 0, 0, 0);
+            ext = (sj.meta >> 16) + (sj.H == 0 ? e : 0u);
         }
     }
     if (SYNC) {
@@ -2701,9 +2715,10 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         uint64_t hw = R0 - (255u - cin.rem) - 1u;
 #pragma unroll
         for (uint32_t s = 0; s < kStageSteps; s++) {
-            const uint32_t nv = si[s].meta & 127u;
+            const uint32_t nv = (uint32_t)__builtin_amdgcn_readlane((int)metav, s) & 127u;
             const uint64_t base = R0 + 64u * s;
-            const uint64_t H = si[s].H, Sm = smk[s];
+            const uint64_t H = ballot64(((hbits >> s) & 1u) != 0);
+            const uint64_t Sm = ballot64(((sbits >> s) & 1u) != 0);
             const uint32_t tpos = woff + si[s].pos;
             const uint64_t below = low_mask(lane + 1);
             const uint64_t sb = Sm & below, hb = H & below;
@@ -2896,7 +2911,8 @@ struct MsgPackSmem {
 __global__ void __launch_bounds__(kThreads)
 msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__ off,
                 uint32_t nchunks, uint32_t nwords, uint8_t* __restrict__ out, uint64_t out_cap,
-                uint64_t* __restrict__ total, uint32_t* __restrict__ flag, uint32_t seq) {
+                uint64_t* __restrict__ total, uint32_t* __restrict__ flag, uint32_t seq,
+                uint8_t* __restrict__ scratch) {
     __shared__ MsgPackSmem S;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -2946,14 +2962,28 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
         if (tid == 0) S.wsum[0] = all;  // (the chunks before the last)
     }
     __syncthreads();
-    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
+    // (pass B's flushes go to device memory -- a step's bytes in 16-byte
+    // stores that a PCIe write path would take one at a time -- and the
+    // packed bytes cross to the host output in one coalesced copy)
+    uint8_t* const dst = scratch ? scratch : out;
+    const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
     uint64_t* last = reinterpret_cast<uint64_t*>(S.chunk_size + nchunks - 1);
     run_streaming<MODE_RING>(S.words, S.off, S.chunk_size, S.chunk_pos, nchunks, wave, lane, ring,
-                             S.sel, out - mis, mis, out_cap, nullptr, last);
+                             S.sel, dst - mis, mis, out_cap, nullptr, last);
+    __syncthreads();
+    const uint64_t tot = S.chunk_pos[nchunks - 1] + S.chunk_size[nchunks - 1];
+    if (scratch) {
+        // (scratch and out both 16-byte aligned: whole vectors, the last one
+        // padded -- out has the bound's room)
+        const uint64_t nv = ((tot < out_cap ? tot : out_cap) + 15) / 16;
+        const uint4* s4 = reinterpret_cast<const uint4*>(scratch);
+        uint4* o4 = reinterpret_cast<uint4*>(out);
+        for (uint64_t i = tid; i < nv; i += kThreads) o4[i] = s4[i];
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's stores have landed)
     __syncthreads();
     if (tid == 0) {
-        total[0] = S.chunk_pos[nchunks - 1] + S.chunk_size[nchunks - 1];
+        total[0] = tot;
         if (flag) {  // (the host waits on this flag: everything above is visible first)
             __threadfence_system();
             __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3144,10 +3174,10 @@ extern "C" uint32_t capnp_msg_pack_words(void) { return kMsgWords; }
 extern "C" hipError_t capnp_launch_msg_pack(const uint64_t* words, const uint64_t* off,
                                             uint32_t nchunks, uint32_t nwords, uint8_t* out,
                                             uint64_t out_cap, uint64_t* total, uint32_t* flag,
-                                            uint32_t seq, hipStream_t stream) {
+                                            uint32_t seq, uint8_t* scratch, hipStream_t stream) {
     if (nwords > kMsgWords || nchunks + 1 > kMsgChunks || nchunks == 0)
         return hipErrorInvalidValue;
     hipLaunchKernelGGL(msg_pack_kernel, dim3(1), dim3(kThreads), 0, stream, words, off, nchunks,
-                       nwords, out, out_cap, total, flag, seq);
+                       nwords, out, out_cap, total, flag, seq, scratch);
     return hipGetLastError();
 }

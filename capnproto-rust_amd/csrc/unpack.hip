@@ -571,7 +571,7 @@ constexpr uint32_t kLuWinBytes = kLuSeg * kThreads;     // 16 KiB of record star
 constexpr uint32_t kLuLead = 64;                         // spec lead-in (tests/emu_long.py: 64 > 48)
 constexpr uint32_t kLuAvail = kLuWinBytes + 2080;        // bytes staged past the window start
 constexpr uint32_t kLuStage = kLuAvail + 32;             // (+ misalignment and a hop's read-ahead)
-constexpr uint32_t kLuWords = 4096;                      // descriptor window (output words)
+constexpr uint32_t kLuWords = 8192;                      // descriptor window (output words)
 constexpr uint32_t kLuMaxRounds = 64;                    // then the exact serial walk
 static_assert(kLuStage + 16 < 0x8000, "LDS positions fit the descriptors' 15 bits");
 struct LongSmem {
@@ -1537,7 +1537,9 @@ __device__ __forceinline__ void unpack_long(USmem& sm, const uint8_t* __restrict
                             const uint64_t* __restrict__ in_off, uint64_t c,
                             uint64_t* __restrict__ out, const uint64_t* __restrict__ out_off,
                             int32_t* __restrict__ status, uint64_t* __restrict__ consumed,
-                            uint32_t tid, uint32_t lane, uint32_t wave) {
+                            uint32_t tid, uint32_t lane, uint32_t wave, uint32_t pre = 0) {
+    // pre: the caller staged in[0, pre) at S.bytes[0, pre) (zeros after it,
+    // to kLuStage): a first window inside those bytes is not loaded again
     LongSmem& S = sm.lu;
     const uint64_t P0 = uniform64(in_off[c]);
     const uint64_t E = uniform64(in_off[c + 1]) - P0;  // the chunk's packed bytes
@@ -1553,12 +1555,14 @@ __device__ __forceinline__ void unpack_long(USmem& sm, const uint8_t* __restrict
         const uint32_t L = rem < kLuAvail ? (uint32_t)rem : kLuAvail;  // bytes staged
         const uint32_t Lc = L < kLuWinBytes ? L : kLuWinBytes;        // record starts cut
         // ---- stage [P, P + L) (16-byte loads from the aligned base below P)
-        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(u + P) & 15u);
+        const bool staged = W == 0 && P0 + L <= pre;  // (uniform; zeros follow `pre`)
+        const uint32_t mis = staged ? (uint32_t)P0
+                                    : (uint32_t)(reinterpret_cast<uintptr_t>(u + P) & 15u);
         const uint4* src = reinterpret_cast<const uint4*>(u + P - mis);
         const uint32_t nblk = (mis + L + 15) / 16;
         __syncthreads();  // (the previous window is done with the LDS)
         LUPROF_T(lt0);
-        {
+        if (!staged) {
             // LDS DMA, 16 bytes a lane, every load in flight at once (no
             // registers held); the vectors past the chunk's bytes are zeroed
             constexpr uint32_t kVec = kLuStage / 16;
@@ -1781,8 +1785,14 @@ __device__ __forceinline__ void unpack_long(USmem& sm, const uint8_t* __restrict
             }
             __syncthreads();
             uint64_t* o = out + obase + W + sw;
-            for (uint32_t i = tid; i < swe - sw; i += kThreads)
-                o[i] = expand_desc(S.bytes, S.sel, S.dpos[i]);
+            // (a zero-run word needs no LDS read past its descriptor: zero-run
+            // windows -- config 4's index-free block decode -- expand at the
+            // stores' rate)
+#pragma unroll 4
+            for (uint32_t i = tid; i < swe - sw; i += kThreads) {
+                const uint32_t d = S.dpos[i];
+                o[i] = d == kNone ? 0ull : expand_desc(S.bytes, S.sel, d);
+            }
         }
         W += Wc;
         P += adv;
@@ -2405,14 +2415,13 @@ constexpr uint32_t kMsgPre = 4096;
 static_assert(kMsgPre == 16 * kThreads, "one 16-byte load per thread");
 
 struct MsgReadSmem {
-    alignas(16) uint8_t pre[kMsgPre];
     alignas(16) FrameResult fr;
     uint64_t offs[4];  // the body unit: packed range, words
     int32_t st;
     uint64_t used;
 };
 
-__global__ void __launch_bounds__(kThreads, 4)
+__global__ void __launch_bounds__(kThreads)  // (one workgroup: registers are free)
 msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_alloc,
                 uint32_t try_mode, uint64_t limit, uint32_t has_limit, uint64_t buffer_len,
                 uint64_t body_cap, FrameResult* __restrict__ fr_out, uint64_t* __restrict__ words,
@@ -2423,20 +2432,25 @@ msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_all
     const uint32_t lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
     const uint64_t npre = in_len < kMsgPre ? in_len : kMsgPre;
+    // The input's first kLuStage - 16 bytes come into the long-unit decode's
+    // staging buffer in one round trip (16-byte loads of whole vectors: the
+    // host buffer is 16-byte aligned and padded; zeros past the input): the
+    // table is read from there, and a body inside them is decoded without
+    // loading its window again.
+    constexpr uint32_t kPreVec = kLuStage / 16 - 1;
+    const uint32_t pre = (uint32_t)(in_len < 16ull * kPreVec ? in_len : 16ull * kPreVec);
     {
-        // (16-byte loads of whole vectors; the host buffer is 16-byte aligned
-        // and padded, so the last vector stays inside it)
         const uint4* src = reinterpret_cast<const uint4*>(in);
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (16ull * tid < npre) v = src[tid];
-        reinterpret_cast<uint4*>(M.pre)[tid] = v;
+        uint4* dst = reinterpret_cast<uint4*>(sm.lu.bytes);
+        for (uint32_t i = tid; i < kLuStage / 16; i += kThreads)
+            dst[i] = 16u * i < pre ? src[i] : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
     if (tid == 0) {
         // (the table's read units end within kMsgPre bytes whenever the input
         // is longer: the staged prefix gives the same results as the input)
-        capnp_frame::frame_table(M.pre, npre, no_alloc, try_mode, limit, has_limit, buffer_len,
-                                 body_cap, &M.fr);
+        capnp_frame::frame_table(sm.lu.bytes, npre, no_alloc, try_mode, limit, has_limit,
+                                 buffer_len, body_cap, &M.fr);
         if (M.fr.status == 0) M.fr.body_in_off[1] = in_len;  // (the unit runs to the input end)
         M.offs[0] = M.fr.body_in_off[0];
         M.offs[1] = M.fr.body_in_off[1];
@@ -2447,7 +2461,7 @@ msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_all
     }
     __syncthreads();
     if (M.fr.status == 0 && M.offs[3] > 0)  // (uniform: LDS after the barrier)
-        unpack_long(sm, in, M.offs, 0, words, M.offs + 2, &M.st, &M.used, tid, lane, wave);
+        unpack_long(sm, in, M.offs, 0, words, M.offs + 2, &M.st, &M.used, tid, lane, wave, pre);
     __syncthreads();
     // results out: the frame record (whole 16-byte vectors) and {status, 0, consumed}
     {

@@ -1,0 +1,131 @@
+"""GPU parity of the long-unit decode (csrc/unpack.hip unpack_long: a chunk
+too large for the tile tables, decoded by the whole workgroup in 16 KiB
+windows; msg_read_kernel decodes read_message bodies with it) against the
+oracle's read_exact (serialize_packed.rs:80-228, io.rs:16-31).
+
+Pins the round-4 r04g2 failure's boundary: a read_message body on the global
+path came back all zero (tests/test_gpu_async.py::test_bufread_refill_messages
+at a 64 KiB BufReader), in a build whose window refill of the serial walk
+(unpack_global1) bounded its 16-byte vector loads by the chunk end without
+the start's misalignment -- so with a body starting mis bytes past a 16-byte
+boundary, the vectors holding its last mis bytes were zero-filled and read as
+zero-run records.  Here: long units starting at every misalignment 0..15,
+ending at every offset of a vector, with spare bytes after (a stream's next
+message), through the batch path and through read_message; malformed units
+at the same starts take the exact serial walk (the fallback) and must give
+the oracle's status and consumed count."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from capnp_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _unit(words, kind, seed):
+    offs = np.array([0, words], np.uint64)
+    w = O.gen_fill(offs, kinds=np.array([kind], np.uint8), pz=O.PZ30, id0=seed)
+    st, p = O.pack(w.tobytes())
+    assert st == 0
+    return w, np.frombuffer(p, np.uint8)
+
+
+def _decode(ctx, buf, a, b, n):
+    """One chunk [a, b) of buf, n words, chunks_per_tile=1 (the overflow path)."""
+    dev = torch.device("cuda", 0)
+    packed = torch.from_numpy(buf.copy()).to(dev)
+    inoff = torch.tensor([a, b], dtype=torch.int64, device=dev)
+    outoff = torch.tensor([0, n], dtype=torch.int64, device=dev)
+    words = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)
+    st = torch.full((1,), -1, dtype=torch.int32, device=dev)
+    used = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctx.unpack_batch_into(packed, inoff, outoff, words, st, used, chunks_per_tile=1)
+    torch.cuda.synchronize()
+    return (words.cpu().numpy().view(np.uint64)[:n], int(st.cpu()[0]), int(used.cpu()[0]))
+
+
+@pytest.mark.parametrize("kind", [0, 2])
+def test_long_unit_every_misalignment(ctx, kind):
+    w, p = _unit(3000 if kind == 0 else 2600, kind, 40 + kind)
+    n = len(w)
+    spare = _unit(64, 0, 99)[1]
+    for mis in range(16):
+        buf = np.concatenate([np.full(mis, 0xA5, np.uint8), p, spare, np.zeros(32, np.uint8)])
+        a, b = mis, mis + len(p) + len(spare)  # (spare bytes: the decode stops after n words)
+        got, st, used = _decode(ctx, buf, a, b, n)
+        rst, rb, rused = O.read_exact(bytes(buf[a:b]), n * 8)
+        assert st == rst == 0 and used == rused == len(p), mis
+        assert np.array_equal(got, w), mis
+
+
+def test_long_unit_every_end_offset(ctx):
+    # units whose packed end falls on each offset of a 16-byte vector, no spare
+    for k in range(16):
+        w, p = _unit(2100 + 7 * k, 0, 60 + k)
+        for mis in (0, 5, 15):
+            buf = np.concatenate([np.zeros(mis, np.uint8), p, np.zeros(32, np.uint8)])
+            got, st, used = _decode(ctx, buf, mis, mis + len(p), len(w))
+            assert st == 0 and used == len(p), (k, mis)
+            assert np.array_equal(got, w), (k, mis)
+
+
+def test_long_unit_malformed_serial_fallback(ctx):
+    # truncated (PrematureEnd / FailedToFill), a run past the words
+    # (DidNotEndCleanly) and too few bytes: the exact serial walk's statuses
+    w, p = _unit(3000, 0, 77)
+    wl, pl = _unit(2600, 2, 78)
+    cases = [(p[:len(p) - 1], len(w)), (p[:len(p) // 2], len(w)), (p, len(w) - 1),
+             (pl[:len(pl) - 100], len(wl)), (pl, len(wl) - 3), (p, len(w) + 5)]
+    for mis in (0, 3, 11):
+        for data, n in cases:
+            buf = np.concatenate([np.zeros(mis, np.uint8), data, np.zeros(32, np.uint8)])
+            got, st, used = _decode(ctx, buf, mis, mis + len(data), n)
+            rst, rb, rused = O.read_exact(bytes(data), n * 8)
+            assert (st, used) == (rst, rused), (mis, len(data), n)
+
+
+def test_read_message_long_bodies_misaligned(ctx):
+    """read_message (one launch: msg_read_kernel) of messages whose body is
+    on the long-unit path, tables of 1..6 segments (so the body starts at
+    several misalignments), the next message's bytes after it."""
+    from capnp_amd import _lib
+    L = _lib.lib()
+    opts = _lib.ReaderOptionsC(0, 0, 64)
+    rng = np.random.default_rng(5)
+    for nseg in range(1, 7):
+        segs = []
+        for i in range(nseg):
+            k = int(rng.integers(1, 2600))
+            offs = np.array([0, k], np.uint64)
+            segs.append(O.gen_fill(offs, kinds=np.array([i % 3], np.uint8), pz=O.PZ30,
+                                   id0=300 + 10 * nseg + i))
+        st, msg = O.write_message(segs)
+        st2, nxt = O.write_message([segs[0][:5]])
+        data = np.frombuffer(msg + nxt, np.uint8).copy()
+        total = sum(len(s) for s in segs)
+        body = np.zeros(total + 1, np.uint64)
+        sw = np.zeros(512, np.uint32)
+        ns, used = C.c_uint32(0), C.c_size_t(0)
+        r = L.capnp_packed_read_message(ctx.handle, data.ctypes.data, len(data), C.byref(opts),
+                                        0, body.ctypes.data, total + 1, sw.ctypes.data,
+                                        C.byref(ns), C.byref(used))
+        rst, rsegs, rused = O.read_message(bytes(data))
+        assert r == rst == 0 and used.value == rused == len(msg), nseg
+        assert ns.value == nseg
+        o = 0
+        for s in segs:
+            assert np.array_equal(body[o:o + len(s)], s), nseg
+            o += len(s)
