@@ -1966,8 +1966,14 @@ unpack_ovf_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
 // workgroups left a few hundred of them serialising the overflow tiles
 // (config 4 index-free: 4.3 ms in the overflow kernel; one workgroup per
 // tile instead cost config 2 0.13 ms of empty workgroups).
-constexpr uint32_t kOvfWindow = 16;  // (64: config 4 index-free overflow 1.86 ms on 1155 workgroups)
-constexpr uint64_t kOvfGrid = 4096;  // (config 2's 65536 tiles: 16 per workgroup, as in round 4)
+#ifndef OVF_WINDOW
+#define OVF_WINDOW 16
+#endif
+#ifndef OVF_GRID
+#define OVF_GRID 4096
+#endif
+constexpr uint32_t kOvfWindow = OVF_WINDOW;  // (64: config 4 index-free overflow 1.86 ms on 1155 workgroups)
+constexpr uint64_t kOvfGrid = OVF_GRID;  // (config 2's 65536 tiles: 16 per workgroup, as in round 4)
 static_assert(kOvfWindow <= CAPNP_WAVE, "one lane per tile of the window");
 
 template <bool SYNC>

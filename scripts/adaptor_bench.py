@@ -125,7 +125,7 @@ def main():
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as O
         wn = np.frombuffer(raw, np.uint64)
-        sample = wn[:min(len(wn), 32 << 17)]  # (256 MiB: a bounded CPU sample)
+        sample = wn[:min(len(wn), 32 << 20)]  # (256 MiB: a bounded CPU sample)
         for threads in (1, 16):
             offs = np.arange(0, len(sample) + 1, call // 8, dtype=np.uint64)
             if offs[-1] != len(sample):

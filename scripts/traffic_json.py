@@ -45,7 +45,7 @@ def role(t):
         return "pack_nosync"  # (bench.py times the index-free pack too)
     if bare in PACK:
         return "pack"
-    if bare in ("unpack_fit_kernel", "unpack_ovf_kernel") and t.endswith("<false>"):
+    if bare in ("unpack_fit_kernel", "unpack_ovf_kernel", "unpack_ovf_win_kernel") and t.endswith("<false>"):
         return "unpack_nosync"
     if bare in UNPACK_SYNC or t in UNPACK_SYNC:
         return "unpack"
