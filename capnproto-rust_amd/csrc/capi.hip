@@ -166,8 +166,8 @@ struct capnp_ctx {
     const int32_t* resync_failed = nullptr;     // its device "a chunk failed" flag (read on demand)
     hipStream_t resync_stream = nullptr;
     hipEvent_t ev_resync = nullptr;  // orders a resync decode after the previous one
-    uint32_t* d_bad = nullptr;  // offset validation flag (check_offsets)
-    uint32_t* h_bad = nullptr;  // pinned copy
+    uint32_t* d_bad = nullptr;  // offset validation: flag, then each array's ends (check_offsets)
+    uint32_t* h_bad = nullptr;  // pinned copy (kCheckBytes)
     uint8_t* h_pin = nullptr;   // pinned staging of the small host calls (kPinnedCall)
     uint8_t* d_pin = nullptr;   // ... its device address (the one-launch calls read and write it)
     size_t pin_cap = 0;
@@ -193,15 +193,27 @@ namespace {
 // length), so these calls return CAPNP_E_INVALID_ARGUMENT before any kernel
 // touches the data.  (The reference takes slices, which cannot be backwards:
 // serialize.rs:53-97, serialize_packed.rs:300-304.)
+// ends = {off[0], off[n]}: the array's range, copied back with the verdict
+// (the callers that size their launches from it read no more).
 __global__ void __launch_bounds__(256) k_check_offsets(const uint64_t* __restrict__ off,
                                                        uint64_t n, uint64_t limit,
-                                                       uint32_t* __restrict__ bad) {
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * blockDim.x) {
+                                                       uint32_t* __restrict__ bad,
+                                                       uint64_t* __restrict__ ends) {
+    const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i0 == 0) {
+        ends[0] = off[0];
+        ends[1] = off[n];
+    }
+    for (uint64_t i = i0; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t a = off[i], b = off[i + 1];
         if (b < a || b > limit) atomicOr(bad, 1u);  // (vector atomic, rare)
     }
 }
+
+// check_offsets' device record: the flag (8 bytes with its pad), then
+// {first, last} of up to kCheckArrays arrays.
+constexpr size_t kCheckArrays = 3;
+constexpr size_t kCheckBytes = 8 + 16 * kCheckArrays;
 
 }  // namespace
 
@@ -341,17 +353,25 @@ capnp_status offsets_verdict(capnp_ctx* ctx) {
     }
     return CAPNP_OK;
 }
+// After the wait: array k's {off[0], off[n]} (arrays with n > 0 only).
+const uint64_t* checked_ends(const capnp_ctx* ctx, size_t k) {
+    return reinterpret_cast<const uint64_t*>(ctx->h_bad + 2) + 2 * k;
+}
 capnp_status check_offsets(capnp_ctx* ctx, hipStream_t s, std::initializer_list<OffCheck> arrays,
                            bool wait = true) {
+    if (arrays.size() > kCheckArrays) return CAPNP_E_INVALID_ARGUMENT;
     HIP_TRY(hipMemsetAsync(ctx->d_bad, 0, 4, s));
+    size_t k = 0;
     for (const OffCheck& a : arrays) {
+        uint64_t* ends = reinterpret_cast<uint64_t*>(ctx->d_bad + 2) + 2 * k++;
         if (a.n == 0 || !a.off) continue;
         const uint64_t blocks = std::min<uint64_t>((a.n + 255) / 256, 2048);
         hipLaunchKernelGGL(k_check_offsets, dim3((uint32_t)blocks), dim3(256), 0, s, a.off,
-                           (uint64_t)a.n, a.limit, ctx->d_bad);
+                           (uint64_t)a.n, a.limit, ctx->d_bad, ends);
         HIP_TRY(hipGetLastError());
     }
-    HIP_TRY(hipMemcpyAsync(ctx->h_bad, ctx->d_bad, 4, hipMemcpyDeviceToHost, s));
+    // the verdict and the ranges in one copy (pinned: no staging)
+    HIP_TRY(hipMemcpyAsync(ctx->h_bad, ctx->d_bad, 8 + 16 * k, hipMemcpyDeviceToHost, s));
     if (!wait) return CAPNP_OK;
     HIP_TRY(hipStreamSynchronize(s));
     return offsets_verdict(ctx);
@@ -405,13 +425,10 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
             wr[0] = host_wr[0];
             wr[1] = host_wr[1];
         } else {
-            capnp_status vst = check_offsets(ctx, s, {{d_off, n, ~0ull}}, false);
+            capnp_status vst = check_offsets(ctx, s, {{d_off, n, ~0ull}});
             if (vst != CAPNP_OK) return vst;
-            HIP_TRY(hipMemcpyAsync(&wr[0], d_off, 8, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipMemcpyAsync(&wr[1], d_off + n, 8, hipMemcpyDeviceToHost, s));
-            HIP_TRY(hipStreamSynchronize(s));
-            vst = offsets_verdict(ctx);
-            if (vst != CAPNP_OK) return vst;
+            wr[0] = checked_ends(ctx, 0)[0];
+            wr[1] = checked_ends(ctx, 0)[1];
         }
         if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
         const uint64_t words = wr[1] - wr[0];
@@ -606,8 +623,8 @@ capnp_ctx* capnp_ctx_create(int device, capnp_status* status) {
         e = hipHostGetDevicePointer(&dp, ctx->h_flag, 0);
         ctx->d_flag = static_cast<uint32_t*>(dp);
     }
-    if (e == hipSuccess) e = hipMalloc(&ctx->d_bad, 4);
-    if (e == hipSuccess) e = hipHostMalloc(&ctx->h_bad, 4, 0);
+    if (e == hipSuccess) e = hipMalloc(&ctx->d_bad, kCheckBytes);
+    if (e == hipSuccess) e = hipHostMalloc(&ctx->h_bad, kCheckBytes, 0);
     if (e != hipSuccess) {
         if (status) *status = CAPNP_E_HIP;
         capnp_ctx_destroy(ctx);
@@ -693,7 +710,8 @@ capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
 static capnp_status unpack_resync_dev(capnp_ctx* ctx, const uint8_t* d_packed,
                                       const uint64_t* d_in_byte_off, size_t nchunks,
                                       uint64_t* d_words, const uint64_t* d_out_word_off,
-                                      int32_t* d_status, uint64_t* d_consumed, hipStream_t s);
+                                      int32_t* d_status, uint64_t* d_consumed, hipStream_t s,
+                                      const uint64_t* checked_byte_ends = nullptr);
 
 static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
                                      const uint64_t* d_in_byte_off, size_t nchunks,
@@ -705,21 +723,21 @@ static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
     if (tc > 256) return CAPNP_E_INVALID_ARGUMENT;
     if (tc == 0 && nchunks) {
         hipStream_t s = pick(ctx, stream);
-        uint64_t wr[2];
+        uint64_t wr[2], br[2];
         capnp_status vst = check_offsets(
-            ctx, s, {{d_in_byte_off, nchunks, ~0ull}, {d_out_word_off, nchunks, ~0ull}}, false);
+            ctx, s, {{d_in_byte_off, nchunks, ~0ull}, {d_out_word_off, nchunks, ~0ull}});
         if (vst != CAPNP_OK) return vst;
-        HIP_TRY(hipMemcpyAsync(&wr[0], d_out_word_off, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipMemcpyAsync(&wr[1], d_out_word_off + nchunks, 8, hipMemcpyDeviceToHost, s));
-        HIP_TRY(hipStreamSynchronize(s));
-        vst = offsets_verdict(ctx);
-        if (vst != CAPNP_OK) return vst;
+        br[0] = checked_ends(ctx, 0)[0];
+        br[1] = checked_ends(ctx, 0)[1];
+        wr[0] = checked_ends(ctx, 1)[0];
+        wr[1] = checked_ends(ctx, 1)[1];
         if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
         const uint64_t words = wr[1] - wr[0];
         const bool longc = words && (words / nchunks >= kWordTileMean || force_word_tiles());
-        if (longc && !d_sync)  // no index: the speculative block walk (resync.hip)
+        if (longc && !d_sync)  // no index: the speculative block walk (resync.hip); both
+                               // offset arrays were checked just above
             return unpack_resync_dev(ctx, d_packed, d_in_byte_off, nchunks, d_words,
-                                     d_out_word_off, d_status, d_consumed, s);
+                                     d_out_word_off, d_status, d_consumed, s, br);
         if (longc) {
             const size_t ws = capnp_unpack_wt_ws_bytes(wr[0], wr[1]);
             capnp_status st = ensure_buf(ctx, &ctx->d_wt, &ctx->wt_cap, ws);
@@ -810,10 +828,14 @@ capnp_status capnp_gpu_unpack_batch_resync(capnp_ctx* ctx, const uint8_t* d_pack
                              d_status, d_consumed, pick(ctx, stream));
 }
 
+// checked_byte_ends: the caller has just checked both offset arrays (and read
+// d_in_byte_off's first and last entries, given here); otherwise this call
+// checks them.
 static capnp_status unpack_resync_dev(capnp_ctx* ctx, const uint8_t* d_packed,
                                       const uint64_t* d_in_byte_off, size_t nchunks,
                                       uint64_t* d_words, const uint64_t* d_out_word_off,
-                                      int32_t* d_status, uint64_t* d_consumed, hipStream_t s) {
+                                      int32_t* d_status, uint64_t* d_consumed, hipStream_t s,
+                                      const uint64_t* checked_byte_ends) {
     // The previous index-free decode returned with its kernels still queued on
     // its own stream, and they read and write the workspace this call is about
     // to reset: a call on another stream waits for them first (an event, no
@@ -828,14 +850,16 @@ static capnp_status unpack_resync_dev(capnp_ctx* ctx, const uint8_t* d_packed,
     ctx->resync_passes = ctx->resync_serial = 0;
     if (nchunks == 0) return CAPNP_OK;
     uint64_t ends[2];
-    capnp_status vst = check_offsets(
-        ctx, s, {{d_in_byte_off, nchunks, ~0ull}, {d_out_word_off, nchunks, ~0ull}}, false);
-    if (vst != CAPNP_OK) return vst;
-    HIP_TRY(hipMemcpyAsync(&ends[0], d_in_byte_off, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(&ends[1], d_in_byte_off + nchunks, 8, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    vst = offsets_verdict(ctx);
-    if (vst != CAPNP_OK) return vst;
+    if (checked_byte_ends) {
+        ends[0] = checked_byte_ends[0];
+        ends[1] = checked_byte_ends[1];
+    } else {
+        capnp_status vst = check_offsets(
+            ctx, s, {{d_in_byte_off, nchunks, ~0ull}, {d_out_word_off, nchunks, ~0ull}});
+        if (vst != CAPNP_OK) return vst;
+        ends[0] = checked_ends(ctx, 0)[0];
+        ends[1] = checked_ends(ctx, 0)[1];
+    }
     if (ends[1] < ends[0]) return CAPNP_E_INVALID_ARGUMENT;
     const size_t ws = capnp_resync_ws_bytes(nchunks, ends[1] - ends[0]);
     capnp_status st = ensure_buf(ctx, &ctx->d_resync, &ctx->resync_cap, ws);
