@@ -2767,6 +2767,16 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
                  lane);
 }
 
+// Zeroes a[0, na) and b[0, nb) (words).
+__global__ void __launch_bounds__(256)
+k_zero2(uint64_t* __restrict__ a, uint64_t na, uint64_t* __restrict__ b, uint64_t nb) {
+    const uint64_t step = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < na + nb; i += step) {
+        if (i < na) a[i] = 0;
+        else b[i - na] = 0;
+    }
+}
+
 // Chunk-start bits (start_bits); cb zeroed beforehand.
 __global__ void __launch_bounds__(256)
 pack_wt_bits(const uint64_t* __restrict__ chunk_off, uint64_t nchunks, uint64_t whi, uint64_t b64,
@@ -2861,12 +2871,16 @@ pack_wt_map(const uint64_t* __restrict__ chunk_off, uint64_t nchunks, uint64_t w
 
 // Sync entries of each tile's first chunk when it started before the tile:
 // tile-relative record positions become chunk-relative.
-__global__ void __launch_bounds__(64)
+// (one wave per tile, four tiles per workgroup: one-wave workgroups left
+// the CUs' workgroup slots, not their waves, as the limit)
+__global__ void __launch_bounds__(256)
 pack_wt_fix_sync(const uint64_t* __restrict__ chunk_off, const uint64_t* __restrict__ out_off,
                  const uint64_t* __restrict__ map, const uint64_t* __restrict__ tile_off,
-                 uint32_t* __restrict__ sync, uint64_t wlo, uint64_t whi, uint64_t g0) {
-    const uint64_t t = blockIdx.x;
-    const uint32_t lane = threadIdx.x;
+                 uint32_t* __restrict__ sync, uint64_t wlo, uint64_t whi, uint64_t g0,
+                 uint64_t ntiles) {
+    const uint64_t t = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (t >= ntiles) return;
     const uint64_t g = g0 + t;
     const uint64_t Ta = g * kWtTile > wlo ? g * kWtTile : wlo;
     const uint64_t Tb = (g + 1) * kWtTile < whi ? (g + 1) * kWtTile : whi;
@@ -3123,10 +3137,15 @@ extern "C" hipError_t capnp_launch_pack_wt(const uint64_t* d_in, const uint64_t*
     uint64_t* toff = map + ntiles * kWaves;
     uint64_t* cbits = toff + ntiles;
     uint32_t* plan = reinterpret_cast<uint32_t*>(cbits + wt_bits_words(wlo, whi));
-    hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(ntiles, 1), stream);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(cbits, 0, wt_bits_words(wlo, whi) * 8, stream);
-    if (e != hipSuccess) return e;
+    {
+        // the look-back state and the chunk-start bits cleared in one launch
+        // (two runtime memsets were four fill kernels, ~20 us a call)
+        const uint64_t na = (capnp_pack_state_bytes(ntiles, 1) + 7) / 8;
+        const uint64_t nb = wt_bits_words(wlo, whi);
+        const uint64_t nt = na + nb;
+        const uint32_t blocks = (uint32_t)std::min<uint64_t>((nt + 255) / 256, 4096);
+        hipLaunchKernelGGL(k_zero2, dim3(blocks), dim3(256), 0, stream, d_state, na, cbits, nb);
+    }
     hipLaunchKernelGGL(pack_wt_bits, dim3((uint32_t)((nchunks + 255) / 256)), dim3(256), 0, stream,
                        d_chunk_off, nchunks, whi, wlo >> 6,
                        reinterpret_cast<unsigned long long*>(cbits));
@@ -3141,8 +3160,8 @@ extern "C" hipError_t capnp_launch_pack_wt(const uint64_t* d_in, const uint64_t*
         hipLaunchKernelGGL(pack_wt_kernel<true>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
                            d_in, d_chunk_off, nchunks, d_out, out_cap, d_out_off, d_state,
                            d_state + ntiles, d_sync, map, toff, cbits, plan, wlo, whi, g0);
-        hipLaunchKernelGGL(pack_wt_fix_sync, dim3((uint32_t)ntiles), dim3(64), 0, stream,
-                           d_chunk_off, d_out_off, map, toff, d_sync, wlo, whi, g0);
+        hipLaunchKernelGGL(pack_wt_fix_sync, dim3((uint32_t)((ntiles + 3) / 4)), dim3(256), 0,
+                           stream, d_chunk_off, d_out_off, map, toff, d_sync, wlo, whi, g0, ntiles);
     } else {
         hipLaunchKernelGGL(pack_wt_kernel<false>, dim3((uint32_t)ntiles), dim3(kThreads), 0, stream,
                            d_in, d_chunk_off, nchunks, d_out, out_cap, d_out_off, d_state,

@@ -674,7 +674,7 @@ k_fail(uint64_t n, const uint64_t* __restrict__ bstart, const int32_t* __restric
 }
 
 // k_tile's look-back records: one per tile (<= nbb / kTileBlocks + 1 tiles),
-// then the ticket; resolve() zeroes all of them before each launch.
+// then the ticket; resolve() zeroes them, with the flags before them, before its launches.
 uint64_t trec_words(uint64_t nbb) { return nbb / kTileBlocks + 2; }
 
 size_t carve(Ws* w, uint8_t* base, uint64_t n, uint64_t nbb, size_t tmp_bytes) {
@@ -724,8 +724,19 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
     *converged = true;
     *capped = false;
     const unsigned ntiles = (unsigned)((nbb + kTileBlocks - 1) / kTileBlocks);
-    if ((e = hipMemsetAsync(w.trec, 0, 8 * trec_words(nbb), s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(w.flags + 2, 0, 4 * kMaxPasses, s)) != hipSuccess) return e;
+    // the flags (round cap, chunk failure, one per fix pass) and the tile
+    // records with their ticket lie together in the workspace: one clear
+    {
+        const size_t zb = (size_t)(reinterpret_cast<uint8_t*>(w.trec + trec_words(nbb)) -
+                                   reinterpret_cast<uint8_t*>(w.flags));
+        if ((e = hipMemsetAsync(w.flags, 0, zb, s)) != hipSuccess) return e;
+    }
+    // (the flags come back through pinned memory: one DMA, no staged copy)
+    static thread_local int32_t* t_hflags = nullptr;
+    if (!t_hflags) {
+        void* p = nullptr;
+        if (hipHostMalloc(&p, 4 * (2 + kMaxPasses), 0) == hipSuccess) t_hflags = (int32_t*)p;
+    }
     k_tile<<<ntiles, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
                                                  w.words, w.spec_exit, w.flags, w.trec, w.ticket,
                                                  g_max_rounds, 0, 0);
@@ -740,12 +751,21 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
                                                          w.entry, w.words, w.spec_exit, w.flags,
                                                          w.trec, w.ticket, g_max_rounds, 1, pass);
         int32_t last = 0, cap = 0;
-        if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
-            hipSuccess)
-            return e;
-        if ((e = hipMemcpyAsync(&cap, w.flags, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
-            return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (t_hflags) {
+            if ((e = hipMemcpyAsync(t_hflags, w.flags, 4 * (2 + pass), hipMemcpyDeviceToHost, s)) !=
+                hipSuccess)
+                return e;
+            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+            cap = t_hflags[0];
+            last = t_hflags[2 + pass - 1];
+        } else {
+            if ((e = hipMemcpyAsync(&last, w.flags + 2 + pass - 1, 4, hipMemcpyDeviceToHost, s)) !=
+                hipSuccess)
+                return e;
+            if ((e = hipMemcpyAsync(&cap, w.flags, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+                return e;
+            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        }
         if (cap) *capped = true;
         if (!last) break;
     }
@@ -818,7 +838,6 @@ extern "C" hipError_t capnp_resync_unpack(const uint8_t* d_in, const uint64_t* d
     if (carve(&w, base, n, nbb, scan_tmp_bytes(m)) + (base - (uint8_t*)d_ws) >
         ws_bytes)
         return hipErrorInvalidValue;
-    if ((e = hipMemsetAsync(w.flags, 0, 4 * 2, s)) != hipSuccess) return e;
     k_count<<<grid(n + 1), kThreads, 0, s>>>(d_in_off, n, d_out_off, w.nblk);
     size_t tb = w.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
@@ -1426,7 +1445,6 @@ extern "C" hipError_t capnp_resync_decode_prefix(const uint8_t* d_in, uint64_t n
     uint64_t* cutk = aux + 10;    // [1]
     const uint64_t h_in_off[2] = {0, nbytes};
     if ((e = hipMemcpyAsync(in_off, h_in_off, 16, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(w.flags, 0, 4 * 2, s)) != hipSuccess) return e;
     k_count<<<grid(n + 1), kThreads, 0, s>>>(in_off, n, in_off, w.nblk);
     size_t tb = w.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(w.tmp, tb, w.nblk, w.bstart, (int)(n + 1), s)) !=
@@ -1534,7 +1552,6 @@ static hipError_t find_messages_impl(const uint8_t* d_in, uint64_t nbytes, uint6
     if ((size_t)(chain + chain_bytes - (uint8_t*)d_ws) > ws_bytes) return hipErrorInvalidValue;
     const uint64_t h_in_off[2] = {0, nbytes};
     if ((e = hipMemcpyAsync(in_off, h_in_off, 16, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(w.flags, 0, 4 * 2, s)) != hipSuccess) return e;
     // (one chunk of nbytes > 0 bytes: k_count never reads its word offsets)
     k_count<<<grid(n + 1), kThreads, 0, s>>>(in_off, n, in_off, w.nblk);
     size_t tb = w.tmp_bytes;
