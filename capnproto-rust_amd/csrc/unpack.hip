@@ -505,7 +505,30 @@ constexpr ExpandTable make_expand_table() {
 }
 __device__ constexpr ExpandTable kExpandTable = make_expand_table();
 
+// expand_selector(tag) in registers, a dword per half (byte k = its rank
+// among the tag's set bits below k, or 0x0C for a zero byte): the nibble's
+// bits spread to bytes by a 24-bit multiply, the ranks by shifted adds, the
+// zero bytes by a bitfield insert.  ~20 VALU ops instead of an LDS table
+// read (whose 2 KiB per workgroup decides the word tiles' occupancy).
+__device__ __forceinline__ uint64_t sel_alu(uint32_t tag) {
+    const uint32_t lo8 = __umul24(tag & 15u, 0x00204081u) & 0x01010101u;
+    const uint32_t hi8 = __umul24((tag >> 4) & 15u, 0x00204081u) & 0x01010101u;
+    const uint32_t loi = lo8 + (lo8 << 8) + (lo8 << 16) + (lo8 << 24);  // inclusive ranks
+    // (+ the low nibble's popcount, loi's byte 3, in every byte: one v_perm)
+    const uint32_t hii = hi8 + (hi8 << 8) + (hi8 << 16) + (hi8 << 24) +
+                         __builtin_amdgcn_perm(0u, loi, 0x03030303u);
+    const uint32_t mlo = (lo8 << 8) - lo8, mhi = (hi8 << 8) - hi8;  // 0xFF where set
+    const uint32_t slo = ((loi - lo8) & mlo) | (0x0C0C0C0Cu & ~mlo);
+    const uint32_t shi = ((hii - hi8) & mhi) | (0x0C0C0C0Cu & ~mhi);
+    return ((uint64_t)shi << 32) | slo;
+}
+
+#ifndef FIT_SEL_ALU
+#define FIT_SEL_ALU 0  // the chunk tiles' expansion computes its selectors
+#endif
+
 // Rebuilds one output word from its descriptor (sel = expand selectors).
+template <bool ALU = false>
 __device__ __forceinline__ uint64_t expand_desc(const uint8_t* B, const uint64_t* sel,
                                                 uint32_t d) {
     const bool none = d == kNone, raw = !none && (d & kRaw);
@@ -522,7 +545,7 @@ __device__ __forceinline__ uint64_t expand_desc(const uint8_t* B, const uint64_t
     const uint64_t v = ((uint64_t)__builtin_amdgcn_alignbyte(x2, x1, src) << 32) |
                        __builtin_amdgcn_alignbyte(x1, x0, src);
     const uint32_t t = none ? 0u : (raw ? 0xFFu : tag);
-    const uint64_t sv = sel[t];
+    const uint64_t sv = ALU ? sel_alu(t) : sel[t];
     const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
     return ((uint64_t)__builtin_amdgcn_perm(hi, lo, (uint32_t)(sv >> 32)) << 32) |
            __builtin_amdgcn_perm(hi, lo, (uint32_t)sv);
@@ -535,12 +558,13 @@ constexpr uint32_t kSyncNone = 0xFFFFFFFFu;
 
 // The staged tables for tiles of up to TW output words and TB packed bytes
 // (chunk tiles: kTileWords / kTileBytes; word tiles: kWtWords / kWtBytes).
-template <uint32_t TW, uint32_t TB>
+// SEL = false: no selector table (the expansion computes the selectors).
+template <uint32_t TW, uint32_t TB, bool SEL = true>
 struct StageSmemT {
     static constexpr uint32_t kDummy = TW;  // dpos[kDummy + 2 lane]: dummy slots
     static constexpr uint32_t kSeg = TW / kSyncWords + 2;
     union {
-        uint64_t sel[256];  // expand_selector(tag): 0x00 -> zeros, 0xFF -> identity
+        uint64_t sel[SEL ? 256 : 1];  // expand_selector(tag): 0x00 -> zeros, 0xFF -> identity
     };
     uint8_t badc[kStageChunks];     // 1 = the chunk needs the exact walk
     uint32_t cw[kStageChunks + 1];  // chunk word offsets (tile-relative)
@@ -1289,7 +1313,7 @@ __device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __
     // round trips before the walk.)
     {
         constexpr uint32_t kLoads = (kTileBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
-        const uint64_t selv = SELW ? kExpandTable.s[tid] : 0;
+        const uint64_t selv = (SELW && !FIT_SEL_ALU) ? kExpandTable.s[tid] : 0;
         uint32_t e_a = 0, e_b = 0;
         const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint64_t*>(out_off + ca), 0, (int)((nc + 1) * 8), 0x00020000);
@@ -1318,7 +1342,7 @@ __device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __
         uint4* dd = reinterpret_cast<uint4*>(S.dpos);
         const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
         for (uint32_t k = tid; k < (Wt + 7) / 8; k += kThreads) dd[k] = none;
-        if (SELW) S.sel[tid] = selv;
+        if (SELW && !FIT_SEL_ALU) S.sel[tid] = selv;
         if (tid <= nc) {
             const uint32_t wa = t_w - (uint32_t)W0;
             S.cw[tid] = wa;
@@ -1411,7 +1435,7 @@ __device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __
 #pragma unroll
             for (int u = 0; u < kGroups; u++) {
                 const uint32_t i = (g0 + u * kWaves) * CAPNP_WAVE + lane;
-                const uint64_t word = expand_desc(S.bytes, S.sel, d[u]);
+                const uint64_t word = expand_desc<FIT_SEL_ALU>(S.bytes, S.sel, d[u]);
                 if (i < Wt) out[W0 + i] = word;
             }
         }
@@ -2061,8 +2085,12 @@ static_assert(kWtWords % kSyncWords == 0 && kWtWords <= kMaxTileChunks * CAPNP_W
 // 649, 1536 -> 632 (7 workgroups per CU), 1792 -> 660, 2048 -> 677 (5 per
 // CU).
 constexpr uint32_t kWtBytes = (kWtWords * 65 / 8 + 2064 + 15) & ~15u;
-using WtStageSmem = StageSmemT<kWtWords, kWtBytes>;
-// (7 waves per SIMD: the LDS, 21.8 KB at 1536 words, allows 7 workgroups per CU)
+#ifndef WT_SEL_ALU
+#define WT_SEL_ALU 1
+#endif
+using WtStageSmem = StageSmemT<kWtWords, kWtBytes, !WT_SEL_ALU>;
+// (with the selector table the LDS, 21.8 KB at 1536 words, allowed 7
+// workgroups per CU; computed selectors (WT_SEL_ALU) leave 19.7 KB: 8)
 // plan flags
 constexpr uint32_t kWtPf = 1, kWtPl = 2, kWtFallback = 4;
 
@@ -2239,7 +2267,7 @@ __device__ __forceinline__ void serial_chunk_at(const uint8_t* __restrict__ in,
     if (consumed) consumed[c] = used;
 }
 
-__global__ void __launch_bounds__(kThreads, 7)
+__global__ void __launch_bounds__(kThreads, WT_SEL_ALU ? 8 : 7)
 unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in_off,
                  uint64_t* __restrict__ out, const uint64_t* __restrict__ out_off,
                  int32_t* __restrict__ status, uint64_t* __restrict__ consumed,
@@ -2280,7 +2308,7 @@ unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
     // selector entry written after them
     {
         constexpr uint32_t kLoads = (kWtBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
-        const uint64_t selv = kExpandTable.s[tid];
+        const uint64_t selv = WT_SEL_ALU ? 0 : kExpandTable.s[tid];
         const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint64_t*>(out_off + ca), 0, (int)((nc + 1) * 8), 0x00020000);
         const __amdgpu_buffer_rsrc_t irs = __builtin_amdgcn_make_buffer_rsrc(
@@ -2311,7 +2339,7 @@ unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
             for (uint32_t i = tid; i < ((Wt + 7) & ~7u); i += kThreads)
                 S.dpos[i] = i < litn ? (uint16_t)(kRaw | (litp + 8 * i)) : kNone;
         }
-        S.sel[tid] = selv;
+        if (!WT_SEL_ALU) S.sel[tid] = selv;
         if (tid <= nc) {
             const uint64_t wo = ((uint64_t)wov[1] << 32) | wov[0];
             const uint32_t wa = wo < Wa ? 0u : (uint32_t)(wo - Wa);
@@ -2376,7 +2404,8 @@ unpack_wt_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
         if (f) atomicAdd(&g_wt_stats[1], 1ull);
     }
     if (anybad) __syncthreads();
-    for (uint32_t i = tid; i < Wt; i += kThreads) out[Wa + i] = expand_desc(S.bytes, S.sel, S.dpos[i]);
+    for (uint32_t i = tid; i < Wt; i += kThreads)
+        out[Wa + i] = expand_desc<WT_SEL_ALU>(S.bytes, S.sel, S.dpos[i]);
 }
 
 // Status of every chunk that spans tiles, in the tile where it ends.
