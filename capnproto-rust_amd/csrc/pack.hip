@@ -868,7 +868,9 @@ __device__ __forceinline__ uint64_t start_bits_s(const uint64_t* __restrict__ cb
 // W: the words examined first are R - W .. R - 1 (lanes 64 - W ..; wp = word
 // R - W - 1): with random data nearly every word is a sure head, so a short
 // window decides almost every range and the deep search takes the rest.
-template <uint32_t W = 64>
+// NW: windows loaded per round of the deep search (fewer: fewer registers,
+// for a caller whose deep searches are rare).
+template <uint32_t W = 64, int NW = 8>
 __device__ __forceinline__ Carry carry_in_b(const uint64_t* __restrict__ in,
                                             const uint64_t* __restrict__ cb, uint64_t b64,
                                             uint64_t wlo, uint64_t R, uint32_t lane, uint64_t w,
@@ -894,13 +896,14 @@ __device__ __forceinline__ Carry carry_in_b(const uint64_t* __restrict__ in,
                               ballot64(tag == 0xFF) & Vj, 1ull << j, 64, Carry{0, 0}).next;
     }
     bool allz = ballot64(v && tag != 0) == 0, allf = ballot64(v && tag != 0xFF) == 0;
-    for (uint64_t hi = R - W; hi > wlo; hi = hi > wlo + 512 ? hi - 512 : wlo) {
-        uint32_t t[8];
-        uint64_t bk[8];
+    constexpr uint64_t kSpan = 64ull * NW;
+    for (uint64_t hi = R - W; hi > wlo; hi = hi > wlo + kSpan ? hi - kSpan : wlo) {
+        uint32_t t[NW];
+        uint64_t bk[NW];
         {
-            uint64_t x[8];
+            uint64_t x[NW];
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
+            for (int k = 0; k < NW; k++) {
                 const uint64_t lo = hi - 64 * (k + 1);  // (may wrap below 0: then invalid)
                 const bool inb = hi >= wlo + 64ull * (k + 1) - lane;  // lo + lane >= wlo
                 x[k] = inb ? in[lo + lane] : 0ull;
@@ -914,18 +917,18 @@ __device__ __forceinline__ Carry carry_in_b(const uint64_t* __restrict__ in,
                 bk[k] = slo + 64 <= (int64_t)wlo ? 0ull : start_bits_s(cb, b64, slo);
             }
 #pragma unroll
-            for (int k = 0; k < 8; k++) t[k] = tag_of(x[k]);
+            for (int k = 0; k < NW; k++) t[k] = tag_of(x[k]);
         }
         int kf = -1;
         uint64_t s = wlo;
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
+        for (int k = 0; k < NW; k++) {
             const bool vk = hi >= wlo + 64ull * (k + 1) - lane;
             const uint32_t tk = vk ? t[k] : 0u;
             const uint32_t pt0 = (uint32_t)__shfl_up((int)tk, 1, 64);
-            const uint32_t below = k < 7 ? (uint32_t)__shfl((int)t[k < 7 ? k + 1 : 7], 63, 64) : 0u;
+            const uint32_t below = k < NW - 1 ? (uint32_t)__shfl((int)t[k < NW - 1 ? k + 1 : NW - 1], 63, 64) : 0u;
             const uint32_t pt = lane ? pt0 : below;
-            const bool sure = vk && (((bk[k] >> lane) & 1) || ((lane || k < 7) && sure_head(tk, pt)));
+            const bool sure = vk && (((bk[k] >> lane) & 1) || ((lane || k < NW - 1) && sure_head(tk, pt)));
             const uint64_t Gk = ballot64(sure);
             if (kf < 0) {
                 if (Gk) {
@@ -2346,6 +2349,10 @@ pack_ovf_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ ch
 // relative to the tile (24-bit two's complement) and pack_wt_fix_sync adds
 // tile offset - chunk offset once every tile is placed.
 
+#ifndef PACK_WT_OCC
+#define PACK_WT_OCC 8
+#endif
+
 struct WtSmem {
     Sel8 sel[kSelCopy + 1];                // record assembly per tag (s0, s1)
     uint64_t wave_bytes[kWaves];
@@ -2355,7 +2362,9 @@ struct WtSmem {
     uint32_t wext[kWaves];                 // words from range w's start its open run absorbs
     alignas(16) uint32_t pad[4];           // (emit_step ORs a zero before a region)
     alignas(16) uint8_t stage[kWaves][kRegion];
-    uint16_t wpos[kWaves][kWtRange];       // region position of chunk-start words
+    // (the region positions of the range's chunk-start words go into the
+    // wave's region after its copy-out: a separate 4 KiB table had held the
+    // kernel at 6 workgroups per CU)
 };
 
 __device__ __forceinline__ void size_step_s(StageState& pk, uint64_t w, uint32_t nvalid,
@@ -2489,9 +2498,9 @@ __device__ __forceinline__ uint32_t range_ext(const uint64_t (&w)[kStageSteps], 
     return lead < c.rem ? lead : c.rem;
 }
 
-// (6 waves per SIMD: the LDS, 24.3 KB, allows 6 workgroups per CU)
+// (8 waves per SIMD: 64 VGPRs, LDS 20.2 KB)
 template <bool SYNC>
-__global__ void __launch_bounds__(kThreads, 6)
+__global__ void __launch_bounds__(kThreads, PACK_WT_OCC)
 pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
                uint64_t nchunks, uint8_t* __restrict__ out, uint64_t out_cap,
                uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts, uint64_t* __restrict__ gs,
@@ -2591,7 +2600,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             Carry c = ex.c;
             uint32_t hg = ex.homog;
             if (hg == 3) {  // no sure head, pop-7/8 words: search before R0 (rare)
-                c = carry_in_b<64>(in, cbits, b64, wlo, R1, lane, cache[kStageSteps - 1],
+                c = carry_in_b<64, 2>(in, cbits, b64, wlo, R1, lane, cache[kStageSteps - 1],
                                    readlane64(cache[kStageSteps - 2], 63),
                                    ballot64(((sbits >> (kStageSteps - 1)) & 1u) != 0));
                 hg = 0;
@@ -2655,6 +2664,7 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     uint32_t lastcs = ~0u;
     uint32_t hbits = 0;  // bit s = this lane heads a record in step s
     uint32_t metav = 0;  // lane s = step s's meta (nvalid | absorbed << 16)
+
 #pragma unroll
     for (uint32_t s = 0; s < kStageSteps; s++) {
         const uint32_t nv = nw > 64u * s ? (nw - 64u * s < 64u ? nw - 64u * s : 64u) : 0u;
@@ -2662,7 +2672,6 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         size_step_s(pk, cache[s], nv, Sm, lane, si[s]);
         hbits |= mask_sel(si[s].H, 1u << s, 0u);
         metav = lane == s ? si[s].meta : metav;
-        if ((sbits >> s) & 1u) wm.wpos[wave][64u * s + lane] = (uint16_t)si[s].pos;
         if (Sm)
             lastcs = (uint32_t)__builtin_amdgcn_readlane((int)si[s].pos, 63 - __builtin_clzll(Sm));
     }
@@ -2751,20 +2760,24 @@ pack_wt_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     }
     __syncthreads();
     const uint64_t excl = lds_u64(&wm.excl);
+    if (!have) return;
+    copy_out(region, outa, excl + woff + mis, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
+    // the chunk-start words' region positions, into the region just copied
+    // out (LDS ops of a wave run in order: its reads are done)
+    uint16_t* const wpos = reinterpret_cast<uint16_t*>(region);
+#pragma unroll
+    for (uint32_t s = 0; s < kStageSteps; s++)
+        if ((sbits >> s) & 1u) wpos[64u * s + lane] = (uint16_t)si[s].pos;
+    wave_lds_sync();
     // offsets of the chunks that start in the range (in the batch's last
     // range also the empty chunks at its end)
-    if (have) {
-        for (uint64_t c0 = cA;; c0 += CAPNP_WAVE) {
-            const uint64_t c = c0 + lane;
-            const uint64_t st = c0 == cA ? st0 : (c < nchunks ? chunk_off[c] : ~0ull);
-            const bool inr = c < nchunks && (st < R1 || (lastr && st == R1));
-            if (inr) out_off[c] = st < R1 ? excl + woff + wm.wpos[wave][st - R0] : excl + agg;
-            if (ballot64(inr) != ~0ull) break;
-        }
+    for (uint64_t c0 = cA;; c0 += CAPNP_WAVE) {
+        const uint64_t c = c0 + lane;
+        const uint64_t st = c0 == cA ? st0 : (c < nchunks ? chunk_off[c] : ~0ull);
+        const bool inr = c < nchunks && (st < R1 || (lastr && st == R1));
+        if (inr) out_off[c] = st < R1 ? excl + woff + wpos[st - R0] : excl + agg;
+        if (ballot64(inr) != ~0ull) break;
     }
-    if (have)
-        copy_out(region, outa, excl + woff + mis, lds_u64(&sm.wave_bytes[wave]), out_cap + mis,
-                 lane);
 }
 
 // Zeroes a[0, na) and b[0, nb) (words).
