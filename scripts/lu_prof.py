@@ -75,6 +75,17 @@ def main():
         torch.cuda.synchronize()
         assert torch.equal(back, w)
         show(f"batch kind {kind} {cw} words x {n}", L)
+    # config 4 without the index: the resync block decode hands the blocks
+    # that expand past a tile (zero-run blocks) to the long-unit decode
+    args = bench.parse(["--workload", "config4"])
+    words, offs, n, _ = bench.make_workload(args, ctx, torch, dev, 0)
+    packed, poffs = ctx.pack_batch(words, offs)
+    torch.cuda.synchronize()
+    reset(L)
+    back, st, _ = ctx.unpack_batch(packed, poffs, offs)
+    torch.cuda.synchronize()
+    assert torch.equal(back, words)
+    show("config 4 index-free (overflow blocks)", L)
 
 
 if __name__ == "__main__":
