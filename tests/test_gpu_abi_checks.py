@@ -159,3 +159,43 @@ def test_messages_checked(env):
     assert L.capnp_gpu_write_messages(ctx.handle, _p(w), _p(swo), _p(dm), 2, 3, 30, _p(out),
                                       out.numel(), _p(mbo), s) == 0
     torch.cuda.synchronize()
+
+
+def test_long_chunk_paths_checked(env):
+    """The long-chunk paths (mean chunk >= 512 words: word-tile pack, and the
+    block decode without the index, which the batch entry point hands its
+    already-checked ranges to) refuse backwards offsets too, and decode a
+    valid batch afterwards."""
+    ctx, L, torch = env
+    n_words = 4096
+    w = _words(torch, n_words)
+    host = w.cpu().numpy().view(np.uint64)
+    offs = np.array([0, 1500, 2600, n_words], np.uint64)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    out = torch.empty(n_words * 10 + 64, dtype=torch.uint8, device="cuda")
+    oo = torch.empty(4, dtype=torch.int64, device="cuda")
+    bad = _dev(torch, [0, 2600, 1500, n_words], np.int64)
+    assert L.capnp_gpu_pack_batch(ctx.handle, _p(w), _p(bad), 3, _p(out), out.numel(),
+                                  _p(oo), s) == BAD
+    good = _dev(torch, offs.view(np.int64), np.int64)
+    assert L.capnp_gpu_pack_batch(ctx.handle, _p(w), _p(good), 3, _p(out), out.numel(),
+                                  _p(oo), s) == 0
+    torch.cuda.synchronize()
+    st, ref, ref_off = O.pack_batch(host, offs)
+    assert np.array_equal(oo.cpu().numpy().view(np.uint64), ref_off)
+    assert np.array_equal(out[:len(ref)].cpu().numpy(), ref)
+    back = torch.zeros(n_words, dtype=torch.int64, device="cuda")
+    status = torch.empty(3, dtype=torch.int32, device="cuda")
+    in_ok = _dev(torch, ref_off.view(np.int64), np.int64)
+    in_bad = _dev(torch, [0, int(ref_off[2]), int(ref_off[1]), int(ref_off[3])], np.int64)
+    out_bad = _dev(torch, [0, 2600, 1500, n_words], np.int64)
+    for fn in (L.capnp_gpu_unpack_batch, L.capnp_gpu_unpack_batch_resync):
+        assert fn(ctx.handle, _p(out), _p(in_bad), 3, _p(back), _p(good), _p(status), None,
+                  s) == BAD
+        assert fn(ctx.handle, _p(out), _p(in_ok), 3, _p(back), _p(out_bad), _p(status), None,
+                  s) == BAD
+    assert L.capnp_gpu_unpack_batch(ctx.handle, _p(out), _p(in_ok), 3, _p(back), _p(good),
+                                    _p(status), None, s) == 0
+    torch.cuda.synchronize()
+    assert (status.cpu().numpy() == 0).all()
+    assert np.array_equal(back.cpu().numpy().view(np.uint64), host)
