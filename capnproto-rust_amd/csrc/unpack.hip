@@ -44,7 +44,7 @@
 // per-tile trace (capnp_unpack_trace): s_memrealtime (100 MHz) at
 // [0] start, [1] staged, [2] walked, [3] expanded; [4] 1 = global path
 __device__ uint64_t* g_utrace;
-__device__ unsigned long long g_uprof[8];
+__device__ unsigned long long g_uprof[16];  // (UNPACK_PROF: [0] serial chunk walks, [1..7] long-unit phases, [8] overflow tiles, [9] their cycles)
 #define UPROF_T(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
 // long-unit phases (unpack_long): g_uprof[1] windows, [2] rounds, [3..7]
 // s_memrealtime ticks (10 ns) in stage, spec, rounds, words (+ the last
@@ -559,10 +559,12 @@ constexpr uint32_t kSyncNone = 0xFFFFFFFFu;
 // The staged tables for tiles of up to TW output words and TB packed bytes
 // (chunk tiles: kTileWords / kTileBytes; word tiles: kWtWords / kWtBytes).
 // SEL = false: no selector table (the expansion computes the selectors).
-template <uint32_t TW, uint32_t TB, bool SEL = true>
+// ENT = false: no sync-walk tables (tiles decoded without the index only).
+template <uint32_t TW, uint32_t TB, bool SEL = true, bool ENT = true>
 struct StageSmemT {
+    static constexpr uint32_t kTW = TW, kTB = TB;
     static constexpr uint32_t kDummy = TW;  // dpos[kDummy + 2 lane]: dummy slots
-    static constexpr uint32_t kSeg = TW / kSyncWords + 2;
+    static constexpr uint32_t kSeg = ENT ? TW / kSyncWords + 2 : 1;
     union {
         uint64_t sel[SEL ? 256 : 1];  // expand_selector(tag): 0x00 -> zeros, 0xFF -> identity
     };
@@ -583,6 +585,17 @@ struct StageSmemT {
     alignas(16) uint16_t dpos[TW + 2 * CAPNP_WAVE];  // [TW + 2 lane]: dummy slots
 };
 using StageSmem = StageSmemT<kTileWords, kTileBytes>;
+// The overflow kernels' staged sub-tiles without the index: their LDS holds
+// the long-unit tables anyway, room for 4x the words of a tile, so a tile
+// that overflows the fit kernel's tables by its words (zero-run units: the
+// block decode of config 4) decodes in one or two staged passes instead of
+// one per unit.
+constexpr uint32_t kBigWords = 4 * kTileWords;
+constexpr uint32_t kBigBytes = 16384;
+using BigStageSmem = StageSmemT<kBigWords, kBigBytes, true, false>;
+#ifndef OVF_BIG
+#define OVF_BIG 1
+#endif
 
 // Long-unit decode (unpack_long): one chunk too large for the tile tables,
 // decoded by the whole workgroup in windows of packed bytes.  Each window
@@ -608,9 +621,13 @@ struct LongSmem {
 
 union USmem {
     StageSmem st;
+    BigStageSmem big;  // (no larger than the long-unit tables: see below)
     uint16_t desc[kGlobalWaves][CAPNP_WAVE][CAPNP_WAVE];  // global path
     LongSmem lu;                                          // long-unit path
 };
+static_assert(sizeof(BigStageSmem) <= sizeof(LongSmem), "the big sub-tiles fit the long-unit LDS");
+static_assert(offsetof(BigStageSmem, sel) == 0 && offsetof(StageSmem, sel) == 0 &&
+                  offsetof(LongSmem, sel) == 0, "one selector table serves every view");
 
 
 // The three bytes of the record whose tag is at LDS byte q-1: tag, q (zero
@@ -1285,8 +1302,8 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
 // SELW: the selector table is written here too, its load issued with the
 // staging loads (the caller's copy had waited for it before any of them).
 // The tile [ca, cb) whose packed bytes are [B0, B1) and words [W0, W1).
-template <bool SYNC, bool SELW = false>
-__device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __restrict__ in,
+template <bool SYNC, bool SELW = false, class SM = StageSmem>
+__device__ __forceinline__ void unpack_staged_at(SM& S, const uint8_t* __restrict__ in,
                                                  const uint64_t* __restrict__ in_off, uint64_t ca,
                                                  uint64_t cb, uint64_t* __restrict__ out,
                                                  const uint64_t* __restrict__ out_off,
@@ -1312,7 +1329,7 @@ __device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __
     // waited for everything before them: with the table copy, ~4 dependent
     // round trips before the walk.)
     {
-        constexpr uint32_t kLoads = (kTileBytes + 15 + 16 * kThreads - 1) / (16 * kThreads);
+        constexpr uint32_t kLoads = (SM::kTB + 15 + 16 * kThreads - 1) / (16 * kThreads);
         const uint64_t selv = (SELW && !FIT_SEL_ALU) ? kExpandTable.s[tid] : 0;
         uint32_t e_a = 0, e_b = 0;
         const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
@@ -1453,8 +1470,8 @@ __device__ __forceinline__ void unpack_staged_at(StageSmem& S, const uint8_t* __
 #endif
 }
 
-template <bool SYNC, bool SELW = false>
-__device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __restrict__ in,
+template <bool SYNC, bool SELW = false, class SM = StageSmem>
+__device__ __forceinline__ void unpack_staged(SM& S, const uint8_t* __restrict__ in,
                                               const uint64_t* __restrict__ in_off, uint64_t ca,
                                               uint64_t cb, uint64_t* __restrict__ out,
                                               const uint64_t* __restrict__ out_off,
@@ -1462,9 +1479,9 @@ __device__ __forceinline__ void unpack_staged(StageSmem& S, const uint8_t* __res
                                               uint64_t* __restrict__ consumed,
                                               const uint32_t* __restrict__ sync, uint32_t tid,
                                               uint32_t lane, uint32_t wave) {
-    unpack_staged_at<SYNC, SELW>(S, in, in_off, ca, cb, out, out_off, status, consumed, sync, tid,
-                                 lane, wave, uniform64(in_off[ca]), uniform64(in_off[cb]),
-                                 uniform64(out_off[ca]), uniform64(out_off[cb]));
+    unpack_staged_at<SYNC, SELW, SM>(S, in, in_off, ca, cb, out, out_off, status, consumed, sync,
+                                     tid, lane, wave, uniform64(in_off[ca]), uniform64(in_off[cb]),
+                                     uniform64(out_off[ca]), uniform64(out_off[cb]));
 }
 
 // ---------------------------------------------------------------------------
@@ -1862,20 +1879,23 @@ __device__ void unpack_tile_rest(USmem& sm, const uint8_t* __restrict__ in,
                                  const uint32_t* __restrict__ sync, uint32_t tid, uint32_t lane,
                                  uint32_t wave) {
     bool first = true, resel = false;
+    // (without the index the sub-tiles take the larger tables)
+    constexpr bool kBig = !SYNC && OVF_BIG;
+    constexpr uint64_t kTW = kBig ? kBigWords : kTileWords, kTB = kBig ? kBigBytes : kTileBytes;
     for (uint64_t lo = ca; lo < cb;) {
         // the longest prefix of [lo, cb) that fits: <= kStageChunks chunks,
-        // <= kTileWords words, <= kTileBytes bytes from lo's 16-byte block
+        // <= kTW words, <= kTB bytes from lo's 16-byte block
         // (the fit is monotone in the prefix, so it is a ballot count)
         const uint64_t B0 = uniform64(in_off[lo]), W0 = uniform64(out_off[lo]);
         const uint32_t off0 = (uint32_t)(reinterpret_cast<uintptr_t>(in + B0) & 15u);
         uint32_t k;
-        if (cb - lo <= kStageChunks && uniform64(in_off[cb]) - B0 <= kTileBytes - off0 &&
-            uniform64(out_off[cb]) - W0 <= kTileWords) {
+        if (cb - lo <= kStageChunks && uniform64(in_off[cb]) - B0 <= kTB - off0 &&
+            uniform64(out_off[cb]) - W0 <= kTW) {
             k = (uint32_t)(cb - lo);  // the usual case: the rest of the tile fits (scalar loads)
         } else {
             const uint64_t c = lo + 1 + lane;
-            const bool fit = c <= cb && in_off[c < cb ? c : cb] - B0 <= kTileBytes - off0 &&
-                             out_off[c < cb ? c : cb] - W0 <= kTileWords;
+            const bool fit = c <= cb && in_off[c < cb ? c : cb] - B0 <= kTB - off0 &&
+                             out_off[c < cb ? c : cb] - W0 <= kTW;
             k = (uint32_t)__builtin_popcountll(ballot64(fit));
         }
         if (!first) __syncthreads();  // the previous sub-tile is done with LDS
@@ -1898,8 +1918,12 @@ __device__ void unpack_tile_rest(USmem& sm, const uint8_t* __restrict__ in,
             sm.st.sel[tid] = kExpandTable.s[tid];
             resel = false;
         }
-        unpack_staged<SYNC>(sm.st, in, in_off, lo, lo + k, out, out_off, status, consumed, sync,
-                            tid, lane, wave);
+        if constexpr (!kBig)
+            unpack_staged<SYNC>(sm.st, in, in_off, lo, lo + k, out, out_off, status, consumed,
+                                sync, tid, lane, wave);
+        else
+            unpack_staged<SYNC, false, BigStageSmem>(sm.big, in, in_off, lo, lo + k, out, out_off,
+                                                     status, consumed, sync, tid, lane, wave);
         lo += k;
     }
 }
@@ -1991,13 +2015,16 @@ unpack_ovf_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict__ i
 // (config 4 index-free: 4.3 ms in the overflow kernel; one workgroup per
 // tile instead cost config 2 0.13 ms of empty workgroups).
 #ifndef OVF_WINDOW
-#define OVF_WINDOW 16
+#define OVF_WINDOW 32
 #endif
 #ifndef OVF_GRID
-#define OVF_GRID 4096
+#define OVF_GRID 2048
 #endif
-constexpr uint32_t kOvfWindow = OVF_WINDOW;  // (64: config 4 index-free overflow 1.86 ms on 1155 workgroups)
-constexpr uint64_t kOvfGrid = OVF_GRID;  // (config 2's 65536 tiles: 16 per workgroup, as in round 4)
+// (round 5, with the 8192-word sub-tiles: windows of 32 on 2048 workgroups,
+// config 2 index-free 451 vs 465 us, config 4 1553 vs 1542; 64 / 1024: 446
+// and 1566)
+constexpr uint32_t kOvfWindow = OVF_WINDOW;
+constexpr uint64_t kOvfGrid = OVF_GRID;
 static_assert(kOvfWindow <= CAPNP_WAVE, "one lane per tile of the window");
 
 template <bool SYNC>
@@ -2038,6 +2065,9 @@ unpack_ovf_win_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict
             const uint64_t ca = t * tc;
             const uint64_t cb = (ca + tc < nchunks) ? ca + tc : nchunks;
             __syncthreads();  // the previous tile is done with the tables
+#if UNPACK_PROF
+            const uint64_t tov0 = __builtin_amdgcn_s_memrealtime();
+#endif
             if (!sel_ok) {
                 sm.st.sel[tid] = kExpandTable.s[tid];
                 sel_ok = true;
@@ -2045,6 +2075,11 @@ unpack_ovf_win_kernel(const uint8_t* __restrict__ in, const uint64_t* __restrict
             unpack_tile_rest<SYNC, true>(sm, in, in_off, ca, cb, out, out_off, status, consumed,
                                          sync, tid, lane, wave);
             sel_ok = false;  // (the global path may overlay the selectors)
+#if UNPACK_PROF
+            __syncthreads();
+            LUPROF_ADD(8, 1);
+            LUPROF_ADD(9, __builtin_amdgcn_s_memrealtime() - tov0);
+#endif
         }
         __syncthreads();  // ovf_mask is rewritten next window
     }
@@ -2616,10 +2651,10 @@ extern "C" hipError_t capnp_unpack_trace(uint64_t* d_buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_utrace), &d_buf, sizeof(d_buf));
 }
 
-extern "C" hipError_t capnp_unpack_prof(unsigned long long* host8, int reset) {
-    hipError_t e = hipMemcpyFromSymbol(host8, HIP_SYMBOL(g_uprof), sizeof(g_uprof));
+extern "C" hipError_t capnp_unpack_prof(unsigned long long* host16, int reset) {
+    hipError_t e = hipMemcpyFromSymbol(host16, HIP_SYMBOL(g_uprof), sizeof(g_uprof));
     if (e == hipSuccess && reset) {
-        static const unsigned long long z[8] = {};
+        static const unsigned long long z[16] = {};
         e = hipMemcpyToSymbol(HIP_SYMBOL(g_uprof), z, sizeof(z));
     }
     return e;

@@ -22,16 +22,19 @@ os.environ["CAPNP_PACKED_LIB"] = os.path.join(ROOT, "capnproto-rust_amd/build/ab
 
 
 def show(tag, L):
-    v = (C.c_ulonglong * 8)()
+    v = (C.c_ulonglong * 16)()
     assert L.capnp_unpack_prof(v, 1) == 0
     nw = max(v[1], 1)
+    if v[8] or v[0]:
+        print(f"{tag}: overflow tiles {v[8]} ({v[9] / max(v[8], 1) / 100:.2f} us each), "
+              f"serial chunk walks {v[0]}", flush=True)
     print(f"{tag}: windows {v[1]} rounds/window {v[2] / nw:.2f} us/window: stage {v[3] / nw / 100:.2f} "
           f"spec {v[4] / nw / 100:.2f} rounds {v[5] / nw / 100:.2f} words {v[6] / nw / 100:.2f} "
           f"desc+expand {v[7] / nw / 100:.2f}", flush=True)
 
 
 def reset(L):
-    v = (C.c_ulonglong * 8)()
+    v = (C.c_ulonglong * 16)()
     assert L.capnp_unpack_prof(v, 1) == 0
 
 

@@ -52,7 +52,7 @@ def main():
     back = torch.empty_like(words)
     status = torch.empty(n, dtype=torch.int32, device="cuda")
     utc = a.utc or unpack_tile_chunks_for(n * cw, n, sync=a.sync)
-    buf = (C.c_ulonglong * 8)()
+    buf = (C.c_ulonglong * 16)()
     ntiles = (n + utc - 1) // utc
     trace = torch.zeros(ntiles * 8, dtype=torch.int64, device="cuda")
     L.capnp_unpack_trace.argtypes = [vp]
