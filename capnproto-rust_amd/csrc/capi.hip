@@ -131,7 +131,10 @@ size_t round16(size_t x) { return (x + 15) & ~size_t(15); }
 
 constexpr size_t kTablePrefixBytes = 4096;  // >= 10 bytes x (1 + 256) table words
 // message bodies of at least this many words decode in parallel (read_body)
-constexpr uint64_t kParallelBodyWords = 32768;
+#ifndef PARALLEL_BODY_WORDS
+#define PARALLEL_BODY_WORDS 65536  // (32768: a 256 KiB read 224 us; 65536: 174; 131072: a 512 KiB read 353 vs 237)
+#endif
+constexpr uint64_t kParallelBodyWords = PARALLEL_BODY_WORDS;
 
 struct capnp_ctx {
     int device = 0;

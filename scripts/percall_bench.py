@@ -24,6 +24,8 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=400)
+    ap.add_argument("--sizes", default="128,512,1500,2048,8192,32768",
+                    help="message words, comma-separated")
     a = ap.parse_args()
     import torch  # noqa: F401
     import oracle_lib as O
@@ -33,7 +35,7 @@ def main():
     h = ctx.handle
     opts = _lib.ReaderOptionsC(0, 0, 64)
     rows = []
-    for words in (128, 512, 1500, 2048, 8192, 32768):
+    for words in [int(x) for x in a.sizes.split(",")]:
         offs = np.array([0, words], np.uint64)
         seg = O.gen_fill(offs, kind0=0, pz=O.PZ30)
         ptrs = (C.c_void_p * 1)(seg.ctypes.data)
