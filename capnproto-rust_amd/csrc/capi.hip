@@ -187,6 +187,13 @@ struct capnp_ctx {
 // drop-in's per-message cost (write_message / read_message at the
 // reference's call granularity).
 constexpr size_t kPinnedCall = size_t(4) << 20;
+// write_message past the one-launch kernel's size goes through the pinned
+// buffer up to this many staged bytes (its host copies are not pipelined
+// with the DMA, the runtime's pageable path is: larger messages take that)
+#ifndef WRITE_PIN_MAX
+#define WRITE_PIN_MAX kPinnedCall  // (1 MiB message: 137 vs 165 us pageable, 64 KiB 69 vs 85)
+#endif
+constexpr size_t kWritePinMax = WRITE_PIN_MAX;
 
 namespace {
 
@@ -1634,6 +1641,36 @@ capnp_status capnp_packed_write_message(capnp_ctx* ctx, const uint64_t* const* s
     capnp_status st = ensure_stage(ctx, o_dout + bound + 16);
     if (st != CAPNP_OK) return st;
     uint8_t* d = ctx->d_stage;
+    if (o_dout + bound + 16 <= kWritePinMax) {
+        // mid-sized: laid out in pinned memory, one DMA in, the batch pack, one
+        // DMA back of the offsets and the output bound, one wait (the
+        // pageable copies each went through the runtime's staging and its
+        // own synchronisation)
+        st = ensure_pin(ctx, o_dout + bound + 16);
+        if (st != CAPNP_OK) return st;
+        uint8_t* h = ctx->h_pin;
+        uint64_t* w = reinterpret_cast<uint64_t*>(h);
+        lay_out(w, reinterpret_cast<uint64_t*>(h + o_off));
+        uint64_t o = tw;
+        for (uint32_t i = 0; i < nseg; i++) {
+            if (seg_words[i]) memcpy(w + o, segs[i], (size_t)seg_words[i] * 8);
+            o += seg_words[i];
+        }
+        HIP_TRY(hipMemcpyAsync(d, h, o_oo, hipMemcpyHostToDevice, s));
+        const uint64_t wr[2] = {0, nw};
+        const uint32_t tc = nw / nch >= kWordTileMean ? 0u : tile_chunks_for(nw, nch);
+        st = pack_batch_dev(ctx, reinterpret_cast<uint64_t*>(d),
+                            reinterpret_cast<uint64_t*>(d + o_off), nch, d + o_dout, bound,
+                            reinterpret_cast<uint64_t*>(d + o_oo), tc, s, nullptr, wr);
+        if (st != CAPNP_OK) return st;
+        HIP_TRY(hipMemcpyAsync(h + o_oo, d + o_oo, o_dout - o_oo + bound, hipMemcpyDeviceToHost, s));
+        HIP_TRY(hipStreamSynchronize(s));
+        const uint64_t total = reinterpret_cast<const uint64_t*>(h + o_oo)[nch];
+        const size_t ncopy = std::min<uint64_t>(total, cap);
+        if (ncopy) memcpy(out, h + o_dout, ncopy);
+        *written = ncopy;
+        return total > cap ? CAPNP_E_BUFFER_NOT_LARGE_ENOUGH : CAPNP_OK;
+    }
     std::vector<uint64_t> small(tw);
     std::vector<uint64_t> off(nch + 1);
     lay_out(small.data(), off.data());
