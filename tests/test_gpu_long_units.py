@@ -129,3 +129,71 @@ def test_read_message_long_bodies_misaligned(ctx):
         for s in segs:
             assert np.array_equal(body[o:o + len(s)], s), nseg
             o += len(s)
+
+
+def _batch(ctx, units, mis=0, resync=False, cpt=0):
+    """Chunks back to back (mis junk bytes first); returns per-chunk words,
+    statuses and consumed counts from the batch (or index-free) decode."""
+    dev = torch.device("cuda", 0)
+    parts = [np.full(mis, 0x5A, np.uint8)] + [p for _, p, _ in units] + [np.zeros(32, np.uint8)]
+    buf = np.concatenate(parts)
+    inoff = np.cumsum([mis] + [len(p) for _, p, _ in units]).astype(np.int64)
+    outoff = np.cumsum([0] + [n for _, _, n in units]).astype(np.int64)
+    packed = torch.from_numpy(buf).to(dev)
+    ti = torch.from_numpy(inoff).to(dev)
+    to = torch.from_numpy(outoff).to(dev)
+    words = torch.zeros(max(int(outoff[-1]), 1), dtype=torch.int64, device=dev)
+    st = torch.full((len(units),), -1, dtype=torch.int32, device=dev)
+    used = torch.zeros(len(units), dtype=torch.int64, device=dev)
+    if resync:
+        ctx.unpack_batch_resync_into(packed, ti, to, words, st, used)
+    else:
+        ctx.unpack_batch_into(packed, ti, to, words, st, used, chunks_per_tile=cpt)
+    torch.cuda.synchronize()
+    return words.cpu().numpy().view(np.uint64), st.cpu().numpy(), used.cpu().numpy(), outoff
+
+
+@pytest.mark.parametrize("resync", [False, True])
+def test_big_staged_units_batch(ctx, resync):
+    """Overflow chunks of 2049..8192 words and <= 16 KiB packed take the
+    staged decode with the 8192-word / 16 KiB tables inside the long-unit LDS
+    (unpack.hip BigStageSmem); past either limit they take unpack_long.  Units
+    on both sides of both limits, zero-heavy (kind 1: 8192 and 8193 words,
+    a few hundred packed bytes) and literal-heavy ones, interleaved with short
+    chunks, plus malformed ones, against read_exact per chunk."""
+    rng = np.random.default_rng(11)
+    spec = [(2049, 0), (3800, 0), (3900, 0), (8192, 1), (8193, 1), (12000, 1),
+            (2040, 2), (2060, 2), (5000, 1), (64, 0), (7, 2), (8191, 1), (3000, 0)]
+    units = []
+    for i, (n, kind) in enumerate(spec):
+        w, p = _unit(n, kind, 500 + i)
+        units.append((w, p, n))
+    # malformed: a truncated big-path unit, a zero-heavy unit one word short
+    # (its last zero run overruns: DidNotEndCleanly), a literal-heavy cut
+    wb, pb = _unit(3000, 0, 601)
+    wz, pz = _unit(6000, 1, 602)
+    wl, pl = _unit(2030, 2, 603)
+    bad = [(wb, pb[:len(pb) - 37], 3000), (wz, pz, 5999), (wl, pl[:len(pl) // 2], 2030)]
+    for order in (units, units + bad, bad[:1] + units[::-1]):
+        for mis in (0, 9):
+            got, st, used, outoff = _batch(ctx, order, mis, resync)
+            for k, (w, p, n) in enumerate(order):
+                rst, rb, rused = O.read_exact(bytes(p), n * 8)
+                assert (int(st[k]), int(used[k])) == (rst, rused), (k, n, mis)
+                if rst == 0:
+                    assert np.array_equal(got[outoff[k]:outoff[k + 1]], w), (k, n, mis)
+
+
+@pytest.mark.parametrize("n,kind", [(8192, 1), (8193, 1), (3800, 0), (4000, 0), (10000, 0)])
+def test_big_and_long_unit_misaligned(ctx, n, kind):
+    """One chunk at each start misalignment 0..15 on both sides of the
+    staged-path limits (8192 words; 16 KiB packed: kind 0 crosses it between
+    3800 and 4000 words) with the next chunk's bytes after it."""
+    w, p = _unit(n, kind, 700 + n)
+    spare = _unit(64, 2, 98)[1]
+    for mis in range(16):
+        buf = np.concatenate([np.full(mis, 0xC3, np.uint8), p, spare, np.zeros(32, np.uint8)])
+        got, st, used = _decode(ctx, buf, mis, mis + len(p) + len(spare), n)
+        rst, rb, rused = O.read_exact(bytes(buf[mis:mis + len(p) + len(spare)]), n * 8)
+        assert st == rst == 0 and used == rused == len(p), mis
+        assert np.array_equal(got, w), mis
