@@ -293,11 +293,13 @@ struct Packer {
         return MODE == MODE_RING ? (uint32_t)(p & kRingMask) : (uint32_t)p;
     }
 
-    // One 64-word step.
+    // One 64-word step.  ext (last step only): the words past the step the
+    // run left open at its end goes on to absorb (a range that ends inside a
+    // chunk: msg_pack_kernel's split segment), counted into its count byte.
     template <int MODE>
     __device__ __forceinline__ void step(uint64_t w, uint32_t nvalid, bool last, uint32_t lane,
                                          uint8_t* buf, uint8_t* __restrict__ out,
-                                         const Sel8* sel) {
+                                         const Sel8* sel, uint32_t ext = 0) {
         const bool valid = lane < nvalid;
         const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
         const uint32_t tag = word_tag(lo, hi);
@@ -331,7 +333,7 @@ struct Packer {
         if (size) {
             // count byte of a Z/F head: words up to the next head (or step end)
             const uint64_t later = sm.H & ~low_mask(lane + 1);
-            const uint32_t cnt = later ? ctz64(later) - lane - 1 : nvalid - lane - 1;
+            const uint32_t cnt = later ? ctz64(later) - lane - 1 : nvalid - lane - 1 + ext;
             uint32_t r0, r1 = 0, r2 = 0;
             if (head && tag == 0) {
                 r0 = cnt << 8;
@@ -367,7 +369,7 @@ struct Packer {
         }
         // resolve a count carried in from earlier steps
         if (pend) {
-            pend_cnt += sm.absorbed_carry;
+            pend_cnt += sm.absorbed_carry + (sm.H == 0 ? ext : 0u);
             if (sm.absorbed_carry < 64 || last) {
                 wave_lds_sync();
                 if (lane == 0) buf[at<MODE>(pend_pos)] = (uint8_t)pend_cnt;
@@ -1092,6 +1094,9 @@ __device__ uint64_t tile_aggregate(const LookbackArgs& A, uint64_t j, uint32_t l
 #ifndef PACK_GROUP
 #define PACK_GROUP 63
 #endif
+#ifndef PACK_LB_FUSED
+#define PACK_LB_FUSED 0
+#endif
 constexpr uint32_t kGroup = PACK_GROUP;  // tiles per look-back group (<= 64: one lane per tile)
 constexpr int kSleep = 2;        // s_sleep between look-back polls (x 64 cycles)
 // group records per poll; measured: 64 -> 564 us, 16 -> 552, 4 -> 555, 1 -> 603
@@ -1135,6 +1140,15 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
     // aggregates of the group's earlier tiles
     uint64_t within;
     uint64_t st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
+#if PACK_LB_FUSED
+    // the first group-record window is read in the same round trip
+    uint64_t rec0;
+    {
+        const int64_t j = (int64_t)g - 1 - (int64_t)lane;
+        rec0 = lane >= kGroupWindow ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc);
+    }
+    bool first = true;
+#endif
     for (uint32_t spins = 0;;) {
         const uint64_t miss = ballot64((st >> 62) == 0);
         if (!miss) break;
@@ -1168,8 +1182,14 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
     for (uint32_t spins = 0; idx >= 0;) {
         const int64_t j = idx - (int64_t)lane;
         const bool in_win = lane < kGroupWindow;
+#if PACK_LB_FUSED
+        const uint64_t rec =
+            first ? rec0 : (!in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc));
+        first = false;
+#else
         const uint64_t rec =
             !in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc);
+#endif
         const uint64_t inc = ballot64((rec & kFlagInc) != 0);
         const uint32_t first_inc = ctz64(inc);
         const uint64_t need = first_inc < 64 ? low_mask(first_inc) : low_mask(kGroupWindow);
@@ -2921,8 +2941,25 @@ pack_wt_fix_sync(const uint64_t* __restrict__ chunk_off, const uint64_t* __restr
 // every chunk with the streaming path's pass A (wave w: chunks w, w + 4, ...),
 // places them by a scan and writes their bytes with pass B into the pinned
 // output.  No look-back state, no second launch, one wait on the host.
-constexpr uint32_t kMsgWords = 4096;   // words staged in LDS (table + segments)
+constexpr uint32_t kMsgWords = 8192;   // words staged in LDS (table + segments)
 constexpr uint32_t kMsgChunks = 516;   // word 0, the table rest, <= 511 segments (+ pad)
+constexpr uint32_t kMsgSplit = 256;    // a last chunk of this many words is split over the waves
+
+// Words from R on (up to `end`, the chunk's end) that the open run c absorbs.
+__device__ __forceinline__ uint32_t run_ext_at(const uint64_t* in, uint64_t R, uint64_t end,
+                                               Carry c, uint32_t lane) {
+    if (c.type == 0 || c.rem == 0) return 0;
+    uint32_t ext = 0;
+    for (uint64_t p = R; p < end; p += 64) {
+        const uint32_t nv = (uint32_t)(end - p < 64 ? end - p : 64);
+        const uint32_t tag = lane < nv ? tag_of(in[p + lane]) : 0u;
+        const bool cls = lane < nv && (c.type == 1 ? tag == 0 : __builtin_popcount(tag) >= 7);
+        const uint32_t lead = ctz64(~ballot64(cls));
+        ext += lead;
+        if (lead < 64 || ext >= c.rem) break;
+    }
+    return ext < c.rem ? ext : c.rem;
+}
 
 struct MsgPackSmem {
     Sel8 sel[kSelCopy + 1];
@@ -2930,6 +2967,7 @@ struct MsgPackSmem {
     uint64_t chunk_size[kMsgChunks];
     uint64_t chunk_pos[kMsgChunks];
     uint32_t wsum[kWaves];
+    uint32_t rsize[kWaves];  // split segment: packed bytes of each wave's range
     alignas(16) uint32_t pad[4];  // (emit ORs a zero into the dword before a region)
     alignas(16) uint8_t ring[kWaves][kRing];
     alignas(16) uint64_t words[kMsgWords];
@@ -2944,15 +2982,41 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
-    // stage: every load in flight at once (one round trip to host memory)
-    for (uint32_t i = tid; i <= nchunks; i += kThreads) S.off[i] = off[i];
+    // stage: every load in flight at once (one round trip to host memory).
+    // The offsets by buffer loads (lanes past them read 0: no branch, so no
+    // wait at a join), the words by LDS DMA in whole 64-vector groups (the
+    // host pads both regions to 16 bytes).  (Plain loops had waited for each
+    // iteration's loads before the next: a 1500-word message took five PCIe
+    // round trips to stage.)
+    constexpr uint32_t kOffIt = (kMsgChunks + 1 + kThreads - 1) / kThreads;
+    uint64_t ov[kOffIt];
     {
+        const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint64_t*>(off), 0, (int)((nchunks + 1) * 8), 0x00020000);
+#pragma unroll
+        for (uint32_t k = 0; k < kOffIt; k++) {
+            const auto x = __builtin_amdgcn_raw_buffer_load_b64(ors, (int)((tid + k * kThreads) * 8u), 0, 0);
+            ov[k] = ((uint64_t)x[1] << 32) | x[0];
+        }
         const uint4* w4 = reinterpret_cast<const uint4*>(words);
         uint4* s4 = reinterpret_cast<uint4*>(S.words);
-        for (uint32_t i = tid; i < nwords / 2; i += kThreads) s4[i] = w4[i];
-        if ((nwords & 1) && tid == 0) S.words[nwords - 1] = words[nwords - 1];
+        const uint32_t nvec = (nwords + 1) / 2;
+        for (uint32_t i0 = wave * CAPNP_WAVE; i0 < nvec; i0 += kThreads) {
+            const uint32_t i = i0 + lane;
+            if (i0 + CAPNP_WAVE <= nvec) {
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(w4 + i),
+                    (__attribute__((address_space(3))) void*)(s4 + i0), 16, 0, 0);
+            } else if (i < nvec) {
+                s4[i] = w4[i];
+            }
+        }
     }
     for (uint32_t i = tid; i <= kSelCopy; i += kThreads) S.sel[i] = kSel8Table.e[i];
+#pragma unroll
+    for (uint32_t k = 0; k < kOffIt; k++)
+        if (tid + k * kThreads <= nchunks) S.off[tid + k * kThreads] = ov[k];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's words are in
     __syncthreads();
     uint8_t* ring = S.ring[wave];
     // (the last chunk -- a message's one segment, usually the longest -- is
@@ -2960,17 +3024,53 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
     if (tid == 0) S.chunk_size[nchunks - 1] = 0;
     run_streaming<MODE_SIZE>(S.words, S.off, S.chunk_size, S.chunk_pos, nchunks - 1, wave, lane,
                              ring, S.sel, nullptr, 0, 0, nullptr);
+    // A long last chunk is split into one range per wave (64-word multiples):
+    // each wave takes the run state entering its range from the words before
+    // it (carry_into), sizes its range here and writes it in pass B, with the
+    // words its open run absorbs past the range end counted into the run's
+    // count byte (serialize_packed.rs:375-427 walk the chunk as one; the
+    // ranges reproduce that walk exactly).  One wave had walked it alone: 64
+    // serial steps for a 4096-word segment.
+    const uint32_t lc = nchunks - 1;
+    const uint64_t la = uniform64(S.off[lc]), lb = uniform64(S.off[nchunks]);
+    const bool split = lb - la >= kMsgSplit;
+    const uint64_t q = ((lb - la + kWaves - 1) / kWaves + 63) & ~63ull;
+    const uint64_t ra = la + wave * q < lb ? la + wave * q : lb;
+    const uint64_t rb = ra + q < lb ? ra + q : lb;
+    Carry rcarry{0, 0};
+    uint32_t rext = 0;
+    if (split) {
+        uint32_t sz = 0;
+        if (ra < rb) {
+            if (ra > la) rcarry = carry_into(S.words, la, ra, lane);
+            Packer pk;
+            pk.begin(0);
+            pk.carry = rcarry;
+            for (uint64_t p = ra; p < rb; p += 64) {
+                const uint32_t nv = (uint32_t)(rb - p < 64 ? rb - p : 64);
+                const uint64_t w = lane < nv ? S.words[p + lane] : 0ull;
+                pk.step<MODE_SIZE>(w, nv, p + 64 >= rb, lane, nullptr, nullptr, nullptr);
+            }
+            sz = (uint32_t)pk.total;
+            rext = run_ext_at(S.words, rb, lb, pk.carry, lane);
+        }
+        if (lane == 0) S.rsize[wave] = sz;
+    }
     __syncthreads();
     // chunk positions: exclusive scan of the sizes, up to 3 chunks per thread
     {
         constexpr uint32_t kPer = (kMsgChunks + kThreads - 1) / kThreads;
         uint32_t v[kPer], sum = 0;
+        uint32_t rsum = 0;
+#pragma unroll
+        for (int k = 0; k < kWaves; k++) rsum += split ? S.rsize[k] : 0u;
 #pragma unroll
         for (uint32_t k = 0; k < kPer; k++) {
             const uint32_t i = tid * kPer + k;
-            v[k] = i < nchunks ? (uint32_t)S.chunk_size[i] : 0u;
+            v[k] = i < nchunks ? (split && i == lc ? rsum : (uint32_t)S.chunk_size[i]) : 0u;
             sum += v[k];
         }
+        if (split && tid == 0) S.chunk_size[lc] = rsum;
         const uint32_t inc = wave_incl_scan(sum);
         if (lane == CAPNP_WAVE - 1) S.wsum[wave] = inc;
         __syncthreads();
@@ -2995,8 +3095,25 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
     uint8_t* const dst = scratch ? scratch : out;
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
     uint64_t* last = reinterpret_cast<uint64_t*>(S.chunk_size + nchunks - 1);
-    run_streaming<MODE_RING>(S.words, S.off, S.chunk_size, S.chunk_pos, nchunks, wave, lane, ring,
-                             S.sel, dst - mis, mis, out_cap, nullptr, last);
+    run_streaming<MODE_RING>(S.words, S.off, S.chunk_size, S.chunk_pos, split ? lc : nchunks, wave,
+                             lane, ring, S.sel, dst - mis, mis, out_cap, nullptr,
+                             split ? nullptr : last);
+    if (split && ra < rb) {
+        const uint64_t cpos = lds_u64(&S.chunk_pos[lc]);
+        if (cpos + lds_u64(&S.chunk_size[lc]) <= out_cap) {  // (as run_streaming: fits or none)
+            uint32_t before = 0;
+            for (uint32_t k = 0; k < wave; k++) before += S.rsize[k];
+            Packer pk;
+            pk.begin(cpos + before + mis);
+            pk.carry = rcarry;
+            for (uint64_t p = ra; p < rb; p += 64) {
+                const uint32_t nv = (uint32_t)(rb - p < 64 ? rb - p : 64);
+                const bool lst = p + 64 >= rb;
+                const uint64_t w = lane < nv ? S.words[p + lane] : 0ull;
+                pk.step<MODE_RING>(w, nv, lst, lane, ring, dst - mis, S.sel, lst ? rext : 0u);
+            }
+        }
+    }
     __syncthreads();
     const uint64_t tot = S.chunk_pos[nchunks - 1] + S.chunk_size[nchunks - 1];
     if (scratch) {

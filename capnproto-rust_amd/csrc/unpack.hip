@@ -2510,10 +2510,24 @@ msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_all
     constexpr uint32_t kPreVec = kLuStage / 16 - 1;
     const uint32_t pre = (uint32_t)(in_len < 16ull * kPreVec ? in_len : 16ull * kPreVec);
     {
+        // (LDS DMA for whole 64-vector groups, as unpack_long's windows: every
+        // load in flight at once.  The plain loop had waited for each
+        // iteration's loads before the next: one PCIe round trip per 4 KiB)
         const uint4* src = reinterpret_cast<const uint4*>(in);
         uint4* dst = reinterpret_cast<uint4*>(sm.lu.bytes);
-        for (uint32_t i = tid; i < kLuStage / 16; i += kThreads)
-            dst[i] = 16u * i < pre ? src[i] : make_uint4(0, 0, 0, 0);
+        const uint32_t nblk = (pre + 15) / 16;
+        constexpr uint32_t kVec = kLuStage / 16;
+        for (uint32_t i0 = wave * CAPNP_WAVE; i0 < kVec; i0 += kThreads) {
+            const uint32_t i = i0 + lane;
+            if (i0 + CAPNP_WAVE <= nblk) {
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(src + i),
+                    (__attribute__((address_space(3))) void*)(sm.lu.bytes + 16u * i0), 16, 0, 0);
+            } else if (i < kVec) {
+                dst[i] = i < nblk ? src[i] : make_uint4(0, 0, 0, 0);
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's bytes are in
     }
     __syncthreads();
     if (tid == 0) {

@@ -132,6 +132,53 @@ def test_message_round_trip_vs_oracle(ctx):
             assert np.array_equal(a, b)
 
 
+def _runs_segment(rng, n):
+    """Words built from runs whose lengths straddle the split ranges of a
+    long last segment (msg_pack_kernel: 64-word multiples per wave): zero
+    runs and 0xFF runs of 1..700 words (past the 255-word cap), runs of
+    words with one zero byte (absorbed by a 0xFF run, not heads of one),
+    and breakers."""
+    w = np.zeros(n, np.uint64)
+    i = 0
+    while i < n:
+        k = min(n - i, rng.choice([1, 2, 63, 64, 65, 127, 128, 129, 191, 255, 256, 257, 300,
+                                   511, 700]))
+        kind = rng.randrange(5)
+        if kind == 0:
+            pass  # zero words
+        elif kind == 1:
+            w[i:i + k] = 0x0102030405060708  # 0xFF words
+        elif kind == 2:
+            w[i] = 0x1111111111111111
+            w[i + 1:i + k] = 0x0011223344556677  # one zero byte: absorbed by a 0xFF run
+        elif kind == 3:
+            w[i:i + k] = 0x0000FF000000AB00  # 2 non-zero bytes: breakers
+        else:
+            for j in range(i, i + k):
+                w[j] = rng.getrandbits(64) & rng.choice([0, 0xFFFFFFFFFFFFFFFF,
+                                                          0x00FF00FF00FF00FF])
+        i += k
+    return w
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_message_split_segment_vs_oracle(ctx, seed):
+    """A long last segment is packed by all four waves of the one-launch
+    write (csrc/pack.hip msg_pack_kernel, ranges with the run state carried
+    in and the open run's count continued past the range end): byte-equal
+    to the oracle's write_message for segments of 256..8184 words built from
+    runs across the range boundaries, after 0..3 short segments."""
+    from capnp_amd import serialize_packed as sp
+    rng = random.Random(1000 + seed)
+    for n in (256, 257, 300, 511, 1024, 1500, 2047, 4000, 4096 - 8, 6000, 8192 - 8):
+        head = [_rand_segment(rng, rng.choice([0, 1, 5])) for _ in range(rng.randrange(0, 4))]
+        segs = head + [_runs_segment(rng, n)]
+        out = bytearray()
+        sp.write_message(out, segs, ctx=ctx)
+        st, ref = O.write_message(segs)
+        assert st == 0 and bytes(out) == ref, (seed, n)
+
+
 # ---------------------------------------------------------------- batch API
 def _check_batch(ctx, words, offs, tc=0, utcs=(0, 1, 7, 256)):
     st, ref, ref_offs = O.pack_batch(words, offs)
