@@ -1086,16 +1086,18 @@ __device__ uint64_t tile_aggregate(const LookbackArgs& A, uint64_t j, uint32_t l
 // the group's tiles and the group window together, one round trip when all
 // is published, 524 vs 506 us (the tile's wait is the group chain, not the
 // polls); a persistent grid pipelining each tile's look-back behind the next
-// tile's pass 1 (4 workgroups per CU) 1262 vs 472 us.
+// tile's pass 1 (4 workgroups per CU) 1262 vs 472 us.  Round 5 (config 2,
+// with the index): the first group window read in the same round trip as the
+// group's tile records: 453.5 vs 442.7 us, carsales 476.7 vs 462.5; the
+// look-back still takes 2.9 us because both polls fail about once a tile
+// (scripts/pack_prof.py: 1.0 failed tile polls and 1.0 -> 1.7 failed window
+// polls per tile; profiles/r05x_pack_lookback.txt).
 //
 // Every wait is bounded: on timeout the waiter computes the missing aggregate
 // itself from the input (records are idempotent), so the kernel finishes with
 // the right answer under any workgroup dispatch order.
 #ifndef PACK_GROUP
 #define PACK_GROUP 63
-#endif
-#ifndef PACK_LB_FUSED
-#define PACK_LB_FUSED 0
 #endif
 constexpr uint32_t kGroup = PACK_GROUP;  // tiles per look-back group (<= 64: one lane per tile)
 constexpr int kSleep = 2;        // s_sleep between look-back polls (x 64 cycles)
@@ -1140,15 +1142,6 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
     // aggregates of the group's earlier tiles
     uint64_t within;
     uint64_t st = lane < r ? poll_agent(&A.ts[g * kGroup + lane]) : kFlagAgg;
-#if PACK_LB_FUSED
-    // the first group-record window is read in the same round trip
-    uint64_t rec0;
-    {
-        const int64_t j = (int64_t)g - 1 - (int64_t)lane;
-        rec0 = lane >= kGroupWindow ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc);
-    }
-    bool first = true;
-#endif
     for (uint32_t spins = 0;;) {
         const uint64_t miss = ballot64((st >> 62) == 0);
         if (!miss) break;
@@ -1182,14 +1175,8 @@ __device__ uint64_t lookback(const LookbackArgs& A, uint64_t t, uint64_t agg, ui
     for (uint32_t spins = 0; idx >= 0;) {
         const int64_t j = idx - (int64_t)lane;
         const bool in_win = lane < kGroupWindow;
-#if PACK_LB_FUSED
-        const uint64_t rec =
-            first ? rec0 : (!in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc));
-        first = false;
-#else
         const uint64_t rec =
             !in_win ? 0 : (j >= 0 ? poll_agent(&A.gs[j]) : kFlagInc);
-#endif
         const uint64_t inc = ballot64((rec & kFlagInc) != 0);
         const uint32_t first_inc = ctz64(inc);
         const uint64_t need = first_inc < 64 ? low_mask(first_inc) : low_mask(kGroupWindow);
