@@ -679,14 +679,14 @@ __device__ __forceinline__ void copy_out(const uint8_t* region, uint8_t* __restr
 
 // Streaming path: wave w owns chunks w, w+4, ...  MODE_SIZE fills
 // chunk_size; MODE_RING re-reads and writes at chunk_pos.
-template <int MODE>
+template <int MODE, uint32_t NWV = kWaves>
 __device__ void run_streaming(const uint64_t* __restrict__ in, const uint64_t* off,
                               uint64_t* chunk_size, const uint64_t* chunk_pos, uint32_t nc,
                               uint32_t wave, uint32_t lane, uint8_t* ring, const Sel8* sel,
                               uint8_t* out, uint32_t mis, uint64_t out_cap,
                               const uint32_t* cgap, uint64_t* last_size = nullptr) {
     Packer pk;
-    for (uint32_t ci = wave; ci < nc; ci += kWaves) {
+    for (uint32_t ci = wave; ci < nc; ci += NWV) {
         const uint64_t woff = uniform64(off[ci]);
         const uint64_t len = uniform64(off[ci + 1]) - woff;
         const uint32_t g = cgap ? uniform(cgap[ci]) : 0u;  // leading gap bytes
@@ -2925,12 +2925,16 @@ pack_wt_fix_sync(const uint64_t* __restrict__ chunk_off, const uint64_t* __restr
 // The host lays the message's write_all chunks out in pinned memory (word 0
 // of the table, the rest of the table, each segment) with their word
 // offsets; one workgroup stages the words into LDS in one round trip, sizes
-// every chunk with the streaming path's pass A (wave w: chunks w, w + 4, ...),
+// every chunk with the streaming path's pass A (wave w: chunks w, w + 16, ...),
 // places them by a scan and writes their bytes with pass B into the pinned
 // output.  No look-back state, no second launch, one wait on the host.
-constexpr uint32_t kMsgWords = 8192;   // words staged in LDS (table + segments)
+constexpr uint32_t kMsgWords = 8448;   // words staged in LDS (table + segments: 64 KiB and a table)
 constexpr uint32_t kMsgChunks = 516;   // word 0, the table rest, <= 511 segments (+ pad)
 constexpr uint32_t kMsgSplit = 256;    // a last chunk of this many words is split over the waves
+// 16 waves (4 per SIMD): a wave's steps are chains of dependent LDS and
+// scalar work, and one wave per SIMD left each SIMD idle between them
+constexpr uint32_t kMsgWaves = 16;
+constexpr uint32_t kMsgThreads = kMsgWaves * CAPNP_WAVE;
 
 // Words from R on (up to `end`, the chunk's end) that the open run c absorbs.
 __device__ __forceinline__ uint32_t run_ext_at(const uint64_t* in, uint64_t R, uint64_t end,
@@ -2953,14 +2957,14 @@ struct MsgPackSmem {
     uint64_t off[kMsgChunks + 1];
     uint64_t chunk_size[kMsgChunks];
     uint64_t chunk_pos[kMsgChunks];
-    uint32_t wsum[kWaves];
-    uint32_t rsize[kWaves];  // split segment: packed bytes of each wave's range
+    uint32_t wsum[kMsgWaves];
+    uint32_t rsize[kMsgWaves];  // split segment: packed bytes of each wave's range
     alignas(16) uint32_t pad[4];  // (emit ORs a zero into the dword before a region)
-    alignas(16) uint8_t ring[kWaves][kRing];
+    alignas(16) uint8_t ring[kMsgWaves][kRing];
     alignas(16) uint64_t words[kMsgWords];
 };
 
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kMsgThreads)
 msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__ off,
                 uint32_t nchunks, uint32_t nwords, uint8_t* __restrict__ out, uint64_t out_cap,
                 uint64_t* __restrict__ total, uint32_t* __restrict__ flag, uint32_t seq,
@@ -2975,20 +2979,20 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
     // host pads both regions to 16 bytes).  (Plain loops had waited for each
     // iteration's loads before the next: a 1500-word message took five PCIe
     // round trips to stage.)
-    constexpr uint32_t kOffIt = (kMsgChunks + 1 + kThreads - 1) / kThreads;
+    constexpr uint32_t kOffIt = (kMsgChunks + 1 + kMsgThreads - 1) / kMsgThreads;
     uint64_t ov[kOffIt];
     {
         const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(
             const_cast<uint64_t*>(off), 0, (int)((nchunks + 1) * 8), 0x00020000);
 #pragma unroll
         for (uint32_t k = 0; k < kOffIt; k++) {
-            const auto x = __builtin_amdgcn_raw_buffer_load_b64(ors, (int)((tid + k * kThreads) * 8u), 0, 0);
+            const auto x = __builtin_amdgcn_raw_buffer_load_b64(ors, (int)((tid + k * kMsgThreads) * 8u), 0, 0);
             ov[k] = ((uint64_t)x[1] << 32) | x[0];
         }
         const uint4* w4 = reinterpret_cast<const uint4*>(words);
         uint4* s4 = reinterpret_cast<uint4*>(S.words);
         const uint32_t nvec = (nwords + 1) / 2;
-        for (uint32_t i0 = wave * CAPNP_WAVE; i0 < nvec; i0 += kThreads) {
+        for (uint32_t i0 = wave * CAPNP_WAVE; i0 < nvec; i0 += kMsgThreads) {
             const uint32_t i = i0 + lane;
             if (i0 + CAPNP_WAVE <= nvec) {
                 __builtin_amdgcn_global_load_lds(
@@ -2999,17 +3003,17 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
             }
         }
     }
-    for (uint32_t i = tid; i <= kSelCopy; i += kThreads) S.sel[i] = kSel8Table.e[i];
+    for (uint32_t i = tid; i <= kSelCopy; i += kMsgThreads) S.sel[i] = kSel8Table.e[i];
 #pragma unroll
     for (uint32_t k = 0; k < kOffIt; k++)
-        if (tid + k * kThreads <= nchunks) S.off[tid + k * kThreads] = ov[k];
+        if (tid + k * kMsgThreads <= nchunks) S.off[tid + k * kMsgThreads] = ov[k];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's words are in
     __syncthreads();
     uint8_t* ring = S.ring[wave];
     // (the last chunk -- a message's one segment, usually the longest -- is
     // placed without its size: pass B measures it)
     if (tid == 0) S.chunk_size[nchunks - 1] = 0;
-    run_streaming<MODE_SIZE>(S.words, S.off, S.chunk_size, S.chunk_pos, nchunks - 1, wave, lane,
+    run_streaming<MODE_SIZE, kMsgWaves>(S.words, S.off, S.chunk_size, S.chunk_pos, nchunks - 1, wave, lane,
                              ring, S.sel, nullptr, 0, 0, nullptr);
     // A long last chunk is split into one range per wave (64-word multiples):
     // each wave takes the run state entering its range from the words before
@@ -3021,7 +3025,7 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
     const uint32_t lc = nchunks - 1;
     const uint64_t la = uniform64(S.off[lc]), lb = uniform64(S.off[nchunks]);
     const bool split = lb - la >= kMsgSplit;
-    const uint64_t q = ((lb - la + kWaves - 1) / kWaves + 63) & ~63ull;
+    const uint64_t q = ((lb - la + kMsgWaves - 1) / kMsgWaves + 63) & ~63ull;
     const uint64_t ra = la + wave * q < lb ? la + wave * q : lb;
     const uint64_t rb = ra + q < lb ? ra + q : lb;
     Carry rcarry{0, 0};
@@ -3046,11 +3050,11 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
     __syncthreads();
     // chunk positions: exclusive scan of the sizes, up to 3 chunks per thread
     {
-        constexpr uint32_t kPer = (kMsgChunks + kThreads - 1) / kThreads;
+        constexpr uint32_t kPer = (kMsgChunks + kMsgThreads - 1) / kMsgThreads;
         uint32_t v[kPer], sum = 0;
         uint32_t rsum = 0;
 #pragma unroll
-        for (int k = 0; k < kWaves; k++) rsum += split ? S.rsize[k] : 0u;
+        for (int k = 0; k < kMsgWaves; k++) rsum += split ? S.rsize[k] : 0u;
 #pragma unroll
         for (uint32_t k = 0; k < kPer; k++) {
             const uint32_t i = tid * kPer + k;
@@ -3063,7 +3067,7 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
         __syncthreads();
         uint32_t run = inc - sum, all = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < (uint32_t)kWaves; k++) {
+        for (uint32_t k = 0; k < (uint32_t)kMsgWaves; k++) {
             if (k < wave) run += S.wsum[k];
             all += S.wsum[k];
         }
@@ -3082,7 +3086,7 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
     uint8_t* const dst = scratch ? scratch : out;
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
     uint64_t* last = reinterpret_cast<uint64_t*>(S.chunk_size + nchunks - 1);
-    run_streaming<MODE_RING>(S.words, S.off, S.chunk_size, S.chunk_pos, split ? lc : nchunks, wave,
+    run_streaming<MODE_RING, kMsgWaves>(S.words, S.off, S.chunk_size, S.chunk_pos, split ? lc : nchunks, wave,
                              lane, ring, S.sel, dst - mis, mis, out_cap, nullptr,
                              split ? nullptr : last);
     if (split && ra < rb) {
@@ -3109,7 +3113,7 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
         const uint64_t nv = ((tot < out_cap ? tot : out_cap) + 15) / 16;
         const uint4* s4 = reinterpret_cast<const uint4*>(scratch);
         uint4* o4 = reinterpret_cast<uint4*>(out);
-        for (uint64_t i = tid; i < nv; i += kThreads) o4[i] = s4[i];
+        for (uint64_t i = tid; i < nv; i += kMsgThreads) o4[i] = s4[i];
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's stores have landed)
     __syncthreads();
@@ -3313,7 +3317,7 @@ extern "C" hipError_t capnp_launch_msg_pack(const uint64_t* words, const uint64_
                                             uint32_t seq, uint8_t* scratch, hipStream_t stream) {
     if (nwords > kMsgWords || nchunks + 1 > kMsgChunks || nchunks == 0)
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL(msg_pack_kernel, dim3(1), dim3(kThreads), 0, stream, words, off, nchunks,
+    hipLaunchKernelGGL(msg_pack_kernel, dim3(1), dim3(kMsgThreads), 0, stream, words, off, nchunks,
                        nwords, out, out_cap, total, flag, seq, scratch);
     return hipGetLastError();
 }
