@@ -1091,7 +1091,11 @@ __device__ uint64_t tile_aggregate(const LookbackArgs& A, uint64_t j, uint32_t l
 // group's tile records: 453.5 vs 442.7 us, carsales 476.7 vs 462.5; the
 // look-back still takes 2.9 us because both polls fail about once a tile
 // (scripts/pack_prof.py: 1.0 failed tile polls and 1.0 -> 1.7 failed window
-// polls per tile; profiles/r05x_pack_lookback.txt).
+// polls per tile; profiles/r05x_pack_lookback.txt).  A second copy of each
+// poll issued 4 / 8 / 16 x 64 cycles after the first (used when the first
+// misses, so a miss costs that delay instead of a round trip): 449 / 447 /
+// 444 vs 434.5 us, carsales 480 / 479 / 472 vs 461 -- the extra uncached
+// reads cost more than the round trips they save.
 //
 // Every wait is bounded: on timeout the waiter computes the missing aggregate
 // itself from the input (records are idempotent), so the kernel finishes with
