@@ -2470,6 +2470,164 @@ unpack_wt_finish(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
 }
 
 // ---------------------------------------------------------------------------
+// A short read unit already staged in the long-unit buffer (read_message's
+// one-launch kernel): wave 0 decodes it alone with the in-tile segment walk's
+// rules (spec_seg_tile) on 64 segments -- the spec walk with its lead-in, the
+// meet / repair rounds by shuffles, the word scan, the segment holding word n
+// walking to it with every check -- and writes the descriptors; then the
+// four waves expand.  unpack_long's workgroup-wide scans and barriers cost
+// about a microsecond a round at these sizes (a 1 KiB body: 6.6 us of its
+// phases).  B = the unit's byte 0 (LDS position mis), L = the bytes the walks
+// may use (staged, <= kSmallBytes), n = the words.  Returns false with
+// nothing written to `out` when the unit does not check out within L bytes
+// (malformed, truncated, or longer than L): the caller then takes
+// unpack_long, which gives the exact status.
+constexpr uint32_t kSmallBytes = 3072;  // (r05z: 1.5-6.5 KB bodies were as fast or faster on unpack_long)
+constexpr uint32_t kSmallLead = 48;  // (spec_seg_tile's kSegOverlap)
+
+__device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
+                             uint64_t* __restrict__ out, uint32_t tid, uint32_t lane,
+                             uint32_t wave, uint32_t& used) {
+    const uint8_t* B = S.bytes + mis;
+    S.sel[tid] = kExpandTable.s[tid];
+    {
+        uint4* d4 = reinterpret_cast<uint4*>(S.dpos);
+        const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
+        for (uint32_t k = tid; k < (n + 7) / 8; k += kThreads) d4[k] = none;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const uint32_t j = lane;
+        const uint32_t sb = (uint32_t)(((uint64_t)L * j) >> 6);
+        const uint32_t se = (uint32_t)(((uint64_t)L * (j + 1u)) >> 6);
+        // spec walk from kSmallLead bytes before the segment (lane 0: byte 0)
+        uint32_t p = j == 0 ? 0u : (sb > kSmallLead ? sb - kSmallLead : 0u), w = 0;
+        while (p < sb) seg_hop(B, p, w);
+        const uint32_t f = p, wf = w;
+        while (p < se) seg_hop(B, p, w);
+        const bool serr = p > L;
+        const uint32_t xs = serr ? 0u : p, ws = w - wf;
+        // (a spec walk that found no record start in its segment owns no exit)
+        const uint32_t xsp = (serr || f >= se) ? 0u : xs;
+        // meet / repair rounds (unpack_long's rules on one wave of 64
+        // segments): each round settles at least one more segment
+        uint32_t own = xsp, x = xsp, wd = ws;
+        bool err = j == 0 && serr;
+        uint32_t e_used = j == 0 ? 0u : ~0u;
+        for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)x, d, 64);
+            if (j >= d) x = max(x, t);
+        }
+        bool ok = true;
+        for (uint32_t round = 0;; round++) {
+            const uint32_t xu = (uint32_t)__shfl_up((int)x, 1, 64);
+            const uint32_t e = j == 0 ? 0u : xu;
+            const bool need = e != e_used;
+            if (ballot64(need) == 0) break;
+            if (round > CAPNP_WAVE + 1) {  // (not reached: lane i is settled after round i + 1)
+                ok = false;
+                break;
+            }
+            if (need) {
+                e_used = e;
+                if (e < sb || e == f) {
+                    // (an entry below the segment -- a predecessor not settled
+                    // yet -- lets the spec walk stand in: a far garbage exit
+                    // of a missed spec walk then cannot send its successors
+                    // walking from far back once it is repaired)
+                    own = xsp;
+                    wd = ws;
+                    err = serr;
+                } else {
+                    // from the entry with the spec chain kept in step (unpack_long's
+                    // meet rule): where they meet, the rest is the spec walk's, so
+                    // a repair is short and the successors' entries stand
+                    uint32_t pt = e, wt = 0, ps = f, wsp = 0;
+                    bool met = false;
+                    while (pt < se) {
+                        while (ps < pt && ps < se) seg_hop(B, ps, wsp);
+                        if (ps == pt) {
+                            met = true;
+                            break;
+                        }
+                        seg_hop(B, pt, wt);
+                    }
+                    if (met) {
+                        own = xsp;
+                        wd = wt + ws - wsp;
+                        err = serr;
+                    } else {
+                        err = pt > L;
+                        own = (err || e >= se) ? 0u : pt;
+                        wd = wt;
+                    }
+                }
+            }
+            x = own;
+            for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
+                const uint32_t t = (uint32_t)__shfl_up((int)x, d, 64);
+                if (j >= d) x = max(x, t);
+            }
+        }
+        const uint32_t e = e_used;
+        // words: the segment holding word n walks to it with every check
+        uint32_t incl = wd;
+        for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, d, 64);
+            if (j >= d) incl += t;
+        }
+        const uint32_t base = incl - wd;
+        const uint64_t hold = ballot64(wd > 0 && base < n && n <= incl);
+        const uint32_t ts = hold ? (uint32_t)__builtin_ctzll(hold) : CAPNP_WAVE;
+        ok = ok && ts < CAPNP_WAVE && ballot64(err && j <= ts) == 0;
+        uint32_t q = e, wq = base;
+        bool fine = true;
+        if (ok && j == ts) {
+            while (wq < n) {
+                uint32_t tag, b1, b9;
+                rec_bytes(B, q + 1u, tag, b1, b9);
+                const bool isz = tag == 0, isf = tag == 0xFF;
+                const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+                const uint32_t qe = q + 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) +
+                                    (isf ? 8u * cnt : 0u);
+                const uint32_t wn = wq + 1u + cnt;
+                if (qe > L || wn > n) {
+                    fine = false;
+                    break;
+                }
+                q = qe;
+                wq = wn;
+            }
+        }
+        ok = ok && ballot64(j == ts && !fine) == 0;
+        used = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)(ts < CAPNP_WAVE ? ts : 0u));
+        // descriptors of the records from each entry (to word n in the last)
+        if (ok && j <= ts) {
+            uint32_t r = e, wr = base;
+            const uint32_t wlim = j == ts ? n : incl;
+            while (wr < wlim) {
+                uint32_t tag, b1, b9;
+                rec_bytes(B, r + 1u, tag, b1, b9);
+                const bool isz = tag == 0, isf = tag == 0xFF;
+                const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+                const uint32_t lp = r + mis;  // (LDS position of the tag)
+                S.dpos[wr] = (uint16_t)lp;
+                if (isf)
+                    for (uint32_t i = 0; i < cnt; i++)
+                        S.dpos[wr + 1u + i] = (uint16_t)(kRaw | (lp + 10u + 8u * i));
+                wr += 1u + cnt;
+                r += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) + (isf ? 8u * cnt : 0u);
+            }
+        }
+        if (lane == 0) S.misc[0] = ok ? 1u : 0u;
+    }
+    __syncthreads();
+    if (S.misc[0] == 0) return false;
+    for (uint32_t i = tid; i < n; i += kThreads) out[i] = expand_desc(S.bytes, S.sel, S.dpos[i]);
+    return true;
+}
+
+// ---------------------------------------------------------------------------
 // One read_message call in one launch (the drop-in at the reference's call
 // granularity: serialize_packed::read_message / try_read_message /
 // read_message_no_alloc once per message, serialize_packed.rs:233-291,
@@ -2544,8 +2702,27 @@ msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_all
         M.used = 0;
     }
     __syncthreads();
-    if (M.fr.status == 0 && M.offs[3] > 0)  // (uniform: LDS after the barrier)
-        unpack_long(sm, in, M.offs, 0, words, M.offs + 2, &M.st, &M.used, tid, lane, wave, pre);
+    if (M.fr.status == 0 && M.offs[3] > 0) {  // (uniform: LDS after the barrier)
+        // a short body inside the staged prefix: wave 0 alone (unpack_small);
+        // the rest, and any body it does not take, unpack_long
+        const uint64_t P0 = M.offs[0], nw = M.offs[3];
+        const uint64_t avail = (uint64_t)pre > P0 ? pre - P0 : 0;
+        const uint64_t span = in_len - P0 < avail ? in_len - P0 : avail;
+        const uint64_t Ls = span < 10 * nw + 16 ? span : 10 * nw + 16;
+        bool done = false;
+        if (Ls > 0 && Ls <= kSmallBytes && nw <= kLuWords) {
+            uint32_t used = 0;
+            done = unpack_small(sm.lu, (uint32_t)P0, (uint32_t)Ls, (uint32_t)nw, words, tid, lane,
+                                wave, used);
+            if (done && tid == 0) {
+                M.st = 0;
+                M.used = used;
+            }
+        }
+        if (!done)
+            unpack_long(sm, in, M.offs, 0, words, M.offs + 2, &M.st, &M.used, tid, lane, wave,
+                        pre);
+    }
     __syncthreads();
     // results out: the frame record (whole 16-byte vectors) and {status, 0, consumed}
     {

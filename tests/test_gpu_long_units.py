@@ -197,3 +197,63 @@ def test_big_and_long_unit_misaligned(ctx, n, kind):
         rst, rb, rused = O.read_exact(bytes(buf[mis:mis + len(p) + len(spare)]), n * 8)
         assert st == rst == 0 and used == rused == len(p), mis
         assert np.array_equal(got, w), mis
+
+
+
+def _read_message_call(handle, data):
+    from capnp_amd import _lib
+    L = _lib.lib()
+    opts = _lib.ReaderOptionsC(0, 0, 64)
+    data = np.frombuffer(bytes(data), np.uint8).copy()
+    cap = len(data) * 128 + 64
+    body = np.zeros(cap + 1, np.uint64)
+    sw = np.zeros(512, np.uint32)
+    ns, used = C.c_uint32(0), C.c_size_t(0)
+    r = L.capnp_packed_read_message(handle, data.ctypes.data, len(data), C.byref(opts), 0,
+                                    body.ctypes.data, cap + 1, sw.ctypes.data, C.byref(ns),
+                                    C.byref(used))
+    return r, body, used.value
+
+
+def _packed(words):
+    st, b = O.pack(np.asarray(words, np.uint64).tobytes())
+    assert st == 0
+    return b
+
+
+def test_read_message_small_bodies_vs_oracle(ctx):
+    """read_message's short bodies (csrc/unpack.hip unpack_small: wave 0
+    alone, 64 segments, inside the staged prefix) against the oracle's
+    read_message: valid bodies of 1..1600 words of every fill kind, alone
+    and with the next message's bytes after them; truncated inputs; tables
+    claiming fewer words than the body's records cover (the last run
+    overruns); random bytes after a valid table -- status, consumed bytes
+    and the segment words."""
+    rng = np.random.default_rng(21)
+    cases = []
+    for k in (1, 2, 7, 64, 65, 128, 300, 777, 1500, 1600):
+        for kind in (0, 1, 2):
+            w = O.gen_fill(np.array([0, k], np.uint64), kinds=np.array([kind], np.uint8),
+                           pz=O.PZ30, id0=900 + k + kind)
+            st, msg = O.write_message([w])
+            assert st == 0 and msg == _packed([k << 32]) + _packed(w)
+            cases.append(msg)
+            cases.append(msg + O.write_message([w[:3]])[1])  # the next message follows
+            cases.append(msg[:len(msg) - 1])                  # truncated by a byte
+            cases.append(msg[:max(9, len(msg) // 2)])         # truncated in the body
+            if k > 1:  # the table claims one word fewer than the records cover
+                cases.append(_packed([(k - 1) << 32]) + _packed(w))
+    for i in range(40):  # a valid one-segment table, then random body bytes
+        k = int(rng.integers(1, 400))
+        body = rng.integers(0, 256, int(rng.integers(1, 12 * k))).astype(np.uint8).tobytes()
+        cases.append(_packed([k << 32]) + body)
+    for data in cases:
+        rst, rsegs, rused = O.read_message(bytes(data))
+        r, body, used = _read_message_call(ctx.handle, data)
+        assert r == rst, (len(data), r, rst)
+        if rst == 0:
+            assert used == rused, (len(data), used, rused)
+            o = 0
+            for sgm in rsegs:
+                assert np.array_equal(body[o:o + len(sgm)], sgm)
+                o += len(sgm)
