@@ -2935,6 +2935,11 @@ pack_wt_fix_sync(const uint64_t* __restrict__ chunk_off, const uint64_t* __restr
 constexpr uint32_t kMsgWords = 8448;   // words staged in LDS (table + segments: 64 KiB and a table)
 constexpr uint32_t kMsgChunks = 516;   // word 0, the table rest, <= 511 segments (+ pad)
 constexpr uint32_t kMsgSplit = 256;    // a last chunk of this many words is split over the waves
+// (64: a 128-word write 13.9 vs 13.1 us, 1500 words the same: r05z)
+// messages of at most this many words flush straight to the output (the few
+// 16-byte flushes cost less than the copy's device round trip: 128 words
+// 12.8 vs 13.1 us, 256 13.9 vs 14.2; 512 and up the same, r05z)
+constexpr uint32_t kMsgDirect = 512;
 // 16 waves (4 per SIMD): a wave's steps are chains of dependent LDS and
 // scalar work, and one wave per SIMD left each SIMD idle between them
 constexpr uint32_t kMsgWaves = 16;
@@ -3087,7 +3092,9 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
     // (pass B's flushes go to device memory -- a step's bytes in 16-byte
     // stores that a PCIe write path would take one at a time -- and the
     // packed bytes cross to the host output in one coalesced copy)
-    uint8_t* const dst = scratch ? scratch : out;
+    // (a short message's few flushes go straight out: kMsgDirect)
+    const bool via = scratch && nwords > kMsgDirect;
+    uint8_t* const dst = via ? scratch : out;
     const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(dst) & 15u);
     uint64_t* last = reinterpret_cast<uint64_t*>(S.chunk_size + nchunks - 1);
     run_streaming<MODE_RING, kMsgWaves>(S.words, S.off, S.chunk_size, S.chunk_pos, split ? lc : nchunks, wave,
@@ -3111,7 +3118,7 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
     }
     __syncthreads();
     const uint64_t tot = S.chunk_pos[nchunks - 1] + S.chunk_size[nchunks - 1];
-    if (scratch) {
+    if (via) {
         // (scratch and out both 16-byte aligned: whole vectors, the last one
         // padded -- out has the bound's room)
         const uint64_t nv = ((tot < out_cap ? tot : out_cap) + 15) / 16;
