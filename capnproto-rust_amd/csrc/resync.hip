@@ -1040,8 +1040,9 @@ __global__ void k_msg_walk(const uint64_t* __restrict__ words, const uint64_t* _
 // try_read_message's loop is a chain over the words: message k's table gives
 // its length and so message k+1's start.  A 1 GiB stream of 12 KiB messages
 // is ~87 k dependent loads for one thread (tens of ms); here the words are cut
-// into kMsgRange-word ranges, one thread each:
-//   spec   thread t > 0 scans its range for the first word that starts a
+// into ranges (msg_range_for), one wave each for the spec, one thread each
+// after it:
+//   spec   range t > 0 scans its words for the first that starts a
 //          chain of kMsgVerify messages the loop would read (a body word
 //          passes one header check easily, pointers have small low halves,
 //          but not kMsgVerify in a row), then follows the chain to its first
@@ -1059,7 +1060,16 @@ __global__ void k_msg_walk(const uint64_t* __restrict__ words, const uint64_t* _
 //          chain's.
 //   list   exclusive scan of the counts; each range writes its messages'
 //          starts (ustart) as k_msg_walk does.
+// Ranges of kMsgRange words, doubled up to kMsgRangeMax while a stream has
+// more than kMsgRanges of them: each range's spec scan costs the same whatever
+// its length (its first message start, ~a message's words in), so fewer,
+// longer ranges do less of it; the chain follow inside them is the serial
+// loop's work anyway.  A 1 GiB stream of 12 KiB messages, one pass: ranges
+// of 4 Ki words 2.9 ms, 16 Ki 2.0, 64 Ki 1.9 (r05z).  Short streams (the
+// tests) keep 4 Ki-word ranges, so their chains still cross many ranges.
 constexpr uint64_t kMsgRange = 4096;
+constexpr uint64_t kMsgRangeMax = 65536;
+constexpr uint64_t kMsgRanges = 2048;
 constexpr uint32_t kMsgVerify = 16;
 constexpr uint64_t kMsgStop = 1ull << 63;
 constexpr uint64_t kMsgBad = ~0ull;
@@ -1125,13 +1135,13 @@ constexpr uint32_t kMsgSpecWaves = kThreads / CAPNP_WAVE;
 
 __global__ void __launch_bounds__(kThreads)
 k_msg_spec(const uint64_t* __restrict__ words, const uint64_t* __restrict__ res, uint64_t T,
-           MsgRanges R) {
+           MsgRanges R, uint64_t rng) {
     const uint32_t lane = threadIdx.x & (CAPNP_WAVE - 1);
     const uint64_t t = (uint64_t)blockIdx.x * kMsgSpecWaves +
                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / CAPNP_WAVE));
     if (t >= T) return;  // (uniform in the wave)
     const uint64_t W = res[0];
-    const uint64_t a = t * kMsgRange, b = min(a + kMsgRange, W);
+    const uint64_t a = t * rng, b = min(a + rng, W);
     uint64_t st = t == 0 ? 0 : kMsgBad;
     for (uint64_t u0 = a; t > 0 && u0 < b; u0 += CAPNP_WAVE) {
         const uint64_t u = u0 + lane;
@@ -1164,7 +1174,7 @@ k_msg_spec(const uint64_t* __restrict__ words, const uint64_t* __restrict__ res,
 
 __global__ void __launch_bounds__(kThreads)
 k_msg_round(const uint64_t* __restrict__ words, const uint64_t* __restrict__ res, uint64_t T,
-            MsgRanges R) {
+            MsgRanges R, uint64_t rng) {
     const uint64_t t = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (t >= T) return;
     const uint64_t W = res[0];
@@ -1172,7 +1182,7 @@ k_msg_round(const uint64_t* __restrict__ words, const uint64_t* __restrict__ res
     if (e == R.eu[t]) return;
     R.eu[t] = e;
     R.flag[0] = 1;
-    const uint64_t a = t * kMsgRange, b = min(a + kMsgRange, W);
+    const uint64_t a = t * rng, b = min(a + rng, W);
     uint64_t own = 0, m = 0;
     if ((e & kMsgStop) || e >= b || a >= W) {
         own = 0;  // passes its entry on
@@ -1188,11 +1198,11 @@ k_msg_round(const uint64_t* __restrict__ words, const uint64_t* __restrict__ res
 
 __global__ void __launch_bounds__(kThreads)
 k_msg_list(const uint64_t* __restrict__ words, const uint64_t* __restrict__ res, uint64_t T,
-           MsgRanges R, uint64_t max_msgs, uint64_t* __restrict__ ustart) {
+           MsgRanges R, uint64_t max_msgs, uint64_t* __restrict__ ustart, uint64_t rng) {
     const uint64_t t = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     if (t >= T) return;
     const uint64_t W = res[0];
-    const uint64_t a = t * kMsgRange, b = min(a + kMsgRange, W);
+    const uint64_t a = t * rng, b = min(a + rng, W);
     const uint64_t e = R.eu[t];
     uint64_t k = R.base[t];
     if (!(e & kMsgStop) && e < b && a < W) {
@@ -1263,8 +1273,15 @@ size_t msg_chain_carve(MsgRanges* R, uint8_t* base, uint64_t T) {
     return off;
 }
 
-// (the ranges for a decoded stream of at most W words)
+// (the ranges' workspace for a decoded stream of at most W words: the most
+// ranges any W' <= W takes)
 uint64_t msg_ranges(uint64_t W) { return W / kMsgRange + 1; }
+// the range length for a stream of W words
+uint64_t msg_range_for(uint64_t W) {
+    uint64_t r = kMsgRange;
+    while (r < kMsgRangeMax && W / r > kMsgRanges) r <<= 1;
+    return r;
+}
 
 size_t msg_chain_ws_bytes(uint64_t W) {
     MsgRanges R;
@@ -1276,7 +1293,8 @@ size_t msg_chain_ws_bytes(uint64_t W) {
 hipError_t msg_chain(const uint64_t* d_words, const uint64_t* res, uint64_t W_host,
                      uint64_t max_msgs, uint64_t* ustart, uint64_t* out, uint64_t* d_total,
                      void* d_chain, size_t chain_bytes, hipStream_t s) {
-    const uint64_t T = msg_ranges(W_host);
+    const uint64_t rng = msg_range_for(W_host);
+    const uint64_t T = W_host / rng + 1;
     MsgRanges R;
     uint8_t* base = (uint8_t*)(((uintptr_t)d_chain + 255) & ~uintptr_t(255));
     if (msg_chain_carve(&R, base, T) + (base - (uint8_t*)d_chain) > chain_bytes)
@@ -1284,7 +1302,7 @@ hipError_t msg_chain(const uint64_t* d_words, const uint64_t* res, uint64_t W_ho
     hipError_t e;
     const dim3 g((uint32_t)((T + kThreads - 1) / kThreads));
     k_msg_spec<<<dim3((uint32_t)((T + kMsgSpecWaves - 1) / kMsgSpecWaves)), kThreads, 0, s>>>(
-        d_words, res, T, R);
+        d_words, res, T, R, rng);
     bool done = false;
     for (int round = 0; round < kMsgMaxRounds; round++) {
         size_t tb = R.tmp_bytes;
@@ -1292,7 +1310,7 @@ hipError_t msg_chain(const uint64_t* d_words, const uint64_t* res, uint64_t W_ho
             hipSuccess)
             return e;
         if ((e = hipMemsetAsync(R.flag, 0, 4, s)) != hipSuccess) return e;
-        k_msg_round<<<g, kThreads, 0, s>>>(d_words, res, T, R);
+        k_msg_round<<<g, kThreads, 0, s>>>(d_words, res, T, R, rng);
         int32_t changed = 0;
         if ((e = hipMemcpyAsync(&changed, R.flag, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
             return e;
@@ -1309,7 +1327,7 @@ hipError_t msg_chain(const uint64_t* d_words, const uint64_t* res, uint64_t W_ho
     size_t tb = R.tmp_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(R.tmp, tb, R.cnt, R.base, (int)T, s)) != hipSuccess)
         return e;
-    k_msg_list<<<g, kThreads, 0, s>>>(d_words, res, T, R, max_msgs, ustart);
+    k_msg_list<<<g, kThreads, 0, s>>>(d_words, res, T, R, max_msgs, ustart, rng);
     k_msg_end<<<1, 64, 0, s>>>(res, T, R, max_msgs, ustart, out, d_total);
     return hipGetLastError();
 }
