@@ -1634,6 +1634,9 @@ static hipError_t find_messages_impl(const uint8_t* d_in, uint64_t nbytes, uint6
     k_blocks<<<grid(nb + 1), kThreads, 0, s>>>(in_off, n, out_off, w.bstart, w.exit, w.wbase,
                                                nullptr, blk_in, blk_out, nb);
     k_set_cut<<<grid(nb + 1), kThreads, 0, s>>>(blk_in, blk_out, nb, tail, cutk);
+    // (block units per decode tile: the unpack's 16; 8 / 12 / sized by the
+    // mean words per block for ~1200-word tiles measured 2.10 / 1.96 / 1.97
+    // vs 1.89 ms for a 1 GiB carsales stream, r05z)
     if ((e = capnp_launch_unpack(d_in, blk_in, nb, 0, d_words, blk_out, blk_status, nullptr,
                                  nullptr, s)) != hipSuccess)
         return e;
