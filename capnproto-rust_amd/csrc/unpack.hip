@@ -1037,6 +1037,7 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
 constexpr uint32_t kSegOverlap = 48;
 constexpr uint32_t kSegChunks = 16;  // tiles of at most this many chunks take the segment walk
 
+
 // One record hop (the walk's loops stop once p >= the segment end, so a
 // record running past the chunk end shows as p > pe at the stop).
 __device__ __forceinline__ void seg_hop(const uint8_t* B, uint32_t& p, uint32_t& w) {
@@ -1080,13 +1081,47 @@ __device__ __forceinline__ void seg_walk_rec(const uint8_t* B, uint32_t& q, uint
 }
 #endif
 
-template <class SM>
+// Inclusive max / sum over the lanes of this lane's group of NS (16: a DPP
+// row; 8: half a row, j = the lane's index in its group).
+template <uint32_t NS>
+__device__ __forceinline__ uint32_t grp_max_scan(uint32_t x, uint32_t j) {
+    if constexpr (NS == 16) {
+        return row_max_scan(x);
+    } else {
+        static_assert(NS == 8, "groups of 8 or 16 lanes");
+        uint32_t t = row_shr<1>(x);  // (unconditional: DPP reads need every lane)
+        x = j >= 1 ? max(x, t) : x;
+        t = row_shr<2>(x);
+        x = j >= 2 ? max(x, t) : x;
+        t = row_shr<4>(x);
+        return j >= 4 ? max(x, t) : x;
+    }
+}
+template <uint32_t NS>
+__device__ __forceinline__ uint32_t grp_sum_scan(uint32_t x, uint32_t j) {
+    if constexpr (NS == 16) {
+        return row_sum_scan(x);
+    } else {
+        static_assert(NS == 8, "groups of 8 or 16 lanes");
+        uint32_t t = row_shr<1>(x);
+        x = j >= 1 ? x + t : x;
+        t = row_shr<2>(x);
+        x = j >= 2 ? x + t : x;
+        t = row_shr<4>(x);
+        return j >= 4 ? x + t : x;
+    }
+}
+
+// LG: 4 = 16 segments per chunk (tiles of <= 16 chunks), 3 = 8 segments per
+// chunk (17..32 chunks: read_messages' interleaved table and body chunks,
+// short-chunk batches; they had taken the one-lane-per-chunk walker)
+template <class SM, uint32_t LG = 4>
 __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
                                               int32_t* __restrict__ status,
                                               uint64_t* __restrict__ consumed, uint32_t tid,
                                               uint32_t lane) {
-    const uint32_t lg = 4u;  // S = 16 segments per chunk (nc <= kSegChunks)
-    const uint32_t nseg = 1u << lg;
+    constexpr uint32_t lg = LG;
+    constexpr uint32_t nseg = 1u << lg;
     const uint32_t c = tid >> lg, j = tid & (nseg - 1u);
     const bool act = c < nc;
     uint32_t cs = 0, pe = 0, n = 0, sb = 0, se = 0;
@@ -1114,7 +1149,7 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
     uint32_t own = xs, wd = ws;
     bool err = j == 0 && serr, rep = false;  // rep: sr holds a repair walk's records
     uint32_t e_used = j == 0 ? sb : ~0u;
-    uint32_t x = row_max_scan(xs);
+    uint32_t x = grp_max_scan<nseg>(xs, j);
     for (;;) {
         const uint32_t xu = row_shr<1>(x);
         const uint32_t e = j == 0 ? sb : xu;
@@ -1135,10 +1170,10 @@ __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
                 wd = wt;
             }
         }
-        x = row_max_scan(own);
+        x = grp_max_scan<nseg>(own, j);
     }
     const uint32_t e = e_used;
-    const uint32_t incl = row_sum_scan(wd);
+    const uint32_t incl = grp_sum_scan<nseg>(wd, j);
     const uint64_t bad_m = ballot64(act && err);
     const uint32_t gl = lane & ~(nseg - 1u);
     const uint64_t gm = ((1ull << nseg) - 1ull) << gl;
@@ -1420,6 +1455,11 @@ __device__ __forceinline__ void unpack_staged_at(SM& S, const uint8_t* __restric
         if (anybad) __syncthreads();
     } else if (nc <= kSegChunks) {
         spec_seg_tile(S, ca, nc, status, consumed, tid, lane);
+    } else if (nc <= 2 * kSegChunks) {
+        // (8 segments a chunk: read_messages 1.117 -> 0.714 ms for 1 Mi 1 KiB
+        // messages, whose table and body chunks interleave; an index-free
+        // batch of 64-word chunks 0.30 -> 0.23 ms; r05z)
+        spec_seg_tile<SM, 3>(S, ca, nc, status, consumed, tid, lane);
     } else if (wave == walker && lane < nc) {
         // (many short chunks -- the resync blocks, ~120 words -- keep 64
         // serial walkers busy; the segment walk is for few long chunks:
