@@ -2063,13 +2063,16 @@ __device__ __forceinline__ void cs_emit_word(uint64_t w, uint32_t info, uint8_t*
     cs_emit_word_sel<SYNC>(w, info, region_m1, cs_sel(sel, info), srs, oc, d, b);
 }
 
-template <bool SYNC>
+// GAP (capnp_gpu_write_messages): chunk c is preceded by gap[c] bytes that the
+// kernel leaves zero (out_off[c] is the gap's start), as pack_kernel's GAP.
+template <bool SYNC, bool GAP = false>
 __global__ void __launch_bounds__(kThreads, 8)
 pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
                uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
                uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts,
                uint64_t* __restrict__ gs, uint32_t* __restrict__ sync,
-               uint8_t* __restrict__ ovf) {
+               uint8_t* __restrict__ ovf, const uint32_t* __restrict__ gap = nullptr) {
+    static_assert(!(SYNC && GAP), "the sync index is not written with gaps");
     __shared__ Smem<false> sm;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
@@ -2115,6 +2118,12 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint64_t*>(toff + wc0), 0, (int)((nw + 1) * 8), 0x00020000);
     const uint32_t o = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(lane * 8u), 0, 0);
+    uint32_t gv = 0;  // GAP: lane s = the gap before the wave's chunk s
+    if constexpr (GAP) {
+        const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t*>(gap + c0 + wc0), 0, (int)(nw * 4), 0x00020000);
+        gv = __builtin_amdgcn_raw_buffer_load_b32(grs, (int)(lane * 4u), 0, 0);
+    }
     const Sel8 selv = kSel8Table.e[tid];
     const uint32_t sb = (uint32_t)(WS0 - TW0);
 #pragma unroll
@@ -2177,7 +2186,7 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     LA.chunk_off = chunk_off;
     LA.nchunks = nchunks;
     LA.tc = tc;
-    LA.gap = nullptr;
+    LA.gap = GAP ? gap : nullptr;
     LA.wt = 0;
     LA.wlo = LA.whi = LA.g0 = 0;
     LA.map = nullptr;
@@ -2191,7 +2200,7 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             for (uint32_t i = tid; i < (uint32_t)(k1 - k0); i += kThreads) sync[k0 + i] = kSyncNone;
         const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
         run_streaming<MODE_SIZE>(in, toff, sm.chunk_size, sm.chunk_pos, nc, wave, lane, region,
-                                 sm.sel, out - mis, mis, out_cap, nullptr);
+                                 sm.sel, out - mis, mis, out_cap, GAP ? gap + c0 : nullptr);
         __syncthreads();
         if (wave == 0) {
             const uint64_t agg = scan_chunks(sm, nc, lane);
@@ -2220,9 +2229,12 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
 #pragma unroll
     for (uint32_t s = 0; s < kCsSteps; s++) {
         const uint32_t n = s < nw ? (uint32_t)__builtin_amdgcn_readlane((int)d_len, s) : 0u;
+        uint32_t g = 0;
+        if constexpr (GAP) g = (uint32_t)__builtin_amdgcn_readlane((int)gv, s);
+        local += g;  // (GAP: the chunk's bytes start after its gap)
         const uint32_t sz = cs_size_step(clo[s], chi[s], n, lane, local, ilo[s], ihi[s]);
         rec_oc = lane == s ? local : rec_oc;
-        if (lane == s && s < nw) sm.chunk_size[wc0 + s] = sz;
+        if (lane == s && s < nw) sm.chunk_size[wc0 + s] = sz + g;
         local += sz;
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -3223,9 +3235,14 @@ extern "C" hipError_t capnp_launch_pack_gap(const uint64_t* d_in, const uint64_t
     hipError_t e = hipMemsetAsync(d_state, 0, capnp_pack_state_bytes(nchunks, tc), stream);
     if (e != hipSuccess) return e;
     uint8_t* ovf = pack_ovf_flags(d_state, ntiles);
-    hipLaunchKernelGGL((pack_kernel<false, true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
-                       stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, d_state,
-                       d_state + ntiles, nullptr, d_gap, ovf);
+    if (tc == kWaves * kCsSteps)  // (chunks of <= 128 words: the chunk-step kernel)
+        hipLaunchKernelGGL((pack_cs_kernel<false, true>), dim3((uint32_t)ntiles), dim3(kThreads),
+                           0, stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
+                           d_state, d_state + ntiles, nullptr, ovf, d_gap);
+    else
+        hipLaunchKernelGGL((pack_kernel<false, true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
+                           stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
+                           d_state, d_state + ntiles, nullptr, d_gap, ovf);
     hipLaunchKernelGGL((pack_ovf_kernel<true>), pack_ovf_grid(ntiles), dim3(kThreads), 0, stream,
                        d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off, ovf, ntiles,
                        d_gap);
