@@ -1,7 +1,7 @@
 set -o pipefail
 # round-5 closing measurements (after the per-call work): tests, smoke, every workload line,
 # config-2 kernel stats, the drop-in and adaptor benches
-O=gpurun_out/r05y
+O=${OUTDIR:-gpurun_out/r05y}
 mkdir -p $O
 PART=${1:-1}
 if [ "$PART" = 1 ]; then
@@ -17,5 +17,7 @@ bash scripts/traffic.sh $O/tr_c4 --workload config4 --steps 3 --warmup 1 --no-cp
 timeout -k 10 300 python -u scripts/stream_bench.py > $O/stream.json 2>/dev/null &&
 timeout -k 10 300 python -u scripts/resync_bench.py > $O/resync.txt 2>&1 &&
 timeout -k 10 400 python -u scripts/dropin_bench.py > $O/dropin.txt 2>&1 &&
-timeout -k 10 300 python -u scripts/adaptor_bench.py > $O/adaptor.txt 2>&1 && echo done
+timeout -k 10 300 python -u scripts/adaptor_bench.py > $O/adaptor.txt 2>&1 &&
+timeout -k 10 120 python -u scripts/msg_bench.py > $O/msg_bench.txt 2>&1 &&
+timeout -k 10 120 python -u scripts/percall_bench.py > $O/percall.txt 2>&1 && echo done
 fi
