@@ -1095,7 +1095,8 @@ __device__ uint64_t tile_aggregate(const LookbackArgs& A, uint64_t j, uint32_t l
 // poll issued 4 / 8 / 16 x 64 cycles after the first (used when the first
 // misses, so a miss costs that delay instead of a round trip): 449 / 447 /
 // 444 vs 434.5 us, carsales 480 / 479 / 472 vs 461 -- the extra uncached
-// reads cost more than the round trips they save.
+// reads cost more than the round trips they save.  Groups of 31 / 47 tiles:
+// 466 / 455 vs 444 us (config 2), 483 / 469 vs 461 (carsales); 63 stays.
 //
 // Every wait is bounded: on timeout the waiter computes the missing aggregate
 // itself from the input (records are idempotent), so the kernel finishes with
