@@ -1112,17 +1112,40 @@ __device__ __forceinline__ uint32_t grp_sum_scan(uint32_t x, uint32_t j) {
     }
 }
 
+// Bit index of the k-th (from 0) set bit of m (k < popcount(m)).
+__device__ __forceinline__ uint32_t nth_set_bit(uint64_t m, uint32_t k) {
+    uint32_t pos = 0;
+#pragma unroll
+    for (uint32_t half = 32; half; half >>= 1) {
+        const uint64_t lo = m & ((1ull << half) - 1ull);
+        const uint32_t cnt = (uint32_t)__builtin_popcountll(lo);
+        if (k >= cnt) {
+            k -= cnt;
+            m >>= half;
+            pos += half;
+        } else {
+            m = lo;
+        }
+    }
+    return pos;
+}
+
 // LG: 4 = 16 segments per chunk (tiles of <= 16 chunks), 3 = 8 segments per
-// chunk (17..32 chunks: read_messages' interleaved table and body chunks,
-// short-chunk batches; they had taken the one-lane-per-chunk walker)
-template <class SM, uint32_t LG = 4>
+// chunk (17..32 chunks: short-chunk batches; they had taken the
+// one-lane-per-chunk walker).  MAP: the lane groups go to the chunks of
+// `am` only (the chunks with words: read_messages interleaves each message's
+// table chunk, which has none, with its body), in order; the others keep
+// badc 0 and the per-chunk pass gives them OK with nothing consumed.
+template <class SM, uint32_t LG = 4, bool MAP = false>
 __device__ __forceinline__ void spec_seg_tile(SM& S, uint64_t ca, uint32_t nc,
                                               int32_t* __restrict__ status,
                                               uint64_t* __restrict__ consumed, uint32_t tid,
-                                              uint32_t lane) {
+                                              uint32_t lane, uint64_t am = 0) {
     constexpr uint32_t lg = LG;
     constexpr uint32_t nseg = 1u << lg;
-    const uint32_t c = tid >> lg, j = tid & (nseg - 1u);
+    const uint32_t j = tid & (nseg - 1u);
+    uint32_t c = tid >> lg;
+    if constexpr (MAP) c = c < (uint32_t)__builtin_popcountll(am) ? nth_set_bit(am, c) : nc;
     const bool act = c < nc;
     uint32_t cs = 0, pe = 0, n = 0, sb = 0, se = 0;
     if (act) {
@@ -1456,10 +1479,16 @@ __device__ __forceinline__ void unpack_staged_at(SM& S, const uint8_t* __restric
     } else if (nc <= kSegChunks) {
         spec_seg_tile(S, ca, nc, status, consumed, tid, lane);
     } else if (nc <= 2 * kSegChunks) {
-        // (8 segments a chunk: read_messages 1.117 -> 0.714 ms for 1 Mi 1 KiB
-        // messages, whose table and body chunks interleave; an index-free
-        // batch of 64-word chunks 0.30 -> 0.23 ms; r05z)
-        spec_seg_tile<SM, 3>(S, ca, nc, status, consumed, tid, lane);
+        // (8 segments a chunk: an index-free batch of 64-word chunks 0.30 ->
+        // 0.23 ms; read_messages, whose table and body chunks interleave,
+        // 1.117 -> 0.714 ms, and with the groups for the bodies only -- 16
+        // segments each -- MAP; r05z)
+        const uint64_t am = ballot64(lane < nc && S.cw[lane + 1u] > S.cw[lane]);
+        const uint32_t na = (uint32_t)__builtin_popcountll(am);
+        if (na <= kSegChunks)
+            spec_seg_tile<SM, 4, true>(S, ca, nc, status, consumed, tid, lane, am);
+        else
+            spec_seg_tile<SM, 3>(S, ca, nc, status, consumed, tid, lane);
     } else if (wave == walker && lane < nc) {
         // (many short chunks -- the resync blocks, ~120 words -- keep 64
         // serial walkers busy; the segment walk is for few long chunks:
