@@ -46,12 +46,13 @@ EXPORTS = [
     "capnp_packed_writer_new", "capnp_packed_writer_free", "capnp_packed_writer_write",
     "capnp_packed_writer_flush", "capnp_packed_writer_carried", "capnp_packed_reader_new",
     "capnp_packed_reader_free", "capnp_packed_reader_read", "capnp_packed_reader_read_exact",
+    "capnp_packed_reader_set_readahead",
     "capnp_packed_reader_read_message", "capnp_packed_reader_buffered",
     "capnp_gpu_find_messages",
     "capnp_gpu_read_message_stream", "capnp_abi_version", "capnp_resync_max_passes",
     "capnp_unpack_prefix",
 ]
-ABI_VERSION = 5  # include/capnp_packed.h CAPNP_ABI_VERSION
+ABI_VERSION = 6  # include/capnp_packed.h CAPNP_ABI_VERSION
 
 
 class ReaderOptionsC(C.Structure):
@@ -104,7 +105,7 @@ def lib():
     L.capnp_packed_batch_bound_bytes.argtypes = [sz, sz]
     L.capnp_packed_batch_bound_bytes.restype = sz
     L.capnp_gpu_pack_batch.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp]
-    L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, u32, vp]
+    L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, u32, vp]
     L.capnp_gpu_unpack_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.capnp_gpu_unpack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, C.c_uint32, vp]
     L.capnp_gpu_gen_batch.argtypes = [vp, vp, vp, sz, u64, vp, u32, u32, vp]
@@ -117,7 +118,7 @@ def lib():
     L.capnp_sync_index_entries.restype = sz
     L.capnp_gpu_pack_batch_sync.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, vp]
     L.capnp_gpu_unpack_batch_sync.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, vp]
-    L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, u32, vp]
+    L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, vp, u32, vp]
     L.capnp_gpu_unpack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, u32, vp]
     L.capnp_ctx_reserve.argtypes = [vp, sz]
     L.capnp_gpu_unpack_batch_resync.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
@@ -157,6 +158,7 @@ def lib():
     L.capnp_packed_reader_new.argtypes = [vp, READ_FN, vp]
     L.capnp_packed_reader_new.restype = vp
     L.capnp_packed_reader_free.argtypes = [vp]
+    L.capnp_packed_reader_set_readahead.argtypes = [vp, i32]
     L.capnp_packed_reader_read.argtypes = [vp, vp, sz, C.POINTER(C.c_size_t)]
     L.capnp_packed_reader_read_exact.argtypes = [vp, vp, sz, C.POINTER(C.c_size_t)]
     L.capnp_packed_reader_read_message.argtypes = [vp, C.POINTER(ReaderOptionsC), i32, vp, sz,

@@ -21,6 +21,8 @@ block_on does.
 """
 import ctypes as C
 import io
+import os
+import stat
 import socket
 
 import numpy as np
@@ -66,19 +68,22 @@ class PackedWrite:
         self._view = bool(inner_copies)
 
         def write_cb(_user, buf, n):
-            addr = C.cast(buf, C.c_void_p).value
-            mv = memoryview((C.c_ubyte * n).from_address(addr)).cast("B")
+            mv = None
+            err = None
             try:
+                addr = C.cast(buf, C.c_void_p).value
+                mv = memoryview((C.c_ubyte * n).from_address(addr)).cast("B")
                 r = self.inner.write(mv if self._view else bytes(mv))
             except Exception as e:  # surfaced as CAPNP_E_IO
-                self._err = e
-                return -2
-            finally:
+                err = e
+            if mv is not None:
                 try:
                     mv.release()
                 except BufferError as e:  # the writer exported the view and kept it
-                    self._err = e
-                    return -2
+                    err = err or e
+            if err is not None:
+                self._err = err
+                return -2
             return _lib.IO_PENDING if r is None else int(r)
 
         self._cb = _lib.WRITE_FN(write_cb)
@@ -126,14 +131,32 @@ class PackedWrite:
             self._h = None
 
 
+def _bulk_source(inner):
+    """Whether `inner` is a source whose reads never wait on a peer."""
+    if isinstance(inner, io.BytesIO):
+        return True
+    try:
+        return stat.S_ISREG(os.fstat(inner.fileno()).st_mode)
+    except (AttributeError, OSError, ValueError, io.UnsupportedOperation):
+        return False
+
+
 class PackedRead:
     """An AsyncRead wrapper that unpacks packed data."""
 
-    def __init__(self, inner, ctx=None):
+    def __init__(self, inner, ctx=None, readahead=None):
+        """`readahead`: pull the inner reader in MiB units past what the
+        current read needs while it returns every byte asked (a file, an
+        in-memory stream).  Off, reads pull no further than the current
+        request can need, as the reference does, so a blocking pipe or socket
+        whose peer awaits a reply is never read past the request.  None =
+        on for `io.BytesIO` and regular files, off otherwise."""
         self.inner = inner
         self.ctx = ctx or default_context()
         self._err = None
         self._extra = None  # bytes an inner reader returned beyond what was asked
+        if readahead is None:
+            readahead = _bulk_source(inner)
 
         def read_cb(_user, buf, n):
             if self._extra is not None and self._extra.size:
@@ -164,6 +187,7 @@ class PackedRead:
         self._h = _lib.lib().capnp_packed_reader_new(self.ctx.handle, self._cb, None)
         if not self._h:
             raise CapnpError(64, "capnp_packed_reader_new")
+        _lib.lib().capnp_packed_reader_set_readahead(self._h, 1 if readahead else 0)
 
     def _raise(self, st):
         if st == 68 and self._err is not None:

@@ -24,7 +24,7 @@
 
 extern "C" hipError_t capnp_launch_pack(const uint64_t*, const uint64_t*, uint64_t, uint32_t,
                                         uint8_t*, uint64_t, uint64_t*, uint64_t*, uint32_t*,
-                                        hipStream_t);
+                                        uint64_t, hipStream_t);
 extern "C" hipError_t capnp_launch_pack_gap(const uint64_t*, const uint64_t*, uint64_t, uint32_t,
                                             uint8_t*, uint64_t, uint64_t*, uint64_t*,
                                             const uint32_t*, hipStream_t);
@@ -178,6 +178,13 @@ struct capnp_ctx {
     uint32_t* h_flag = nullptr;  // pinned: the one-launch calls' completion flag
     uint32_t* d_flag = nullptr;  // ... its device address
     uint32_t call_seq = 0;
+    // Caller streams that ran this context's device work: an event recorded on
+    // each after its last call, so a workspace that has to grow waits for that
+    // work only (not for every stream of the device), and destroy too.
+    static constexpr int kUseSlots = 8;
+    hipStream_t use_s[kUseSlots] = {};
+    hipEvent_t use_ev[kUseSlots] = {};
+    int use_next = 0;
     std::string err;
 };
 
@@ -244,11 +251,56 @@ capnp_status fail(capnp_ctx* ctx, hipError_t e, const char* what) {
 // (default) stream, as everywhere in HIP.
 hipStream_t pick(capnp_ctx*, void* s) { return (hipStream_t)s; }
 
+// Records that `s` now holds work of this context (called when a call that
+// enqueued on a caller's stream returns).  Work under stream capture is the
+// caller's graph: it is not tracked.
+void mark_use(capnp_ctx* ctx, hipStream_t s) {
+    if (s == ctx->stream) return;  // (ctx->stream is synchronised directly)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+    int k = 0;
+    while (k < capnp_ctx::kUseSlots && !(ctx->use_ev[k] && ctx->use_s[k] == s)) k++;
+    if (k == capnp_ctx::kUseSlots) {
+        k = ctx->use_next;
+        ctx->use_next = (k + 1) % capnp_ctx::kUseSlots;
+        if (ctx->use_ev[k]) {
+            (void)hipEventSynchronize(ctx->use_ev[k]);  // (the slot's stream drops out)
+        } else if (hipEventCreateWithFlags(&ctx->use_ev[k], hipEventDisableTiming) != hipSuccess) {
+            ctx->use_ev[k] = nullptr;
+            (void)hipStreamSynchronize(s);  // (no event: wait now instead)
+            return;
+        }
+    }
+    ctx->use_s[k] = s;
+    if (hipEventRecord(ctx->use_ev[k], s) != hipSuccess) (void)hipStreamSynchronize(s);
+}
+
+struct UseMark {
+    capnp_ctx* ctx;
+    hipStream_t s;
+    ~UseMark() {
+        if (ctx) mark_use(ctx, s);
+    }
+};
+
+// Waits for every piece of work this context has queued: its own streams and
+// the caller streams marked above (before a workspace is freed).
+hipError_t wait_uses(capnp_ctx* ctx) {
+    hipError_t e = hipSuccess, r;
+    if (ctx->stream && (r = hipStreamSynchronize(ctx->stream)) != hipSuccess) e = r;
+    for (int k = 0; k < capnp_ctx::kUseSlots; k++)
+        if (ctx->use_ev[k] && ctx->use_s[k] && (r = hipEventSynchronize(ctx->use_ev[k])) != hipSuccess)
+            e = r;
+    for (int k = 0; k < 3; k++)
+        if (ctx->sstream[k] && (r = hipStreamSynchronize(ctx->sstream[k])) != hipSuccess) e = r;
+    return e;
+}
+
 capnp_status ensure_state(capnp_ctx* ctx, size_t bytes) {
     if (bytes <= ctx->state_cap) return CAPNP_OK;
     HIP_TRY(hipSetDevice(ctx->device));
     if (ctx->d_state) {
-        HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(wait_uses(ctx));
         HIP_TRY(hipFree(ctx->d_state));
         ctx->d_state = nullptr;
         ctx->state_cap = 0;
@@ -289,8 +341,9 @@ capnp_status ensure_buf(capnp_ctx* ctx, uint8_t** buf, size_t* cap_io, size_t by
     HIP_TRY(hipSetDevice(ctx->device));
     if (*buf) {
         // (work queued on a caller's stream, not only ctx->stream, may still
-        // use the buffer: the device batch calls run on the caller's stream)
-        HIP_TRY(hipDeviceSynchronize());
+        // use the buffer: the device batch calls run on the caller's stream
+        // and are marked there, mark_use)
+        HIP_TRY(wait_uses(ctx));
         HIP_TRY(hipFree(*buf));
         *buf = nullptr;
         *cap_io = 0;
@@ -426,9 +479,10 @@ constexpr uint64_t kWordTileMean = 512;
 capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint64_t* d_off,
                             size_t n, uint8_t* d_out, size_t cap, uint64_t* d_out_off,
                             uint32_t tc, hipStream_t s, uint32_t* d_sync = nullptr,
-                            const uint64_t* host_wr = nullptr) {
+                            const uint64_t* host_wr = nullptr, uint64_t in_words = 0) {
     if (n > 0 && !d_off) return CAPNP_E_INVALID_ARGUMENT;
     if (!d_out_off) return CAPNP_E_INVALID_ARGUMENT;
+    UseMark um{ctx, s};
     if (tc == 0 && n > 0) {
         uint64_t wr[2];
         if (host_wr) {
@@ -442,6 +496,7 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
         }
         if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
         const uint64_t words = wr[1] - wr[0];
+        if (wr[0] == 0) in_words = std::max<uint64_t>(in_words, wr[1]);  // (d_words holds them)
         if (words && (words / n >= kWordTileMean || force_word_tiles())) {
             const uint64_t ntiles = capnp_pack_wt_tiles(wr[0], wr[1]);
             capnp_status st = ensure_state(ctx, capnp_pack_state_bytes(ntiles, 1) + 16);
@@ -460,8 +515,12 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
     const size_t sb = state_bytes_for(n, tc);
     capnp_status st = ensure_state(ctx, sb);
     if (st != CAPNP_OK) return st;
+    // a batch of 1 KiB segments (as many words as 128 per chunk): the kernel
+    // loads each tile's words at the guessed offsets with the offsets
+    // themselves (pack_cs_kernel spec_words; a wrong guess only costs a reload)
+    const uint64_t spec = (in_words == (uint64_t)n * 128 && tc == 16) ? in_words : 0;
     HIP_TRY(capnp_launch_pack(d_words, d_off, n, tc, d_out, cap, d_out_off,
-                              reinterpret_cast<uint64_t*>(ctx->d_state), d_sync, s));
+                              reinterpret_cast<uint64_t*>(ctx->d_state), d_sync, spec, s));
     return CAPNP_OK;
 }
 
@@ -650,8 +709,7 @@ int capnp_ctx_device(const capnp_ctx* ctx) { return ctx ? ctx->device : 0; }
 void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
-    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->resync_failed) (void)hipStreamSynchronize(ctx->resync_stream);  // (still decoding)
+    (void)wait_uses(ctx);  // (an index-free decode may still be running on its caller's stream)
     if (ctx->d_state) (void)hipFree(ctx->d_state);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_body) (void)hipFree(ctx->d_body);
@@ -666,6 +724,8 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (ctx->d_wt) (void)hipFree(ctx->d_wt);
     if (ctx->d_pwt) (void)hipFree(ctx->d_pwt);
     if (ctx->ev_resync) (void)hipEventDestroy(ctx->ev_resync);
+    for (int k = 0; k < capnp_ctx::kUseSlots; k++)
+        if (ctx->use_ev[k]) (void)hipEventDestroy(ctx->use_ev[k]);
     for (int k = 0; k < 3; k++)
         if (ctx->sstream[k]) {
             (void)hipStreamSynchronize(ctx->sstream[k]);
@@ -702,13 +762,14 @@ capnp_status capnp_gpu_pack_batch(capnp_ctx* ctx, const uint64_t* d_words,
 }
 
 capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
-                                        const uint64_t* d_chunk_word_off, size_t nchunks,
-                                        uint8_t* d_out, size_t out_cap,
+                                        size_t in_words, const uint64_t* d_chunk_word_off,
+                                        size_t nchunks, uint8_t* d_out, size_t out_cap,
                                         uint64_t* d_out_byte_off, uint32_t chunks_per_tile,
                                         void* stream) {
     if (!ctx) return CAPNP_E_INVALID_ARGUMENT;
     return pack_batch_dev(ctx, d_words, d_chunk_word_off, nchunks, d_out, out_cap,
-                          d_out_byte_off, chunks_per_tile, pick(ctx, stream));
+                          d_out_byte_off, chunks_per_tile, pick(ctx, stream), nullptr, nullptr,
+                          in_words);
 }
 
 // With the record sync index and chunks_per_tile == 0 the launch is sized
@@ -731,6 +792,7 @@ static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
     if (!ctx || (nchunks && (!d_in_byte_off || !d_out_word_off || !d_status)))
         return CAPNP_E_INVALID_ARGUMENT;
     if (tc > 256) return CAPNP_E_INVALID_ARGUMENT;
+    UseMark um{ctx, pick(ctx, stream)};
     if (tc == 0 && nchunks) {
         hipStream_t s = pick(ctx, stream);
         uint64_t wr[2], br[2];
@@ -807,13 +869,14 @@ capnp_status capnp_gpu_unpack_batch_sync(capnp_ctx* ctx, const uint8_t* d_packed
 }
 
 capnp_status capnp_gpu_pack_batch_sync_tuned(capnp_ctx* ctx, const uint64_t* d_words,
-                                             const uint64_t* d_chunk_word_off, size_t nchunks,
-                                             uint8_t* d_out, size_t out_cap,
+                                             size_t in_words, const uint64_t* d_chunk_word_off,
+                                             size_t nchunks, uint8_t* d_out, size_t out_cap,
                                              uint64_t* d_out_byte_off, uint32_t* d_sync,
                                              uint32_t chunks_per_tile, void* stream) {
     if (!ctx || !d_sync) return CAPNP_E_INVALID_ARGUMENT;
     return pack_batch_dev(ctx, d_words, d_chunk_word_off, nchunks, d_out, out_cap,
-                          d_out_byte_off, chunks_per_tile, pick(ctx, stream), d_sync);
+                          d_out_byte_off, chunks_per_tile, pick(ctx, stream), d_sync, nullptr,
+                          in_words);
 }
 
 capnp_status capnp_gpu_unpack_batch_sync_tuned(capnp_ctx* ctx, const uint8_t* d_packed,
@@ -846,6 +909,7 @@ static capnp_status unpack_resync_dev(capnp_ctx* ctx, const uint8_t* d_packed,
                                       uint64_t* d_words, const uint64_t* d_out_word_off,
                                       int32_t* d_status, uint64_t* d_consumed, hipStream_t s,
                                       const uint64_t* checked_byte_ends) {
+    UseMark um{ctx, s};
     // The previous index-free decode returned with its kernels still queued on
     // its own stream, and they read and write the workspace this call is about
     // to reset: a call on another stream waits for them first (an event, no
@@ -1184,6 +1248,7 @@ capnp_status capnp_gpu_write_messages(capnp_ctx* ctx, const uint64_t* d_words,
     if (!ctx || !d_msg_byte_off || (nmsg && (!d_seg_word_off || !d_msg_seg_off)))
         return CAPNP_E_INVALID_ARGUMENT;
     hipStream_t s = pick(ctx, stream);
+    UseMark um{ctx, s};
     if (nmsg == 0) {
         HIP_TRY(hipMemsetAsync(d_msg_byte_off, 0, sizeof(uint64_t), s));
         return CAPNP_OK;
@@ -1277,6 +1342,7 @@ capnp_status capnp_gpu_read_messages(capnp_ctx* ctx, const uint8_t* d_packed,
         (nmsg && (!d_msg_byte_off || !d_status)))
         return CAPNP_E_INVALID_ARGUMENT;
     hipStream_t s = pick(ctx, stream);
+    UseMark um{ctx, s};
     if (nmsg == 0) {
         HIP_TRY(hipMemsetAsync(d_msg_word_off, 0, 8, s));
         HIP_TRY(hipMemsetAsync(d_msg_seg_off, 0, 8, s));
@@ -1341,6 +1407,7 @@ capnp_status capnp_gpu_find_messages(capnp_ctx* ctx, const uint8_t* d_packed, si
                                      void* stream) {
     if (!ctx || !nmsg || !d_msg_byte_off || (nbytes && !d_packed)) return CAPNP_E_INVALID_ARGUMENT;
     hipStream_t s = pick(ctx, stream);
+    UseMark um{ctx, s};
     *nmsg = 0;
     size_t found = 0;
     uint64_t start = 0;
@@ -1403,6 +1470,7 @@ capnp_status capnp_gpu_read_message_stream(capnp_ctx* ctx, const uint8_t* d_pack
         (msgs_cap && !d_body_word_off) || (words_cap && !d_words))
         return CAPNP_E_INVALID_ARGUMENT;
     hipStream_t s = pick(ctx, stream);
+    UseMark um{ctx, s};
     *nmsg = 0;
     *clean = 0;
     if (words_need) *words_need = 0;
@@ -1538,6 +1606,7 @@ capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf, 
     if (!ctx || !d_msg_seg_off || (nmsg && (!d_slice_off || !d_status)))
         return CAPNP_E_INVALID_ARGUMENT;
     hipStream_t s = pick(ctx, stream);
+    UseMark um{ctx, s};
     if (nmsg == 0) {
         HIP_TRY(hipMemsetAsync(d_msg_seg_off, 0, 8, s));
         return CAPNP_OK;

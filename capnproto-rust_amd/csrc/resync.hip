@@ -34,6 +34,8 @@
 // by spare bytes in its range) is decoded serially as one unit of that same
 // launch, so its status, consumed count and partial output are exactly
 // capnp_gpu_unpack_batch's; the other chunks keep the block decode.
+#include <mutex>
+#include <vector>
 #include <hipcub/hipcub.hpp>
 
 #include "common.h"
@@ -718,6 +720,40 @@ unsigned grid(uint64_t items) { return (unsigned)((items + kThreads - 1) / kThre
 // pass before the first flag read-back, then kPassBatch per read-back.
 // *converged = false if the passes reach kMaxPasses; *capped = true if a
 // tile hit the round cap (its segments carry error exits).  Blocking.
+// Pinned flag buffers for resolve()'s read-back, shared by every thread: a
+// call borrows one and returns it, so the pool holds at most as many buffers
+// as calls that ever ran at once (they live until the process ends).  Null if
+// pinned memory is unavailable (resolve then reads the flags through pageable
+// copies).
+struct PinnedFlags {
+    int32_t* p = nullptr;
+    static std::mutex& mu() {
+        static std::mutex m;
+        return m;
+    }
+    static std::vector<int32_t*>& pool() {
+        static std::vector<int32_t*> v;
+        return v;
+    }
+    PinnedFlags() {
+        {
+            std::lock_guard<std::mutex> g(mu());
+            if (!pool().empty()) {
+                p = pool().back();
+                pool().pop_back();
+                return;
+            }
+        }
+        void* q = nullptr;
+        if (hipHostMalloc(&q, 4 * (2 + kMaxPasses), 0) == hipSuccess) p = (int32_t*)q;
+    }
+    ~PinnedFlags() {
+        if (!p) return;
+        std::lock_guard<std::mutex> g(mu());
+        pool().push_back(p);
+    }
+};
+
 hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, const Ws& w,
                    uint64_t nbb, hipStream_t s, bool* converged, bool* capped, int* passes) {
     hipError_t e;
@@ -731,12 +767,10 @@ hipError_t resolve(const uint8_t* d_in, const uint64_t* in_off, uint64_t n, cons
                                    reinterpret_cast<uint8_t*>(w.flags));
         if ((e = hipMemsetAsync(w.flags, 0, zb, s)) != hipSuccess) return e;
     }
-    // (the flags come back through pinned memory: one DMA, no staged copy)
-    static thread_local int32_t* t_hflags = nullptr;
-    if (!t_hflags) {
-        void* p = nullptr;
-        if (hipHostMalloc(&p, 4 * (2 + kMaxPasses), 0) == hipSuccess) t_hflags = (int32_t*)p;
-    }
+    // (the flags come back through pinned memory: one DMA, no staged copy;
+    // the buffer is borrowed from a process-wide pool for the call)
+    PinnedFlags pf;
+    int32_t* const t_hflags = pf.p;
     k_tile<<<ntiles, kTileThreads, kTileLds, s>>>(d_in, in_off, n, w.bstart, w.exit, w.entry,
                                                  w.words, w.spec_exit, w.flags, w.trec, w.ticket,
                                                  g_max_rounds, 0, 0);

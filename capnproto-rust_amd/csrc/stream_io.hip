@@ -219,6 +219,13 @@ struct capnp_packed_reader {
     // ready than that, so pulling ahead of need is safe (a short read means
     // the source is drained for now, and a blocking reader would block)
     bool last_full = false;
+    // bulk read-ahead allowed (capnp_packed_reader_set_readahead): pulls past
+    // what the caller's current request can need, while pulls come back
+    // full.  Off by default: then a read first decodes what is staged and
+    // pulls only when no complete record is, as the reference reads no
+    // further than the current request needs, so a blocking peer that sent
+    // exactly one request's worth and awaits a reply is never read past it.
+    bool readahead = false;
     PBytes dec;                // decoded bytes not yet handed out
     PBytes spare;              // the next decode's buffer (swapped with dec)
     size_t dp = 0;
@@ -356,7 +363,7 @@ capnp_status reader_pull(capnp_packed_reader* r, size_t ask = kPull) {
 // first short read, so with a blocking inner reader the same holds: every
 // further pull is one the decode of the staged bytes showed it needs.
 bool may_pull_ahead(const capnp_packed_reader* r) {
-    return r->in.size() == r->ip || r->last_full;
+    return r->in.size() == r->ip || (r->readahead && r->last_full);
 }
 
 // One PackedRead::read of `nw` words at the current position, on the GPU.
@@ -453,7 +460,9 @@ constexpr size_t kBigUnit = size_t(1) << STREAM_BIGUNIT_LG;
 // fails here leaves the next call to meet it.
 void reader_ahead(capnp_packed_reader* r, size_t nw) {
     for (size_t need = nw * 10 + 16; r->in.size() - r->ip < need;) {
-        if (!r->last_full) break;  // (never a pull the caller's request does not need)
+        // (never a pull the caller's request does not need; without bulk
+        // read-ahead the next unit decodes only from what is staged)
+        if (!r->last_full || !r->readahead) break;
         const capnp_status p = reader_pull(r, need - (r->in.size() - r->ip));
         if (p == CAPNP_OK) continue;
         if (p == CAPNP_NONE) break;      // end of stream: the rest is staged
@@ -574,7 +583,8 @@ capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
         // reference's read returns what it has decoded, and a pull is made
         // only when there is none.
         capnp_status p = r->eof ? CAPNP_NONE : CAPNP_PENDING;
-        if (r->last_full) {
+        const bool pulled = may_pull_ahead(r);
+        if (pulled) {
             p = reader_pull(r);
             if (p == CAPNP_OK) continue;
             if (p != CAPNP_NONE && p != CAPNP_PENDING) return p;
@@ -596,7 +606,7 @@ capnp_status reader_fill(capnp_packed_reader* r, size_t want) {
             r->dp = 0;
             return CAPNP_OK;
         }
-        if (!r->last_full && !r->eof) {  // nothing complete staged: the request needs input
+        if (!pulled && !r->eof) {  // nothing complete staged: the request needs input
             p = reader_pull(r);
             if (p == CAPNP_OK) continue;
             if (p != CAPNP_NONE && p != CAPNP_PENDING) return p;
@@ -680,6 +690,10 @@ capnp_packed_reader* capnp_packed_reader_new(capnp_ctx* ctx, capnp_read_fn fn, v
     r->fn = fn;
     r->user = user;
     return r;
+}
+
+void capnp_packed_reader_set_readahead(capnp_packed_reader* r, int on) {
+    if (r) r->readahead = on != 0;
 }
 
 void capnp_packed_reader_free(capnp_packed_reader* r) {

@@ -90,7 +90,7 @@ def main():
         packed = bytes(sink.value())
         # read: calls of up to 1 MiB into the caller's buffer (poll_read(&mut
         # [u8]) -> readinto) until the end, the first `warm` bytes untimed
-        r = spa.PackedRead(MemRead(packed), ctx=ctx)
+        r = spa.PackedRead(MemRead(packed), ctx=ctx, readahead=True)  # (a memory source: bulk)
         got = bytearray(len(raw) + call)
         gv = memoryview(got)
         pos = 0

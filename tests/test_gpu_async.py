@@ -687,6 +687,32 @@ def test_reader_stops_at_request_over_blocking_pipe(A, body_words, piece):
     assert pipe.pos == len(msg)
 
 
+@pytest.mark.parametrize("total", [1 << 16, 1 << 17, 3 << 16])
+def test_reader_no_pull_past_full_request(A, total):
+    """A blocking peer that sent exactly a multiple of the adaptor's pull size
+    (64 KiB) and now awaits a reply: the reads that the staged bytes can
+    serve are served without another pull (stream_io.hip: a pull
+    that came back full no longer licenses a pull past the request)."""
+    # one message of 1-byte words (2 packed bytes each) padded to `total`
+    n = (total - 16) // 2
+    for k in range(n, n - 64, -1):
+        seg = np.ones(k, np.uint64)
+        st, msg = O.write_message([seg])
+        assert st == 0
+        if len(msg) <= total and (total - len(msg)) % 3 == 0:
+            break
+    extra = (total - len(msg)) // 3  # words of 2 nonzero bytes: 3 packed bytes each
+    seg = np.ones(k + extra, np.uint64)
+    seg[:extra] = 0x0101
+    st, msg = O.write_message([seg])
+    assert st == 0 and len(msg) == total, (len(msg), total)
+    pipe = _Pipe(msg, None)
+    pr = A.PackedRead(pipe)
+    m = A.read_message(pr)
+    assert np.array_equal(np.asarray(m.segments()[0]).view(np.uint64), seg)
+    assert pipe.pos == len(msg)
+
+
 def test_writer_list_sink_keeps_its_bytes(A):
     """An inner writer that keeps what it is given (no copy) sees bytes that
     stay valid after the adaptor reuses its queue."""
