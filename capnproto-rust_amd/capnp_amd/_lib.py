@@ -105,7 +105,7 @@ def lib():
     L.capnp_packed_batch_bound_bytes.argtypes = [sz, sz]
     L.capnp_packed_batch_bound_bytes.restype = sz
     L.capnp_gpu_pack_batch.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp]
-    L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, u32, vp]
+    L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, u32, vp]
     L.capnp_gpu_unpack_batch.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]
     L.capnp_gpu_unpack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, C.c_uint32, vp]
     L.capnp_gpu_gen_batch.argtypes = [vp, vp, vp, sz, u64, vp, u32, u32, vp]
@@ -118,7 +118,7 @@ def lib():
     L.capnp_sync_index_entries.restype = sz
     L.capnp_gpu_pack_batch_sync.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, vp]
     L.capnp_gpu_unpack_batch_sync.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, vp]
-    L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, vp, u32, vp]
+    L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, u32, vp]
     L.capnp_gpu_unpack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, u32, vp]
     L.capnp_ctx_reserve.argtypes = [vp, sz]
     L.capnp_gpu_unpack_batch_resync.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp]

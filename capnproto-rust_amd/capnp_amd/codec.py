@@ -104,15 +104,14 @@ class Context:
         n = chunk_word_off.numel() - 1
         L = _lib.lib()
         if sync is None:
-            st = L.capnp_gpu_pack_batch_tuned(self._h, _ptr(words), words.numel(),
-                                              _ptr(chunk_word_off), n, _ptr(out), out.numel(),
-                                              _ptr(out_off), int(chunks_per_tile),
-                                              self._stream(stream))
+            st = L.capnp_gpu_pack_batch_tuned(self._h, _ptr(words), _ptr(chunk_word_off), n,
+                                              _ptr(out), out.numel(), _ptr(out_off),
+                                              int(chunks_per_tile), self._stream(stream))
         else:
-            st = L.capnp_gpu_pack_batch_sync_tuned(self._h, _ptr(words), words.numel(),
-                                                   _ptr(chunk_word_off), n, _ptr(out),
-                                                   out.numel(), _ptr(out_off), _ptr(sync),
-                                                   int(chunks_per_tile), self._stream(stream))
+            st = L.capnp_gpu_pack_batch_sync_tuned(self._h, _ptr(words), _ptr(chunk_word_off),
+                                                   n, _ptr(out), out.numel(), _ptr(out_off),
+                                                   _ptr(sync), int(chunks_per_tile),
+                                                   self._stream(stream))
         _check(st, self._h)
 
     def unpack_batch_into(self, packed, in_byte_off, out_word_off, words, status,

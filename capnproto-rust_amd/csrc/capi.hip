@@ -24,7 +24,7 @@
 
 extern "C" hipError_t capnp_launch_pack(const uint64_t*, const uint64_t*, uint64_t, uint32_t,
                                         uint8_t*, uint64_t, uint64_t*, uint64_t*, uint32_t*,
-                                        uint64_t, hipStream_t);
+                                        hipStream_t);
 extern "C" hipError_t capnp_launch_pack_gap(const uint64_t*, const uint64_t*, uint64_t, uint32_t,
                                             uint8_t*, uint64_t, uint64_t*, uint64_t*,
                                             const uint32_t*, hipStream_t);
@@ -479,7 +479,7 @@ constexpr uint64_t kWordTileMean = 512;
 capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint64_t* d_off,
                             size_t n, uint8_t* d_out, size_t cap, uint64_t* d_out_off,
                             uint32_t tc, hipStream_t s, uint32_t* d_sync = nullptr,
-                            const uint64_t* host_wr = nullptr, uint64_t in_words = 0) {
+                            const uint64_t* host_wr = nullptr) {
     if (n > 0 && !d_off) return CAPNP_E_INVALID_ARGUMENT;
     if (!d_out_off) return CAPNP_E_INVALID_ARGUMENT;
     UseMark um{ctx, s};
@@ -496,7 +496,6 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
         }
         if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
         const uint64_t words = wr[1] - wr[0];
-        if (wr[0] == 0) in_words = std::max<uint64_t>(in_words, wr[1]);  // (d_words holds them)
         if (words && (words / n >= kWordTileMean || force_word_tiles())) {
             const uint64_t ntiles = capnp_pack_wt_tiles(wr[0], wr[1]);
             capnp_status st = ensure_state(ctx, capnp_pack_state_bytes(ntiles, 1) + 16);
@@ -515,12 +514,8 @@ capnp_status pack_batch_dev(capnp_ctx* ctx, const uint64_t* d_words, const uint6
     const size_t sb = state_bytes_for(n, tc);
     capnp_status st = ensure_state(ctx, sb);
     if (st != CAPNP_OK) return st;
-    // a batch of 1 KiB segments (as many words as 128 per chunk): the kernel
-    // loads each tile's words at the guessed offsets with the offsets
-    // themselves (pack_cs_kernel spec_words; a wrong guess only costs a reload)
-    const uint64_t spec = (in_words == (uint64_t)n * 128 && tc == 16) ? in_words : 0;
     HIP_TRY(capnp_launch_pack(d_words, d_off, n, tc, d_out, cap, d_out_off,
-                              reinterpret_cast<uint64_t*>(ctx->d_state), d_sync, spec, s));
+                              reinterpret_cast<uint64_t*>(ctx->d_state), d_sync, s));
     return CAPNP_OK;
 }
 
@@ -762,14 +757,13 @@ capnp_status capnp_gpu_pack_batch(capnp_ctx* ctx, const uint64_t* d_words,
 }
 
 capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
-                                        size_t in_words, const uint64_t* d_chunk_word_off,
-                                        size_t nchunks, uint8_t* d_out, size_t out_cap,
+                                        const uint64_t* d_chunk_word_off, size_t nchunks,
+                                        uint8_t* d_out, size_t out_cap,
                                         uint64_t* d_out_byte_off, uint32_t chunks_per_tile,
                                         void* stream) {
     if (!ctx) return CAPNP_E_INVALID_ARGUMENT;
     return pack_batch_dev(ctx, d_words, d_chunk_word_off, nchunks, d_out, out_cap,
-                          d_out_byte_off, chunks_per_tile, pick(ctx, stream), nullptr, nullptr,
-                          in_words);
+                          d_out_byte_off, chunks_per_tile, pick(ctx, stream));
 }
 
 // With the record sync index and chunks_per_tile == 0 the launch is sized
@@ -869,14 +863,13 @@ capnp_status capnp_gpu_unpack_batch_sync(capnp_ctx* ctx, const uint8_t* d_packed
 }
 
 capnp_status capnp_gpu_pack_batch_sync_tuned(capnp_ctx* ctx, const uint64_t* d_words,
-                                             size_t in_words, const uint64_t* d_chunk_word_off,
-                                             size_t nchunks, uint8_t* d_out, size_t out_cap,
+                                             const uint64_t* d_chunk_word_off, size_t nchunks,
+                                             uint8_t* d_out, size_t out_cap,
                                              uint64_t* d_out_byte_off, uint32_t* d_sync,
                                              uint32_t chunks_per_tile, void* stream) {
     if (!ctx || !d_sync) return CAPNP_E_INVALID_ARGUMENT;
     return pack_batch_dev(ctx, d_words, d_chunk_word_off, nchunks, d_out, out_cap,
-                          d_out_byte_off, chunks_per_tile, pick(ctx, stream), d_sync, nullptr,
-                          in_words);
+                          d_out_byte_off, chunks_per_tile, pick(ctx, stream), d_sync);
 }
 
 capnp_status capnp_gpu_unpack_batch_sync_tuned(capnp_ctx* ctx, const uint8_t* d_packed,

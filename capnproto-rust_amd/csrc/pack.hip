@@ -1924,8 +1924,9 @@ pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ c
 // kCsSteps chunks of its tile.  Tiles with a longer chunk (or more chunks per
 // wave) take the streaming size pass and leave their bytes to
 // pack_ovf_kernel.
-#ifndef PACK_SPEC_BASE
-#define PACK_SPEC_BASE 1  // 0: no guessed tile base (A/B builds)
+#ifndef PACK_ABL
+#define PACK_ABL 0  // ablation builds (timing only, wrong bytes): 1 no LDS ORs, 2 no sync
+                    // stores, 4 no look-back (a fixed tile offset), 8 no copy-out
 #endif
 constexpr uint32_t kCsSteps = 4;   // chunks (steps) per wave
 constexpr uint32_t kCsWords = 128; // words per step
@@ -2038,11 +2039,15 @@ __device__ __forceinline__ void cs_emit_word_sel(uint64_t w, uint32_t info, uint
     const uint32_t e3 = __builtin_amdgcn_alignbyte(0u, r2, s);
     const uint32_t pos = info & ((1u << kInfoPosBits) - 1u);
     uint32_t* b32 = reinterpret_cast<uint32_t*>(__builtin_align_down(region_m1 + pos, 4));
+    if (!(PACK_ABL & 1)) {
     __hip_atomic_fetch_or(b32 + 0, e0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 1, e1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 2, e2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
     __hip_atomic_fetch_or(b32 + 3, e3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    if constexpr (SYNC) {
+    } else {
+        asm volatile("" ::"v"(e0), "v"(e1), "v"(e2), "v"(e3), "v"(b32));
+    }
+    if constexpr (SYNC && !(PACK_ABL & 2)) {
         if (idx < kSelCopy && d <= cnt) {
             const uint32_t rel = pos - oc;
             __builtin_amdgcn_raw_buffer_store_b32(rel | (d << 24), srs, (int)b, 0, 0);
@@ -2069,14 +2074,13 @@ __device__ __forceinline__ void cs_emit_word(uint64_t w, uint32_t info, uint8_t*
 
 // GAP (capnp_gpu_write_messages): chunk c is preceded by gap[c] bytes that the
 // kernel leaves zero (out_off[c] is the gap's start), as pack_kernel's GAP.
-template <bool SYNC, bool GAP = false, bool SPEC = false>
+template <bool SYNC, bool GAP = false>
 __global__ void __launch_bounds__(kThreads, 8)
 pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chunk_off,
                uint64_t nchunks, uint32_t tc, uint8_t* __restrict__ out, uint64_t out_cap,
                uint64_t* __restrict__ out_off, uint64_t* __restrict__ ts,
                uint64_t* __restrict__ gs, uint32_t* __restrict__ sync,
-               uint8_t* __restrict__ ovf, const uint32_t* __restrict__ gap = nullptr,
-               uint64_t spec_words = 0) {
+               uint8_t* __restrict__ ovf, const uint32_t* __restrict__ gap = nullptr) {
     static_assert(!(SYNC && GAP), "the sync index is not written with gaps");
     __shared__ Smem<false> sm;
     const uint32_t tid = threadIdx.x;
@@ -2102,51 +2106,13 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     const uint32_t wc0 = wave * q < nc ? wave * q : nc;
     const uint32_t wc1 = wc0 + q < nc ? wc0 + q : nc;
     const uint32_t nw = wc1 - wc0;
-    // (the wave's chunk offsets and its selector entry first: they depend on
-    // nothing loaded, and the waits for them must not wait for the words)
-    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint64_t*>(toff + wc0), 0, (int)((nw + 1) * 8), 0x00020000);
-    const uint32_t o = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(lane * 8u), 0, 0);
-    uint32_t gv = 0;  // GAP: lane s = the gap before the wave's chunk s
-    if constexpr (GAP) {
-        const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint32_t*>(gap + c0 + wc0), 0, (int)(nw * 4), 0x00020000);
-        gv = __builtin_amdgcn_raw_buffer_load_b32(grs, (int)(lane * 4u), 0, 0);
-    }
-    const Sel8 selv = kSel8Table.e[tid];
-    uint64_t clo[kCsSteps], chi[kCsSteps];
-    // spec_words != 0: the caller's batch is spec_words words in chunks of
-    // 128 (1 KiB segments): chunk c is guessed at word 128 c, so the word
-    // loads go out first, before the offset loads, instead of after them (one
-    // round trip instead of two); the guess is checked below (WS0) and the
-    // steps load again if it was wrong.  The guessed range lies inside the
-    // caller's spec_words words.
-    const uint64_t GW = (c0 + wc0) * kCsWords;  // (the guess of WS0)
-    if constexpr (SPEC) {
-        const uint64_t G0 = c0 * kCsWords;
-        const uint64_t avail = G0 < spec_words ? (spec_words - G0) * 8 : 0;
-        const uint32_t lim = (uint32_t)(avail < (uint64_t)tc * kCsWords * 8 ? avail
-                                                                             : (uint64_t)tc * kCsWords * 8);
-        const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint64_t*>(in + G0), 0, (int)lim, 0x00020000);
-        const uint32_t gsb = wc0 * kCsWords;
-#pragma unroll
-        for (uint32_t s = 0; s < kCsSteps; s++) {
-            const uint32_t vlo = s < nw ? (gsb + kCsWords * s + lane) * 8u : 0x80000000u;
-            const uint32_t vhi = s < nw ? (gsb + kCsWords * s + 64u + lane) * 8u : 0x80000000u;
-            const auto x = __builtin_amdgcn_raw_buffer_load_b64(grs, (int)vlo, 0, 0);
-            const auto y = __builtin_amdgcn_raw_buffer_load_b64(grs, (int)vhi, 0, 0);
-            clo[s] = ((uint64_t)x[1] << 32) | x[0];
-            chi[s] = ((uint64_t)y[1] << 32) | y[0];
-        }
-    }
-    __builtin_amdgcn_sched_barrier(0);
     const uint64_t TW0 = uniform64(chunk_off[c0]);
     const uint64_t WS0 = uniform64(toff[wc0]);
     const uint64_t TW1 = uniform64(chunk_off[c1]);
     const uint32_t tile_bytes = (uint32_t)((TW1 - TW0) * 8);
     const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint64_t*>(in + TW0), 0, (int)tile_bytes, 0x00020000);
+    uint64_t clo[kCsSteps], chi[kCsSteps];
     // Every load of the prologue is issued in one round trip: the scalar
     // offsets (TW0, TW1, the wave's first chunk WS0), the wave's chunk offsets
     // (one buffer load, lane l <= nw: toff[wc0 + l]; lanes past them read 0,
@@ -2158,24 +2124,32 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     // (The compiler had waited for the table entry, then for each of the two
     // offset loads, before the word loads: four round trips.)
     // (the offsets' low words: lengths and tile offsets fit 32 bits)
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint64_t*>(toff + wc0), 0, (int)((nw + 1) * 8), 0x00020000);
+    const uint32_t o = __builtin_amdgcn_raw_buffer_load_b32(crs, (int)(lane * 8u), 0, 0);
+    uint32_t gv = 0;  // GAP: lane s = the gap before the wave's chunk s
+    if constexpr (GAP) {
+        const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t*>(gap + c0 + wc0), 0, (int)(nw * 4), 0x00020000);
+        gv = __builtin_amdgcn_raw_buffer_load_b32(grs, (int)(lane * 4u), 0, 0);
+    }
+    const Sel8 selv = kSel8Table.e[tid];
     const uint32_t sb = (uint32_t)(WS0 - TW0);
-    if constexpr (!SPEC) {
 #pragma unroll
-        for (uint32_t s = 0; s < kCsSteps; s++) {
-            const uint32_t vlo = s < nw ? (sb + kCsWords * s + lane) * 8u : 0x80000000u;
-            const uint32_t vhi = s < nw ? (sb + kCsWords * s + 64u + lane) * 8u : 0x80000000u;
-            const auto x = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vlo, 0, 0);
-            const auto y = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vhi, 0, 0);
-            clo[s] = ((uint64_t)x[1] << 32) | x[0];
-            chi[s] = ((uint64_t)y[1] << 32) | y[0];
-        }
+    for (uint32_t s = 0; s < kCsSteps; s++) {
+        const uint32_t vlo = s < nw ? (sb + kCsWords * s + lane) * 8u : 0x80000000u;
+        const uint32_t vhi = s < nw ? (sb + kCsWords * s + 64u + lane) * 8u : 0x80000000u;
+        const auto x = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vlo, 0, 0);
+        const auto y = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (int)vhi, 0, 0);
+        clo[s] = ((uint64_t)x[1] << 32) | x[0];
+        chi[s] = ((uint64_t)y[1] << 32) | y[0];
     }
     const uint32_t onext = (uint32_t)__shfl_down((int)o, 1, 64);
     const uint32_t d_off = lane < nw ? o - (uint32_t)TW0 : 0u;
     const uint32_t d_len = lane < nw ? onext - o : 0u;
     const bool ok = nw <= kCsSteps && ballot64(lane < nw && d_len > kCsWords) == 0;
     if (lane == 0) sm.wave_steps[wave] = ok ? 0u : 1u;
-    if ((SPEC && WS0 != GW) || ballot64(lane + 1u < nw && d_len != kCsWords) != 0) {
+    if (ballot64(lane + 1u < nw && d_len != kCsWords) != 0) {
         // (the speculative values enter the reloaded ones through an opaque
         // zero, so the compiler keeps their loads ahead of this branch)
         uint64_t z;
@@ -2322,7 +2296,12 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
         wave_lds_sync();
         if (lane == 0) TRACE(tile, 3, RT());
 #endif
+#if PACK_ABL & 4
+        const uint64_t excl = tile * 8800ull;
+        (void)early_group;
+#else
         const uint64_t excl = tile_offset(LA, tile, agg, lane, early_group);
+#endif
 #if PACK_PROF == 3
         if (lane == 0) TRACE(tile, 4, RT());
 #endif
@@ -2332,7 +2311,7 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     __syncthreads();
     for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
     if (fits) {
-        if (nw) {
+        if (nw && !(PACK_ABL & 8)) {
             const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
             const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
             copy_out(region, out - mis, D0, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
@@ -3221,9 +3200,8 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_
                                         uint64_t nchunks, uint32_t tc, uint8_t* d_out,
                                         uint64_t out_cap, uint64_t* d_out_off,
                                         uint64_t* d_state, uint32_t* d_sync,
-                                        uint64_t spec_words, hipStream_t stream) {
+                                        hipStream_t stream) {
     if (tc == 0 || tc > kMaxTileChunks) return hipErrorInvalidValue;
-    if (!PACK_SPEC_BASE) spec_words = 0;
     const uint64_t ntiles = (nchunks + tc - 1) / tc;
     if (nchunks == 0) {
         return hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), stream);
@@ -3234,24 +3212,14 @@ extern "C" hipError_t capnp_launch_pack(const uint64_t* d_in, const uint64_t* d_
     if (tc == kWaves * kCsSteps) {
         // chunks of at most 128 words (tc chosen for a mean of 65-128 words;
         // a tile with a longer chunk takes the streaming size pass)
-        if (d_sync && spec_words)
-            hipLaunchKernelGGL((pack_cs_kernel<true, false, true>), dim3((uint32_t)ntiles),
-                               dim3(kThreads), 0, stream, d_in, d_chunk_off, nchunks, tc, d_out,
-                               out_cap, d_out_off, d_state, d_state + ntiles, d_sync, ovf, nullptr,
-                               spec_words);
-        else if (d_sync)
+        if (d_sync)
             hipLaunchKernelGGL((pack_cs_kernel<true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
                                stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,
-                               d_state, d_state + ntiles, d_sync, ovf, nullptr, 0);
-        else if (spec_words)
-            hipLaunchKernelGGL((pack_cs_kernel<false, false, true>), dim3((uint32_t)ntiles),
-                               dim3(kThreads), 0, stream, d_in, d_chunk_off, nchunks, tc, d_out,
-                               out_cap, d_out_off, d_state, d_state + ntiles, d_sync, ovf, nullptr,
-                               spec_words);
+                               d_state, d_state + ntiles, d_sync, ovf);
         else
             hipLaunchKernelGGL((pack_cs_kernel<false>), dim3((uint32_t)ntiles), dim3(kThreads),
                                0, stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap,
-                               d_out_off, d_state, d_state + ntiles, d_sync, ovf, nullptr, 0);
+                               d_out_off, d_state, d_state + ntiles, d_sync, ovf);
     } else if (d_sync) {
         hipLaunchKernelGGL((pack_lean_kernel<true>), dim3((uint32_t)ntiles), dim3(kThreads), 0,
                            stream, d_in, d_chunk_off, nchunks, tc, d_out, out_cap, d_out_off,

@@ -214,13 +214,10 @@ capnp_status capnp_gpu_unpack_batch_sync(capnp_ctx* ctx, const uint8_t* d_packed
    output words and <= 4.5x that many packed bytes.  The offset arrays are
    not validated by these forms: the caller guarantees them non-decreasing
    (a decreasing offset is a chunk of negative length, read or written out
-   of bounds).  Pack: in_words = the words d_words holds (0 = not given);
-   when it is 128 x nchunks (1 KiB segments) each tile's words are loaded at
-   their guessed offsets together with the offsets (one round trip instead
-   of two; a wrong guess costs a reload, never a different result). */
+   of bounds). */
 capnp_status capnp_gpu_pack_batch_tuned(capnp_ctx* ctx, const uint64_t* d_words,
-                                        size_t in_words, const uint64_t* d_chunk_word_off,
-                                        size_t nchunks, uint8_t* d_out, size_t out_cap,
+                                        const uint64_t* d_chunk_word_off, size_t nchunks,
+                                        uint8_t* d_out, size_t out_cap,
                                         uint64_t* d_out_byte_off, uint32_t chunks_per_tile,
                                         void* stream);
 
@@ -232,8 +229,8 @@ capnp_status capnp_gpu_unpack_batch_tuned(capnp_ctx* ctx, const uint8_t* d_packe
 
 /* The record-sync-index batch calls with an explicit tile size. */
 capnp_status capnp_gpu_pack_batch_sync_tuned(capnp_ctx* ctx, const uint64_t* d_words,
-                                             size_t in_words, const uint64_t* d_chunk_word_off,
-                                             size_t nchunks, uint8_t* d_out, size_t out_cap,
+                                             const uint64_t* d_chunk_word_off, size_t nchunks,
+                                             uint8_t* d_out, size_t out_cap,
                                              uint64_t* d_out_byte_off, uint32_t* d_sync,
                                              uint32_t chunks_per_tile, void* stream);
 capnp_status capnp_gpu_unpack_batch_sync_tuned(capnp_ctx* ctx, const uint8_t* d_packed,
@@ -538,10 +535,11 @@ capnp_packed_reader* capnp_packed_reader_new(capnp_ctx* ctx, capnp_read_fn fn, v
 void capnp_packed_reader_free(capnp_packed_reader* r);
 /* Bulk read-ahead (off by default): pull input in MiB units past what the
    current read can need, while the inner reader returns every byte asked
-   (a file, a memory stream).  Off, a read pulls only until the staged
-   input can complete it (at most 10 bytes a word), as the reference reads
-   no further than the current request: a blocking pipe or socket whose peer
-   sent exactly one request's worth and awaits a reply is not read past it. */
+   (a file, a memory stream).  Off, a read first decodes what is staged and
+   pulls only when no complete record is (a read may then return fewer bytes
+   than asked, as poll_read does), so, as the reference reads no further than
+   the current request, a blocking pipe or socket whose peer sent exactly one
+   request's worth and awaits a reply is never read past it. */
 void capnp_packed_reader_set_readahead(capnp_packed_reader* r, int on);
 /* poll_read (:74-225): 1..len unpacked bytes in *nread, 0 at a clean end of
    the stream, CAPNP_PENDING when the inner reader pends, and

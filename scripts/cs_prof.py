@@ -35,8 +35,8 @@ def main():
     vp, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
     L.capnp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int)]
     L.capnp_ctx_create.restype = vp
-    L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, u32, vp]
-    L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, vp, u32, vp]
+    L.capnp_gpu_pack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, u32, vp]
+    L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, u32, vp]
     L.capnp_ctx_reserve.argtypes = [vp, sz]
     L.capnp_pack_trace.argtypes = [vp]
     st = C.c_int(0)
@@ -63,11 +63,11 @@ def main():
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         if a.sync:
-            L.capnp_gpu_pack_batch_sync_tuned(h, P(words.data_ptr()), words.numel(), P(offs.data_ptr()), n,
+            L.capnp_gpu_pack_batch_sync_tuned(h, P(words.data_ptr()), P(offs.data_ptr()), n,
                                               P(out.data_ptr()), cap, P(oo.data_ptr()),
                                               P(sync.data_ptr()), tc, P(stream.cuda_stream))
         else:
-            L.capnp_gpu_pack_batch_tuned(h, P(words.data_ptr()), words.numel(), P(offs.data_ptr()), n,
+            L.capnp_gpu_pack_batch_tuned(h, P(words.data_ptr()), P(offs.data_ptr()), n,
                                          P(out.data_ptr()), cap, P(oo.data_ptr()), tc,
                                          P(stream.cuda_stream))
         e1.record(stream)

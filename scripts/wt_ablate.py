@@ -20,7 +20,7 @@ def load(path):
     vp, sz, u32 = C.c_void_p, C.c_size_t, C.c_uint32
     L.capnp_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_int)]
     L.capnp_ctx_create.restype = vp
-    L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, sz, vp, sz, vp, sz, vp, vp, u32, vp]
+    L.capnp_gpu_pack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, sz, vp, vp, u32, vp]
     L.capnp_gpu_unpack_batch_sync_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, vp, u32, vp]
     L.capnp_gpu_unpack_batch_tuned.argtypes = [vp, vp, vp, sz, vp, vp, vp, vp, u32, vp]
     st = C.c_int(0)
@@ -81,7 +81,7 @@ def main():
                 e0.record(stream)
                 for _ in range(5):
                     if kind == "pack":
-                        L.capnp_gpu_pack_batch_sync_tuned(h, P(words.data_ptr()), words.numel(), P(offs.data_ptr()), n,
+                        L.capnp_gpu_pack_batch_sync_tuned(h, P(words.data_ptr()), P(offs.data_ptr()), n,
                                                           P(out.data_ptr()), cap, P(oo.data_ptr()),
                                                           P(sync.data_ptr()), tc, P(stream.cuda_stream))
                     elif kind == "nosync":
