@@ -469,6 +469,11 @@ bool force_word_tiles() {
 // Batches whose mean chunk is at least this many words pack (and, with the
 // record sync index, unpack) in word tiles.
 constexpr uint64_t kWordTileMean = 512;
+// index-free batches of at least kLongUnitsMin units whose mean is in
+// [kLongUnitWords, kBlockDecodeWords) decode one unit per workgroup
+constexpr uint64_t kLongUnitsMin = 256;
+constexpr uint64_t kLongUnitWords = 2048;
+constexpr uint64_t kBlockDecodeWords = 32768;
 
 // tc == 0: the launch is sized from the batch's word range (one
 // synchronisation to read it): word tiles (capnp_launch_pack_wt: chunks of
@@ -800,11 +805,25 @@ static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
         if (wr[1] < wr[0]) return CAPNP_E_INVALID_ARGUMENT;
         const uint64_t words = wr[1] - wr[0];
         const bool longc = words && (words / nchunks >= kWordTileMean || force_word_tiles());
-        if (longc && !d_sync)  // no index: the speculative block walk (resync.hip); both
-                               // offset arrays were checked just above
+        const uint64_t mean = words / nchunks;
+        if (longc && !d_sync && !force_word_tiles() && nchunks >= kLongUnitsMin &&
+            mean >= kLongUnitWords && mean < kBlockDecodeWords) {
+            // no index, enough units of a few thousand words each to fill the
+            // chip: one workgroup per unit (the long-unit decode, unpack.hip
+            // unpack_long) beats resolving blocks (scripts/long_unit_bench.py:
+            // 256 x 8192 words 67 vs 152 us, 2300 x 8192 178 vs 292,
+            // profiles/r06b_long_unit_auto.txt)
+            tc = 1;
+        } else if (longc && !d_sync) {
+            // no index, few units or mixed sizes: the speculative block walk
+            // spreads every unit over the chip (resync.hip; 2 x 1 Mi words 211 us
+            // against 4.4 ms on two workgroups, config 4 1.65 ms against
+            // 2.14-2.47 in chunk tiles, profiles/r06d_route_probe.txt); both offset
+            // arrays were checked just above
             return unpack_resync_dev(ctx, d_packed, d_in_byte_off, nchunks, d_words,
                                      d_out_word_off, d_status, d_consumed, s, br);
-        if (longc) {
+        }
+        if (longc && d_sync) {
             const size_t ws = capnp_unpack_wt_ws_bytes(wr[0], wr[1]);
             capnp_status st = ensure_buf(ctx, &ctx->d_wt, &ctx->wt_cap, ws);
             if (st != CAPNP_OK) return st;
@@ -813,9 +832,11 @@ static capnp_status unpack_batch_dev(capnp_ctx* ctx, const uint8_t* d_packed,
                                            wr[1], ctx->d_wt, ctx->wt_cap, s));
             return CAPNP_OK;
         }
-        const uint64_t mean = words / nchunks ? words / nchunks : 1;
-        const uint64_t t = capnp_unpack_tile_words() / mean;
-        tc = (uint32_t)(t < 1 ? 1 : (t > 64 ? 64 : t));
+        if (tc == 0) {
+            const uint64_t m = mean ? mean : 1;
+            const uint64_t t = capnp_unpack_tile_words() / m;
+            tc = (uint32_t)(t < 1 ? 1 : (t > 64 ? 64 : t));
+        }
     }
     HIP_TRY(capnp_launch_unpack(d_packed, d_in_byte_off, nchunks, tc, d_words, d_out_word_off,
                                 d_status, d_consumed, d_sync, pick(ctx, stream)));

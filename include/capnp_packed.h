@@ -164,7 +164,9 @@ capnp_status capnp_gpu_pack_batch(capnp_ctx* ctx, const uint64_t* d_words,
    d_out_word_off[0] and [nchunks] to size the launch); a batch whose mean
    chunk is >= 512 words then takes the index-free block decode of
    capnp_gpu_unpack_batch_resync (one more synchronisation, before its
-   decode).  The decode itself is only enqueued: d_words, d_status and
+   decode), which spreads each unit over the whole chip -- except a batch of
+   >= 256 units of 2048-32767 words on average, which fills the chip with one
+   workgroup per unit.  The decode itself is only enqueued: d_words, d_status and
    d_consumed are ordered on `stream` (read them after a synchronisation of
    `stream`, or from work queued on it) -- never with a plain hipMemcpy or
    from another stream without an event.
