@@ -69,10 +69,7 @@ namespace {
 
 constexpr int kWaves = 4;  // waves per workgroup (tile = kWaves x kStageSteps x 64 words)
 constexpr int kThreads = kWaves * CAPNP_WAVE;
-#ifndef PACK_W0COPY
-#define PACK_W0COPY 0  // probe: smaller regions; waves 1-3 end after pass 2, wave 0 copies all
-#endif
-constexpr uint32_t kRing = PACK_W0COPY ? 2048 : 4096;  // streaming path: per-wave ring (bytes)
+constexpr uint32_t kRing = 4096;           // streaming path: per-wave ring (bytes)
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr int kMaxTileChunks = 64;
 constexpr uint32_t kZeroAhead = 1024;      // ring bytes zeroed per refill
@@ -98,7 +95,7 @@ constexpr uint32_t kRegion = (kStageBytesMax + kGapSlack + 32 + 15) & ~15u;
 // smaller regions and the 8-byte selector entries fit 8 workgroups per CU
 // (20.3 KB each) where the worst-case layout fit 6 (23.8 KB): 608 -> 570 us
 // at config 2 in a trial build.
-constexpr uint32_t kStageBytes = PACK_W0COPY ? PACK_W0COPY : 4192;
+constexpr uint32_t kStageBytes = 4192;
 static_assert(kStageBytes <= kStageBytesMax && kStageBytes % 16 == 0, "stage capacity");
 constexpr uint32_t kStageRegion = (kStageBytes + 32 + 15) & ~15u;
 // per-wave LDS region of the chunk tiles: the staged bytes, or the
@@ -2294,28 +2291,6 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             __builtin_amdgcn_sched_barrier(0);
         }
     }
-#if PACK_W0COPY
-    if (fits) {
-        // waves 1-3 end here (their registers free for the next tile); wave 0
-        // finds the offset and copies every wave's region
-        __syncthreads();
-        if (wave != 0) return;
-        const uint64_t excl = tile_offset(LA, tile, agg, lane, early_group);
-        if (lane < nc) sm.chunk_pos[lane] += excl;
-        if (c1 == nchunks && lane == 0) out_off[nchunks] = excl + agg;
-        wave_lds_sync();
-        if (lane < nc) out_off[c0 + lane] = sm.chunk_pos[lane];
-        const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
-        const uint32_t q = (nc + kWaves - 1) / kWaves;
-        for (uint32_t w = 0; w < kWaves; w++) {
-            const uint32_t a = w * q;
-            if (a >= nc) break;
-            const uint64_t D0 = lds_u64(&sm.chunk_pos[a]) + mis;
-            copy_out(sm.stage[w], out - mis, D0, lds_u64(&sm.wave_bytes[w]), out_cap + mis, lane);
-        }
-        return;
-    }
-#endif
     if (wave == 0) {
 #if PACK_PROF == 3
         wave_lds_sync();
