@@ -7,6 +7,8 @@ the C oracle on small inputs.  Written independently of the C restatement
     pack(data)                  PackedWrite::write_all  capnp/src/serialize_packed.rs:304-439
     read(data, out_len)         PackedRead::read        capnp/src/serialize_packed.rs:80-228
     read_exact(data, out_len)   io::Read::read_exact    capnp/src/io.rs:16-31
+    async_poll_reads(...)       capnp-futures PackedRead::poll_read
+                                capnp-futures/src/serialize_packed.rs:87-225
 """
 
 OK = 0
@@ -102,3 +104,90 @@ def read_exact(data: bytes, out_len: int):
     if st == OK and nread != out_len:
         st = FAILED_TO_FILL_WHOLE_BUFFER
     return st, out, used
+
+
+def async_poll_reads(packed, size, inner_max=1 << 30):
+    """capnp-futures PackedRead::poll_read (capnp-futures/src/
+    serialize_packed.rs:87-225: stages Start :101-141, WritingZeroes
+    :142-155, BufferingWord :156-172, DrainingBuffer :173-198,
+    WritingPassthrough :199-221) over a slice reader that returns up to
+    `inner_max` bytes a read, polled with reads of `size` bytes until one
+    returns 0 bytes or UnexpectedEof.  Returns (the bytes handed out, b"" for
+    the clean end or "EOF" for UnexpectedEof)."""
+    data, pos = bytes(packed), 0
+    st = {"stage": "start", "buf": [0] * 10, "bp": 0, "bs": 10, "bit": 0, "rem": 0}
+
+    def inner(n):
+        nonlocal pos
+        b = data[pos:pos + min(n, inner_max)]
+        pos += len(b)
+        return b
+
+    def poll():
+        while True:
+            s = st["stage"]
+            if s == "start":
+                b = inner(2 - st["bp"])
+                if not b:
+                    return "EOF" if st["bp"] > 0 else b""
+                st["buf"][st["bp"]:st["bp"] + len(b)] = list(b)
+                st["bp"] += len(b)
+                if st["bp"] >= 2:
+                    tag, cnt = st["buf"][0], st["buf"][1]
+                    if tag == 0:
+                        st["stage"], st["rem"] = "zero", (cnt + 1) * 8
+                    else:
+                        st["stage"] = "buffering"
+                        st["bs"] = bin(tag).count("1") + 1
+                        if st["bs"] == 9:
+                            st["bs"] = 10
+                        if st["bp"] >= st["bs"]:
+                            st["stage"], st["bp"], st["bit"] = "drain", 1, 0
+            elif s == "zero":
+                k = min(size, st["rem"])
+                if k >= st["rem"]:
+                    st["bp"], st["stage"] = 0, "start"
+                else:
+                    st["rem"] -= k
+                return bytes(k)
+            elif s == "buffering":
+                b = inner(st["bs"] - st["bp"])
+                if not b:
+                    return "EOF"
+                st["buf"][st["bp"]:st["bp"] + len(b)] = list(b)
+                st["bp"] += len(b)
+                if st["bp"] >= st["bs"]:
+                    st["stage"], st["bp"], st["bit"] = "drain", 1, 0
+            elif s == "drain":
+                out = []
+                while len(out) < size and st["bit"] < 8:
+                    nz = (st["buf"][0] >> st["bit"]) & 1
+                    out.append(st["buf"][st["bp"]] if nz else 0)
+                    st["bp"] += nz
+                    st["bit"] += 1
+                if st["bit"] == 8:
+                    if st["bp"] == st["bs"]:
+                        st["stage"] = "start"
+                    else:
+                        st["rem"], st["stage"] = st["buf"][st["bp"]] * 8, "pass"
+                    st["bp"] = 0
+                return bytes(out)
+            else:  # pass
+                ub = min(st["rem"], size)
+                if ub == 0:
+                    st["stage"] = "start"
+                    continue
+                b = inner(ub)
+                if not b:
+                    return "EOF"
+                if len(b) >= st["rem"]:
+                    st["stage"] = "start"
+                st["rem"] -= len(b)
+                return b
+
+    got = b""
+    while True:
+        r = poll()
+        if r == "EOF" or r == b"":
+            return got, r
+        got += r

@@ -301,3 +301,37 @@ def test_generator_statistics():
     st, packed, poffs = O.pack_batch(w, offs)
     ratio = len(packed) / (8 * len(w))
     assert 0.50 < ratio < 0.58, ratio
+
+
+# ---- the async PackedRead restatement, pinned by the reference's own tests
+def test_async_poll_reads_golden_blocking_periods():
+    """capnp-futures serialize_packed.rs:603-671: every packing vector read
+    back through readers that return at most 1..9 bytes a read, with reads
+    of 1..9 bytes (check_packing's blocking periods)."""
+    with open(GOLDEN) as f:
+        g = json.load(f)
+    for v in g["packing"]:
+        u, p = bytes(v["unpacked"]), bytes(v["packed"])
+        for inner_max in range(1, 10):
+            for size in range(1, 10):
+                got, end = R.async_poll_reads(p, size, inner_max)
+                assert got == u and end == b"", (v["ref"], inner_max, size)
+
+
+def test_async_poll_reads_reference_cases():
+    """The reference's async edge tests (capnp-futures
+    serialize_packed.rs:747-814)."""
+    # unpacks_across_partial_output_buffers (:748-760)
+    assert R.async_poll_reads(bytes([0x81, 42, 99]), 1) == (bytes([42, 0, 0, 0, 0, 0, 0, 99]), b"")
+    assert R.async_poll_reads(
+        bytes([0xff, 1, 3, 2, 4, 5, 7, 6, 8, 1, 8, 6, 7, 4, 5, 2, 3, 1]), 3) == (
+        bytes([1, 3, 2, 4, 5, 7, 6, 8, 8, 6, 7, 4, 5, 2, 3, 1]), b"")
+    # eof_mid_tag_word (:762-773): one byte of a tag word, then the end
+    assert R.async_poll_reads(bytes([0x81]), 8)[1] == "EOF"
+    # eof_mid_passthrough_run (:775-790): two raw words promised, four bytes there
+    got, end = R.async_poll_reads(bytes([0xff, 1, 2, 3, 4, 5, 6, 7, 8, 2, 10, 11, 12, 13]), 64)
+    assert end == "EOF" and got == bytes([1, 2, 3, 4, 5, 6, 7, 8, 10, 11, 12, 13])
+    # read_empty (:792-800): a clean end at once
+    assert R.async_poll_reads(b"", 8) == (b"", b"")
+    # eof_mid_message (:802-813): the first table word's tag wants 7 bytes, 2 are there
+    assert R.async_poll_reads(bytes([0xfe, 3, 3]), 8)[1] == "EOF"
