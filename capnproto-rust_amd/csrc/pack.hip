@@ -677,6 +677,58 @@ __device__ __forceinline__ void copy_out(const uint8_t* region, uint8_t* __restr
     if (lane < hi - b) out[b + lane] = region[(b - D0) + lane];
 }
 
+// The same for a whole tile whose waves' bytes lie back to back in LDS
+// (PACK_TILECOPY): the tile's 16-byte output blocks are cut into one range
+// per wave, and only the tile's two edges take byte stores.
+__device__ __forceinline__ void copy_out_tile(const uint8_t* region, uint8_t* __restrict__ out,
+                                              uint64_t D0, uint64_t len, uint64_t cap,
+                                              uint32_t lane, uint32_t wave) {
+    const uint64_t lo = D0;
+    const uint64_t hi = (D0 + len < cap) ? D0 + len : cap;
+    if (hi <= lo) return;
+    const uint64_t a = (lo + 15) & ~15ull, b = hi & ~15ull;
+    if (a > b) {
+        if (wave == 0 && lane < hi - lo) out[lo + lane] = region[lane];
+        return;
+    }
+    if (wave == 0 && lane < a - lo) out[lo + lane] = region[lane];
+    if (wave == kWaves - 1 && lane < hi - b) out[b + lane] = region[(b - D0) + lane];
+    const uint32_t nb = (uint32_t)((b - a) >> 4);
+    const uint32_t k0 = nb * wave / kWaves, k1 = nb * (wave + 1) / kWaves;
+    const uint32_t m = (uint32_t)((a - D0) & 15);  // source misalignment (uniform)
+    const uint32_t q = m >> 2, sb = m & 3;
+    for (uint32_t k = k0 + lane; k < k1; k += CAPNP_WAVE) {
+        const uint64_t blk = a + 16ull * k;
+        const uint32_t s = (uint32_t)(blk - D0) & ~15u;
+        const uint4 A = *reinterpret_cast<const uint4*>(region + s);
+        const uint4 B = *reinterpret_cast<const uint4*>(region + s + 16);
+        const uint32_t w[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+        uint4 o;
+        if (q == 0) {
+            o = make_uint4(__builtin_amdgcn_alignbyte(w[1], w[0], sb),
+                           __builtin_amdgcn_alignbyte(w[2], w[1], sb),
+                           __builtin_amdgcn_alignbyte(w[3], w[2], sb),
+                           __builtin_amdgcn_alignbyte(w[4], w[3], sb));
+        } else if (q == 1) {
+            o = make_uint4(__builtin_amdgcn_alignbyte(w[2], w[1], sb),
+                           __builtin_amdgcn_alignbyte(w[3], w[2], sb),
+                           __builtin_amdgcn_alignbyte(w[4], w[3], sb),
+                           __builtin_amdgcn_alignbyte(w[5], w[4], sb));
+        } else if (q == 2) {
+            o = make_uint4(__builtin_amdgcn_alignbyte(w[3], w[2], sb),
+                           __builtin_amdgcn_alignbyte(w[4], w[3], sb),
+                           __builtin_amdgcn_alignbyte(w[5], w[4], sb),
+                           __builtin_amdgcn_alignbyte(w[6], w[5], sb));
+        } else {
+            o = make_uint4(__builtin_amdgcn_alignbyte(w[4], w[3], sb),
+                           __builtin_amdgcn_alignbyte(w[5], w[4], sb),
+                           __builtin_amdgcn_alignbyte(w[6], w[5], sb),
+                           __builtin_amdgcn_alignbyte(w[7], w[6], sb));
+        }
+        *reinterpret_cast<uint4*>(out + blk) = o;
+    }
+}
+
 // Streaming path: wave w owns chunks w, w+4, ...  MODE_SIZE fills
 // chunk_size; MODE_RING re-reads and writes at chunk_pos.
 template <int MODE, uint32_t NWV = kWaves>
@@ -1924,6 +1976,9 @@ pack_lean_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ c
 // kCsSteps chunks of its tile.  Tiles with a longer chunk (or more chunks per
 // wave) take the streaming size pass and leave their bytes to
 // pack_ovf_kernel.
+#ifndef PACK_TILECOPY
+#define PACK_TILECOPY 1  // chunk-step tiles: the waves' bytes back to back in LDS, one tile copy-out
+#endif
 #ifndef PACK_ABL
 #define PACK_ABL 0  // ablation builds (timing only, wrong bytes): 1 no LDS ORs, 2 no sync
                     // stores, 4 no look-back (a fixed tile offset), 8 no copy-out
@@ -2023,7 +2078,8 @@ __device__ __forceinline__ uint32_t cs_size_step(uint64_t wlo, uint64_t whi, uin
 template <bool SYNC>
 __device__ __forceinline__ void cs_emit_word_sel(uint64_t w, uint32_t info, uint8_t* region_m1,
                                                  Sel8 se, __amdgpu_buffer_rsrc_t srs,
-                                                 uint32_t oc, uint32_t d, uint32_t b) {
+                                                 uint32_t oc, uint32_t d, uint32_t b,
+                                                 uint32_t wof = 0) {
     if (info >= kCsSkip) return;  // (the skip flag is the top field)
     const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
     const uint32_t idx = __builtin_amdgcn_ubfe(info, kInfoPosBits, 9);
@@ -2032,7 +2088,9 @@ __device__ __forceinline__ void cs_emit_word_sel(uint64_t w, uint32_t info, uint
     const uint32_t r0 = __builtin_amdgcn_perm(hi, lo, se.s0) | hdr;
     const uint32_t r1 = __builtin_amdgcn_perm(hi, lo, se.s1);
     const uint32_t r2 = idx == 0xFFu ? ((hi >> 24) | (cnt << 8)) : 0u;
-    const uint32_t s = 0u - info;  // (alignbyte reads bits 1:0: -pos mod 4)
+    // (alignbyte reads bits 1:0: -(wof + pos) mod 4; wof = the wave's start
+    // in a tile-contiguous layout, PACK_TILECOPY)
+    const uint32_t s = 0u - info - wof;
     const uint32_t e0 = __builtin_amdgcn_alignbyte(r0, 0u, s);
     const uint32_t e1 = __builtin_amdgcn_alignbyte(r1, r0, s);
     const uint32_t e2 = __builtin_amdgcn_alignbyte(r2, r1, s);
@@ -2067,9 +2125,10 @@ __device__ __forceinline__ Sel8 cs_sel(const Sel8* sel, uint32_t info) {
 template <bool SYNC>
 __device__ __forceinline__ void cs_emit_word(uint64_t w, uint32_t info, uint8_t* region_m1,
                                              const Sel8* sel, __amdgpu_buffer_rsrc_t srs,
-                                             uint32_t oc, uint32_t d, uint32_t b) {
+                                             uint32_t oc, uint32_t d, uint32_t b,
+                                             uint32_t wof = 0) {
     if (info >= kCsSkip) return;  // (the skip flag is the top field)
-    cs_emit_word_sel<SYNC>(w, info, region_m1, cs_sel(sel, info), srs, oc, d, b);
+    cs_emit_word_sel<SYNC>(w, info, region_m1, cs_sel(sel, info), srs, oc, d, b, wof);
 }
 
 // GAP (capnp_gpu_write_messages): chunk c is preceded by gap[c] bytes that the
@@ -2250,9 +2309,20 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     if (lane == 0) sm.wave_bytes[wave] = local;
     __syncthreads();
     bool fits = true;
+    uint32_t woff = 0, tbytes = 0;  // (PACK_TILECOPY: this wave's start, the tile's bytes)
 #pragma unroll
-    for (int w = 0; w < kWaves; w++) fits &= sm.wave_bytes[w] <= kStageBytes;
+    for (int w = 0; w < kWaves; w++) {
+        const uint32_t wb = (uint32_t)sm.wave_bytes[w];
+        if (PACK_TILECOPY) {
+            woff += (uint32_t)w < wave ? wb : 0u;
+            tbytes += wb;
+        } else {
+            fits &= wb <= kStageBytes;
+        }
+    }
+    if (PACK_TILECOPY) fits = tbytes <= kWaves * kStageBytes;
     fits = __builtin_amdgcn_readfirstlane((int)fits) != 0;
+    woff = (uint32_t)__builtin_amdgcn_readfirstlane((int)woff);
     uint64_t agg = 0;
     if (wave == 0) {
         agg = scan_chunks32(sm, nc, lane);
@@ -2274,7 +2344,7 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     }
     // ---- pass 2: the bytes (the look-back loads are in flight)
     if (fits) {
-        uint8_t* const region_m1 = region - 1;
+        uint8_t* const region_m1 = (PACK_TILECOPY ? &sm.stage[0][0] + woff : region) - 1;
         const uint32_t t0 = (uint32_t)(k0 * kSyncWords - TW0);
         const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
             SYNC ? sync + k0 : nullptr, 0, SYNC ? (int)((k1 - k0) * 4) : 0, 0x00020000);
@@ -2285,9 +2355,10 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
             const uint32_t c = t0 - g;
             const uint32_t d = (c - lane) & (kSyncWords - 1);
             const uint32_t b = (lane + d - c) / (kSyncWords / 4u);
-            cs_emit_word<SYNC>(clo[s], ilo[s], region_m1, sm.sel, srs, oc, d, b);
+            cs_emit_word<SYNC>(clo[s], ilo[s], region_m1, sm.sel, srs, oc, d, b,
+                               PACK_TILECOPY ? woff : 0u);
             cs_emit_word<SYNC>(chi[s], ihi[s], region_m1, sm.sel, srs, oc, d,
-                               b + 64u / (kSyncWords / 4u));
+                               b + 64u / (kSyncWords / 4u), PACK_TILECOPY ? woff : 0u);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -2311,7 +2382,11 @@ pack_cs_kernel(const uint64_t* __restrict__ in, const uint64_t* __restrict__ chu
     __syncthreads();
     for (uint32_t i = tid; i < nc; i += kThreads) out_off[c0 + i] = sm.chunk_pos[i];
     if (fits) {
-        if (nw && !(PACK_ABL & 8)) {
+        if (PACK_TILECOPY && !(PACK_ABL & 8)) {
+            const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
+            const uint64_t D0 = lds_u64(&sm.chunk_pos[0]) + mis;
+            copy_out_tile(&sm.stage[0][0], out - mis, D0, tbytes, out_cap + mis, lane, wave);
+        } else if (nw && !(PACK_ABL & 8)) {
             const uint32_t mis = (uint32_t)(reinterpret_cast<uintptr_t>(out) & 15u);
             const uint64_t D0 = lds_u64(&sm.chunk_pos[wc0]) + mis;
             copy_out(region, out - mis, D0, lds_u64(&sm.wave_bytes[wave]), out_cap + mis, lane);
