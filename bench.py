@@ -332,7 +332,12 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # a process group whenever a launcher started this rank (torchrun sets
+    # the rendezvous variables even at one rank), so the barrier /
+    # max-over-ranks path the 8-GPU run takes is one a one-GPU box exercises
+    dist_on = world > 1 or all(k in os.environ for k in
+                               ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"))
+    if dist_on:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
@@ -389,18 +394,18 @@ def main():
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(True)
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:  # measurement only: the shards never exchange data
+    if dist_on:  # measurement only: the shards never exchange data
         from capnp_amd import shard
         elapsed = shard.max_over_ranks(elapsed, device=dev)
 
@@ -484,6 +489,7 @@ def main():
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
+            "process_group": dist.get_backend() if dist_on else None,
             "steps": args.steps,
             "warmup": args.warmup,
             "settle": {"steps": settle_steps, "ms": round(settle_ms, 1),
@@ -529,7 +535,7 @@ def main():
         if not args.no_cpu and world == 1:  # (the CPU baseline is an N=1 figure)
             line["cpu_baseline"] = cpu_baseline(args, cpu_threads(args))
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
     if not ok:
         sys.exit(3)

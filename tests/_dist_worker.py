@@ -45,3 +45,38 @@ def pack_concat_worker(rank, world, port, outdir):
         f.write(f"{c0} {c1} {starts[rank]} {starts[-1]} {elapsed}\n")
     dist.barrier()
     dist.destroy_process_group()
+
+
+def pack_concat_worker_gpu(rank, world, port, outdir):
+    """The same assembly with the device codec: every rank packs its shard
+    on cuda:0 through the C ABI (a one-GPU box runs the ranks side by side
+    on its one device), the ranks exchange shard totals over gloo, and the
+    concatenated stream and offsets are written for the parent to check."""
+    import torch
+    import torch.distributed as dist
+    from capnp_amd import Context, shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    ctx = Context(0)
+    words, offs = batch(seed=23, n=3000)
+    b = shard.shard_by_words(offs, world)
+    c0, c1 = b[rank], b[rank + 1]
+    local_offs = (offs[c0:c1 + 1] - offs[c0]).astype(np.int64)
+    dw = torch.from_numpy(words[int(offs[c0]):int(offs[c1])].view(np.int64).copy()).cuda()
+    do = torch.from_numpy(local_offs).cuda()
+    packed, loff = ctx.pack_batch(dw, do)
+    torch.cuda.synchronize()
+    packed = packed.cpu().numpy()
+    loff = loff.cpu().numpy().view(np.uint64)
+    totals = shard.gather_totals(int(loff[-1]))
+    starts = shard.exclusive_offsets(totals)
+    goff = shard.global_chunk_offsets(loff, starts[rank])
+    np.save(os.path.join(outdir, f"packed{rank}.npy"), packed)
+    np.save(os.path.join(outdir, f"offs{rank}.npy"), goff)
+    with open(os.path.join(outdir, f"meta{rank}.txt"), "w") as f:
+        f.write(f"{c0} {c1} {starts[rank]} {starts[-1]}\n")
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
