@@ -10,16 +10,19 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
 #include <chrono>
 #include <string>
 #include <cmath>
+#include <mutex>
 #include <vector>
 
 #include "../../include/capnp_packed.h"
 #include "../../include/capnp_packed_bench.h"
+#include "common.h"
 #include "frame.h"
 
 extern "C" hipError_t capnp_launch_pack(const uint64_t*, const uint64_t*, uint64_t, uint32_t,
@@ -119,6 +122,10 @@ extern "C" hipError_t capnp_launch_msg_pack(const uint64_t*, const uint64_t*, ui
                                             uint8_t*, hipStream_t);
 extern "C" hipError_t capnp_launch_frame(const uint8_t*, uint64_t, uint32_t, uint32_t, uint64_t,
                                          uint32_t, uint64_t, uint64_t, FrameResult*, hipStream_t);
+extern "C" hipError_t capnp_launch_msg_read_service(const uint64_t*, uint64_t*, uint32_t, uint64_t,
+                                                    FrameResult*, uint32_t*, hipStream_t);
+extern "C" hipError_t capnp_launch_msg_pack_service(const uint64_t*, uint64_t*, uint32_t, uint64_t,
+                                                    uint32_t*, hipStream_t);
 
 namespace {
 
@@ -135,6 +142,20 @@ constexpr size_t kTablePrefixBytes = 4096;  // >= 10 bytes x (1 + 256) table wor
 #define PARALLEL_BODY_WORDS 65536  // (32768: a 256 KiB read 224 us; 65536: 174; 131072: a 512 KiB read 353 vs 237)
 #endif
 constexpr uint64_t kParallelBodyWords = PARALLEL_BODY_WORDS;
+
+// A resident service for one kind of one-launch call (0: msg_read_kernel,
+// 1: msg_pack_kernel): one workgroup on its own stream polls a pinned
+// request line and serves each request without a launch (common.h,
+// svc_next).  Pinned block: [0, 8) the request line (bell, six arguments,
+// check), [8] the exit mark (the last generation that exited).
+struct CallSvc {
+    hipStream_t s = nullptr;
+    uint64_t* h = nullptr;
+    uint64_t* d = nullptr;
+    uint32_t gen = 0;
+    bool live = false;  // a service of `gen` was started and may still run
+    std::chrono::steady_clock::time_point last{};  // its last completed request
+};
 
 struct capnp_ctx {
     int device = 0;
@@ -178,6 +199,9 @@ struct capnp_ctx {
     uint32_t* h_flag = nullptr;  // pinned: the one-launch calls' completion flag
     uint32_t* d_flag = nullptr;  // ... its device address
     uint32_t call_seq = 0;
+    CallSvc svc[2];  // resident services of the per-message calls (read, write)
+    std::chrono::steady_clock::time_point percall_last{};  // the last per-message call
+    bool percall_any = false;
     // Caller streams that ran this context's device work: an event recorded on
     // each after its last call, so a workspace that has to grow waits for that
     // work only (not for every stream of the device), and destroy too.
@@ -285,7 +309,10 @@ struct UseMark {
 
 // Waits for every piece of work this context has queued: its own streams and
 // the caller streams marked above (before a workspace is freed).
+void svc_stop_all(capnp_ctx* ctx);
+
 hipError_t wait_uses(capnp_ctx* ctx) {
+    svc_stop_all(ctx);  // (a resident per-call service: stopped before buffers move)
     hipError_t e = hipSuccess, r;
     if (ctx->stream && (r = hipStreamSynchronize(ctx->stream)) != hipSuccess) e = r;
     for (int k = 0; k < capnp_ctx::kUseSlots; k++)
@@ -362,6 +389,7 @@ capnp_status ensure_pin(capnp_ctx* ctx, size_t bytes) {
     if (bytes <= ctx->pin_cap) return CAPNP_OK;
     HIP_TRY(hipSetDevice(ctx->device));
     if (ctx->h_pin) {
+        svc_stop_all(ctx);
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         HIP_TRY(hipHostFree(ctx->h_pin));
         ctx->h_pin = nullptr;
@@ -398,6 +426,169 @@ capnp_status wait_call(capnp_ctx* ctx, uint32_t seq, hipStream_t s) {
     }
     return CAPNP_OK;
 }
+
+// ---- resident per-call services (CallSvc) ----
+// A per-message call within kSvcWarm of the previous one goes to the resident
+// service of its kind instead of a launch (profiles/r06j_doorbell*.txt: a
+// request's round trip 2.9 vs 7.2 us for an empty call, 4.9 vs 9.2 for a
+// 1 KiB one).  A service that completed a request within kSvcTrust is rung
+// directly; otherwise a new generation starts (an older one, if still
+// polling, exits when it sees the new bell).  The workgroup exits after
+// kSvcIdleTicks without a request: while resident it holds its hardware
+// queue, so it must not outlive a burst of calls by long.  Its streams are
+// non-blocking and of the highest priority (the normal-priority streams'
+// queues are not shared with it: profiles/r06j_doorbell_queues.txt).
+constexpr auto kSvcWarm = std::chrono::microseconds(1000);
+constexpr auto kSvcTrust = std::chrono::microseconds(150);
+constexpr uint64_t kSvcIdleTicks = 100 * 250;  // 250 us of the 100 MHz clock
+constexpr auto kSvcCheck = std::chrono::microseconds(100);
+constexpr auto kSvcGiveUp = std::chrono::milliseconds(200);
+
+std::mutex g_svc_mu;
+std::vector<capnp_ctx*>* g_svc_ctxs = nullptr;  // contexts that started a service
+
+void svc_bell(CallSvc& v, uint64_t b) {
+    // (the arguments, the check and the payload before the bell, non-temporal
+    // stores included)
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    __atomic_store_n(&v.h[0], b, __ATOMIC_RELEASE);
+}
+
+// The request line for bell b (the arguments are in v.h[1, 7)), then the bell.
+void svc_ring(CallSvc& v, uint64_t b) {
+    v.h[7] = svc_mix(b, v.h + 1);
+    svc_bell(v, b);
+}
+
+// Stops service k (it exits at its next poll) and waits for it.
+void svc_stop(capnp_ctx* ctx, int k) {
+    CallSvc& v = ctx->svc[k];
+    if (!v.s || !v.live) return;
+    svc_bell(v, 0);  // (generation 0 is never started)
+    (void)hipStreamSynchronize(v.s);
+    v.live = false;
+}
+
+void svc_stop_all(capnp_ctx* ctx) {
+    svc_stop(ctx, 0);
+    svc_stop(ctx, 1);
+}
+
+// Process exit with a service still resident (a context never destroyed):
+// the stop bell, then a bounded wait for its exit mark (no runtime calls).
+void svc_atexit() {
+    std::lock_guard<std::mutex> g(g_svc_mu);
+    if (!g_svc_ctxs) return;
+    for (capnp_ctx* ctx : *g_svc_ctxs)
+        for (CallSvc& v : ctx->svc) {
+            if (!v.live || !v.h) continue;
+            svc_bell(v, 0);
+            const auto t0 = std::chrono::steady_clock::now();
+            while (__atomic_load_n(&v.h[8], __ATOMIC_ACQUIRE) != v.gen &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20))
+                __builtin_ia32_pause();
+        }
+}
+
+capnp_status svc_init(capnp_ctx* ctx, int k) {
+    CallSvc& v = ctx->svc[k];
+    if (v.s) return CAPNP_OK;
+    int lo = 0, hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_TRY(hipHostMalloc(&v.h, 256, 0));
+    memset(v.h, 0, 256);
+    void* dp = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&dp, v.h, 0));
+    v.d = static_cast<uint64_t*>(dp);
+    HIP_TRY(hipStreamCreateWithPriority(&v.s, hipStreamNonBlocking, hi));
+    std::lock_guard<std::mutex> g(g_svc_mu);
+    if (!g_svc_ctxs) {
+        g_svc_ctxs = new std::vector<capnp_ctx*>();
+        atexit(svc_atexit);
+    }
+    if (std::find(g_svc_ctxs->begin(), g_svc_ctxs->end(), ctx) == g_svc_ctxs->end())
+        g_svc_ctxs->push_back(ctx);
+    return CAPNP_OK;
+}
+
+// A new generation of service k, rung for request `seq` before its launch.
+capnp_status svc_start(capnp_ctx* ctx, int k, uint32_t seq) {
+    CallSvc& v = ctx->svc[k];
+    if (++v.gen == 0) v.gen = 1;
+    svc_ring(v, ((uint64_t)v.gen << 32) | seq);
+    v.live = true;
+    HIP_TRY(k == 0 ? capnp_launch_msg_read_service(v.d, v.d + 8, v.gen, kSvcIdleTicks,
+                                                   ctx->d_hframe, ctx->d_flag, v.s)
+                   : capnp_launch_msg_pack_service(v.d, v.d + 8, v.gen, kSvcIdleTicks,
+                                                   ctx->d_flag, v.s));
+    return CAPNP_OK;
+}
+
+// One request to service k: the arguments (kSvcArgs), the request line, the
+// wait for the completion flag (`seq`).  A service that has exited before
+// seeing the bell (its stream is idle and the flag not set) is started again.
+capnp_status svc_call(capnp_ctx* ctx, int k, const uint64_t* args, uint32_t seq) {
+    capnp_status st = svc_init(ctx, k);
+    if (st != CAPNP_OK) return st;
+    CallSvc& v = ctx->svc[k];
+    memcpy(v.h + 1, args, kSvcArgs * sizeof(uint64_t));
+    const auto t0 = std::chrono::steady_clock::now();
+    if (v.live && t0 - v.last <= kSvcTrust) {
+        svc_ring(v, ((uint64_t)v.gen << 32) | seq);
+    } else if ((st = svc_start(ctx, k, seq)) != CAPNP_OK) {
+        return st;
+    }
+    auto check = t0;
+    for (uint32_t i = 1;; i++) {
+        if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) == seq) {
+            v.last = std::chrono::steady_clock::now();
+            return CAPNP_OK;
+        }
+        __builtin_ia32_pause();
+        if ((i & 255) == 0) {
+            const auto t = std::chrono::steady_clock::now();
+            if (t - check > kSvcCheck) {
+                check = t;
+                if (hipStreamQuery(v.s) == hipSuccess &&
+                    __atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) != seq &&
+                    (st = svc_start(ctx, k, seq)) != CAPNP_OK)
+                    return st;
+            }
+            if (t - t0 > kSvcGiveUp) break;
+        }
+    }
+    const hipError_t q = hipStreamQuery(v.s);
+    char diag[200];
+    snprintf(diag, sizeof diag, " (kind %d, bell %llx, exit mark %llu, flag %u, seq %u, stream %d)",
+             k, (unsigned long long)v.h[0], (unsigned long long)v.h[8],
+             __atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE), seq, (int)q);
+    svc_stop(ctx, k);
+    if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) == seq) return CAPNP_OK;
+    ctx->err = std::string("the per-call service did not complete the request") + diag;
+    return CAPNP_E_HIP;
+}
+
+// The next call's completion value (never 0: a new service has served none).
+uint32_t next_seq(capnp_ctx* ctx) {
+    if (++ctx->call_seq == 0) ++ctx->call_seq;
+    return ctx->call_seq;
+}
+
+// Whether this per-message call goes to a resident service (the previous one
+// was recent); percall_done notes when the call ended.
+bool percall_warm(capnp_ctx* ctx) {
+    // (CAPNP_PERCALL_SERVICE=0: every call launches, for A/B measurements)
+    static const bool enabled = [] {
+        const char* e = getenv("CAPNP_PERCALL_SERVICE");
+        return !(e && e[0] == '0');
+    }();
+    if (!enabled) return false;
+    const auto now = std::chrono::steady_clock::now();
+    const bool warm = ctx->percall_any && now - ctx->percall_last <= kSvcWarm;
+    ctx->percall_any = true;
+    return warm;
+}
+void percall_done(capnp_ctx* ctx) { ctx->percall_last = std::chrono::steady_clock::now(); }
 
 // Enqueues the checks of `arrays` (device offset arrays of n + 1 entries with
 // their limits) on `s`, copies the verdict to the pinned flag and waits for
@@ -710,6 +901,16 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)wait_uses(ctx);  // (an index-free decode may still be running on its caller's stream)
+    {
+        std::lock_guard<std::mutex> g(g_svc_mu);
+        if (g_svc_ctxs)
+            g_svc_ctxs->erase(std::remove(g_svc_ctxs->begin(), g_svc_ctxs->end(), ctx),
+                              g_svc_ctxs->end());
+    }
+    for (CallSvc& v : ctx->svc) {
+        if (v.s) (void)hipStreamDestroy(v.s);
+        if (v.h) (void)hipHostFree(v.h);
+    }
     if (ctx->d_state) (void)hipFree(ctx->d_state);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_body) (void)hipFree(ctx->d_body);
@@ -1703,12 +1904,25 @@ capnp_status capnp_packed_write_message(capnp_ctx* ctx, const uint64_t* const* s
             if (seg_words[i]) memcpy(w + o, segs[i], (size_t)seg_words[i] * 8);
             o += seg_words[i];
         }
-        HIP_TRY(capnp_launch_msg_pack(reinterpret_cast<uint64_t*>(dh),
-                                      reinterpret_cast<uint64_t*>(dh + o_off), (uint32_t)nch,
-                                      (uint32_t)nw, dh + o_out, bound,
-                                      reinterpret_cast<uint64_t*>(dh + o_tot), ctx->d_flag,
-                                      ++ctx->call_seq, ctx->d_stage, s));
-        st = wait_call(ctx, ctx->call_seq, s);
+        const uint32_t seq = next_seq(ctx);
+        if (percall_warm(ctx)) {
+            SvcPackReq q;
+            q.words = (uint64_t)dh;
+            q.off = (uint64_t)(dh + o_off);
+            q.out = (uint64_t)(dh + o_out);  // (*total at dh + o_tot = out - 16)
+            q.counts = nch | ((uint64_t)nw << 32);
+            q.out_cap = bound;
+            q.scratch = (uint64_t)ctx->d_stage;
+            st = svc_call(ctx, 1, reinterpret_cast<const uint64_t*>(&q), seq);
+        } else {
+            HIP_TRY(capnp_launch_msg_pack(reinterpret_cast<uint64_t*>(dh),
+                                          reinterpret_cast<uint64_t*>(dh + o_off), (uint32_t)nch,
+                                          (uint32_t)nw, dh + o_out, bound,
+                                          reinterpret_cast<uint64_t*>(dh + o_tot), ctx->d_flag,
+                                          seq, ctx->d_stage, s));
+            st = wait_call(ctx, seq, s);
+        }
+        percall_done(ctx);
         if (st != CAPNP_OK) return st;
         const uint64_t total = *reinterpret_cast<volatile uint64_t*>(h + o_tot);
         const size_t ncopy = std::min<uint64_t>(total, cap);
@@ -1816,13 +2030,27 @@ static capnp_status read_message_fast(capnp_ctx* ctx, const uint8_t* in, size_t 
     if (stage) memcpy(h, in, stage);
     // one launch: the kernel reads the staged bytes and writes the frame
     // record, the body's status and its words in pinned memory
-    HIP_TRY(capnp_launch_msg_read(dh, stage, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
-                                  o.traversal_limit_in_words,
-                                  (uint32_t)(o.has_traversal_limit != 0), buffer_len, cap,
-                                  ctx->d_hframe, reinterpret_cast<uint64_t*>(dh + h_out),
-                                  reinterpret_cast<uint64_t*>(dh + h_out + o_st), ctx->d_flag,
-                                  ++ctx->call_seq, s));
-    st = wait_call(ctx, ctx->call_seq, s);
+    const uint32_t seq = next_seq(ctx);
+    if (percall_warm(ctx)) {
+        SvcReadReq q;
+        q.in = (uint64_t)dh;
+        q.words = (uint64_t)(dh + h_out);  // (res at + o_st = round16(8 cap))
+        q.flags = stage | ((uint64_t)(no_alloc != 0) << 32) | ((uint64_t)(try_mode != 0) << 33) |
+                  ((uint64_t)(o.has_traversal_limit != 0) << 34);
+        q.limit = o.traversal_limit_in_words;
+        q.buffer_len = buffer_len;
+        q.cap = cap;
+        st = svc_call(ctx, 0, reinterpret_cast<const uint64_t*>(&q), seq);
+    } else {
+        HIP_TRY(capnp_launch_msg_read(dh, stage, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
+                                      o.traversal_limit_in_words,
+                                      (uint32_t)(o.has_traversal_limit != 0), buffer_len, cap,
+                                      ctx->d_hframe, reinterpret_cast<uint64_t*>(dh + h_out),
+                                      reinterpret_cast<uint64_t*>(dh + h_out + o_st), ctx->d_flag,
+                                      seq, s));
+        st = wait_call(ctx, seq, s);
+    }
+    percall_done(ctx);
     if (st != CAPNP_OK) return st;
     *fr = *ctx->h_frame;
     if (fr->status != CAPNP_OK || fr->total_words > cap) return CAPNP_OK;  // (the caller decides)

@@ -166,3 +166,165 @@ __device__ __forceinline__ uint64_t poll_agent(uint64_t* p) {
 __device__ __forceinline__ void publish_agent(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// ---- resident per-call service (capi.hip: the one-launch per-message calls
+// without their launch).  One workgroup stays resident and polls one pinned
+// 64-byte line: [0] the bell {gen << 32 | seq}, [1, 7) the request's
+// arguments, [7] a check word (svc_mix of the other seven).  The host writes
+// the arguments and the check, then the bell; a poll reads the whole line in
+// one load, so a request costs no second round trip for its arguments, and a
+// line read while the host was writing it fails the check and is read again.
+// The workgroup serves every new seq of its own gen and exits on another gen
+// (a newer service, or stop) or after `idle_ticks` of the 100 MHz real-time
+// clock without a request, so it never outlives its last caller by more than
+// that.
+constexpr uint32_t kSvcArgs = 6;
+// (one poll at a time: profiles/r06l_svc_ab.txt -- 2 or 4 polls in flight
+// to the same line cost 1-3 us a call more than one)
+#ifndef SVC_POLLS
+#define SVC_POLLS 1
+#endif
+#ifndef SVC_POLL_GAP
+#define SVC_POLL_GAP 1
+#endif
+constexpr uint32_t kSvcPolls = SVC_POLLS;  // poll loads in flight (spread over a PCIe round trip)
+constexpr int kSvcPollGap = SVC_POLL_GAP;  // s_sleep between them (x 64 cycles)
+#ifndef SVC_PROF
+#define SVC_PROF 0  // diagnostic builds: per-request phase times (capnp_svc_prof)
+#endif
+#if SVC_PROF
+// [0] requests, [2] bell seen -> body done (100 MHz ticks); msg_read_body:
+// [3] table, [4] decode, [5] results landed, [6] - [7] staging (sums of
+// stamps); [8] the body in shader clock cycles (s_memtime: [8] / [2] = the
+// clock in units of 100 MHz); unpack_small: [9] selector table and init,
+// [10] wave 0's walks, [11] expansion, [12] calls; within [10]: [16] spec
+// walks, [17] rounds, [18] the last segment's walk, [19] descriptors, [20]
+// rounds taken
+__device__ unsigned long long g_svc_prof[24];
+#endif
+struct SvcCmd {
+    uint64_t bell;
+    uint64_t a[kSvcArgs];
+#if SVC_PROF
+    uint64_t t_args, c_args;
+#endif
+};
+
+// The request line's arguments of each service, by name (host and device
+// share these layouts): msg_read_service's and msg_pack_service's.
+struct SvcReadReq {
+    uint64_t in;      // the staged input (pinned)
+    uint64_t words;   // the body's words (pinned); {status, 0, consumed} at round16(8 cap) bytes on
+    uint64_t flags;   // stage bytes | no_alloc << 32 | try_mode << 33 | has_limit << 34
+    uint64_t limit, buffer_len, cap;
+};
+struct SvcPackReq {
+    uint64_t words, off;  // the message's chunks and their offsets (pinned)
+    uint64_t out;         // the packed output (pinned); *total sits 16 bytes before it
+    uint64_t counts;      // nchunks | nwords << 32
+    uint64_t out_cap;
+    uint64_t scratch;     // device scratch for the bytes before their copy out
+};
+static_assert(sizeof(SvcReadReq) == kSvcArgs * 8 && sizeof(SvcPackReq) == kSvcArgs * 8,
+              "a request fills the line's arguments");
+
+// The line's check word (host and device).
+__host__ __device__ __forceinline__ uint64_t svc_mix(uint64_t b, const uint64_t* r) {
+    uint64_t h = 0x9E3779B97F4A7C15ull ^ b;
+    for (uint32_t i = 0; i < kSvcArgs; i++) {
+        h ^= r[i];
+        h *= 0xFF51AFD7ED558CCDull;
+        h ^= h >> 33;
+    }
+    return h;
+}
+
+// Waits for the next request (wave 0 polls; the workgroup meets at a
+// barrier).  false: exit.  On true, cmd.a holds the request's arguments and
+// `last` its seq.
+__device__ __forceinline__ bool svc_next(const uint64_t* line, SvcCmd& cmd, uint32_t gen,
+                                         uint32_t& last, uint64_t idle_ticks, uint32_t wave,
+                                         uint32_t lane) {
+    if (wave == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint64_t* const p = const_cast<uint64_t*>(line) + (lane & 7u);
+        uint64_t v[kSvcPolls];
+#pragma unroll
+        for (uint32_t k = 0; k < kSvcPolls; k++) {
+            v[k] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (k + 1 < kSvcPolls) __builtin_amdgcn_s_sleep(kSvcPollGap);
+        }
+        uint64_t b = 0, hit = 0;
+        for (bool more = true; more;) {
+#pragma unroll
+            for (uint32_t k = 0; k < kSvcPolls && more; k++) {
+                const uint64_t bk = readlane64(v[k], 0);
+                if ((uint32_t)(bk >> 32) != gen) {
+                    more = false;  // (b = 0: exit)
+                } else if ((uint32_t)bk != last) {
+                    uint64_t r[kSvcArgs];
+#pragma unroll
+                    for (uint32_t i = 0; i < kSvcArgs; i++) r[i] = readlane64(v[k], i + 1);
+                    if (svc_mix(bk, r) == readlane64(v[k], 7)) {
+                        b = bk;
+                        hit = v[k];
+                        more = false;
+                    }
+                }
+                if (more) {
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+                        more = false;
+                    } else {
+                        v[k] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __builtin_amdgcn_s_sleep(kSvcPollGap);
+                    }
+                }
+            }
+        }
+        if (b) {
+#if SVC_PROF
+            const uint64_t ta = __builtin_amdgcn_s_memrealtime();
+            if (lane == 0) {
+                atomicAdd(&g_svc_prof[0], 1ull);
+                atomicAdd(&g_svc_prof[7], (unsigned long long)ta);
+            }
+            cmd.t_args = ta;  // (the body's start, for svc_prof_done)
+            cmd.c_args = __builtin_amdgcn_s_memtime();
+#endif
+            // (system scope: the caches drop what earlier requests left, so the
+            // payload the host wrote before the bell is seen)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            if (lane >= 1 && lane <= kSvcArgs) cmd.a[lane - 1] = hit;
+        }
+        if (lane == 0) cmd.bell = b;
+    }
+    __syncthreads();
+    const uint64_t b = uniform64(cmd.bell);
+    if (!b) return false;
+    last = (uint32_t)b;
+    return true;
+}
+
+// SVC_PROF: the body's time.
+__device__ __forceinline__ void svc_prof_done(SvcCmd& cmd, uint32_t tid) {
+#if SVC_PROF
+    __syncthreads();
+    if (tid == 0) {
+        const uint64_t td = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(&g_svc_prof[2], (unsigned long long)(td - cmd.t_args));
+        atomicAdd(&g_svc_prof[8], (unsigned long long)(__builtin_amdgcn_s_memtime() - cmd.c_args));
+    }
+#else
+    (void)cmd;
+    (void)tid;
+#endif
+}
+
+// The service's exit mark for the host (process-exit path): {gen}, stored
+// after the last request's results.
+__device__ __forceinline__ void svc_exit(uint64_t* mark, uint32_t gen, uint32_t tid) {
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(mark, (uint64_t)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}

@@ -3074,12 +3074,11 @@ struct MsgPackSmem {
     alignas(16) uint64_t words[kMsgWords];
 };
 
-__global__ void __launch_bounds__(kMsgThreads)
-msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__ off,
-                uint32_t nchunks, uint32_t nwords, uint8_t* __restrict__ out, uint64_t out_cap,
-                uint64_t* __restrict__ total, uint32_t* __restrict__ flag, uint32_t seq,
-                uint8_t* __restrict__ scratch) {
-    __shared__ MsgPackSmem S;
+__device__ __forceinline__ void msg_pack_body(MsgPackSmem& S, const uint64_t* words,
+                                              const uint64_t* off, uint32_t nchunks,
+                                              uint32_t nwords, uint8_t* out, uint64_t out_cap,
+                                              uint64_t* total, uint32_t* flag, uint32_t seq,
+                                              uint8_t* scratch) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
@@ -3236,6 +3235,42 @@ msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__
             __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
+}
+
+__global__ void __launch_bounds__(kMsgThreads)
+msg_pack_kernel(const uint64_t* __restrict__ words, const uint64_t* __restrict__ off,
+                uint32_t nchunks, uint32_t nwords, uint8_t* __restrict__ out, uint64_t out_cap,
+                uint64_t* __restrict__ total, uint32_t* __restrict__ flag, uint32_t seq,
+                uint8_t* __restrict__ scratch) {
+    __shared__ MsgPackSmem S;
+    msg_pack_body(S, words, off, nchunks, nwords, out, out_cap, total, flag, seq, scratch);
+}
+
+// The same call served by a resident workgroup (common.h, svc_next; the
+// request's arguments: SvcPackReq).  The completion flag is the context's
+// own.
+__global__ void __launch_bounds__(kMsgThreads)
+msg_pack_service(const uint64_t* line, uint64_t* mark, uint32_t gen, uint64_t idle_ticks,
+                 uint32_t* flag) {
+    __shared__ MsgPackSmem S;
+    __shared__ SvcCmd cmd;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    uint32_t last = 0;
+    while (svc_next(line, cmd, gen, last, idle_ticks, wave, lane)) {
+        const SvcPackReq& q = *reinterpret_cast<const SvcPackReq*>(cmd.a);
+        const uint64_t nn = uniform64(q.counts);
+        uint8_t* const out = reinterpret_cast<uint8_t*>(uniform64(q.out));
+        msg_pack_body(S, reinterpret_cast<const uint64_t*>(uniform64(q.words)),
+                      reinterpret_cast<const uint64_t*>(uniform64(q.off)), (uint32_t)nn,
+                      (uint32_t)(nn >> 32), out, uniform64(q.out_cap),
+                      reinterpret_cast<uint64_t*>(out - 16), flag, last,
+                      reinterpret_cast<uint8_t*>(uniform64(q.scratch)));
+        svc_prof_done(cmd, tid);
+        __syncthreads();
+    }
+    svc_exit(mark, gen, tid);
 }
 
 }  // namespace
@@ -3428,6 +3463,23 @@ extern "C" hipError_t capnp_pack_prof(unsigned long long* host8, int reset) {
 // output and *total may be pinned host memory.  Bytes at or past out_cap are
 // not written; *total is the size needed.
 extern "C" uint32_t capnp_msg_pack_words(void) { return kMsgWords; }
+#if SVC_PROF
+extern "C" int capnp_svc_prof_w(unsigned long long* out8, int reset) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_svc_prof), 192) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[24] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_svc_prof), z, 192) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+extern "C" hipError_t capnp_launch_msg_pack_service(const uint64_t* line, uint64_t* mark,
+                                                    uint32_t gen, uint64_t idle_ticks,
+                                                    uint32_t* flag, hipStream_t stream) {
+    hipLaunchKernelGGL(msg_pack_service, dim3(1), dim3(kMsgThreads), 0, stream, line, mark, gen,
+                       idle_ticks, flag);
+    return hipGetLastError();
+}
 extern "C" hipError_t capnp_launch_msg_pack(const uint64_t* words, const uint64_t* off,
                                             uint32_t nchunks, uint32_t nwords, uint8_t* out,
                                             uint64_t out_cap, uint64_t* total, uint32_t* flag,

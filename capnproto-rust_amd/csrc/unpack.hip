@@ -2558,6 +2558,9 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
                              uint64_t* __restrict__ out, uint32_t tid, uint32_t lane,
                              uint32_t wave, uint32_t& used) {
     const uint8_t* B = S.bytes + mis;
+#if SVC_PROF
+    const uint64_t tq0 = __builtin_amdgcn_s_memrealtime();
+#endif
     S.sel[tid] = kExpandTable.s[tid];
     {
         uint4* d4 = reinterpret_cast<uint4*>(S.dpos);
@@ -2565,6 +2568,9 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
         for (uint32_t k = tid; k < (n + 7) / 8; k += kThreads) d4[k] = none;
     }
     __syncthreads();
+#if SVC_PROF
+    const uint64_t tq1 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (wave == 0) {
         const uint32_t j = lane;
         const uint32_t sb = (uint32_t)(((uint64_t)L * j) >> 6);
@@ -2574,6 +2580,9 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
         while (p < sb) seg_hop(B, p, w);
         const uint32_t f = p, wf = w;
         while (p < se) seg_hop(B, p, w);
+#if SVC_PROF
+        const uint64_t tw0 = __builtin_amdgcn_s_memrealtime();
+#endif
         const bool serr = p > L;
         const uint32_t xs = serr ? 0u : p, ws = w - wf;
         // (a spec walk that found no record start in its segment owns no exit)
@@ -2588,7 +2597,13 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
             if (j >= d) x = max(x, t);
         }
         bool ok = true;
+#if SVC_PROF
+        uint32_t n_rounds = 0;
+#endif
         for (uint32_t round = 0;; round++) {
+#if SVC_PROF
+            n_rounds++;
+#endif
             const uint32_t xu = (uint32_t)__shfl_up((int)x, 1, 64);
             const uint32_t e = j == 0 ? 0u : xu;
             const bool need = e != e_used;
@@ -2639,6 +2654,9 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
             }
         }
         const uint32_t e = e_used;
+#if SVC_PROF
+        const uint64_t tw1 = __builtin_amdgcn_s_memrealtime();
+#endif
         // words: the segment holding word n walks to it with every check
         uint32_t incl = wd;
         for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
@@ -2669,6 +2687,9 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
             }
         }
         ok = ok && ballot64(j == ts && !fine) == 0;
+#if SVC_PROF
+        const uint64_t tw2 = __builtin_amdgcn_s_memrealtime();
+#endif
         used = (uint32_t)__builtin_amdgcn_readlane((int)q, (int)(ts < CAPNP_WAVE ? ts : 0u));
         // descriptors of the records from each entry (to word n in the last)
         if (ok && j <= ts) {
@@ -2689,10 +2710,33 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
             }
         }
         if (lane == 0) S.misc[0] = ok ? 1u : 0u;
+#if SVC_PROF
+        wave_lds_sync();
+        const uint64_t tw3 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) {
+            atomicAdd(&g_svc_prof[16], (unsigned long long)(tw0 - tq1));
+            atomicAdd(&g_svc_prof[17], (unsigned long long)(tw1 - tw0));
+            atomicAdd(&g_svc_prof[18], (unsigned long long)(tw2 - tw1));
+            atomicAdd(&g_svc_prof[19], (unsigned long long)(tw3 - tw2));
+            atomicAdd(&g_svc_prof[20], (unsigned long long)n_rounds);
+        }
+#endif
     }
     __syncthreads();
+#if SVC_PROF
+    const uint64_t tq2 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (S.misc[0] == 0) return false;
     for (uint32_t i = tid; i < n; i += kThreads) out[i] = expand_desc(S.bytes, S.sel, S.dpos[i]);
+#if SVC_PROF
+    __syncthreads();
+    if (tid == 0) {
+        atomicAdd(&g_svc_prof[9], (unsigned long long)(tq1 - tq0));
+        atomicAdd(&g_svc_prof[10], (unsigned long long)(tq2 - tq1));
+        atomicAdd(&g_svc_prof[11], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - tq2));
+        atomicAdd(&g_svc_prof[12], 1ull);
+    }
+#endif
     return true;
 }
 
@@ -2718,13 +2762,12 @@ struct MsgReadSmem {
     uint64_t used;
 };
 
-__global__ void __launch_bounds__(kThreads)  // (one workgroup: registers are free)
-msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_alloc,
-                uint32_t try_mode, uint64_t limit, uint32_t has_limit, uint64_t buffer_len,
-                uint64_t body_cap, FrameResult* __restrict__ fr_out, uint64_t* __restrict__ words,
-                uint64_t* __restrict__ res, uint32_t* __restrict__ flag, uint32_t seq) {
-    __shared__ USmem sm;
-    __shared__ MsgReadSmem M;
+__device__ __forceinline__ void msg_read_body(USmem& sm, MsgReadSmem& M, const uint8_t* in,
+                                              uint64_t in_len, uint32_t no_alloc, uint32_t try_mode,
+                                              uint64_t limit, uint32_t has_limit,
+                                              uint64_t buffer_len, uint64_t body_cap,
+                                              FrameResult* fr_out, uint64_t* words, uint64_t* res,
+                                              uint32_t* flag, uint32_t seq) {
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63u;
     const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
@@ -2757,6 +2800,9 @@ msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_all
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's bytes are in
     }
     __syncthreads();
+#if SVC_PROF
+    const uint64_t tp0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (tid == 0) {
         // (the table's read units end within kMsgPre bytes whenever the input
         // is longer: the staged prefix gives the same results as the input)
@@ -2771,6 +2817,9 @@ msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_all
         M.used = 0;
     }
     __syncthreads();
+#if SVC_PROF
+    const uint64_t tp1 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (M.fr.status == 0 && M.offs[3] > 0) {  // (uniform: LDS after the barrier)
         // a short body inside the staged prefix: wave 0 alone (unpack_small);
         // the rest, and any body it does not take, unpack_long
@@ -2793,6 +2842,9 @@ msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_all
                         pre);
     }
     __syncthreads();
+#if SVC_PROF
+    const uint64_t tp2 = __builtin_amdgcn_s_memrealtime();
+#endif
     // results out: the frame record (whole 16-byte vectors) and {status, 0, consumed}
     {
         constexpr uint32_t kV = (uint32_t)(sizeof(FrameResult) / 16);
@@ -2808,11 +2860,58 @@ msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_all
     if (flag) {  // (the host waits on this flag: everything above is visible first)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+#if SVC_PROF
+        const uint64_t tp3 = __builtin_amdgcn_s_memrealtime();
+        if (tid == 0) {
+            atomicAdd(&g_svc_prof[3], (unsigned long long)(tp1 - tp0));
+            atomicAdd(&g_svc_prof[4], (unsigned long long)(tp2 - tp1));
+            atomicAdd(&g_svc_prof[5], (unsigned long long)(tp3 - tp2));
+            atomicAdd(&g_svc_prof[6], (unsigned long long)tp0);
+        }
+#endif
         if (tid == 0) {
             __threadfence_system();
             __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
+}
+
+__global__ void __launch_bounds__(kThreads)  // (one workgroup: registers are free)
+msg_read_kernel(const uint8_t* __restrict__ in, uint64_t in_len, uint32_t no_alloc,
+                uint32_t try_mode, uint64_t limit, uint32_t has_limit, uint64_t buffer_len,
+                uint64_t body_cap, FrameResult* __restrict__ fr_out, uint64_t* __restrict__ words,
+                uint64_t* __restrict__ res, uint32_t* __restrict__ flag, uint32_t seq) {
+    __shared__ USmem sm;
+    __shared__ MsgReadSmem M;
+    msg_read_body(sm, M, in, in_len, no_alloc, try_mode, limit, has_limit, buffer_len, body_cap,
+                  fr_out, words, res, flag, seq);
+}
+
+// The same call served by a resident workgroup (common.h, svc_next; the
+// request's arguments: SvcReadReq).  fr_out and the completion flag are the
+// context's own.
+__global__ void __launch_bounds__(kThreads)
+msg_read_service(const uint64_t* line, uint64_t* mark, uint32_t gen, uint64_t idle_ticks,
+                 FrameResult* fr_out, uint32_t* flag) {
+    __shared__ USmem sm;
+    __shared__ MsgReadSmem M;
+    __shared__ SvcCmd cmd;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63u;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+    uint32_t last = 0;
+    while (svc_next(line, cmd, gen, last, idle_ticks, wave, lane)) {
+        const SvcReadReq& q = *reinterpret_cast<const SvcReadReq*>(cmd.a);
+        const uint64_t f = uniform64(q.flags), cap = uniform64(q.cap);
+        uint64_t* const words = reinterpret_cast<uint64_t*>(uniform64(q.words));
+        msg_read_body(sm, M, reinterpret_cast<const uint8_t*>(uniform64(q.in)), (uint32_t)f,
+                      (uint32_t)(f >> 32) & 1u, (uint32_t)(f >> 33) & 1u, uniform64(q.limit),
+                      (uint32_t)(f >> 34) & 1u, uniform64(q.buffer_len), cap, fr_out, words,
+                      words + ((8 * cap + 15) & ~15ull) / 8, flag, last);
+        svc_prof_done(cmd, tid);
+        __syncthreads();
+    }
+    svc_exit(mark, gen, tid);
 }
 
 }  // namespace
@@ -2924,6 +3023,26 @@ extern "C" hipError_t capnp_unpack_prof(unsigned long long* host16, int reset) {
 // One read_message call in one launch (msg_read_kernel): `in` (in_len bytes,
 // 16-byte aligned, readable to the next multiple of 16) and the three outputs
 // may be pinned host memory.  res = {status of the body, 0, consumed bytes}.
+#if SVC_PROF
+extern "C" int capnp_svc_prof(unsigned long long* out8, int reset) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_svc_prof), 192) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[24] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_svc_prof), z, 192) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
+extern "C" hipError_t capnp_launch_msg_read_service(const uint64_t* line, uint64_t* mark,
+                                                    uint32_t gen, uint64_t idle_ticks,
+                                                    FrameResult* fr_out, uint32_t* flag,
+                                                    hipStream_t stream) {
+    hipLaunchKernelGGL(msg_read_service, dim3(1), dim3(kThreads), 0, stream, line, mark, gen,
+                       idle_ticks, fr_out, flag);
+    return hipGetLastError();
+}
+
 extern "C" hipError_t capnp_launch_msg_read(const uint8_t* in, uint64_t in_len, uint32_t no_alloc,
                                             uint32_t try_mode, uint64_t limit, uint32_t has_limit,
                                             uint64_t buffer_len, uint64_t body_cap,

@@ -31,11 +31,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reqs", type=int, default=2000)
     ap.add_argument("--max-mib", type=int, default=64)
+    ap.add_argument("--lib", default=None, help="a library variant (A/B, profiling builds)")
     args = ap.parse_args()
     import torch  # noqa: F401  (device init through the library)
     import oracle_lib as O
     from capnp_amd import Context, _lib
+    if args.lib:
+        _lib.LIB_PATH = os.path.abspath(args.lib)
     L = _lib.lib()
+    prof = []
+    for name in ("capnp_svc_prof", "capnp_svc_prof_w"):
+        if hasattr(L, name):
+            getattr(L, name).restype = C.c_int
+            prof.append(getattr(L, name))
+    p16 = (C.c_ulonglong * 16)()
     ctx = Context(0)
     h = ctx.handle
     opts = _lib.ReaderOptionsC(0, 0, 64)  # no traversal limit: the sweep goes to 64 MiB
@@ -95,6 +104,8 @@ def main():
     lens = [(C.c_uint32 * 1)(len(x)) for x in segs_l]
     ub = sum(8 * len(x) for x in segs_l)
     t_gpu = None
+    for f in prof:
+        f(p16, 1)
     for rep in range(3):
         tw = tr = 0.0
         t0 = time.perf_counter()
@@ -124,6 +135,18 @@ def main():
         "cpu_1thread_us_per_request": round(t_cpu / m * 1e6, 3),
         "cpu_1thread_requests_per_s": round(m / t_cpu, 1),
     }
+    for f, kind in zip(prof, ("read", "write")):
+        f(p16, 1)
+        if p16[0]:
+            res["carsales"][kind + "_svc"] = {
+                "requests": p16[0], "args_us": round(p16[1] / p16[0] / 100, 2),
+                "body_us": round(p16[2] / p16[0] / 100, 2)}
+            if kind == "read" and p16[6]:
+                res["carsales"]["read_phases_us"] = {
+                    "stage": round((p16[6] - p16[7]) / p16[0] / 100, 2),
+                    "table": round(p16[3] / p16[0] / 100, 2),
+                    "decode": round(p16[4] / p16[0] / 100, 2),
+                    "results_landed": round(p16[5] / p16[0] / 100, 2)}
     print(json.dumps(res["carsales"]), file=sys.stderr, flush=True)
     # size sweep
     sweep = []

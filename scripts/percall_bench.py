@@ -5,7 +5,11 @@ capnp_packed_read_message, one message per call as the reference's
 median and 10th percentile over many calls, write and read separately, for
 one-segment messages of config-2 words of several sizes.
 
-    python3 scripts/percall_bench.py [--reps N]
+    python3 scripts/percall_bench.py [--reps N] [--lib PATH]
+
+--lib loads a library variant; one built with -DSVC_PROF=1 also reports
+the resident services' per-request phases (bell seen -> arguments in, and
+the body), averaged per size.  CAPNP_PERCALL_SERVICE=0 launches every call.
 """
 import argparse
 import ctypes as C
@@ -26,11 +30,23 @@ def main():
     ap.add_argument("--reps", type=int, default=400)
     ap.add_argument("--sizes", default="128,512,1500,2048,8192,32768",
                     help="message words, comma-separated")
+    ap.add_argument("--lib", default=None)
     a = ap.parse_args()
     import torch  # noqa: F401
     import oracle_lib as O
     from capnp_amd import Context, _lib
+    if a.lib:
+        _lib.LIB_PATH = os.path.abspath(a.lib)
     L = _lib.lib()
+    prof = []
+    for name in ("capnp_svc_prof", "capnp_svc_prof_w"):
+        try:
+            f = getattr(L, name)
+            f.restype = C.c_int
+            prof.append(f)
+        except AttributeError:
+            pass
+    p8 = (C.c_ulonglong * 24)()
     ctx = Context(0)
     h = ctx.handle
     opts = _lib.ReaderOptionsC(0, 0, 64)
@@ -46,6 +62,8 @@ def main():
         segs = np.empty(512, np.uint32)
         n, used, nseg = C.c_size_t(0), C.c_size_t(0), C.c_uint32(0)
         tw, tr = [], []
+        for f in prof:
+            f(p8, 1)
         for r in range(a.reps + 10):
             t0 = time.perf_counter()
             st = L.capnp_packed_write_message(h, ptrs, lens, 1, out.ctypes.data, cap, C.byref(n))
@@ -67,6 +85,28 @@ def main():
              "write_us_p10": round(float(np.percentile(tw, 10)), 1),
              "read_us_median": round(float(np.median(tr)), 1),
              "read_us_p10": round(float(np.percentile(tr, 10)), 1)}
+        for f, kind in zip(prof, ("read", "write")):
+            f(p8, 1)
+            if p8[0]:
+                r[kind + "_svc"] = {"requests": p8[0], "args_us": round(p8[1] / p8[0] / 100, 2),
+                                    "body_us": round(p8[2] / p8[0] / 100, 2),
+                                    "body_clock_mhz": round(100 * p8[8] / max(p8[2], 1))}
+                if kind == "read" and p8[6]:
+                    r["read_phases_us"] = {
+                        "stage": round((p8[6] - p8[7]) / p8[0] / 100, 2),
+                        "table": round(p8[3] / p8[0] / 100, 2),
+                        "decode": round(p8[4] / p8[0] / 100, 2),
+                        "results_landed": round(p8[5] / p8[0] / 100, 2)}
+                    if p8[12]:
+                        r["read_small_us"] = {"n": p8[12],
+                                              "sel_init": round(p8[9] / p8[12] / 100, 2),
+                                              "walk": round(p8[10] / p8[12] / 100, 2),
+                                              "expand": round(p8[11] / p8[12] / 100, 2),
+                                              "spec": round(p8[16] / p8[12] / 100, 2),
+                                              "rounds": round(p8[17] / p8[12] / 100, 2),
+                                              "last_walk": round(p8[18] / p8[12] / 100, 2),
+                                              "descriptors": round(p8[19] / p8[12] / 100, 2),
+                                              "rounds_taken": round(p8[20] / p8[12], 2)}
         rows.append(r)
         print(json.dumps(r), flush=True)
 
