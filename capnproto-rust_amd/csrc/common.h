@@ -72,6 +72,17 @@ __device__ __forceinline__ uint32_t wave_max_scan(uint32_t x) {
     return x;
 }
 
+// Inclusive sum over lanes 0..i of the wave (DPP, as wave_max_scan).
+__device__ __forceinline__ uint32_t wave_sum_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+    return x;
+}
+
 // The value of lane i - 1 (DPP wave_shr:1); 0 in lane 0.
 __device__ __forceinline__ uint32_t wave_shr1(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, false);

@@ -1584,17 +1584,6 @@ __device__ __forceinline__ void lu_walk(const uint8_t* B, uint32_t& q, uint32_t 
     while (q < se) seg_hop(B, q, w);
 }
 
-// Inclusive sum over lanes 0..i of the wave (the DPP pattern of wave_max_scan).
-__device__ __forceinline__ uint32_t wave_sum_scan(uint32_t x) {
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
-    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
-    return x;
-}
-
 // Exclusive max (MAX) or sum over the workgroup's threads in order; *total
 // = the value over all of them.  One barrier inside; two uses of wsum need a
 // barrier between them (the caller's).
@@ -2592,10 +2581,9 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
         uint32_t own = xsp, x = xsp, wd = ws;
         bool err = j == 0 && serr;
         uint32_t e_used = j == 0 ? 0u : ~0u;
-        for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)x, d, 64);
-            if (j >= d) x = max(x, t);
-        }
+        // (the wave scans by DPP: VALU ops, where __shfl_up's ds_bpermute is an
+        // LDS round trip each -- the rounds are chains of them)
+        x = wave_max_scan(x);
         bool ok = true;
 #if SVC_PROF
         uint32_t n_rounds = 0;
@@ -2604,8 +2592,7 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
 #if SVC_PROF
             n_rounds++;
 #endif
-            const uint32_t xu = (uint32_t)__shfl_up((int)x, 1, 64);
-            const uint32_t e = j == 0 ? 0u : xu;
+            const uint32_t e = wave_shr1(x);  // (0 in lane 0)
             const bool need = e != e_used;
             if (ballot64(need) == 0) break;
             if (round > CAPNP_WAVE + 1) {  // (not reached: lane i is settled after round i + 1)
@@ -2647,22 +2634,14 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
                     }
                 }
             }
-            x = own;
-            for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
-                const uint32_t t = (uint32_t)__shfl_up((int)x, d, 64);
-                if (j >= d) x = max(x, t);
-            }
+            x = wave_max_scan(own);
         }
         const uint32_t e = e_used;
 #if SVC_PROF
         const uint64_t tw1 = __builtin_amdgcn_s_memrealtime();
 #endif
         // words: the segment holding word n walks to it with every check
-        uint32_t incl = wd;
-        for (uint32_t d = 1; d < CAPNP_WAVE; d <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)incl, d, 64);
-            if (j >= d) incl += t;
-        }
+        const uint32_t incl = wave_sum_scan(wd);
         const uint32_t base = incl - wd;
         const uint64_t hold = ballot64(wd > 0 && base < n && n <= incl);
         const uint32_t ts = hold ? (uint32_t)__builtin_ctzll(hold) : CAPNP_WAVE;
