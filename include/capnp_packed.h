@@ -410,6 +410,15 @@ capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf, 
                                           void* stream);
 
 /* ---- host message API (mirrors serialize_packed) ----------------------- */
+/* Latency of the per-message calls below: a message that fits the one-launch
+   kernels (writes of <= 8448 words, reads of bodies < 64 Ki words) is served
+   by one workgroup reading and writing pinned host memory.  A call within
+   1 ms of the context's previous per-message call goes to a resident
+   service workgroup of its kind instead of a launch: it polls a pinned
+   request line, serves each request, and exits 250 us after its last one
+   (so a device-wide synchronisation right after a burst of calls waits up to
+   that long, and a context destroyed mid-burst stops it first).  The
+   environment variable CAPNP_PERCALL_SERVICE=0 makes every call launch. */
 /* serialize_packed::write_message (serialize_packed.rs:446-453 ->
    serialize.rs:574-582): packs the segment table word 0, the rest of the
    table, then each segment as separate write_all chunks
