@@ -2540,7 +2540,10 @@ unpack_wt_finish(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
 // nothing written to `out` when the unit does not check out within L bytes
 // (malformed, truncated, or longer than L): the caller then takes
 // unpack_long, which gives the exact status.
-constexpr uint32_t kSmallBytes = 3072;  // (r05z: 1.5-6.5 KB bodies were as fast or faster on unpack_long)
+#ifndef UNPACK_SMALL_BYTES
+#define UNPACK_SMALL_BYTES 5120  // (r06n, DPP scans: a 4.4 KB body 24.0 vs 26.0 us; 6.5 KB slower)
+#endif
+constexpr uint32_t kSmallBytes = UNPACK_SMALL_BYTES;
 constexpr uint32_t kSmallLead = 48;  // (spec_seg_tile's kSegOverlap)
 
 __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
