@@ -33,7 +33,8 @@ def main():
     st = torch.empty(n, dtype=torch.int32, device=dev)
     s = torch.cuda.current_stream()
     print(f"{wl}: {n} chunks, {words.numel()} words, {int(poffs[-1])} packed bytes", flush=True)
-    for tc in (0, 1, 2, 4, 8, 16):
+    tcs = [int(x) for x in os.environ.get("TCS", "0,1,2,4,8,16").split(",")]
+    for tc in tcs:
         for _ in range(3):
             ctx.unpack_batch_into(packed, poffs, offs, back, st, chunks_per_tile=tc)
         torch.cuda.synchronize()
