@@ -29,6 +29,11 @@ def workload(ctx, name):
         kinds = rng.choice([0, 1, 2], len(sizes), p=[0.8, 0.1, 0.1]).astype(np.uint8)
         keep = np.cumsum(sizes) <= (1 << 27)
         sizes, kinds = sizes[keep], kinds[keep]
+    elif name.startswith("config4k"):  # config4k<K>_1GiB: config 4's sizes, every segment kind K
+        sizes = np.exp(rng.uniform(np.log(8), np.log(8192), 200000)).astype(np.int64)
+        keep = np.cumsum(sizes) <= (1 << 27)
+        sizes = sizes[keep]
+        kinds = np.full(len(sizes), int(name[len("config4k")]), np.uint8)
     elif name == "config2_1GiB":
         sizes = np.full(1 << 20, 128, np.int64)
         kinds = np.zeros(len(sizes), np.uint8)
