@@ -605,7 +605,10 @@ using BigStageSmem = StageSmemT<kBigWords, kBigBytes, true, false>;
 constexpr uint32_t kLuSeg = 64;
 constexpr uint32_t kLuSegMin = 8;  // (a short last window: segments of at least this many bytes)
 constexpr uint32_t kLuWinBytes = kLuSeg * kThreads;     // 16 KiB of record starts
-constexpr uint32_t kLuLead = 64;                         // spec lead-in (tests/emu_long.py: 64 > 48)
+#ifndef UNPACK_LU_LEAD
+#define UNPACK_LU_LEAD 64
+#endif
+constexpr uint32_t kLuLead = UNPACK_LU_LEAD;             // spec lead-in (tests/emu_long.py: 64 > 48)
 constexpr uint32_t kLuAvail = kLuWinBytes + 2080;        // bytes staged past the window start
 constexpr uint32_t kLuStage = kLuAvail + 32;             // (+ misalignment and a hop's read-ahead)
 constexpr uint32_t kLuWords = 8192;                      // descriptor window (output words)
