@@ -2726,6 +2726,206 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
 }
 
 // ---------------------------------------------------------------------------
+// A mid-size read unit staged in the long-unit buffer (bodies of more than
+// kSmallBytes, up to kMidBytes): unpack_small's walk on all four waves, 256
+// segments, each wave settling its 64 by DPP rounds of its own; the waves
+// then meet once through LDS: wave w assumed its first segment's spec start
+// as its entry, and is re-run from the true one (the running maximum of the
+// earlier waves' exits) when that differs, until no entry changes.
+// unpack_long's workgroup-wide rounds took two barriers each (a 1500-word
+// body: 3 rounds, 5.7 of its 12.3 us; profiles/r06m_luprof_percall.txt).
+// Returns false with nothing written to `out` when the unit does not check
+// out (the caller then takes unpack_long, which gives the exact status).
+#ifndef UNPACK_MID_BYTES
+#define UNPACK_MID_BYTES 16384
+#endif
+constexpr uint32_t kMidBytes = UNPACK_MID_BYTES;
+static_assert(kMidBytes + 32 <= kLuStage, "a mid-size unit lies in the staged bytes");
+
+__device__ bool unpack_mid(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
+                           uint64_t* __restrict__ out, uint32_t tid, uint32_t lane,
+                           uint32_t wave, uint32_t& used) {
+    __shared__ uint32_t wx[2][kWaves];   // each wave's last exit (the running max), per pass
+    __shared__ uint32_t we[2][kWaves];   // the entry each wave assumed, per pass
+    __shared__ uint32_t wok[2][kWaves];  // the wave's rounds settled
+    __shared__ uint32_t wtot[kWaves];    // each wave's words
+    __shared__ uint32_t wts[kWaves];     // the wave's segment holding word n (or kThreads)
+    __shared__ uint32_t wbad[kWaves];
+    const uint8_t* B = S.bytes + mis;
+    S.sel[tid] = kExpandTable.s[tid];
+    {
+        uint4* d4 = reinterpret_cast<uint4*>(S.dpos);
+        const uint4 none = make_uint4(~0u, ~0u, ~0u, ~0u);
+        for (uint32_t k = tid; k < (n + 7) / 8; k += kThreads) d4[k] = none;
+    }
+    const uint32_t j = tid;
+    const uint32_t sb = (uint32_t)(((uint64_t)L * j) / kThreads);
+    const uint32_t se = (uint32_t)(((uint64_t)L * (j + 1u)) / kThreads);
+    // spec walk from kSmallLead bytes before the segment (segment 0: byte 0)
+    uint32_t p = j == 0 ? 0u : (sb > kSmallLead ? sb - kSmallLead : 0u), w = 0;
+    while (p < sb) seg_hop(B, p, w);
+    const uint32_t f = p, wf = w;
+    while (p < se) seg_hop(B, p, w);
+    const bool serr = p > L;
+    const uint32_t xs = serr ? 0u : p, ws = w - wf;
+    const uint32_t xsp = (serr || f >= se) ? 0u : xs;
+    // the wave's entry: wave 0's is byte 0; the others assume their first
+    // segment's spec start until the earlier waves have settled
+    uint32_t E = wave == 0 ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)f);
+    uint32_t own = xsp, wd = ws;
+    bool err = j == 0 && serr;
+    uint32_t e_used = ~0u, x = 0;
+    bool ok = true, run = true;
+    for (uint32_t pass = 0;; pass++) {
+        if (run) {
+            // rounds within the wave to its fixed point for entry E
+            x = wave_max_scan(own);
+            for (uint32_t round = 0;; round++) {
+                // (the wave's entry E bounds every lane's: a record of an
+                // earlier wave may cover this wave's first segments.  No
+                // lane-dependent select around the DPP shift: the compiler
+                // sank it into the select's branch, and lane 1 then read a
+                // disabled lane 0 as 0 -- one word short, r06p)
+                const uint32_t e = max(E, wave_shr1(x));  // (wave_shr1: 0 in lane 0)
+                const bool need = e != e_used;
+                if (ballot64(need) == 0) break;
+                if (round > CAPNP_WAVE + 1) {  // (not reached: lane i is settled after round i + 1)
+                    ok = false;
+                    break;
+                }
+                if (need) {
+                    e_used = e;
+                    if (e < sb || e == f) {
+                        own = xsp;
+                        wd = ws;
+                        err = serr;
+                    } else {
+                        uint32_t pt = e, wt = 0, ps = f, wsp = 0;
+                        bool met = false;
+                        while (pt < se) {
+                            while (ps < pt && ps < se) seg_hop(B, ps, wsp);
+                            if (ps == pt) {
+                                met = true;
+                                break;
+                            }
+                            seg_hop(B, pt, wt);
+                        }
+                        if (met) {
+                            own = xsp;
+                            wd = wt + ws - wsp;
+                            err = serr;
+                        } else {
+                            err = pt > L;
+                            own = (err || e >= se) ? 0u : pt;
+                            wd = wt;
+                        }
+                    }
+                }
+                x = wave_max_scan(own);
+            }
+        }
+        // the waves meet: wave v's true entry is the largest exit before it
+        const uint32_t b = pass & 1u;
+        if (lane == CAPNP_WAVE - 1) {
+            wx[b][wave] = max(x, E);
+            we[b][wave] = E;
+            wok[b][wave] = ok ? 1u : 0u;
+        }
+        __syncthreads();
+        // (every wave reads the same records: the decisions below are the
+        // workgroup's, so the waves meet at the same barriers)
+        bool any = false;
+        uint32_t mine = E, m = 0, allok = 1;
+#pragma unroll
+        for (uint32_t v = 0; v < (uint32_t)kWaves; v++) {
+            if (v > 0 && we[b][v] != m) any = true;
+            if (v == wave) mine = v == 0 ? 0u : m;
+            m = max(m, wx[b][v]);
+            allok &= wok[b][v];
+        }
+        ok = allok != 0 && pass <= (uint32_t)kWaves;  // (each pass settles at least one more wave)
+        if (!any || !ok) break;
+        run = mine != E;
+        E = mine;
+    }
+    // words: the waves' totals place each segment; the segment holding word
+    // n walks to it with every check
+    const uint32_t incl_w = wave_sum_scan(wd);
+    if (lane == CAPNP_WAVE - 1) wtot[wave] = incl_w;
+    __syncthreads();
+    uint32_t before = 0;
+#pragma unroll
+    for (uint32_t v = 0; v < (uint32_t)kWaves; v++) before += v < wave ? wtot[v] : 0u;
+    const uint32_t incl = before + incl_w, base = incl - wd;
+    const uint64_t hold = ballot64(wd > 0 && base < n && n <= incl);
+    if (lane == 0) wts[wave] = hold ? wave * CAPNP_WAVE + (uint32_t)__builtin_ctzll(hold) : kThreads;
+    __syncthreads();
+    uint32_t ts = kThreads;
+#pragma unroll
+    for (uint32_t v = 0; v < (uint32_t)kWaves; v++) ts = min(ts, wts[v]);
+    const bool wave_bad = ballot64(err && j <= ts) != 0;  // (the ballot before the lane-0 store)
+    if (lane == 0) wbad[wave] = wave_bad ? 1u : 0u;
+    uint32_t q = e_used, wq = base;
+    bool fine = true;
+    if (ok && ts < kThreads && j == ts) {
+        while (wq < n) {
+            uint32_t tag, b1, b9;
+            rec_bytes(B, q + 1u, tag, b1, b9);
+            const bool isz = tag == 0, isf = tag == 0xFF;
+            const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+            const uint32_t qe = q + 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) +
+                                (isf ? 8u * cnt : 0u);
+            const uint32_t wn = wq + 1u + cnt;
+            if (qe > L || wn > n) {
+                fine = false;
+                break;
+            }
+            q = qe;
+            wq = wn;
+        }
+        S.misc[0] = fine ? 1u : 0u;
+        S.misc[1] = q;
+    }
+    __syncthreads();
+    bool bad = !ok || ts >= kThreads || S.misc[0] == 0;
+#pragma unroll
+    for (uint32_t v = 0; v < (uint32_t)kWaves; v++) bad |= wbad[v] != 0;
+#ifdef MID_DEBUG
+    if (tid == 0) printf("MID bad %d ts %u misc0 %u\n", (int)bad, ts, S.misc[0]);
+#endif
+    if (__builtin_amdgcn_readfirstlane((int)bad)) return false;  // (uniform: LDS after the barrier)
+    used = S.misc[1];
+#ifdef MID_DEBUG
+    if (lane == 0) printf("MID wave %u E %u x63 %u tot %u ts %u L %u n %u\n", wave, E,
+                          (uint32_t)__builtin_amdgcn_readlane((int)x, 63), wtot[wave], ts, L, n);
+    if (j == ts) printf("MID ts %u e_used %u base %u wd %u used %u\n", ts, e_used, base, wd, S.misc[1]);
+    if (err) printf("MID err lane %u e_used %u own %u wd %u\n", j, e_used, own, wd);
+    if (lane == 0) printf("MID wbad %u %u %u %u ok %d\n", wbad[0], wbad[1], wbad[2], wbad[3], (int)ok);
+#endif
+    // descriptors of the records from each entry (to word n in the last)
+    if (j <= ts) {
+        uint32_t r = e_used, wr = base;
+        const uint32_t wlim = j == ts ? n : incl;
+        while (wr < wlim) {
+            uint32_t tag, b1, b9;
+            rec_bytes(B, r + 1u, tag, b1, b9);
+            const bool isz = tag == 0, isf = tag == 0xFF;
+            const uint32_t cnt = isz ? b1 : (isf ? b9 : 0u);
+            const uint32_t lp = r + mis;  // (LDS position of the tag)
+            S.dpos[wr] = (uint16_t)lp;
+            if (isf)
+                for (uint32_t i = 0; i < cnt; i++)
+                    S.dpos[wr + 1u + i] = (uint16_t)(kRaw | (lp + 10u + 8u * i));
+            wr += 1u + cnt;
+            r += 1u + __builtin_popcount(tag) + ((isz || isf) ? 1u : 0u) + (isf ? 8u * cnt : 0u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < n; i += kThreads) out[i] = expand_desc(S.bytes, S.sel, S.dpos[i]);
+    return true;
+}
+
+// ---------------------------------------------------------------------------
 // One read_message call in one launch (the drop-in at the reference's call
 // granularity: serialize_packed::read_message / try_read_message /
 // read_message_no_alloc once per message, serialize_packed.rs:233-291,
@@ -2813,10 +3013,13 @@ __device__ __forceinline__ void msg_read_body(USmem& sm, MsgReadSmem& M, const u
         const uint64_t span = in_len - P0 < avail ? in_len - P0 : avail;
         const uint64_t Ls = span < 10 * nw + 16 ? span : 10 * nw + 16;
         bool done = false;
-        if (Ls > 0 && Ls <= kSmallBytes && nw <= kLuWords) {
+        if (Ls > 0 && Ls <= kMidBytes && nw <= kLuWords) {
             uint32_t used = 0;
-            done = unpack_small(sm.lu, (uint32_t)P0, (uint32_t)Ls, (uint32_t)nw, words, tid, lane,
-                                wave, used);
+            done = Ls <= kSmallBytes
+                       ? unpack_small(sm.lu, (uint32_t)P0, (uint32_t)Ls, (uint32_t)nw, words, tid,
+                                      lane, wave, used)
+                       : unpack_mid(sm.lu, (uint32_t)P0, (uint32_t)Ls, (uint32_t)nw, words, tid,
+                                    lane, wave, used);
             if (done && tid == 0) {
                 M.st = 0;
                 M.used = used;

@@ -257,3 +257,53 @@ def test_read_message_small_bodies_vs_oracle(ctx):
             for sgm in rsegs:
                 assert np.array_equal(body[o:o + len(sgm)], sgm)
                 o += len(sgm)
+
+
+def test_read_message_mid_bodies_vs_oracle(ctx):
+    """read_message's mid-size bodies (csrc/unpack.hip unpack_mid: bodies of
+    5-16 KB packed inside the staged prefix, four waves of 64 segments that
+    settle by themselves and meet through LDS) against the oracle's
+    read_message: every fill kind at sizes around both edges (the short-body
+    path below 5 KB, the long-unit decode above 16 KB), with the next
+    message after them, truncated by a byte and inside the body, tables
+    claiming fewer words than the records cover, literal runs and zero runs
+    across the waves' quarters, a flipped byte, and random bytes after a
+    valid table -- status, consumed bytes and the segment words."""
+    rng = np.random.default_rng(33)
+    cases = []
+    for k in (560, 600, 700, 900, 1024, 1500, 1800, 2000, 2200, 2400, 8192):
+        for kind in (0, 1, 2):
+            w = O.gen_fill(np.array([0, k], np.uint64), kinds=np.array([kind], np.uint8),
+                           pz=O.PZ30, id0=1900 + k + kind)
+            st, msg = O.write_message([w])
+            assert st == 0
+            cases.append(msg)
+            cases.append(msg + O.write_message([w[:3]])[1])
+            cases.append(msg[:len(msg) - 1])
+            cases.append(msg[:max(9, len(msg) // 2)])
+            cases.append(_packed([(k - 1) << 32]) + _packed(w))
+            bad = bytearray(msg)
+            bad[8 + int(rng.integers(0, len(msg) - 8))] ^= 0x5A
+            cases.append(bytes(bad))
+    # runs crossing the quarter cuts: literal words then zeros then literal
+    for k in (800, 1500, 2000):
+        w = np.zeros(k, np.uint64)
+        a, b = k // 4 - 7, k // 2 + 5
+        w[:a] = 0x0102030405060708
+        w[b:] = 0x1112131415161718
+        w[rng.integers(0, k, 5)] = 0x0000000400000001
+        cases.append(O.write_message([w])[1])
+    for i in range(30):  # a valid one-segment table, then random body bytes
+        k = int(rng.integers(500, 2000))
+        body = rng.integers(0, 256, int(rng.integers(5200, 16000))).astype(np.uint8).tobytes()
+        cases.append(_packed([k << 32]) + body)
+    for data in cases:
+        rst, rsegs, rused = O.read_message(bytes(data))
+        r, body, used = _read_message_call(ctx.handle, data)
+        assert r == rst, (len(data), r, rst)
+        if rst == 0:
+            assert used == rused, (len(data), used, rused)
+            o = 0
+            for sgm in rsegs:
+                assert np.array_equal(body[o:o + len(sgm)], sgm)
+                o += len(sgm)
