@@ -261,17 +261,17 @@ def test_read_message_small_bodies_vs_oracle(ctx):
 
 def test_read_message_mid_bodies_vs_oracle(ctx):
     """read_message's mid-size bodies (csrc/unpack.hip unpack_mid: bodies of
-    5-16 KB packed inside the staged prefix, four waves of 64 segments that
+    5-18 KB packed inside the staged prefix, four waves of 64 segments that
     settle by themselves and meet through LDS) against the oracle's
     read_message: every fill kind at sizes around both edges (the short-body
-    path below 5 KB, the long-unit decode above 16 KB), with the next
+    path below 5 KB, the long-unit decode above 18 KB), with the next
     message after them, truncated by a byte and inside the body, tables
     claiming fewer words than the records cover, literal runs and zero runs
     across the waves' quarters, a flipped byte, and random bytes after a
     valid table -- status, consumed bytes and the segment words."""
     rng = np.random.default_rng(33)
     cases = []
-    for k in (560, 600, 700, 900, 1024, 1500, 1800, 2000, 2200, 2400, 8192):
+    for k in (560, 600, 700, 900, 1024, 1500, 1800, 2000, 2200, 2400, 3600, 4096, 4300, 8192):
         for kind in (0, 1, 2):
             w = O.gen_fill(np.array([0, k], np.uint64), kinds=np.array([kind], np.uint8),
                            pz=O.PZ30, id0=1900 + k + kind)
