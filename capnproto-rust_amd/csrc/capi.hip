@@ -196,6 +196,8 @@ struct capnp_ctx {
     uint8_t* d_pin = nullptr;   // ... its device address (the one-launch calls read and write it)
     size_t pin_cap = 0;
     FrameResult* d_hframe = nullptr;  // h_frame's device address
+    uint8_t* d_req = nullptr;    // per-message calls' inputs, written by the host through the BAR
+    int req_ok = -1;             // ... whether the device allows that (-1: not asked yet)
     uint32_t* h_flag = nullptr;  // pinned: the one-launch calls' completion flag
     uint32_t* d_flag = nullptr;  // ... its device address
     uint32_t call_seq = 0;
@@ -403,6 +405,44 @@ capnp_status ensure_pin(capnp_ctx* ctx, size_t bytes) {
     ctx->d_pin = static_cast<uint8_t*>(dp);
     return CAPNP_OK;
 }
+
+// The per-message calls' inputs (the staged read prefix, the laid-out write
+// words and offsets) go to device memory that the host writes through the
+// PCI BAR, on devices whose whole memory is mapped there (large BAR): the
+// host's stores are posted writes and the kernel reads HBM, where from
+// pinned memory every fetch was a PCIe read round trip
+// (scripts/bar_probe.hip, profiles/r06q_bar_probe.txt: a 12 KB request
+// 8.98 -> 5.6 us, 6.6 KB 6.62 -> 4.7).  Fine-grained memory: the kernel's
+// system-scope acquire (the service) or its launch sees the bytes.  Outputs
+// stay in pinned memory (host reads through the BAR are uncached).  Inputs
+// past kReqBytes, devices without a large BAR and CAPNP_PERCALL_BAR=0 use
+// the pinned buffer.
+constexpr size_t kReqBytes = size_t(1) << 20;
+
+uint8_t* req_buf(capnp_ctx* ctx, size_t bytes) {
+    if (bytes > kReqBytes) return nullptr;
+    if (ctx->req_ok < 0) {
+        static const bool enabled = [] {
+            const char* e = getenv("CAPNP_PERCALL_BAR");
+            return !(e && e[0] == '0');
+        }();
+        int large = 0;
+        ctx->req_ok = 0;
+        if (enabled &&
+            hipDeviceGetAttribute(&large, hipDeviceAttributeIsLargeBar, ctx->device) == hipSuccess &&
+            large == 1 &&
+            hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->d_req), kReqBytes + 64,
+                                  hipDeviceMallocFinegrained) == hipSuccess)
+            ctx->req_ok = 1;
+        else
+            ctx->d_req = nullptr;
+    }
+    return ctx->req_ok ? ctx->d_req : nullptr;
+}
+
+// The host's stores into req_buf reach the device before what follows them
+// (a service's bell, a launch's doorbell).
+inline void req_done() { __builtin_ia32_sfence(); }
 
 // Waits for a one-launch call (msg_read_kernel / msg_pack_kernel) by its
 // completion flag in pinned memory: the kernel stores `seq` there after its
@@ -919,6 +959,7 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     if (ctx->d_bad) (void)hipFree(ctx->d_bad);
     if (ctx->h_bad) (void)hipHostFree(ctx->h_bad);
     if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+    if (ctx->d_req) (void)hipFree(ctx->d_req);
     if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
     if (ctx->d_msg) (void)hipFree(ctx->d_msg);
     if (ctx->d_resync) (void)hipFree(ctx->d_resync);
@@ -1897,26 +1938,31 @@ capnp_status capnp_packed_write_message(capnp_ctx* ctx, const uint64_t* const* s
         if (st != CAPNP_OK) return st;
         uint8_t* h = ctx->h_pin;
         uint8_t* dh = ctx->d_pin;
-        uint64_t* w = reinterpret_cast<uint64_t*>(h);
-        lay_out(w, reinterpret_cast<uint64_t*>(h + o_off));
+        // the words and offsets: through the BAR when the device allows it
+        uint8_t* dr = req_buf(ctx, o_tot);
+        uint8_t* hw = dr ? dr : h;
+        uint64_t* w = reinterpret_cast<uint64_t*>(hw);
+        lay_out(w, reinterpret_cast<uint64_t*>(hw + o_off));
         uint64_t o = tw;
         for (uint32_t i = 0; i < nseg; i++) {
             if (seg_words[i]) memcpy(w + o, segs[i], (size_t)seg_words[i] * 8);
             o += seg_words[i];
         }
+        if (dr) req_done();
+        uint8_t* dw = dr ? dr : dh;  // (the kernel's view of the words and offsets)
         const uint32_t seq = next_seq(ctx);
         if (percall_warm(ctx)) {
             SvcPackReq q;
-            q.words = (uint64_t)dh;
-            q.off = (uint64_t)(dh + o_off);
+            q.words = (uint64_t)dw;
+            q.off = (uint64_t)(dw + o_off);
             q.out = (uint64_t)(dh + o_out);  // (*total at dh + o_tot = out - 16)
             q.counts = nch | ((uint64_t)nw << 32);
             q.out_cap = bound;
             q.scratch = (uint64_t)ctx->d_stage;
             st = svc_call(ctx, 1, reinterpret_cast<const uint64_t*>(&q), seq);
         } else {
-            HIP_TRY(capnp_launch_msg_pack(reinterpret_cast<uint64_t*>(dh),
-                                          reinterpret_cast<uint64_t*>(dh + o_off), (uint32_t)nch,
+            HIP_TRY(capnp_launch_msg_pack(reinterpret_cast<uint64_t*>(dw),
+                                          reinterpret_cast<uint64_t*>(dw + o_off), (uint32_t)nch,
                                           (uint32_t)nw, dh + o_out, bound,
                                           reinterpret_cast<uint64_t*>(dh + o_tot), ctx->d_flag,
                                           seq, ctx->d_stage, s));
@@ -2027,13 +2073,17 @@ static capnp_status read_message_fast(capnp_ctx* ctx, const uint8_t* in, size_t 
     uint8_t* h = ctx->h_pin;
     uint8_t* dh = ctx->d_pin;
     hipStream_t s = ctx->stream;
-    if (stage) memcpy(h, in, stage);
+    // the staged input: through the BAR when the device allows it (req_buf)
+    uint8_t* dr = req_buf(ctx, round16(stage) + 16);
+    if (stage) memcpy(dr ? dr : h, in, stage);
+    if (dr) req_done();
+    uint8_t* din = dr ? dr : dh;
     // one launch: the kernel reads the staged bytes and writes the frame
     // record, the body's status and its words in pinned memory
     const uint32_t seq = next_seq(ctx);
     if (percall_warm(ctx)) {
         SvcReadReq q;
-        q.in = (uint64_t)dh;
+        q.in = (uint64_t)din;
         q.words = (uint64_t)(dh + h_out);  // (res at + o_st = round16(8 cap))
         q.flags = stage | ((uint64_t)(no_alloc != 0) << 32) | ((uint64_t)(try_mode != 0) << 33) |
                   ((uint64_t)(o.has_traversal_limit != 0) << 34);
@@ -2042,7 +2092,7 @@ static capnp_status read_message_fast(capnp_ctx* ctx, const uint8_t* in, size_t 
         q.cap = cap;
         st = svc_call(ctx, 0, reinterpret_cast<const uint64_t*>(&q), seq);
     } else {
-        HIP_TRY(capnp_launch_msg_read(dh, stage, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
+        HIP_TRY(capnp_launch_msg_read(din, stage, (uint32_t)no_alloc, (uint32_t)(try_mode != 0),
                                       o.traversal_limit_in_words,
                                       (uint32_t)(o.has_traversal_limit != 0), buffer_len, cap,
                                       ctx->d_hframe, reinterpret_cast<uint64_t*>(dh + h_out),

@@ -13,6 +13,7 @@ struct FrameResult {
     uint32_t seg_words[512];
     uint8_t table[2064];       // decoded table bytes
 };
+static_assert(__builtin_offsetof(FrameResult, table) % 8 == 0, "first_unit's 8-byte store");
 
 #ifdef __HIPCC__
 // The segment-table read units of serialize_packed::{read_message,
@@ -65,6 +66,41 @@ __device__ inline int32_t serial_read(const uint8_t* in, uint64_t in_len, uint8_
     return ST_OK;
 }
 
+// serial_read of the table's first 8-byte unit into out (8-byte aligned) and
+// *word, with every byte it may use read up front (independent loads and the
+// word built in registers, instead of a dependent chain of byte reads and
+// stores; a read_message call spent ~0.8 us in the table, r06q): a tag other
+// than 0x00 / 0xFF takes 1 + popcount(tag) bytes and no run.  The others,
+// and inputs shorter than 10 bytes, take serial_read.
+__device__ inline int32_t first_unit(const uint8_t* in, uint64_t in_len, uint8_t* out,
+                                     uint64_t* word, uint64_t* used, uint64_t* nread) {
+    if (in_len >= 10) {
+        uint32_t b[10];
+#pragma unroll
+        for (int i = 0; i < 10; i++) b[i] = in[i];
+        const uint32_t tag = b[0];
+        if (tag != 0u && tag != 0xFFu) {
+            uint64_t v = 0;  // the unit's non-zero bytes, in order
+#pragma unroll
+            for (int i = 8; i >= 1; i--) v = (v << 8) | b[i];
+            uint64_t x = 0;
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                const uint32_t k = __builtin_popcount(tag & ((1u << i) - 1u));
+                if ((tag >> i) & 1u) x |= ((v >> (8 * k)) & 0xFFull) << (8 * i);
+            }
+            *reinterpret_cast<uint64_t*>(out) = x;
+            *word = x;
+            *used = 1u + __builtin_popcount(tag);
+            *nread = 8;
+            return ST_OK;
+        }
+    }
+    const int32_t st = serial_read(in, in_len, out, 8, used, nread);
+    *word = *reinterpret_cast<const uint64_t*>(out);
+    return st;
+}
+
 // read_exact over PackedRead (io.rs:16-31).
 __device__ inline int32_t serial_read_exact(const uint8_t* in, uint64_t in_len, uint8_t* out,
                                      uint64_t out_len, uint64_t* used) {
@@ -95,14 +131,15 @@ __device__ inline void frame_table(const uint8_t* __restrict__ in, uint64_t in_l
     r->total_words = 0;
     r->table_bytes = 0;
     r->table_consumed = 0;
-    int32_t st = serial_read(in, in_len, t, 8, &used, &nread);
+    uint64_t w0 = 0;
+    int32_t st = first_unit(in, in_len, t, &w0, &used, &nread);
     if (st != ST_OK) { r->status = st; return; }
     if (nread == 0) { r->status = try_mode ? ST_NONE : ST_EOF; return; }
     pos += used;
-    const uint32_t nseg = le32(t) + 1u;
+    const uint32_t nseg = (uint32_t)w0 + 1u;
     if (nseg >= 512u || nseg == 0) { r->status = ST_BAD_NSEG; return; }
-    uint64_t total = le32(t + 4);
-    r->seg_words[0] = le32(t + 4);
+    uint64_t total = (uint32_t)(w0 >> 32);
+    r->seg_words[0] = (uint32_t)(w0 >> 32);
     uint64_t start;
     if (!no_alloc) {
         // serialize.rs:476-496: the rest of the table is ONE read unit

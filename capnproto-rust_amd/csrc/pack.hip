@@ -3118,6 +3118,9 @@ __device__ __forceinline__ void msg_pack_body(MsgPackSmem& S, const uint64_t* wo
         if (tid + k * kMsgThreads <= nchunks) S.off[tid + k * kMsgThreads] = ov[k];
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's words are in
     __syncthreads();
+#if SVC_PROF
+    const uint64_t tp0 = __builtin_amdgcn_s_memrealtime();
+#endif
     uint8_t* ring = S.ring[wave];
     // (the last chunk -- a message's one segment, usually the longest -- is
     // placed without its size: pass B measures it)
@@ -3157,6 +3160,9 @@ __device__ __forceinline__ void msg_pack_body(MsgPackSmem& S, const uint64_t* wo
         if (lane == 0) S.rsize[wave] = sz;
     }
     __syncthreads();
+#if SVC_PROF
+    const uint64_t tp1 = __builtin_amdgcn_s_memrealtime();
+#endif
     // chunk positions: exclusive scan of the sizes, up to 3 chunks per thread
     {
         constexpr uint32_t kPer = (kMsgChunks + kMsgThreads - 1) / kMsgThreads;
@@ -3189,6 +3195,9 @@ __device__ __forceinline__ void msg_pack_body(MsgPackSmem& S, const uint64_t* wo
         if (tid == 0) S.wsum[0] = all;  // (the chunks before the last)
     }
     __syncthreads();
+#if SVC_PROF
+    const uint64_t tp2 = __builtin_amdgcn_s_memrealtime();
+#endif
     // (pass B's flushes go to device memory -- a step's bytes in 16-byte
     // stores that a PCIe write path would take one at a time -- and the
     // packed bytes cross to the host output in one coalesced copy)
@@ -3217,6 +3226,9 @@ __device__ __forceinline__ void msg_pack_body(MsgPackSmem& S, const uint64_t* wo
         }
     }
     __syncthreads();
+#if SVC_PROF
+    const uint64_t tp3 = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint64_t tot = S.chunk_pos[nchunks - 1] + S.chunk_size[nchunks - 1];
     if (via) {
         // (scratch and out both 16-byte aligned: whole vectors, the last one
@@ -3228,6 +3240,15 @@ __device__ __forceinline__ void msg_pack_body(MsgPackSmem& S, const uint64_t* wo
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this wave's stores have landed)
     __syncthreads();
+#if SVC_PROF
+    if (tid == 0) {  // (slots 3-6, 9: sizes, scan, pass B, copy-out; the stage's end)
+        atomicAdd(&g_svc_prof[3], (unsigned long long)(tp1 - tp0));
+        atomicAdd(&g_svc_prof[4], (unsigned long long)(tp2 - tp1));
+        atomicAdd(&g_svc_prof[5], (unsigned long long)(tp3 - tp2));
+        atomicAdd(&g_svc_prof[9], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - tp3));
+        atomicAdd(&g_svc_prof[6], (unsigned long long)tp0);
+    }
+#endif
     if (tid == 0) {
         total[0] = tot;
         if (flag) {  // (the host waits on this flag: everything above is visible first)

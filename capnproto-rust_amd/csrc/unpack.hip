@@ -2752,6 +2752,9 @@ __device__ bool unpack_mid(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
     __shared__ uint32_t wts[kWaves];     // the wave's segment holding word n (or kThreads)
     __shared__ uint32_t wbad[kWaves];
     const uint8_t* B = S.bytes + mis;
+#if SVC_PROF
+    const uint64_t tm0 = __builtin_amdgcn_s_memrealtime();
+#endif
     S.sel[tid] = kExpandTable.s[tid];
     {
         uint4* d4 = reinterpret_cast<uint4*>(S.dpos);
@@ -2769,6 +2772,10 @@ __device__ bool unpack_mid(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
     const bool serr = p > L;
     const uint32_t xs = serr ? 0u : p, ws = w - wf;
     const uint32_t xsp = (serr || f >= se) ? 0u : xs;
+#if SVC_PROF
+    const uint64_t tm1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t n_pass = 0;
+#endif
     // the wave's entry: wave 0's is byte 0; the others assume their first
     // segment's spec start until the earlier waves have settled
     uint32_t E = wave == 0 ? 0u : (uint32_t)__builtin_amdgcn_readfirstlane((int)f);
@@ -2826,6 +2833,9 @@ __device__ bool unpack_mid(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
         }
         // the waves meet: wave v's true entry is the largest exit before it
         const uint32_t b = pass & 1u;
+#if SVC_PROF
+        n_pass++;
+#endif
         if (lane == CAPNP_WAVE - 1) {
             wx[b][wave] = max(x, E);
             we[b][wave] = E;
@@ -2848,6 +2858,9 @@ __device__ bool unpack_mid(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
         run = mine != E;
         E = mine;
     }
+#if SVC_PROF
+    const uint64_t tm2 = __builtin_amdgcn_s_memrealtime();
+#endif
     // words: the waves' totals place each segment; the segment holding word
     // n walks to it with every check
     const uint32_t incl_w = wave_sum_scan(wd);
@@ -2895,6 +2908,9 @@ __device__ bool unpack_mid(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
 #endif
     if (__builtin_amdgcn_readfirstlane((int)bad)) return false;  // (uniform: LDS after the barrier)
     used = S.misc[1];
+#if SVC_PROF
+    const uint64_t tm3 = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef MID_DEBUG
     if (lane == 0) printf("MID wave %u E %u x63 %u tot %u ts %u L %u n %u\n", wave, E,
                           (uint32_t)__builtin_amdgcn_readlane((int)x, 63), wtot[wave], ts, L, n);
@@ -2921,7 +2937,21 @@ __device__ bool unpack_mid(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
         }
     }
     __syncthreads();
+#if SVC_PROF
+    const uint64_t tm4 = __builtin_amdgcn_s_memrealtime();
+#endif
     for (uint32_t i = tid; i < n; i += kThreads) out[i] = expand_desc(S.bytes, S.sel, S.dpos[i]);
+#if SVC_PROF
+    __syncthreads();
+    if (tid == 0) {  // (slots 13-15, 21-23: spec, passes, words, descriptors, expand, count)
+        atomicAdd(&g_svc_prof[13], (unsigned long long)(tm1 - tm0));
+        atomicAdd(&g_svc_prof[14], (unsigned long long)(tm2 - tm1));
+        atomicAdd(&g_svc_prof[15], (unsigned long long)(tm3 - tm2));
+        atomicAdd(&g_svc_prof[21], (unsigned long long)(tm4 - tm3));
+        atomicAdd(&g_svc_prof[22], (unsigned long long)(__builtin_amdgcn_s_memrealtime() - tm4));
+        atomicAdd(&g_svc_prof[23], (unsigned long long)n_pass + (1ull << 32));
+    }
+#endif
     return true;
 }
 

@@ -39,11 +39,11 @@ def main():
         _lib.LIB_PATH = os.path.abspath(a.lib)
     L = _lib.lib()
     prof = []
-    for name in ("capnp_svc_prof", "capnp_svc_prof_w"):
+    for name, kind in (("capnp_svc_prof", "read"), ("capnp_svc_prof_w", "write")):
         try:
             f = getattr(L, name)
             f.restype = C.c_int
-            prof.append(f)
+            prof.append((f, kind))
         except AttributeError:
             pass
     p8 = (C.c_ulonglong * 24)()
@@ -62,7 +62,7 @@ def main():
         segs = np.empty(512, np.uint32)
         n, used, nseg = C.c_size_t(0), C.c_size_t(0), C.c_uint32(0)
         tw, tr = [], []
-        for f in prof:
+        for f, _ in prof:
             f(p8, 1)
         for r in range(a.reps + 10):
             t0 = time.perf_counter()
@@ -85,12 +85,19 @@ def main():
              "write_us_p10": round(float(np.percentile(tw, 10)), 1),
              "read_us_median": round(float(np.median(tr)), 1),
              "read_us_p10": round(float(np.percentile(tr, 10)), 1)}
-        for f, kind in zip(prof, ("read", "write")):
+        for f, kind in prof:
             f(p8, 1)
             if p8[0]:
                 r[kind + "_svc"] = {"requests": p8[0], "args_us": round(p8[1] / p8[0] / 100, 2),
                                     "body_us": round(p8[2] / p8[0] / 100, 2),
                                     "body_clock_mhz": round(100 * p8[8] / max(p8[2], 1))}
+                if kind == "write" and p8[6]:
+                    r["write_phases_us"] = {
+                        "stage": round((p8[6] - p8[7]) / p8[0] / 100, 2),
+                        "sizes": round(p8[3] / p8[0] / 100, 2),
+                        "scan": round(p8[4] / p8[0] / 100, 2),
+                        "pass_b": round(p8[5] / p8[0] / 100, 2),
+                        "copy_out": round(p8[9] / p8[0] / 100, 2)}
                 if kind == "read" and p8[6]:
                     r["read_phases_us"] = {
                         "stage": round((p8[6] - p8[7]) / p8[0] / 100, 2),
@@ -107,6 +114,15 @@ def main():
                                               "last_walk": round(p8[18] / p8[12] / 100, 2),
                                               "descriptors": round(p8[19] / p8[12] / 100, 2),
                                               "rounds_taken": round(p8[20] / p8[12], 2)}
+                    if p8[23] >> 32:
+                        k = p8[23] >> 32
+                        r["read_mid_us"] = {"n": k,
+                                            "spec": round(p8[13] / k / 100, 2),
+                                            "passes": round(p8[14] / k / 100, 2),
+                                            "words": round(p8[15] / k / 100, 2),
+                                            "descriptors": round(p8[21] / k / 100, 2),
+                                            "expand": round(p8[22] / k / 100, 2),
+                                            "passes_taken": round((p8[23] & 0xFFFFFFFF) / k, 2)}
         rows.append(r)
         print(json.dumps(r), flush=True)
 
