@@ -152,6 +152,14 @@ struct CallSvc {
     hipStream_t s = nullptr;
     uint64_t* h = nullptr;
     uint64_t* d = nullptr;
+    // The request line: h, or with CAPNP_SVC_LINE_BAR=1 device memory the
+    // host writes through the BAR (req_buf; the service then polls HBM
+    // instead of reading across PCIe: profiles/r06q_bar_probe.txt "fgfg").
+    uint64_t* line = nullptr;         // the host's view
+    const uint64_t* line_d = nullptr;  // the service's
+    bool line_dev = false;
+    uint64_t args[kSvcArgs] = {};     // the current request's (the check is made from these)
+    uint64_t bell = 0;                // the last bell rung
     uint32_t gen = 0;
     bool live = false;  // a service of `gen` was started and may still run
     std::chrono::steady_clock::time_point last{};  // its last completed request
@@ -489,14 +497,18 @@ std::vector<capnp_ctx*>* g_svc_ctxs = nullptr;  // contexts that started a servi
 
 void svc_bell(CallSvc& v, uint64_t b) {
     // (the arguments, the check and the payload before the bell, non-temporal
-    // stores included)
+    // and write-combined stores included)
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
-    __atomic_store_n(&v.h[0], b, __ATOMIC_RELEASE);
+    __atomic_store_n(&v.line[0], b, __ATOMIC_RELEASE);
+    __builtin_ia32_sfence();
+    v.bell = b;
 }
 
-// The request line for bell b (the arguments are in v.h[1, 7)), then the bell.
+// The request line for bell b (the arguments from v.args; the line is only
+// written: host reads through the BAR are uncached), then the bell.
 void svc_ring(CallSvc& v, uint64_t b) {
-    v.h[7] = svc_mix(b, v.h + 1);
+    for (uint32_t i = 0; i < kSvcArgs; i++) v.line[1 + i] = v.args[i];
+    v.line[7] = svc_mix(b, v.args);
     svc_bell(v, b);
 }
 
@@ -521,7 +533,7 @@ void svc_atexit() {
     if (!g_svc_ctxs) return;
     for (capnp_ctx* ctx : *g_svc_ctxs)
         for (CallSvc& v : ctx->svc) {
-            if (!v.live || !v.h) continue;
+            if (!v.live || !v.line) continue;
             svc_bell(v, 0);
             const auto t0 = std::chrono::steady_clock::now();
             while (__atomic_load_n(&v.h[8], __ATOMIC_ACQUIRE) != v.gen &&
@@ -540,6 +552,24 @@ capnp_status svc_init(capnp_ctx* ctx, int k) {
     void* dp = nullptr;
     HIP_TRY(hipHostGetDevicePointer(&dp, v.h, 0));
     v.d = static_cast<uint64_t*>(dp);
+    v.line = v.h;
+    v.line_d = v.d;
+    void* ld = nullptr;
+    // (off by default: measured no faster -- carsales pair 35.3 / 35.4 vs
+    // 35.2 / 35.1 us, writes 0.3-0.5 us slower, reads 0.1-0.3 faster,
+    // profiles/r06q_line_ab.txt; CAPNP_SVC_LINE_BAR=1 turns it on)
+    static const bool line_bar = [] {
+        const char* e = getenv("CAPNP_SVC_LINE_BAR");
+        return e && e[0] == '1';
+    }();
+    if (line_bar && req_buf(ctx, 0) &&
+        hipExtMallocWithFlags(&ld, 256, hipDeviceMallocFinegrained) == hipSuccess) {
+        v.line = static_cast<uint64_t*>(ld);
+        v.line_d = v.line;
+        v.line_dev = true;
+        for (int i = 0; i < 8; i++) v.line[i] = 0;
+        __builtin_ia32_sfence();
+    }
     HIP_TRY(hipStreamCreateWithPriority(&v.s, hipStreamNonBlocking, hi));
     std::lock_guard<std::mutex> g(g_svc_mu);
     if (!g_svc_ctxs) {
@@ -557,9 +587,9 @@ capnp_status svc_start(capnp_ctx* ctx, int k, uint32_t seq) {
     if (++v.gen == 0) v.gen = 1;
     svc_ring(v, ((uint64_t)v.gen << 32) | seq);
     v.live = true;
-    HIP_TRY(k == 0 ? capnp_launch_msg_read_service(v.d, v.d + 8, v.gen, kSvcIdleTicks,
+    HIP_TRY(k == 0 ? capnp_launch_msg_read_service(v.line_d, v.d + 8, v.gen, kSvcIdleTicks,
                                                    ctx->d_hframe, ctx->d_flag, v.s)
-                   : capnp_launch_msg_pack_service(v.d, v.d + 8, v.gen, kSvcIdleTicks,
+                   : capnp_launch_msg_pack_service(v.line_d, v.d + 8, v.gen, kSvcIdleTicks,
                                                    ctx->d_flag, v.s));
     return CAPNP_OK;
 }
@@ -571,7 +601,7 @@ capnp_status svc_call(capnp_ctx* ctx, int k, const uint64_t* args, uint32_t seq)
     capnp_status st = svc_init(ctx, k);
     if (st != CAPNP_OK) return st;
     CallSvc& v = ctx->svc[k];
-    memcpy(v.h + 1, args, kSvcArgs * sizeof(uint64_t));
+    memcpy(v.args, args, kSvcArgs * sizeof(uint64_t));
     const auto t0 = std::chrono::steady_clock::now();
     if (v.live && t0 - v.last <= kSvcTrust) {
         svc_ring(v, ((uint64_t)v.gen << 32) | seq);
@@ -600,7 +630,7 @@ capnp_status svc_call(capnp_ctx* ctx, int k, const uint64_t* args, uint32_t seq)
     const hipError_t q = hipStreamQuery(v.s);
     char diag[200];
     snprintf(diag, sizeof diag, " (kind %d, bell %llx, exit mark %llu, flag %u, seq %u, stream %d)",
-             k, (unsigned long long)v.h[0], (unsigned long long)v.h[8],
+             k, (unsigned long long)v.bell, (unsigned long long)v.h[8],
              __atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE), seq, (int)q);
     svc_stop(ctx, k);
     if (__atomic_load_n(ctx->h_flag, __ATOMIC_ACQUIRE) == seq) return CAPNP_OK;
@@ -950,6 +980,7 @@ void capnp_ctx_destroy(capnp_ctx* ctx) {
     for (CallSvc& v : ctx->svc) {
         if (v.s) (void)hipStreamDestroy(v.s);
         if (v.h) (void)hipHostFree(v.h);
+        if (v.line_dev) (void)hipFree(v.line);
     }
     if (ctx->d_state) (void)hipFree(ctx->d_state);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);

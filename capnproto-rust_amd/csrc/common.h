@@ -224,13 +224,13 @@ struct SvcCmd {
 // The request line's arguments of each service, by name (host and device
 // share these layouts): msg_read_service's and msg_pack_service's.
 struct SvcReadReq {
-    uint64_t in;      // the staged input (pinned)
+    uint64_t in;      // the staged input (device memory written through the BAR, or pinned)
     uint64_t words;   // the body's words (pinned); {status, 0, consumed} at round16(8 cap) bytes on
     uint64_t flags;   // stage bytes | no_alloc << 32 | try_mode << 33 | has_limit << 34
     uint64_t limit, buffer_len, cap;
 };
 struct SvcPackReq {
-    uint64_t words, off;  // the message's chunks and their offsets (pinned)
+    uint64_t words, off;  // the message's chunks and their offsets (as SvcReadReq::in)
     uint64_t out;         // the packed output (pinned); *total sits 16 bytes before it
     uint64_t counts;      // nchunks | nwords << 32
     uint64_t out_cap;
