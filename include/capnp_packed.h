@@ -412,7 +412,10 @@ capnp_status capnp_gpu_read_flat_messages(capnp_ctx* ctx, const uint8_t* d_buf, 
 /* ---- host message API (mirrors serialize_packed) ----------------------- */
 /* Latency of the per-message calls below: a message that fits the one-launch
    kernels (writes of <= 8448 words, reads of bodies < 64 Ki words) is served
-   by one workgroup reading and writing pinned host memory.  A call within
+   by one workgroup; the host writes its inputs into device memory through
+   the PCI BAR on large-BAR devices (1 MiB per context; pinned memory
+   otherwise, or with CAPNP_PERCALL_BAR=0) and its results land in pinned
+   host memory.  A call within
    1 ms of the context's previous per-message call goes to a resident
    service workgroup of its kind instead of a launch: it polls a pinned
    request line, serves each request, and exits 250 us after its last one

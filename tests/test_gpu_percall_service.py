@@ -154,3 +154,21 @@ def test_malformed_inputs_through_service():
             _read_check(ctx, bytes(bad), ("flip", k))
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("env", [{"CAPNP_PERCALL_BAR": "0"}, {"CAPNP_SVC_LINE_BAR": "1"},
+                                 {"CAPNP_PERCALL_SERVICE": "0"}])
+def test_staging_variants(env):
+    """The inputs staged in pinned memory (no BAR path), the request line in
+    device memory, and one launch per call: each in its own process (the
+    switches are read once)."""
+    import os
+    import subprocess
+    import sys
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "_percall_worker.py"), "31"],
+                       env={**os.environ, **env}, capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (r.stdout[-2000:],
+                                                                   r.stderr[-2000:])
