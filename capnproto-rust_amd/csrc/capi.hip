@@ -436,7 +436,7 @@ uint8_t* req_buf(capnp_ctx* ctx, size_t bytes) {
         }();
         int large = 0;
         ctx->req_ok = 0;
-        if (enabled &&
+        if (enabled && hipSetDevice(ctx->device) == hipSuccess &&
             hipDeviceGetAttribute(&large, hipDeviceAttributeIsLargeBar, ctx->device) == hipSuccess &&
             large == 1 &&
             hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->d_req), kReqBytes + 64,
@@ -545,6 +545,7 @@ void svc_atexit() {
 capnp_status svc_init(capnp_ctx* ctx, int k) {
     CallSvc& v = ctx->svc[k];
     if (v.s) return CAPNP_OK;
+    HIP_TRY(hipSetDevice(ctx->device));  // (the stream and the line are this device's)
     int lo = 0, hi = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIP_TRY(hipHostMalloc(&v.h, 256, 0));
