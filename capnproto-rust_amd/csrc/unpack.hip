@@ -2544,10 +2544,16 @@ unpack_wt_finish(const uint8_t* __restrict__ in, const uint64_t* __restrict__ in
 // (malformed, truncated, or longer than L): the caller then takes
 // unpack_long, which gives the exact status.
 #ifndef UNPACK_SMALL_BYTES
-#define UNPACK_SMALL_BYTES 5120  // (r06n, DPP scans: a 4.4 KB body 24.0 vs 26.0 us; 6.5 KB slower)
+// (r06n, DPP scans, before unpack_mid: 5120, a 4.4 KB body 24.0 vs 26.0 us
+// on unpack_long; with unpack_mid, 2048: 500-1000-word reads 14.3-16.3 us
+// against 16.4-20.6 at 5120, profiles/r06q_small_ab.txt)
+#define UNPACK_SMALL_BYTES 2048
 #endif
 constexpr uint32_t kSmallBytes = UNPACK_SMALL_BYTES;
-constexpr uint32_t kSmallLead = 48;  // (spec_seg_tile's kSegOverlap)
+#ifndef UNPACK_SMALL_LEAD
+#define UNPACK_SMALL_LEAD 96  // (48 as spec_seg_tile's kSegOverlap until r06q: a 1 KiB read 13.8 -> 12.4-12.6 us)
+#endif
+constexpr uint32_t kSmallLead = UNPACK_SMALL_LEAD;
 
 __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
                              uint64_t* __restrict__ out, uint32_t tid, uint32_t lane,
@@ -2727,7 +2733,7 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
 
 // ---------------------------------------------------------------------------
 // A mid-size read unit staged in the long-unit buffer (bodies of more than
-// kSmallBytes, up to kMidBytes, 5-18 KB): unpack_small's walk on all four waves, 256
+// kSmallBytes, up to kMidBytes, 2-18 KB): unpack_small's walk on all four waves, 256
 // segments, each wave settling its 64 by DPP rounds of its own; the waves
 // then meet once through LDS: wave w assumed its first segment's spec start
 // as its entry, and is re-run from the true one (the running maximum of the
@@ -2740,6 +2746,14 @@ __device__ bool unpack_small(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
 #define UNPACK_MID_BYTES 18432  // (the staged prefix's limit; a 4 Ki-word read 40.8 -> 30.7 us, r06p)
 #endif
 constexpr uint32_t kMidBytes = UNPACK_MID_BYTES;
+#ifndef UNPACK_MID_LEAD
+// spec walk lead-in (bytes) of the mid-size decode: 48 -> 96 took a
+// 1500-word read 21.7 -> 17.2-17.9 us and the carsales pair 34.9 -> 32.1-33.5
+// (profiles/r06q_midlead_ab*.txt; 128-160 are as good on carsales, worse on
+// 2200- and 3000-word bodies; 320 worse everywhere)
+#define UNPACK_MID_LEAD 96
+#endif
+constexpr uint32_t kMidLead = UNPACK_MID_LEAD;
 static_assert(kMidBytes + 32 <= kLuStage, "a mid-size unit lies in the staged bytes");
 
 __device__ bool unpack_mid(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
@@ -2764,8 +2778,8 @@ __device__ bool unpack_mid(LongSmem& S, uint32_t mis, uint32_t L, uint32_t n,
     const uint32_t j = tid;
     const uint32_t sb = (uint32_t)(((uint64_t)L * j) / kThreads);
     const uint32_t se = (uint32_t)(((uint64_t)L * (j + 1u)) / kThreads);
-    // spec walk from kSmallLead bytes before the segment (segment 0: byte 0)
-    uint32_t p = j == 0 ? 0u : (sb > kSmallLead ? sb - kSmallLead : 0u), w = 0;
+    // spec walk from kMidLead bytes before the segment (segment 0: byte 0)
+    uint32_t p = j == 0 ? 0u : (sb > kMidLead ? sb - kMidLead : 0u), w = 0;
     while (p < sb) seg_hop(B, p, w);
     const uint32_t f = p, wf = w;
     while (p < se) seg_hop(B, p, w);

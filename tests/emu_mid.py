@@ -4,7 +4,7 @@ rounds, the waves meeting through LDS), for tests/test_emu_mid.py.  Test
 infrastructure only: the oracle (serialize_packed.rs:80-228) is the
 reference; this checks the decode's logic on many inputs on the CPU."""
 
-LEAD = 48  # unpack.hip kSmallLead
+LEAD = 96  # unpack.hip kMidLead (UNPACK_MID_LEAD)
 
 
 def hop(B, p, w):

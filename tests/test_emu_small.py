@@ -1,5 +1,5 @@
 """CPU restatement of read_message's short-body decode (csrc/unpack.hip
-unpack_small: 64 segments, a 48-byte spec lead-in, meet / repair rounds with
+unpack_small: 64 segments, a 96-byte spec lead-in, meet / repair rounds with
 unpack_long's rules) checked against the true record chain: the rounds reach
 their fixed point within 65, every settled entry is a true record start (or
 passes through inside a record), and the words before the segment holding
@@ -20,7 +20,7 @@ def _hop(B, p, w):
     return p + bin(tag).count("1") + ext + 1, w + 1 + cnt
 
 
-def _emulate(body, n, lead=48, ns=64):
+def _emulate(body, n, lead=96, ns=64):  # (unpack.hip UNPACK_SMALL_LEAD)
     L = len(body)
     B = list(body) + [0] * 4200
     sb = [L * j // ns for j in range(ns)]
@@ -79,7 +79,7 @@ def test_small_rounds_match_true_chain(kind, words):
                    pz=O.PZ30, id0=77 + words + kind)
     st, body = O.pack(w.tobytes())
     assert st == 0
-    if len(body) > 3072:
+    if len(body) > 3072:  # (kSmallBytes is 2048 now; the emulator's logic holds past it)
         pytest.skip("past the short-body limit")
     used, wd, rounds, max_hops, B = _emulate(body, words)
     # the true chain's record starts and the words before each
