@@ -210,7 +210,10 @@ constexpr uint32_t kTileBlocks = kTileWaves * kWaveBlocks;  // 52
 constexpr uint32_t kTileThreads = kTileWaves * CAPNP_WAVE;
 // spec walk lead-in (bytes); 48 -> 64: config 4 index-free -2.7 % on two
 // boxes (32 / 80 / 96: 2478 / 2340 / 2295 us against 2311-2329)
-constexpr uint64_t kLead = 64;
+#ifndef RESYNC_LEAD
+#define RESYNC_LEAD 64
+#endif
+constexpr uint64_t kLead = RESYNC_LEAD;
 // hops a re-walk lets its spec chain catch up per step (32: 2439 us, slower)
 constexpr uint32_t kCatchUp = 16;
 constexpr uint32_t kTileLds = (uint32_t)(kTileBlocks * kBlock + kLead + 64);

@@ -1037,7 +1037,10 @@ __device__ __forceinline__ bool walk_segment(SM& S, uint32_t nc, uint32_t b, uin
 // Speculation changes the speed only, never the result.
 // spec walk lead-in (bytes); config 2 nosync: 0 -> 724 us, 16 -> 699,
 // 32 -> 646, 48 -> 614, 64 -> 640 (re-checked in round 3: 40-64 within noise)
-constexpr uint32_t kSegOverlap = 48;
+#ifndef UNPACK_SEG_OVERLAP
+#define UNPACK_SEG_OVERLAP 48
+#endif
+constexpr uint32_t kSegOverlap = UNPACK_SEG_OVERLAP;
 constexpr uint32_t kSegChunks = 16;  // tiles of at most this many chunks take the segment walk
 
 
