@@ -72,29 +72,35 @@ __device__ inline int32_t serial_read(const uint8_t* in, uint64_t in_len, uint8_
 // stores; a read_message call spent ~0.8 us in the table, r06q): a tag other
 // than 0x00 / 0xFF takes 1 + popcount(tag) bytes and no run.  The others,
 // and inputs shorter than 10 bytes, take serial_read.
+// (first_word: that fast case alone, in registers; false for the others)
+__device__ __forceinline__ bool first_word(const uint8_t* in, uint64_t in_len, uint64_t* word,
+                                           uint64_t* used) {
+    if (in_len < 10) return false;
+    uint32_t b[10];
+#pragma unroll
+    for (int i = 0; i < 10; i++) b[i] = in[i];
+    const uint32_t tag = b[0];
+    if (tag == 0u || tag == 0xFFu) return false;
+    uint64_t v = 0;  // the unit's non-zero bytes, in order
+#pragma unroll
+    for (int i = 8; i >= 1; i--) v = (v << 8) | b[i];
+    uint64_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t k = __builtin_popcount(tag & ((1u << i) - 1u));
+        if ((tag >> i) & 1u) x |= ((v >> (8 * k)) & 0xFFull) << (8 * i);
+    }
+    *word = x;
+    *used = 1u + __builtin_popcount(tag);
+    return true;
+}
+
 __device__ inline int32_t first_unit(const uint8_t* in, uint64_t in_len, uint8_t* out,
                                      uint64_t* word, uint64_t* used, uint64_t* nread) {
-    if (in_len >= 10) {
-        uint32_t b[10];
-#pragma unroll
-        for (int i = 0; i < 10; i++) b[i] = in[i];
-        const uint32_t tag = b[0];
-        if (tag != 0u && tag != 0xFFu) {
-            uint64_t v = 0;  // the unit's non-zero bytes, in order
-#pragma unroll
-            for (int i = 8; i >= 1; i--) v = (v << 8) | b[i];
-            uint64_t x = 0;
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                const uint32_t k = __builtin_popcount(tag & ((1u << i) - 1u));
-                if ((tag >> i) & 1u) x |= ((v >> (8 * k)) & 0xFFull) << (8 * i);
-            }
-            *reinterpret_cast<uint64_t*>(out) = x;
-            *word = x;
-            *used = 1u + __builtin_popcount(tag);
-            *nread = 8;
-            return ST_OK;
-        }
+    if (first_word(in, in_len, word, used)) {
+        *reinterpret_cast<uint64_t*>(out) = *word;
+        *nread = 8;
+        return ST_OK;
     }
     const int32_t st = serial_read(in, in_len, out, 8, used, nread);
     *word = *reinterpret_cast<const uint64_t*>(out);

@@ -3035,27 +3035,61 @@ __device__ __forceinline__ void msg_read_body(USmem& sm, MsgReadSmem& M, const u
 #if SVC_PROF
     const uint64_t tp0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (tid == 0) {
-        // (the table's read units end within kMsgPre bytes whenever the input
-        // is longer: the staged prefix gives the same results as the input)
-        capnp_frame::frame_table(sm.lu.bytes, npre, no_alloc, try_mode, limit, has_limit,
-                                 buffer_len, body_cap, &M.fr);
-        if (M.fr.status == 0) M.fr.body_in_off[1] = in_len;  // (the unit runs to the input end)
-        M.offs[0] = M.fr.body_in_off[0];
-        M.offs[1] = M.fr.body_in_off[1];
-        M.offs[2] = 0;
-        M.offs[3] = M.fr.body_out_off[1];
-        M.st = 0;
-        M.used = 0;
+    // The common table -- one segment, a first read unit that is no run, a
+    // body within the caps -- is decoded by every thread from the staged
+    // bytes (the same LDS bytes, broadcast reads), and a short or mid-size
+    // body's decode starts at once; the rest take lane 0's frame_table and
+    // a barrier (0.75 us of a read, r06q_bar_svcprof).
+    uint64_t w0 = 0, u0 = 0;
+    const bool fw = !no_alloc && capnp_frame::first_word(sm.lu.bytes, npre, &w0, &u0);
+    const uint64_t ftot = w0 >> 32;
+    const bool fast = fw && (uint32_t)w0 == 0u && ftot > 0 && ftot <= body_cap &&
+                      !(has_limit && ftot > limit);  // (uniform: the same bytes everywhere)
+    if (fast) {
+        if (tid == 0) {  // (frame_table's record for this table)
+            M.fr.status = 0;
+            M.fr.nseg = 1;
+            M.fr.table_consumed = u0;
+            M.fr.total_words = ftot;
+            M.fr.table_bytes = 8;
+            M.fr.body_in_off[0] = u0;
+            M.fr.body_in_off[1] = in_len;
+            M.fr.body_out_off[0] = 0;
+            M.fr.body_out_off[1] = ftot;
+            M.fr.seg_words[0] = (uint32_t)ftot;
+            *reinterpret_cast<uint64_t*>(M.fr.table) = w0;
+            M.offs[0] = u0;
+            M.offs[1] = in_len;
+            M.offs[2] = 0;
+            M.offs[3] = ftot;
+            M.st = 0;
+            M.used = 0;
+        }
+    } else {
+        if (tid == 0) {
+            // (the table's read units end within kMsgPre bytes whenever the
+            // input is longer: the staged prefix gives the same results as
+            // the input)
+            capnp_frame::frame_table(sm.lu.bytes, npre, no_alloc, try_mode, limit, has_limit,
+                                     buffer_len, body_cap, &M.fr);
+            if (M.fr.status == 0) M.fr.body_in_off[1] = in_len;  // (the unit runs to the input end)
+            M.offs[0] = M.fr.body_in_off[0];
+            M.offs[1] = M.fr.body_in_off[1];
+            M.offs[2] = 0;
+            M.offs[3] = M.fr.body_out_off[1];
+            M.st = 0;
+            M.used = 0;
+        }
+        __syncthreads();
     }
-    __syncthreads();
 #if SVC_PROF
     const uint64_t tp1 = __builtin_amdgcn_s_memrealtime();
 #endif
-    if (M.fr.status == 0 && M.offs[3] > 0) {  // (uniform: LDS after the barrier)
+    // (uniform: registers, or LDS after the barrier)
+    if (fast || (M.fr.status == 0 && M.offs[3] > 0)) {
         // a short body inside the staged prefix: wave 0 alone (unpack_small);
         // the rest, and any body it does not take, unpack_long
-        const uint64_t P0 = M.offs[0], nw = M.offs[3];
+        const uint64_t P0 = fast ? u0 : M.offs[0], nw = fast ? ftot : M.offs[3];
         const uint64_t avail = (uint64_t)pre > P0 ? pre - P0 : 0;
         const uint64_t span = in_len - P0 < avail ? in_len - P0 : avail;
         const uint64_t Ls = span < 10 * nw + 16 ? span : 10 * nw + 16;
@@ -3072,9 +3106,11 @@ __device__ __forceinline__ void msg_read_body(USmem& sm, MsgReadSmem& M, const u
                 M.used = used;
             }
         }
-        if (!done)
+        if (!done) {
+            if (fast) __syncthreads();  // (lane 0's M.offs)
             unpack_long(sm, in, M.offs, 0, words, M.offs + 2, &M.st, &M.used, tid, lane, wave,
                         pre);
+        }
     }
     __syncthreads();
 #if SVC_PROF
